@@ -1,0 +1,92 @@
+/* libmmt_hip — C ABI of the MI355X (gfx950) hot path of an OCTO-style multimodal transformer
+ * training step with token merging (ToMe).
+ *
+ * The reference (maggieHao/multi_modal_transformers_TokenMerge, JAX/Flax) has no FFI: its
+ * "interface" is the Flax module / function API. Each entry point below names the reference
+ * function or Flax layer it replaces (paths relative to the reference's multi_modal_transformers/).
+ *
+ * Conventions
+ *   - All tensor arguments are caller-owned DEVICE pointers; the library allocates nothing.
+ *   - Strides are in ELEMENTS. Shapes are int, strides int64_t.
+ *   - Every call is ordered on `stream` (a hipStream_t passed as void*), is graph-capturable
+ *     (no host sync, no allocation) and returns MMT_OK (0) or a negative MMT_ERR_* code.
+ *   - mmt_last_error() returns a thread-local description of the last failure.
+ *   - dtype codes: MMT_F32 = 0, MMT_BF16 = 1.
+ */
+#ifndef MMT_API_H
+#define MMT_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* mmt_stream_t;
+
+enum { MMT_OK = 0, MMT_ERR_INVALID = -1, MMT_ERR_HIP = -2, MMT_ERR_UNSUPPORTED = -3 };
+enum { MMT_F32 = 0, MMT_BF16 = 1 };
+/* ToMe flags. CLASS/DISTILL: token_compression.py:57-64. PLAIN_SUM: the bare merge(x, "sum")
+ * closure (no size weighting, no division). NO_SCATTER: merge(x, mode) with mode != "sum", which
+ * in the reference leaves dst unchanged (:99-101). */
+enum {
+  MMT_TOME_CLASS_TOKEN = 1,
+  MMT_TOME_DISTILL_TOKEN = 2,
+  MMT_TOME_PLAIN_SUM = 4,
+  MMT_TOME_NO_SCATTER = 8
+};
+
+const char* mmt_last_error(void);
+int mmt_version(void);
+
+/* ------------------------------------------------------------------ ToMe
+ * mmt_tome_match replaces tokenizers/token_compression.py:54-112 (bipartite_soft_matching)
+ * for an r that the caller has already clamped to min(r, (t - protected) // 2) > 0
+ * (token_compression.py:66-70; the r <= 0 "do nothing" branch is the caller's).
+ *
+ * metric element (b, i, h, k) lives at metric[b*s_n + i*s_t + h*s_h + k]; the matching metric is
+ * the fp32 sum over h = 0..heads-1 (heads = 1 for a plain (n, t, c) metric; heads = H gives the
+ * ToMe key metric  sum_h K  of tome_attention.py:253).
+ * Outputs (int32, per batch row contiguous): unm_idx[n][ta - r], src_idx[n][r], dst_idx[n][r],
+ * where ta = ceil(t/2) (indices into the a = x[::2] / b = x[1::2] halves, exactly as the
+ * reference's edge_idx / node_idx). node_max[n][ta] (fp32) is optional (may be NULL).
+ * Arithmetic is canonical (see DESIGN.md "ToMe canonical arithmetic") so indices are bit-exact
+ * with oracle/tome_ref.c.
+ */
+int mmt_tome_match(const void* metric, int dtype, int n, int t, int heads, int c, int64_t s_n,
+                   int64_t s_t, int64_t s_h, int r, int flags, int32_t* unm_idx, int32_t* src_idx,
+                   int32_t* dst_idx, float* node_max, mmt_stream_t stream);
+
+/* mmt_tome_merge_wavg_fwd replaces token_compression.py:114-129 (merge_wavg) applied with the
+ * merge closure of :90-109 (mode "sum"), fused with the surrounding sequence copy:
+ * x is a sequence (n, L, D) whose rows [set_start, set_start + t) are the merged token set; the
+ * output sequence (n, L - r, D) holds rows [0, set_start) copied, then the t - r merged rows
+ * (concat[unm, dst], or the distill interleave), then the remaining rows copied.
+ * size_in (n, t) fp32 may be NULL (= ones). size_out (n, t - r) receives the merged sizes.
+ * pos_map (n, t) int32 (optional) receives, for each set token, the merged row it went to.
+ */
+int mmt_tome_merge_wavg_fwd(const void* x, int dtype, int n, int L, int D, int64_t x_s_n,
+                            int64_t x_s_t, int set_start, int t, int r, int flags,
+                            const float* size_in, const int32_t* unm_idx, const int32_t* src_idx,
+                            const int32_t* dst_idx, void* x_out, int64_t o_s_n, int64_t o_s_t,
+                            float* size_out, int32_t* pos_map, mmt_stream_t stream);
+
+/* Selects the score path of mmt_tome_match: 1 = f32 MFMA (v_mfma_f32_32x32x2_f32, default),
+ * 0 = VALU fmaf chain. Both produce the same canonical fmaf chain; the switch exists so the
+ * parity tests can check each against the oracle. */
+void mmt_tome_set_match_path(int use_mfma);
+
+/* Backward of mmt_tome_merge_wavg_fwd w.r.t. x (sizes carry no gradient; the metric carries
+ * none either: argmax/argsort):  g_in[row] = g_out[pos(row)] * size_in[row] / size_out[pos(row)]
+ * for set rows, plain copy for the others.  pos_map comes from the forward. size_in and size_out
+ * may both be NULL: the bare merge(x, "sum") closure, whose Jacobian is a 0/1 gather. */
+int mmt_tome_merge_wavg_bwd(const void* g_out, int dtype, int n, int L, int D, int64_t go_s_n,
+                            int64_t go_s_t, int set_start, int t, int r, const float* size_in,
+                            const float* size_out, const int32_t* pos_map, void* g_in,
+                            int64_t gi_s_n, int64_t gi_s_t, mmt_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMT_API_H */

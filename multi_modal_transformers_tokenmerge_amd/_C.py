@@ -1,0 +1,72 @@
+"""ctypes binding of libmmt_hip.so (the C ABI declared in include/mmt_api.h).
+
+There is deliberately no CPU or PyTorch fallback: if the library is missing every op raises.
+Build it with ``python -m multi_modal_transformers_tokenmerge_amd.csrc.build`` (or
+``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+
+_LIB_PATH = Path(__file__).resolve().parent / "libmmt_hip.so"
+_lib = None
+
+P, I, L, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+U32, U64, Z = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
+
+# name -> argtypes (every entry point returns int status unless listed in _VOID)
+SIGNATURES: dict[str, list] = {
+    "mmt_version": [],
+    "mmt_tome_set_match_path": [I],
+    "mmt_tome_match": [P, I, I, I, I, I, L, L, L, I, I, P, P, P, P, P],
+    "mmt_tome_merge_wavg_fwd": [P, I, I, I, I, L, L, I, I, I, I, P, P, P, P, P, L, L, P, P, P],
+    "mmt_tome_merge_wavg_bwd": [P, I, I, I, I, L, L, I, I, I, P, P, P, P, L, L, P],
+}
+_VOID = {"mmt_tome_set_match_path"}
+
+
+class MMTError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not _LIB_PATH.exists():
+            raise ImportError(f"{_LIB_PATH} is missing: build it with "
+                              "`python -m multi_modal_transformers_tokenmerge_amd.csrc.build` "
+                              "(no CPU fallback exists by design)")
+        h = ctypes.CDLL(str(_LIB_PATH))
+        h.mmt_last_error.restype = ctypes.c_char_p
+        h.mmt_last_error.argtypes = []
+        for name, args in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.argtypes = args
+            fn.restype = None if name in _VOID else I
+        _lib = h
+    return _lib
+
+
+def call(name: str, *args) -> int:
+    rc = getattr(lib(), name)(*args)
+    if name in _VOID:
+        return 0
+    if rc != 0:
+        msg = lib().mmt_last_error().decode(errors="replace")
+        raise MMTError(f"{name} failed ({rc}): {msg}")
+    return rc
+
+
+def exported_symbols() -> list[str]:
+    return ["mmt_last_error", *SIGNATURES.keys()]
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_ptr() -> int:
+    import torch
+    return torch.cuda.current_stream().cuda_stream

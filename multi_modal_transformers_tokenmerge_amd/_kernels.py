@@ -1,0 +1,103 @@
+"""Torch-facing wrappers of the C ABI (device tensors in, device tensors out).
+
+Each wrapper validates shapes/dtypes/devices on the host BEFORE launching (a bad shape must never
+reach a kernel) and calls exactly one libmmt_hip entry point on the current HIP stream. Nothing
+here computes on the CPU: a missing library raises (see _C.py).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _C
+from ._C import ptr
+
+DT = {torch.float32: 0, torch.bfloat16: 1}
+
+
+def _dtype_code(t: torch.Tensor) -> int:
+    if t.dtype not in DT:
+        raise TypeError(f"unsupported dtype {t.dtype}; expected float32 or bfloat16")
+    return DT[t.dtype]
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("libmmt_hip ops take device (cuda/HIP) tensors only")
+
+
+# ------------------------------------------------------------------------------------ ToMe
+FLAG_CLASS, FLAG_DISTILL, FLAG_PLAIN_SUM, FLAG_NO_SCATTER = 1, 2, 4, 8
+
+
+def set_tome_match_path(use_mfma: bool) -> None:
+    _C.call("mmt_tome_set_match_path", int(bool(use_mfma)))
+
+
+def tome_match(metric: torch.Tensor, r: int, flags: int = 0, return_node_max: bool = False):
+    """metric (n, t, c) or (n, t, heads, c) (any strides with unit inner stride) -> (unm, src, dst
+    [, node_max]) int32 device tensors. r must already be clamped (> 0)."""
+    _dev(metric)
+    if metric.dim() == 3:
+        n, t, c = metric.shape
+        heads, s_h = 1, 0
+        s_n, s_t = metric.stride(0), metric.stride(1)
+        if metric.stride(2) != 1:
+            raise ValueError("metric must have unit stride along c")
+    elif metric.dim() == 4:
+        n, t, heads, c = metric.shape
+        s_n, s_t, s_h = metric.stride(0), metric.stride(1), metric.stride(2)
+        if metric.stride(3) != 1:
+            raise ValueError("metric must have unit stride along c")
+    else:
+        raise ValueError("metric must be (n, t, c) or (n, t, heads, c)")
+    ta = (t + 1) // 2
+    dev = metric.device
+    unm = torch.empty((n, ta - r), dtype=torch.int32, device=dev)
+    src = torch.empty((n, r), dtype=torch.int32, device=dev)
+    dst = torch.empty((n, r), dtype=torch.int32, device=dev)
+    nmax = torch.empty((n, ta), dtype=torch.float32, device=dev) if return_node_max else None
+    _C.call("mmt_tome_match", ptr(metric), _dtype_code(metric), n, t, heads, c, s_n, s_t, s_h, r,
+            flags, ptr(unm), ptr(src), ptr(dst), ptr(nmax), _C.stream_ptr())
+    return (unm, src, dst, nmax) if return_node_max else (unm, src, dst)
+
+
+def tome_merge_fwd(x: torch.Tensor, set_start: int, t: int, r: int, unm, src, dst,
+                   size_in: torch.Tensor | None = None, flags: int = 0, out: torch.Tensor | None = None,
+                   want_pos_map: bool = True):
+    """x (n, L, D) sequence; merges rows [set_start, set_start+t). Returns (x_out (n, L-r, D),
+    size_out (n, t-r) fp32, pos_map (n, t) int32 or None)."""
+    _dev(x, size_in, unm, src, dst)
+    n, L, D = x.shape
+    if x.stride(2) != 1:
+        raise ValueError("x must have unit stride along D")
+    if not (0 <= set_start and set_start + t <= L):
+        raise ValueError("token set out of range")
+    for a, shape in ((unm, (n, (t + 1) // 2 - r)), (src, (n, r)), (dst, (n, r))):
+        if tuple(a.shape) != shape or a.dtype != torch.int32 or not a.is_contiguous():
+            raise ValueError(f"index tensor must be contiguous int32 {shape}")
+    if size_in is not None:
+        if tuple(size_in.shape) != (n, t) or size_in.dtype != torch.float32 or not size_in.is_contiguous():
+            raise ValueError("size_in must be contiguous fp32 (n, t)")
+    if out is None:
+        out = torch.empty((n, L - r, D), dtype=x.dtype, device=x.device)
+    size_out = torch.empty((n, t - r), dtype=torch.float32, device=x.device)
+    pos_map = torch.empty((n, t), dtype=torch.int32, device=x.device) if want_pos_map else None
+    _C.call("mmt_tome_merge_wavg_fwd", ptr(x), _dtype_code(x), n, L, D, x.stride(0), x.stride(1),
+            set_start, t, r, flags, ptr(size_in), ptr(unm), ptr(src), ptr(dst), ptr(out),
+            out.stride(0), out.stride(1), ptr(size_out), ptr(pos_map), _C.stream_ptr())
+    return out, size_out, pos_map
+
+
+def tome_merge_bwd(g_out: torch.Tensor, set_start: int, t: int, r: int, pos_map: torch.Tensor,
+                   size_in: torch.Tensor | None, size_out: torch.Tensor | None,
+                   out: torch.Tensor | None = None):
+    _dev(g_out, pos_map, size_in, size_out)
+    n, Lr, D = g_out.shape
+    L = Lr + r
+    if out is None:
+        out = torch.empty((n, L, D), dtype=g_out.dtype, device=g_out.device)
+    _C.call("mmt_tome_merge_wavg_bwd", ptr(g_out), _dtype_code(g_out), n, L, D, g_out.stride(0),
+            g_out.stride(1), set_start, t, r, ptr(size_in), ptr(size_out), ptr(pos_map), ptr(out),
+            out.stride(0), out.stride(1), _C.stream_ptr())
+    return out

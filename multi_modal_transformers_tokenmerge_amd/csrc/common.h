@@ -1,0 +1,97 @@
+// Shared device/host helpers for libmmt_hip (gfx950 / CDNA4 only).
+//
+// Conventions of the C ABI (include/mmt_api.h):
+//   * every tensor is a caller-owned device pointer; the library never allocates on the hot path;
+//   * every entry point is stream-ordered and returns 0 (MMT_OK) or a negative code, never aborts;
+//   * mmt_last_error() returns a thread-local message for the last failing call.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/mmt_api.h"
+
+namespace mmt {
+
+// ---------------------------------------------------------------- errors
+void set_error(const char* fmt, ...);
+
+#define MMT_CHECK_ARG(cond, ...)              \
+  do {                                        \
+    if (!(cond)) {                            \
+      ::mmt::set_error(__VA_ARGS__);          \
+      return MMT_ERR_INVALID;                 \
+    }                                         \
+  } while (0)
+
+#define MMT_CHECK_LAUNCH(name)                                             \
+  do {                                                                     \
+    hipError_t e_ = hipGetLastError();                                     \
+    if (e_ != hipSuccess) {                                                \
+      ::mmt::set_error("%s: launch failed: %s", name, hipGetErrorString(e_)); \
+      return MMT_ERR_HIP;                                                  \
+    }                                                                      \
+  } while (0)
+
+// ---------------------------------------------------------------- bf16
+typedef uint16_t bf16_t;
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+// round-to-nearest-even; NaN stays NaN (the compiler emits v_cvt_pk_bf16_f32 for the cast).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+template <typename T> __device__ __forceinline__ float ld_f32(const T* p);
+template <> __device__ __forceinline__ float ld_f32<float>(const float* p) { return *p; }
+template <> __device__ __forceinline__ float ld_f32<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+template <typename T> __device__ __forceinline__ void st_f32(T* p, float v);
+template <> __device__ __forceinline__ void st_f32<float>(float* p, float v) { *p = v; }
+template <> __device__ __forceinline__ void st_f32<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
+
+// ---------------------------------------------------------------- counter-based RNG
+// lowbias32 (a bijective 32-bit mixer). The oracle (oracle/rng.py) restates it in numpy uint32
+// arithmetic, so dropout masks / sampled tokens are bit-identical on both sides.
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+// Key of one random stream: (seed, step, layer, site). Element draw = mix32(key ^ mix32(ctr)).
+__host__ __device__ __forceinline__ uint32_t stream_key(uint32_t seed, uint32_t step, uint32_t layer,
+                                                        uint32_t site) {
+  uint32_t k = mix32(seed ^ 0x9e3779b9u);
+  k = mix32(k ^ (step * 0x85ebca6bu));
+  k = mix32(k ^ (layer * 0xc2b2ae35u) ^ (site << 24));
+  return k;
+}
+__host__ __device__ __forceinline__ uint32_t draw_u32(uint32_t key, uint32_t ctr) {
+  return mix32(key ^ mix32(ctr));
+}
+// keep-probability threshold: keep iff draw < thresh, thresh = floor(keep_prob * 2^32)
+__host__ __device__ __forceinline__ bool keep_draw(uint32_t key, uint32_t ctr, uint32_t thresh) {
+  return draw_u32(key, ctr) < thresh;
+}
+
+// ---------------------------------------------------------------- wave helpers (wave64)
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+inline hipStream_t as_stream(mmt_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace mmt

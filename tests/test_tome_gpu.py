@@ -1,0 +1,140 @@
+"""GPU parity: gfx950 ToMe kernels vs the canonical C oracle — bit-exact indices and merges."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import tome as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf16_round(a: np.ndarray) -> np.ndarray:
+    return torch.from_numpy(a).bfloat16().float().numpy()
+
+
+@pytest.fixture(params=[True, False], ids=["mfma", "valu"])
+def match_path(request):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    K.set_tome_match_path(request.param)
+    yield request.param
+    K.set_tome_match_path(True)
+
+
+CASES = [(4, 256, 64, 1, 16, 0), (3, 257, 64, 1, 16, 0), (2, 64, 32, 1, 8, 1), (2, 64, 32, 1, 8, 2),
+         (2, 64, 32, 1, 8, 3), (2, 31, 6, 1, 7, 0), (5, 292, 64, 6, 16, 0), (2, 512, 64, 1, 32, 0),
+         (64, 256, 64, 6, 16, 0)]
+
+
+@pytest.mark.parametrize("n,t,c,heads,r,flags", CASES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_match_bit_exact(dev, match_path, n, t, c, heads, r, flags, dtype):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    if c % 2 and match_path:
+        pass  # odd c falls back to the VALU path inside the library
+    g = torch.Generator().manual_seed(n * 1000 + t + c + heads + flags)
+    m = torch.randn((n, t, heads, c), generator=g).to(dtype)
+    exact = m.float().numpy()
+    cu, cs, cd, cn = O.canon_match(exact, r, flags)
+    dm = m.to(dev) if heads > 1 else m[:, :, 0].to(dev)
+    unm, src, dst, nmax = K.tome_match(dm, r, flags, return_node_max=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(unm.cpu().numpy(), cu)
+    np.testing.assert_array_equal(src.cpu().numpy(), cs)
+    np.testing.assert_array_equal(dst.cpu().numpy(), cd)
+    np.testing.assert_array_equal(nmax.cpu().numpy().view(np.uint32), cn.view(np.uint32))
+
+
+def test_match_ties_and_zero_rows(dev, match_path):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    m = np.ones((2, 16, 4), np.float32)
+    m[1, 3] = 0.0  # zero row -> NaN scores (no eps in the reference, :72)
+    m[1, 8] = 0.0
+    cu, cs, cd, _ = O.canon_match(m, 5)
+    unm, src, dst = K.tome_match(torch.from_numpy(m).to(dev), 5)
+    np.testing.assert_array_equal(src.cpu().numpy(), cs)
+    np.testing.assert_array_equal(dst.cpu().numpy(), cd)
+    np.testing.assert_array_equal(unm.cpu().numpy(), cu)
+    # KAT-1 through the kernel
+    unm, src, dst = K.tome_match(torch.ones((1, 8, 4), device=dev), 2)
+    assert src.tolist() == [[3, 2]] and dst.tolist() == [[0, 0]] and unm.tolist() == [[1, 0]]
+
+
+@pytest.mark.parametrize("n,L,set_start,t,D,r,flags", [
+    (3, 256, 0, 256, 64, 16, 0), (4, 292, 32, 256, 384, 16, 0), (2, 100, 10, 61, 64, 20, 0),
+    (2, 80, 5, 64, 128, 8, 2), (2, 80, 5, 64, 128, 8, 4), (2, 80, 5, 64, 128, 8, 12),
+    (8, 1060, 32, 1024, 768, 32, 0)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_merge_fwd_bwd_bit_exact(dev, n, L, set_start, t, D, r, flags, dtype):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    rng = np.random.default_rng(n + L + t + D + r + flags)
+    metric = rng.standard_normal((n, t, 16)).astype(np.float32)
+    cu, cs, cd, _ = O.canon_match(metric, r)
+    x = rng.standard_normal((n, L, D)).astype(np.float32)
+    if dtype == torch.bfloat16:
+        x = _bf16_round(x)
+    size = rng.integers(1, 6, (n, t)).astype(np.float32)
+    xo_ref, so_ref = O.canon_merge_wavg(x[:, set_start:set_start + t], size, cu, cs, cd, r, flags)
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    xd = tt(x).to(dtype)
+    out, so, pos = K.tome_merge_fwd(xd, set_start, t, r, tt(cu), tt(cs), tt(cd), size_in=tt(size),
+                                    flags=flags)
+    torch.cuda.synchronize()
+    out = out.float().cpu().numpy()
+    exp = xo_ref if dtype == torch.float32 else _bf16_round(xo_ref)
+    np.testing.assert_array_equal(out[:, set_start:set_start + t - r].view(np.uint32),
+                                  exp.view(np.uint32))
+    np.testing.assert_array_equal(out[:, :set_start], x[:, :set_start])
+    np.testing.assert_array_equal(out[:, set_start + t - r:], x[:, set_start + t:])
+    np.testing.assert_array_equal(so.cpu().numpy(), so_ref)
+    if flags & 8:
+        return  # dropped src tokens have no merged row: pos_map only covers scattered merges
+    pos_ref = O.canon_pos_map(cu, cs, cd, t, r, flags)
+    np.testing.assert_array_equal(pos.cpu().numpy(), pos_ref)
+    # backward
+    g = rng.standard_normal((n, L - r, D)).astype(np.float32)
+    if dtype == torch.bfloat16:
+        g = _bf16_round(g)
+    plain = bool(flags & 4)
+    gi = K.tome_merge_bwd(tt(g).to(dtype), set_start, t, r, pos, None if plain else tt(size),
+                          None if plain else so)
+    torch.cuda.synchronize()
+    gi = gi.float().cpu().numpy()
+    gref = O.canon_merge_bwd(g[:, set_start:set_start + t - r], None if plain else size,
+                             np.ones_like(so_ref) if plain else so_ref, pos_ref)
+    if dtype == torch.bfloat16:
+        gref = _bf16_round(gref)
+    np.testing.assert_array_equal(gi[:, set_start:set_start + t].view(np.uint32), gref.view(np.uint32))
+    np.testing.assert_array_equal(gi[:, :set_start], g[:, :set_start])
+    np.testing.assert_array_equal(gi[:, set_start + t:], g[:, set_start + t - r:])
+
+
+def test_reference_api_merge_wavg_autograd(dev):
+    from multi_modal_transformers_tokenmerge_amd.tokenizers.token_compression import (
+        bipartite_soft_matching, merge_wavg, do_nothing)
+    rng = np.random.default_rng(3)
+    metric = torch.from_numpy(rng.standard_normal((2, 40, 8)).astype(np.float32)).to(dev)
+    x = torch.from_numpy(rng.standard_normal((2, 40, 16)).astype(np.float32)).to(dev).requires_grad_()
+    merge = bipartite_soft_matching(metric, 6)
+    out, size = merge_wavg(merge, x)
+    assert out.shape == (2, 34, 16) and size.shape == (2, 34, 1)
+    lit_merge, *_ = O.literal_bipartite_soft_matching(metric.cpu().numpy(), 6)
+    lo, ls = O.literal_merge_wavg(lit_merge, x.detach().cpu().numpy())
+    np.testing.assert_allclose(out.detach().cpu().numpy(), lo, rtol=1e-6, atol=1e-6)
+    w = torch.randn_like(out)
+    (out * w).sum().backward()
+    # torch-CPU autograd reference of the same gather/scatter
+    xc = x.detach().cpu().double().requires_grad_()
+    unm, src, dst = (a.long().cpu() for a in (merge.unm_idx, merge.src_idx, merge.dst_idx))
+    a, b = xc[:, ::2], xc[:, 1::2]
+    rows = []
+    for bi in range(2):
+        dstb = b[bi].clone()
+        sz = torch.ones(b.shape[1], dtype=torch.float64)
+        for i in range(6):
+            dstb[dst[bi, i]] = dstb[dst[bi, i]] + a[bi, src[bi, i]]
+            sz[dst[bi, i]] += 1
+        rows.append(torch.cat([a[bi, unm[bi]], dstb / sz[:, None]]))
+    (torch.stack(rows) * w.cpu().double()).sum().backward()
+    np.testing.assert_allclose(x.grad.cpu().numpy(), xc.grad.numpy(), rtol=1e-5, atol=1e-6)
+    # r = 0: reference returns the do_nothing pair
+    assert bipartite_soft_matching(metric[:, :1], 3) == (do_nothing, do_nothing)
