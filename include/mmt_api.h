@@ -86,6 +86,46 @@ int mmt_tome_merge_wavg_bwd(const void* g_out, int dtype, int n, int L, int D, i
                             const float* size_out, const int32_t* pos_map, void* g_in,
                             int64_t gi_s_n, int64_t gi_s_t, mmt_stream_t stream);
 
+
+/* ------------------------------------------------------------------ GEMM (MFMA bf16)
+ * C = epilogue(op(A) . op(B)), fp32 accumulation, replacing every flax.linen.Dense /
+ * DenseGeneral on the path (attention.py:32-37 MLPBlock; Flax SelfAttention q/k/v/out
+ * projections configured in model_configs/attention_blocks/vanilla_decoder.yaml:19-31; the
+ * image stem and output Dense, image_tokenizer.py:158-176; diffusion.py:41-65; T5 layers) and
+ * their backward products (dX = dY.W, dW = dY^T.X).
+ *   transA = 0: A is [M][K] (lda >= K);  transA = 1: A is stored [K][M] (lda >= M)
+ *   transB = 0: B is [K][N] (ldb >= N);  transB = 1: B is stored [N][K] (ldb >= K)
+ * A, B bf16; contiguous dims and strides multiples of 8 elements, base pointers 16-B aligned.
+ * c_mode: MMT_OUT_BF16 (store), MMT_OUT_F32 (C = epi + beta*C), MMT_OUT_F32_ATOMIC (C += alpha*acc,
+ * the split-K / gradient-accumulation form; no other epilogue).
+ * Batched: blockIdx.z = batch index, with element strides sA, sB, sC.
+ * Epilogue order: v = alpha*acc + bias[n]; act; v *= (gate[m][n] > 0 ? gate_scale : 0);
+ * dropout (keep iff mix32(key ^ mix32(ctr)) < keep_prob*2^32, ctr = (drop_row_offset + m)*N + n,
+ * key = stream_key(rng[0], rng[1], drop_layer, drop_site); kept values scaled by 1/keep_prob —
+ * flax.linen.Dropout semantics with a counter-based stream); v += residual[m][n].
+ */
+enum { MMT_ACT_NONE = 0, MMT_ACT_RELU = 1 };
+enum { MMT_OUT_BF16 = 0, MMT_OUT_F32 = 1, MMT_OUT_F32_ATOMIC = 2 };
+
+typedef struct {
+  const float* bias;          /* [N] fp32 or NULL */
+  int act;                    /* MMT_ACT_* */
+  const uint32_t* rng;        /* device {seed, step} or NULL (no dropout) */
+  uint32_t drop_layer, drop_site;
+  float keep_prob;
+  int64_t drop_row_offset;
+  const void* gate;           /* bf16 [M][ld_gate] or NULL */
+  int64_t ld_gate;
+  float gate_scale;
+  const void* residual;       /* bf16 [M][ld_res] or NULL */
+  int64_t ld_res;
+  float alpha, beta;
+} mmt_epilogue_t;
+
+int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t lda, const void* B,
+             int transB, int64_t ldb, void* C, int c_mode, int64_t ldc, int batch, int64_t sA,
+             int64_t sB, int64_t sC, int split_k, const mmt_epilogue_t* epi, mmt_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -15,6 +15,13 @@ _lib = None
 P, I, L, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
 U32, U64, Z = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
 
+class Epilogue(ctypes.Structure):
+    """mmt_epilogue_t (include/mmt_api.h)."""
+    _fields_ = [("bias", P), ("act", I), ("rng", P), ("drop_layer", U32), ("drop_site", U32),
+                ("keep_prob", F), ("drop_row_offset", L), ("gate", P), ("ld_gate", L),
+                ("gate_scale", F), ("residual", P), ("ld_res", L), ("alpha", F), ("beta", F)]
+
+
 # name -> argtypes (every entry point returns int status unless listed in _VOID)
 SIGNATURES: dict[str, list] = {
     "mmt_version": [],
@@ -22,6 +29,7 @@ SIGNATURES: dict[str, list] = {
     "mmt_tome_match": [P, I, I, I, I, I, L, L, L, I, I, P, P, P, P, P],
     "mmt_tome_merge_wavg_fwd": [P, I, I, I, I, L, L, I, I, I, I, P, P, P, P, P, L, L, P, P, P],
     "mmt_tome_merge_wavg_bwd": [P, I, I, I, I, L, L, I, I, I, P, P, P, P, L, L, P],
+    "mmt_gemm": [I, I, I, P, I, L, P, I, L, P, I, L, I, L, L, L, I, P, P],
 }
 _VOID = {"mmt_tome_set_match_path"}
 

@@ -101,3 +101,59 @@ def tome_merge_bwd(g_out: torch.Tensor, set_start: int, t: int, r: int, pos_map:
             g_out.stride(1), set_start, t, r, ptr(size_in), ptr(size_out), ptr(pos_map), ptr(out),
             out.stride(0), out.stride(1), _C.stream_ptr())
     return out
+
+
+# ------------------------------------------------------------------------------------ GEMM
+OUT_BF16, OUT_F32, OUT_F32_ATOMIC = 0, 1, 2
+ACT_NONE, ACT_RELU = 0, 1
+
+
+def _epi(bias=None, act=ACT_NONE, rng=None, drop_layer=0, drop_site=0, keep_prob=1.0,
+         drop_row_offset=0, gate=None, gate_scale=1.0, residual=None, alpha=1.0, beta=0.0):
+    e = _C.Epilogue()
+    e.bias = ptr(bias)
+    e.act = act
+    e.rng = ptr(rng)
+    e.drop_layer, e.drop_site = drop_layer, drop_site
+    e.keep_prob = keep_prob
+    e.drop_row_offset = drop_row_offset
+    e.gate = ptr(gate)
+    e.ld_gate = gate.stride(0) if gate is not None else 0
+    e.gate_scale = gate_scale
+    e.residual = ptr(residual)
+    e.ld_res = residual.stride(0) if residual is not None else 0
+    e.alpha, e.beta = alpha, beta
+    return e
+
+
+def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool = False,
+         out: torch.Tensor | None = None, out_mode: int = OUT_BF16, split_k: int = 1, **epi):
+    """2-D GEMM: op(a) (M x K) . op(b) (K x N). a/b bf16 with unit inner stride.
+    trans_a: a is stored (K, M); trans_b: b is stored (N, K) (a weight W[N][K])."""
+    _dev(a, b, out)
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        raise TypeError("gemm operands must be bfloat16")
+    if a.stride(-1) != 1 or b.stride(-1) != 1:
+        raise ValueError("gemm operands need unit inner stride")
+    M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    N, Kb = (b.shape[0], b.shape[1]) if trans_b else (b.shape[1], b.shape[0])
+    if K != Kb:
+        raise ValueError(f"gemm inner dims differ: {K} vs {Kb}")
+    odt = torch.bfloat16 if out_mode == OUT_BF16 else torch.float32
+    if out is None:
+        out = (torch.zeros if out_mode == OUT_F32_ATOMIC else torch.empty)(
+            (M, N), dtype=odt, device=a.device)
+    if out.dtype != odt or tuple(out.shape) != (M, N) or out.stride(-1) != 1:
+        raise ValueError("bad gemm output tensor")
+    for name in ("gate", "residual"):
+        t = epi.get(name)
+        if t is not None and (tuple(t.shape) != (M, N) or t.dtype != torch.bfloat16 or t.stride(-1) != 1):
+            raise ValueError(f"gemm {name} must be bf16 (M, N) with unit inner stride")
+    bias = epi.get("bias")
+    if bias is not None and (bias.numel() != N or bias.dtype != torch.float32):
+        raise ValueError("gemm bias must be fp32 [N]")
+    e = _epi(**epi)
+    _C.call("mmt_gemm", M, N, K, ptr(a), int(trans_a), a.stride(0), ptr(b), int(trans_b),
+            b.stride(0), ptr(out), out_mode, out.stride(0), 1, 0, 0, 0, split_k,
+            _C.ctypes.byref(e), _C.stream_ptr())
+    return out

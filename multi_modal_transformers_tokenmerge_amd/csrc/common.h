@@ -80,6 +80,12 @@ __host__ __device__ __forceinline__ bool keep_draw(uint32_t key, uint32_t ctr, u
   return draw_u32(key, ctr) < thresh;
 }
 
+// thresh = min(2^32 - 1, floor(keep_prob * 2^32)), computed in double on the host
+inline uint32_t keep_threshold(float keep_prob) {
+  double t = (double)keep_prob * 4294967296.0;
+  return t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+}
+
 // ---------------------------------------------------------------- wave helpers (wave64)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -314,6 +314,7 @@ __global__ __launch_bounds__(256) void tome_merge_fwd_kernel(
       continue;
     }
     const int q = o - set_start;
+    const T* xs = xb + (int64_t)set_start * xs_t;  // the merged token set
     int tok, j;
     merged_row_source(q, ta, r, dis, s_unm, &tok, &j);
     const float sp = (sb && !plain) ? sb[tok] : 1.f;
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(256) void tome_merge_fwd_kernel(
         if (s_dst[i] == j) S = S + (sb ? sb[2 * s_src[i]] : 1.f);
     for (int ch = lane; ch < nchunk; ch += 64) {
       float acc[V], v[V];
-      Vec<T>::load(xb + (int64_t)tok * xs_t + ch * V, v);
+      Vec<T>::load(xs + (int64_t)tok * xs_t + ch * V, v);
 #pragma unroll
       for (int e = 0; e < V; ++e) acc[e] = v[e] * sp;
       if (j >= 0 && scatter) {
@@ -332,7 +333,7 @@ __global__ __launch_bounds__(256) void tome_merge_fwd_kernel(
           if (s_dst[i] != j) continue;
           const int st = 2 * s_src[i];
           const float ss = (sb && !plain) ? sb[st] : 1.f;
-          Vec<T>::load(xb + (int64_t)st * xs_t + ch * V, v);
+          Vec<T>::load(xs + (int64_t)st * xs_t + ch * V, v);
 #pragma unroll
           for (int e = 0; e < V; ++e) acc[e] = acc[e] + v[e] * ss;
         }

@@ -1,0 +1,96 @@
+"""GPU numerics: MFMA bf16 GEMM (all operand layouts, tails, epilogues) vs a torch fp32 reference
+of the same bf16 inputs. Tolerance: fp32 accumulation order only (products of bf16 are exact in
+fp32) -> rel 1e-5 before the bf16 output rounding; bf16 outputs compared to 1 bf16 ulp."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import rng as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _mk(shape, dev, g):
+    return torch.randn(shape, generator=g).to(torch.bfloat16).to(dev)
+
+
+def _ref(a, b, ta, tb):
+    A = a.float().t() if ta else a.float()
+    B = b.float().t() if tb else b.float()
+    return A @ B
+
+
+def _close_bf16(out, ref):
+    ref_b = ref.to(torch.bfloat16).float()
+    err = (out.float() - ref).abs()
+    tol = (ref.abs() * 2 ** -7) + 1e-3 * ref.abs().max()
+    assert bool((err <= tol).all()), f"max err {err.max().item()}"
+    # most elements round identically
+    assert (out.float() == ref_b).float().mean().item() > 0.97
+
+
+SHAPES = [(128, 128, 64), (256, 384, 384), (300, 200, 136), (18688 // 8, 1152, 384), (64, 8, 776),
+          (33, 1536, 72), (1, 8, 8)]
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+def test_gemm_layouts(dev, M, N, K, ta, tb):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K + ta * 2 + tb)
+    if (ta and M % 8) or (not tb and N % 8) or (not ta and K % 8) or (tb and K % 8):
+        pytest.skip("contiguous dim must be a multiple of 8")
+    a = _mk((K, M) if ta else (M, K), dev, g)
+    b = _mk((N, K) if tb else (K, N), dev, g)
+    out = Kn.gemm(a, b, ta, tb)
+    ref = _ref(a, b, ta, tb)
+    _close_bf16(out, ref)
+    out32 = Kn.gemm(a, b, ta, tb, out_mode=Kn.OUT_F32)
+    torch.testing.assert_close(out32, ref, rtol=1e-5, atol=1e-5 * ref.abs().max().item())
+
+
+def test_gemm_epilogue_bias_relu_dropout_residual(dev):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    g = torch.Generator().manual_seed(1)
+    M, N, K = 300, 256, 192
+    a, w = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    bias = torch.randn(N, generator=g).to(dev)
+    res = _mk((M, N), dev, g)
+    rng = torch.tensor([1234, 7], dtype=torch.int32, device=dev)
+    out = Kn.gemm(a, w, False, True, bias=bias, act=Kn.ACT_RELU, rng=rng, drop_layer=3,
+                  drop_site=2, keep_prob=0.9, drop_row_offset=5 * M, residual=res)
+    keep = torch.from_numpy(R.dropout_mask_2d(1234, 7, 3, 2, M, N, 5 * M, 0.9)).to(dev)
+    ref = torch.relu(a.float() @ w.float().t() + bias)
+    ref = torch.where(keep, ref / 0.9, torch.zeros_like(ref)) + res.float()
+    _close_bf16(out, ref)
+    frac = keep.float().mean().item()
+    assert 0.88 < frac < 0.92
+
+
+def test_gemm_gate_and_beta_and_atomic_splitk(dev):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    g = torch.Generator().manual_seed(2)
+    M, N, K = 200, 128, 512
+    a, b = _mk((M, K), dev, g), _mk((K, N), dev, g)
+    gate = _mk((M, N), dev, g)
+    out = Kn.gemm(a, b, False, False, gate=gate, gate_scale=1 / 0.9)
+    ref = (a.float() @ b.float()) * (gate.float() > 0).float() / 0.9
+    _close_bf16(out, ref)
+    c = torch.randn(M, N, generator=g).to(dev)
+    c0 = c.clone()
+    Kn.gemm(a, b, out=c, out_mode=Kn.OUT_F32, beta=1.0)
+    torch.testing.assert_close(c, c0 + a.float() @ b.float(), rtol=1e-5, atol=1e-3)
+    # dW-style: A^T . B with split-K atomics over a long reduction
+    x, dy = _mk((4096, 96), dev, g), _mk((4096, 160), dev, g)
+    dw = torch.zeros(160, 96, device=dev)
+    Kn.gemm(dy, x, trans_a=True, out=dw, out_mode=Kn.OUT_F32_ATOMIC, split_k=8)
+    ref = dy.float().t() @ x.float()
+    torch.testing.assert_close(dw, ref, rtol=1e-4, atol=1e-3)
+
+
+def test_gemm_rejects_bad_shapes(dev):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn, _C
+    a = torch.zeros((16, 12), dtype=torch.bfloat16, device=dev)
+    b = torch.zeros((12, 16), dtype=torch.bfloat16, device=dev)
+    with pytest.raises(_C.MMTError):
+        Kn.gemm(a, b)  # K = 12 not a multiple of 8
