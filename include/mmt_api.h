@@ -126,6 +126,61 @@ int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t lda, const 
              int transB, int64_t ldb, void* C, int c_mode, int64_t ldc, int batch, int64_t sA,
              int64_t sB, int64_t sC, int split_k, const mmt_epilogue_t* epi, mmt_stream_t stream);
 
+/* ------------------------------------------------------------------ attention
+ * Blockwise-causal MHA replacing flax.linen.SelfAttention / dot_product_attention as the
+ * reference configures it (vanilla_decoder.yaml:19-31, mask token_sequencer.py:313-321,
+ * octo.py:66-68,119): softmax(where(mask, q.k * scale, finfo.min)) with attention dropout
+ * sharing ONE (L, L) keep-mask across batch and heads (Flax broadcast_dropout) times v.
+ * qkv: bf16 rows (b, t) at qkv + b*s_b + t*s_t holding [q(H,Dh) | k(H,Dh) | v(H,Dh)].
+ * Mask = token-set table: n_sets (<= 16) contiguous sets tiling [0, L) (set_start/set_len HOST
+ * arrays) and set_vis[s] = bitmask of key sets that query set s attends to; n_sets = 0: no mask.
+ * drop_bits: (L, ceil(L/32)) uint32 keep bitmask from mmt_dropout_bits, or NULL (no dropout);
+ * kept probabilities are scaled by 1/keep_prob. bias: optional fp32 (H, L, L) added to the
+ * scaled logits (T5 relative position bias; forward only). o: bf16 (b, t) rows of (H, Dh);
+ * lse: fp32 (B, H, L) natural-log softmax normaliser. Dh in {64, 128}.
+ */
+int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, int L, int H, int Dh,
+                 float scale, int n_sets, const int32_t* set_start, const int32_t* set_len,
+                 const uint32_t* set_vis, const uint32_t* drop_bits, float keep_prob,
+                 const float* bias, void* o, int64_t o_s_b, int64_t o_s_t, float* lse,
+                 mmt_stream_t stream);
+/* Backward: writes dq, dk, dv into dqkv (same row layout as qkv). delta: fp32 (B, H, L)
+ * workspace (rowsum(dO * O)). */
+int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, int L, int H, int Dh,
+                 float scale, int n_sets, const int32_t* set_start, const int32_t* set_len,
+                 const uint32_t* set_vis, const uint32_t* drop_bits, float keep_prob,
+                 const void* o, int64_t o_s_b, int64_t o_s_t, const void* dout, int64_t d_s_b,
+                 int64_t d_s_t, const float* lse, float* delta, void* dqkv, int64_t dq_s_b,
+                 int64_t dq_s_t, mmt_stream_t stream);
+/* Keep bitmask (rows, ceil(cols/32)) of a dropout stream: bit c of word (r, c/32) set iff
+ * draw(key(rng, layer, site), r*cols + c) < keep_prob * 2^32. */
+int mmt_dropout_bits(const uint32_t* rng, uint32_t layer, uint32_t site, int rows, int cols,
+                     float keep_prob, uint32_t* out, mmt_stream_t stream);
+
+/* ------------------------------------------------------------------ sequence LayerNorm
+ * flax.linen.LayerNorm(reduction_axes=[1], feature_axes=[-1], epsilon) as used in
+ * attention.py:58,66 (vanilla_decoder.yaml:5-13): stats per (b, d) over the SEQUENCE axis L,
+ * fast variance; x, y bf16 (B, L, D) strided; mean/rstd fp32 (B, D) saved for the backward. */
+int mmt_seqnorm_fwd(const void* x, int64_t xs_b, int64_t xs_t, int B, int L, int D,
+                    const float* gamma, const float* beta, float eps, void* y, int64_t ys_b,
+                    int64_t ys_t, float* mean, float* rstd, mmt_stream_t stream);
+/* dx = LN backward (+ addend, which may alias dx); dgamma/dbeta fp32 [D] are ACCUMULATED. */
+int mmt_seqnorm_bwd(const void* dy, int64_t ds_b, int64_t ds_t, const void* x, int64_t xs_b,
+                    int64_t xs_t, int B, int L, int D, const float* mean, const float* rstd,
+                    const float* gamma, const void* addend, int64_t as_b, int64_t as_t, void* dx,
+                    int64_t dxs_b, int64_t dxs_t, float* dgamma, float* dbeta,
+                    mmt_stream_t stream);
+
+/* ------------------------------------------------------------------ reductions / dropout
+ * out[n] += sum_m x[m][n] (bf16 x, fp32 out): Dense bias gradients. */
+int mmt_colsum(const void* x, int64_t ldx, int M, int N, float* out, mmt_stream_t stream);
+/* Backward of a GEMM-epilogue dropout (flax.linen.Dropout, attention.py:34-37,60):
+ * dz = dy * keep / keep_prob with the same stream/counters as the forward; colsum (optional)
+ * += column sums of dz (the bias gradient of the Dense before the dropout). */
+int mmt_dropout_bwd(const void* dy, int64_t ldy, int M, int N, const uint32_t* rng,
+                    uint32_t layer, uint32_t site, float keep_prob, int64_t row_offset, void* dz,
+                    int64_t ldz, float* colsum, mmt_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

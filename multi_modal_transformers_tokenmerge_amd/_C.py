@@ -30,6 +30,13 @@ SIGNATURES: dict[str, list] = {
     "mmt_tome_merge_wavg_fwd": [P, I, I, I, I, L, L, I, I, I, I, P, P, P, P, P, L, L, P, P, P],
     "mmt_tome_merge_wavg_bwd": [P, I, I, I, I, L, L, I, I, I, P, P, P, P, L, L, P],
     "mmt_gemm": [I, I, I, P, I, L, P, I, L, P, I, L, I, L, L, L, I, P, P],
+    "mmt_attn_fwd": [P, L, L, I, I, I, I, F, I, P, P, P, P, F, P, P, L, L, P, P],
+    "mmt_attn_bwd": [P, L, L, I, I, I, I, F, I, P, P, P, P, F, P, L, L, P, L, L, P, P, P, L, L, P],
+    "mmt_dropout_bits": [P, U32, U32, I, I, F, P, P],
+    "mmt_seqnorm_fwd": [P, L, L, I, I, I, P, P, F, P, L, L, P, P, P],
+    "mmt_seqnorm_bwd": [P, L, L, P, L, L, I, I, I, P, P, P, P, L, L, P, L, L, P, P, P],
+    "mmt_colsum": [P, L, I, I, P, P],
+    "mmt_dropout_bwd": [P, L, I, I, P, U32, U32, F, L, P, L, P, P],
 }
 _VOID = {"mmt_tome_set_match_path"}
 

@@ -157,3 +157,121 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
             b.stride(0), ptr(out), out_mode, out.stride(0), 1, 0, 0, 0, split_k,
             _C.ctypes.byref(e), _C.stream_ptr())
     return out
+
+
+# ------------------------------------------------------------------------------- attention
+class SetTable:
+    """Host-side token-set table of one layer: contiguous sets tiling [0, L) and, per query set,
+    the bitmask of key sets it attends to (the blockwise mask of token_sequencer.py:94-183)."""
+
+    def __init__(self, starts, lens, vis):
+        n = len(starts)
+        if n > 16:
+            raise ValueError("at most 16 token sets")
+        self.n = n
+        self.starts = (_C.ctypes.c_int32 * max(n, 1))(*starts)
+        self.lens = (_C.ctypes.c_int32 * max(n, 1))(*lens)
+        self.vis = (_C.ctypes.c_uint32 * max(n, 1))(*vis)
+        self.L = int(sum(lens))
+
+    @staticmethod
+    def none(L):
+        return SetTable([0], [L], [1])
+
+
+def dropout_bits(rng: torch.Tensor, layer: int, site: int, rows: int, cols: int, keep_prob: float,
+                 out: torch.Tensor | None = None):
+    words = (cols + 31) // 32
+    if out is None:
+        out = torch.empty((rows, words), dtype=torch.int32, device=rng.device)
+    _C.call("mmt_dropout_bits", ptr(rng), layer, site, rows, cols, keep_prob, ptr(out), _C.stream_ptr())
+    return out
+
+
+def _qkv_geo(qkv: torch.Tensor, H: int):
+    if qkv.dim() != 3 or qkv.stride(2) != 1 or qkv.dtype != torch.bfloat16:
+        raise ValueError("qkv must be bf16 (B, L, 3*H*Dh) with unit inner stride")
+    B, L, three_d = qkv.shape
+    if three_d % (3 * H):
+        raise ValueError("qkv last dim must be 3*H*Dh")
+    return B, L, three_d // (3 * H)
+
+
+def attn_fwd(qkv: torch.Tensor, H: int, scale: float, table: SetTable | None = None,
+             drop_bits: torch.Tensor | None = None, keep_prob: float = 1.0,
+             bias: torch.Tensor | None = None, out: torch.Tensor | None = None):
+    _dev(qkv, drop_bits, bias, out)
+    B, L, Dh = _qkv_geo(qkv, H)
+    t = table or SetTable.none(L)
+    if t.L != L:
+        raise ValueError(f"set table covers {t.L} tokens, sequence has {L}")
+    if bias is not None and (tuple(bias.shape) != (H, L, L) or bias.dtype != torch.float32 or not bias.is_contiguous()):
+        raise ValueError("bias must be contiguous fp32 (H, L, L)")
+    if out is None:
+        out = torch.empty((B, L, H * Dh), dtype=torch.bfloat16, device=qkv.device)
+    lse = torch.empty((B, H, L), dtype=torch.float32, device=qkv.device)
+    _C.call("mmt_attn_fwd", ptr(qkv), qkv.stride(0), qkv.stride(1), B, L, H, Dh, scale, t.n,
+            t.starts, t.lens, t.vis, ptr(drop_bits), keep_prob, ptr(bias), ptr(out), out.stride(0),
+            out.stride(1), ptr(lse), _C.stream_ptr())
+    return out, lse
+
+
+def attn_bwd(qkv, o, dout, lse, H: int, scale: float, table: SetTable | None = None,
+             drop_bits=None, keep_prob: float = 1.0, dqkv: torch.Tensor | None = None):
+    _dev(qkv, o, dout, lse, drop_bits, dqkv)
+    B, L, Dh = _qkv_geo(qkv, H)
+    t = table or SetTable.none(L)
+    if dout.stride(-1) != 1 or o.stride(-1) != 1:
+        raise ValueError("o/dout need unit inner stride")
+    if dqkv is None:
+        dqkv = torch.empty_like(qkv)
+    delta = torch.empty((B, H, L), dtype=torch.float32, device=qkv.device)
+    _C.call("mmt_attn_bwd", ptr(qkv), qkv.stride(0), qkv.stride(1), B, L, H, Dh, scale, t.n,
+            t.starts, t.lens, t.vis, ptr(drop_bits), keep_prob, ptr(o), o.stride(0), o.stride(1),
+            ptr(dout), dout.stride(0), dout.stride(1), ptr(lse), ptr(delta), ptr(dqkv),
+            dqkv.stride(0), dqkv.stride(1), _C.stream_ptr())
+    return dqkv
+
+
+# ------------------------------------------------------------------------ seq LayerNorm etc.
+def seqnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float,
+                out: torch.Tensor | None = None):
+    _dev(x, gamma, beta, out)
+    B, L, D = x.shape
+    if out is None:
+        out = torch.empty((B, L, D), dtype=torch.bfloat16, device=x.device)
+    mean = torch.empty((B, D), dtype=torch.float32, device=x.device)
+    rstd = torch.empty((B, D), dtype=torch.float32, device=x.device)
+    _C.call("mmt_seqnorm_fwd", ptr(x), x.stride(0), x.stride(1), B, L, D, ptr(gamma), ptr(beta),
+            eps, ptr(out), out.stride(0), out.stride(1), ptr(mean), ptr(rstd), _C.stream_ptr())
+    return out, mean, rstd
+
+
+def seqnorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, addend=None, out=None):
+    _dev(dy, x, mean, rstd, gamma, dgamma, dbeta, addend, out)
+    B, L, D = x.shape
+    if out is None:
+        out = torch.empty((B, L, D), dtype=torch.bfloat16, device=x.device)
+    a_sb, a_st = (addend.stride(0), addend.stride(1)) if addend is not None else (0, 0)
+    _C.call("mmt_seqnorm_bwd", ptr(dy), dy.stride(0), dy.stride(1), ptr(x), x.stride(0),
+            x.stride(1), B, L, D, ptr(mean), ptr(rstd), ptr(gamma), ptr(addend), a_sb, a_st,
+            ptr(out), out.stride(0), out.stride(1), ptr(dgamma), ptr(dbeta), _C.stream_ptr())
+    return out
+
+
+def colsum(x2d: torch.Tensor, out: torch.Tensor):
+    _dev(x2d, out)
+    M, N = x2d.shape
+    _C.call("mmt_colsum", ptr(x2d), x2d.stride(0), M, N, ptr(out), _C.stream_ptr())
+    return out
+
+
+def dropout_bwd(dy2d: torch.Tensor, rng, layer: int, site: int, keep_prob: float,
+                row_offset: int = 0, out: torch.Tensor | None = None, colsum_out=None):
+    _dev(dy2d, rng, out, colsum_out)
+    M, N = dy2d.shape
+    if out is None:
+        out = torch.empty_like(dy2d)
+    _C.call("mmt_dropout_bwd", ptr(dy2d), dy2d.stride(0), M, N, ptr(rng), layer, site, keep_prob,
+            row_offset, ptr(out), out.stride(0), ptr(colsum_out), _C.stream_ptr())
+    return out

@@ -1,0 +1,147 @@
+"""GPU numerics: attention fwd/bwd, sequence LayerNorm fwd/bwd, dropout/colsum kernels vs plain
+PyTorch fp32 references of the same ops on the same bf16 inputs.
+Tolerances (bf16 outputs, fp32 math): attention O rel-L2 < 1e-2, grads rel-L2 < 2e-2;
+seqnorm y rel-L2 < 1e-2, dx rel-L2 < 2e-2, dgamma/dbeta rel 1e-3."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import rng as R
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+def dense_mask(starts, lens, vis, L, dev):
+    sid = torch.zeros(L, dtype=torch.long)
+    for i, (s, n) in enumerate(zip(starts, lens)):
+        sid[s:s + n] = i
+    v = torch.tensor(vis, dtype=torch.long)
+    m = ((v[sid][:, None] >> sid[None, :]) & 1).bool()
+    return m.to(dev)
+
+
+def octo_small_table(n_text=32, n_img=256, n_read=4):
+    # T sees T; I sees T, I; R sees T, I, R  (token_sequencer.py:94-183, one timestep)
+    return [0, n_text, n_text + n_img], [n_text, n_img, n_read], [0b001, 0b011, 0b111]
+
+
+def bits_to_keep(bits, L):
+    b = bits.cpu().numpy().view(np.uint32)
+    keep = ((b[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(b.shape[0], -1)[:, :L]
+    return torch.from_numpy(keep.astype(bool))
+
+
+def ref_attention(qkv, H, scale, mask, keep, keep_prob, bias=None):
+    B, L, three = qkv.shape
+    Dh = three // (3 * H)
+    q, k, v = qkv.float().view(B, L, 3, H, Dh).unbind(2)
+    s = torch.einsum("bqhd,bkhd->bhqk", q, k) * scale
+    if bias is not None:
+        s = s + bias[None]
+    if mask is not None:
+        s = torch.where(mask[None, None], s, torch.finfo(torch.float32).min)
+    p = torch.softmax(s, dim=-1)
+    if keep is not None:
+        p = torch.where(keep[None, None], p / keep_prob, torch.zeros_like(p))
+    return torch.einsum("bhqk,bkhd->bqhd", p, v).reshape(B, L, H * Dh)
+
+
+@pytest.mark.parametrize("B,L,H,Dh,masked,drop", [
+    (2, 292, 6, 64, True, True), (3, 292, 6, 64, True, False), (2, 130, 2, 64, False, False),
+    (1, 1064, 2, 64, True, True), (2, 33, 3, 128, False, True), (4, 276, 6, 64, True, True)])
+def test_attention_fwd_bwd(dev, B, L, H, Dh, masked, drop):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    g = torch.Generator().manual_seed(B * 100 + L + H)
+    qkv = torch.randn((B, L, 3 * H * Dh), generator=g).bfloat16().to(dev)
+    scale = Dh ** -0.5
+    if masked:
+        if L == 1064:  # base 2-cam, 2 steps: [T32] [I256; I256; R4]*2
+            starts = [0, 32, 288, 544, 548, 804, 1060]
+            lens = [32, 256, 256, 4, 256, 256, 4]
+            # T:{T}; I_t: T, I_t', (t'<=t), not R; R_t: T, I_t'<=t, R_t (own)
+            vis = [0b0000001, 0b0000111, 0b0000111, 0b0001111, 0b0110111, 0b0110111, 0b1110111]
+        else:
+            starts, lens, vis = octo_small_table(32, L - 36, 4)
+        table = K.SetTable(starts, lens, vis)
+        mask = dense_mask(starts, lens, vis, L, dev)
+    else:
+        table, mask = None, None
+    keep_prob = 0.9 if drop else 1.0
+    rng = torch.tensor([77, 5], dtype=torch.int32, device=dev)
+    bits = K.dropout_bits(rng, 3, 7, L, L, keep_prob) if drop else None
+    keep = bits_to_keep(bits, L).to(dev) if drop else None
+    if drop:  # the bitmask is the oracle's stream
+        ref_keep = R.dropout_mask_2d(77, 5, 3, 7, L, L, 0, 0.9)
+        assert (keep.cpu().numpy() == ref_keep).all()
+    o, lse = K.attn_fwd(qkv, H, scale, table, bits, keep_prob)
+    qf = qkv.float().requires_grad_()
+    ref = ref_attention(qf, H, scale, mask, keep, keep_prob)
+    assert rel(o, ref) < 1e-2
+    dout = torch.randn((B, L, H * Dh), generator=g).bfloat16().to(dev)
+    dqkv = K.attn_bwd(qkv, o, dout, lse, H, scale, table, bits, keep_prob)
+    ref.backward(dout.float())
+    gr = qf.grad.view(B, L, 3, H * Dh)
+    gk = dqkv.float().view(B, L, 3, H * Dh)
+    for i in range(3):
+        assert rel(gk[:, :, i], gr[:, :, i]) < 2e-2, ("qkv"[i], rel(gk[:, :, i], gr[:, :, i]))
+
+
+def test_attention_bias_mode(dev):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    g = torch.Generator().manual_seed(9)
+    B, L, H, Dh = 3, 32, 12, 64
+    qkv = torch.randn((B, L, 3 * H * Dh), generator=g).bfloat16().to(dev)
+    bias = torch.randn((H, L, L), generator=g).to(dev)
+    o, _ = K.attn_fwd(qkv, H, 1.0, None, None, 1.0, bias=bias)
+    ref = ref_attention(qkv, H, 1.0, None, None, 1.0, bias)
+    assert rel(o, ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,L,D", [(4, 292, 384), (2, 74, 768), (3, 20, 192), (2, 1, 64)])
+def test_seqnorm(dev, B, L, D):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    g = torch.Generator().manual_seed(B + L + D)
+    x = (torch.randn((B, L, D), generator=g) * 2 + 0.5).bfloat16().to(dev)
+    gamma = torch.randn(D, generator=g).to(dev)
+    beta = torch.randn(D, generator=g).to(dev)
+    y, mean, rstd = K.seqnorm_fwd(x, gamma, beta, 1e-6)
+    xf = x.float().requires_grad_()
+    mu = xf.mean(dim=1, keepdim=True)
+    var = torch.clamp((xf * xf).mean(dim=1, keepdim=True) - mu * mu, min=0)
+    ref = (xf - mu) * (torch.rsqrt(var + 1e-6) * gamma) + beta
+    assert rel(y, ref) < 1e-2
+    dy = torch.randn((B, L, D), generator=g).bfloat16().to(dev)
+    add = torch.randn((B, L, D), generator=g).bfloat16().to(dev)
+    dg = torch.zeros(D, device=dev)
+    db = torch.zeros(D, device=dev)
+    dx = K.seqnorm_bwd(dy, x, mean, rstd, gamma, dg, db, addend=add)
+    gam = gamma.clone().requires_grad_()
+    bet = beta.clone().requires_grad_()
+    ref = (xf - mu) * (torch.rsqrt(var + 1e-6) * gam) + bet
+    ref.backward(dy.float())
+    if L > 1:
+        assert rel(dx.float() - add.float(), xf.grad) < 2e-2
+    torch.testing.assert_close(dg, gam.grad, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(db, bet.grad, rtol=1e-3, atol=1e-3)
+
+
+def test_colsum_and_dropout_bwd(dev):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    g = torch.Generator().manual_seed(4)
+    M, N = 1000, 384
+    x = torch.randn((M, N), generator=g).bfloat16().to(dev)
+    out = torch.zeros(N, device=dev)
+    K.colsum(x, out)
+    torch.testing.assert_close(out, x.float().sum(0), rtol=1e-4, atol=1e-3)
+    rng = torch.tensor([5, 9], dtype=torch.int32, device=dev)
+    cs = torch.zeros(N, device=dev)
+    dz = K.dropout_bwd(x, rng, 2, 1, 0.9, row_offset=3 * M, colsum_out=cs)
+    keep = torch.from_numpy(R.dropout_mask_2d(5, 9, 2, 1, M, N, 3 * M, 0.9)).to(dev)
+    ref = torch.where(keep, x.float() / 0.9, torch.zeros_like(x.float()))
+    assert (dz.float() - ref).abs().max().item() <= 2 ** -7 * ref.abs().max().item()
+    torch.testing.assert_close(cs, ref.sum(0), rtol=1e-3, atol=1e-2)
