@@ -117,9 +117,10 @@ typedef struct {
   const void* gate;           /* bf16 [M][ld_gate] or NULL */
   int64_t ld_gate;
   float gate_scale;
-  const void* residual;       /* bf16 [M][ld_res] or NULL */
+  const void* residual;       /* [M][ld_res] bf16 or fp32 (res_dtype) or NULL */
   int64_t ld_res;
   float alpha, beta;
+  int res_dtype;              /* MMT_BF16 / MMT_F32 */
 } mmt_epilogue_t;
 
 int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t lda, const void* B,
@@ -160,26 +161,120 @@ int mmt_dropout_bits(const uint32_t* rng, uint32_t layer, uint32_t site, int row
 /* ------------------------------------------------------------------ sequence LayerNorm
  * flax.linen.LayerNorm(reduction_axes=[1], feature_axes=[-1], epsilon) as used in
  * attention.py:58,66 (vanilla_decoder.yaml:5-13): stats per (b, d) over the SEQUENCE axis L,
- * fast variance; x, y bf16 (B, L, D) strided; mean/rstd fp32 (B, D) saved for the backward. */
-int mmt_seqnorm_fwd(const void* x, int64_t xs_b, int64_t xs_t, int B, int L, int D,
+ * fast variance; x (B, L, D) strided, bf16 or fp32 (x_dtype; the training path keeps the residual
+ * stream in fp32 because this normalisation subtracts a large per-feature sequence mean); y bf16;
+ * mean/rstd fp32 (B, D) saved for the backward. */
+int mmt_seqnorm_fwd(const void* x, int x_dtype, int64_t xs_b, int64_t xs_t, int B, int L, int D,
                     const float* gamma, const float* beta, float eps, void* y, int64_t ys_b,
                     int64_t ys_t, float* mean, float* rstd, mmt_stream_t stream);
-/* dx = LN backward (+ addend, which may alias dx); dgamma/dbeta fp32 [D] are ACCUMULATED. */
-int mmt_seqnorm_bwd(const void* dy, int64_t ds_b, int64_t ds_t, const void* x, int64_t xs_b,
-                    int64_t xs_t, int B, int L, int D, const float* mean, const float* rstd,
+/* dx = LN backward (+ addend, which may alias dx); x, addend and dx have x_dtype, dy has
+ * dy_dtype; dgamma/dbeta fp32 [D] are ACCUMULATED. */
+int mmt_seqnorm_bwd(const void* dy, int dy_dtype, int64_t ds_b, int64_t ds_t, const void* x,
+                    int x_dtype, int64_t xs_b, int64_t xs_t, int B, int L, int D,
+                    const float* mean, const float* rstd,
                     const float* gamma, const void* addend, int64_t as_b, int64_t as_t, void* dx,
                     int64_t dxs_b, int64_t dxs_t, float* dgamma, float* dbeta,
                     mmt_stream_t stream);
 
 /* ------------------------------------------------------------------ reductions / dropout
  * out[n] += sum_m x[m][n] (bf16 x, fp32 out): Dense bias gradients. */
-int mmt_colsum(const void* x, int64_t ldx, int M, int N, float* out, mmt_stream_t stream);
+int mmt_colsum(const void* x, int dtype, int64_t ldx, int M, int N, float* out,
+               mmt_stream_t stream);
 /* Backward of a GEMM-epilogue dropout (flax.linen.Dropout, attention.py:34-37,60):
- * dz = dy * keep / keep_prob with the same stream/counters as the forward; colsum (optional)
- * += column sums of dz (the bias gradient of the Dense before the dropout). */
-int mmt_dropout_bwd(const void* dy, int64_t ldy, int M, int N, const uint32_t* rng,
+ * dz = dy * keep / keep_prob (bf16) with the same stream/counters as the forward (rng NULL:
+ * keep everything — a cast); colsum (optional) += column sums of dz (the bias gradient of the
+ * Dense before the dropout). dy: bf16 or fp32 (dtype). */
+int mmt_dropout_bwd(const void* dy, int dtype, int64_t ldy, int M, int N, const uint32_t* rng,
                     uint32_t layer, uint32_t site, float keep_prob, int64_t row_offset, void* dz,
                     int64_t ldz, float* colsum, mmt_stream_t stream);
+
+/* ------------------------------------------------------------------ image tokenizer stem
+ * tokenizers/images/image_tokenizer.py: image_to_patches (:35-71, raster "(h p1)(w p2) -> (h w)",
+ * normalise 2*(x/255)-1) fused with the im2col of the input Conv (KHxKW stride S VALID, Flax HWIO
+ * kernel order (ky, kx, c)), :158. img: (B, I, H, H, C) fp32 (in_dtype 0) or uint8 (in_dtype 2);
+ * out: bf16 [B*I*NP*OH*OW][KH*KW*C]. H % P != 0 is rejected (the reference's resize branch,
+ * :54-59, is broken). */
+int mmt_patch_im2col(const void* img, int in_dtype, int B, int I, int Himg, int C, int P, int KH,
+                     int KW, int S, int normalize, void* out, mmt_stream_t stream);
+/* max_pool over the `win` conv outputs of each patch (3x3 s1 VALID on the 3x3 map, :159) with
+ * first-max argmax for the backward (bf16 conv [npatch][win][C] -> pooled [npatch][C]). */
+int mmt_maxpool_patch(const void* conv, int64_t npatch, int win, int C, void* pooled,
+                      uint8_t* argmax, mmt_stream_t stream);
+int mmt_maxpool_patch_bwd(const void* dpooled, const uint8_t* argmax, int64_t npatch, int win,
+                          int C, void* G, mmt_stream_t stream);
+/* flax GroupNorm(num_groups=G, eps) over every non-batch axis + gelu(tanh approx)
+ * (gato_resnet.yaml:77-86, image_tokenizer.py:165-167): x (B, R, C) bf16. */
+int mmt_groupnorm_gelu_fwd(const void* x, int B, int R, int C, int G, float eps,
+                           const float* gamma, const float* beta, void* y, float* mean,
+                           float* rstd, mmt_stream_t stream);
+/* backward; dx += result when accumulate != 0; dgamma/dbeta accumulated. */
+int mmt_groupnorm_gelu_bwd(const void* dy, const void* x, int B, int R, int C, int G,
+                           const float* gamma, const float* beta, const float* mean,
+                           const float* rstd, void* dx, int accumulate, float* dgamma,
+                           float* dbeta, mmt_stream_t stream);
+/* encode_patch_position (:74-132) for every (b, image, patch): Q quantisation levels, row token
+ * from interval p % PPD, col from p // PPD; train: randint[start, stop) on the counter stream keyed
+ * by the global sample index (sample_offset + b); eval: (start + stop) // 2. */
+int mmt_patch_positions(const uint32_t* rng, uint32_t site, int B, int I, int Himg, int P, int Q,
+                        int train, int64_t sample_offset, int32_t* row_tok, int32_t* col_tok,
+                        mmt_stream_t stream);
+
+/* ------------------------------------------------------------------ sequence assembly
+ * x0[b, l] = source(l) + pe[l] with source = text[b, j] | img[b, j] + row_emb[rtok] + col_emb[ctok]
+ * | readout_pe[j]  (row_src[l] = kind << 24 | j, kind 0 text / 1 image / 2 readout):
+ * TokenSequence.assemble_embeddings (token_sequencer.py:255-269), readout AddPositionEmbedding
+ * on zeros (readout.py:18-33, octo.py:103-108), ImageTokenizer embeddings (:300-307) and the
+ * encoder's learned position embedding (attention.py:71-85,97-100), fused. fp32 tables. */
+int mmt_seq_assemble_fwd(int B, int L, int D, const int32_t* row_src, const void* text, int T,
+                         const void* img, int NI, const int32_t* rtok, const int32_t* ctok,
+                         const float* row_emb, const float* col_emb, const float* readout_pe,
+                         const float* pe, void* x0, mmt_stream_t stream);
+/* backward: gathers d(text), d(img) (bf16), accumulates d(row_emb), d(col_emb), d(readout_pe)
+ * (fp32 atomics). d(pe) is mmt_colsum over the batch. */
+int mmt_seq_assemble_bwd(int B, int L, int D, const int32_t* row_src, const void* dx0,
+                         void* dtext, int T, void* dimg, int NI, const int32_t* rtok,
+                         const int32_t* ctok, float* drow_emb, float* dcol_emb,
+                         float* dreadout_pe, mmt_stream_t stream);
+/* readout gather + mean (octo.py:122-124, diffusion.py:102): out[b] = mean_i x[b, rows[i]]. */
+int mmt_rows_mean_fwd(const void* x, int64_t xs_b, int64_t xs_t, int B, int D,
+                      const int32_t* rows, int nrows, void* out, int64_t ld_out,
+                      mmt_stream_t stream);
+int mmt_rows_mean_bwd(const void* de, int64_t ld_de, int B, int L, int D, const int32_t* row_flag,
+                      int nrows, void* dx, mmt_stream_t stream);
+
+/* ------------------------------------------------------------------ diffusion head
+ * DiffusionActionHead.denoise_loss (diffusion.py:110-143) pieces: t ~ U{0..steps-1}, eps ~ N(0,1)
+ * (or injected), noisy = sqrt(abar_t) a + sqrt(1-abar_t) eps written to cat[:, :A] (bf16),
+ * FourierFeatures (:41-51) [cos 2 pi t W, sin 2 pi t W] (bf16 (B, 2F)). */
+int mmt_diffusion_prep(const uint32_t* rng, int B, int A, int steps, int64_t sample_offset,
+                       const float* actions, const float* alpha_hats, const float* fourier_w,
+                       int F, const int32_t* t_in, const float* eps_in, int32_t* t_out,
+                       float* eps_out, void* cat, int64_t ld_cat, void* feats,
+                       mmt_stream_t stream);
+int mmt_fourier_bwd(const void* dfeats, int B, int F, const int32_t* t, const float* fourier_w,
+                    float* dw, mmt_stream_t stream);
+/* optax.l2_loss summed over actions, mean over batch; dpred = (pred-eps)*grad_scale/B (bf16). */
+int mmt_diffusion_loss(const float* pred, int64_t ld_pred, const float* eps, int B, int A,
+                       float grad_scale, float* loss, void* dpred, mmt_stream_t stream);
+
+/* ------------------------------------------------------------------ T5 encoder pieces
+ * (tokenizers/text/t5_base.py:8-15, frozen FlaxT5 encoder): T5LayerNorm and the shared
+ * embedding lookup. */
+int mmt_rmsnorm_fwd(const void* x, int64_t rows, int D, const void* w, float eps, void* y,
+                    mmt_stream_t stream);
+int mmt_embedding_gather(const int32_t* ids, int64_t n, int D, const void* table, int vocab,
+                         void* out, mmt_stream_t stream);
+
+/* ------------------------------------------------------------------ optimizer / state
+ * Fused AdamW over the flat fp32 parameter buffer (the reference takes an optax tx from the
+ * caller, octo.py:228,341; this is optax.adamw semantics), writing the bf16 shadow copy.
+ * state = device {seed, step}: step+1 is the bias-correction count; mmt_step_advance
+ * increments it (keys every random stream of the next step). */
+int mmt_adamw(float* p, const float* g, float* m, float* v, void* shadow_bf16, int64_t n,
+              const int32_t* state, float lr, float b1, float b2, float eps, float wd,
+              float grad_scale, mmt_stream_t stream);
+int mmt_cast_f32_bf16(const float* a, void* b, int64_t n, mmt_stream_t stream);
+int mmt_step_advance(int32_t* state, mmt_stream_t stream);
 
 #ifdef __cplusplus
 }

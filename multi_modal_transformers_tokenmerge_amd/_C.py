@@ -19,7 +19,8 @@ class Epilogue(ctypes.Structure):
     """mmt_epilogue_t (include/mmt_api.h)."""
     _fields_ = [("bias", P), ("act", I), ("rng", P), ("drop_layer", U32), ("drop_site", U32),
                 ("keep_prob", F), ("drop_row_offset", L), ("gate", P), ("ld_gate", L),
-                ("gate_scale", F), ("residual", P), ("ld_res", L), ("alpha", F), ("beta", F)]
+                ("gate_scale", F), ("residual", P), ("ld_res", L), ("alpha", F), ("beta", F),
+                ("res_dtype", I)]
 
 
 # name -> argtypes (every entry point returns int status unless listed in _VOID)
@@ -33,10 +34,28 @@ SIGNATURES: dict[str, list] = {
     "mmt_attn_fwd": [P, L, L, I, I, I, I, F, I, P, P, P, P, F, P, P, L, L, P, P],
     "mmt_attn_bwd": [P, L, L, I, I, I, I, F, I, P, P, P, P, F, P, L, L, P, L, L, P, P, P, L, L, P],
     "mmt_dropout_bits": [P, U32, U32, I, I, F, P, P],
-    "mmt_seqnorm_fwd": [P, L, L, I, I, I, P, P, F, P, L, L, P, P, P],
-    "mmt_seqnorm_bwd": [P, L, L, P, L, L, I, I, I, P, P, P, P, L, L, P, L, L, P, P, P],
-    "mmt_colsum": [P, L, I, I, P, P],
-    "mmt_dropout_bwd": [P, L, I, I, P, U32, U32, F, L, P, L, P, P],
+    "mmt_seqnorm_fwd": [P, I, L, L, I, I, I, P, P, F, P, L, L, P, P, P],
+    "mmt_seqnorm_bwd": [P, I, L, L, P, I, L, L, I, I, I, P, P, P, P, L, L, P, L, L, P, P, P],
+    "mmt_colsum": [P, I, L, I, I, P, P],
+    "mmt_dropout_bwd": [P, I, L, I, I, P, U32, U32, F, L, P, L, P, P],
+    "mmt_patch_im2col": [P, I, I, I, I, I, I, I, I, I, I, P, P],
+    "mmt_maxpool_patch": [P, L, I, I, P, P, P],
+    "mmt_maxpool_patch_bwd": [P, P, L, I, I, P, P],
+    "mmt_groupnorm_gelu_fwd": [P, I, I, I, I, F, P, P, P, P, P, P],
+    "mmt_groupnorm_gelu_bwd": [P, P, I, I, I, I, P, P, P, P, P, I, P, P, P],
+    "mmt_patch_positions": [P, U32, I, I, I, I, I, I, L, P, P, P],
+    "mmt_seq_assemble_fwd": [I, I, I, P, P, I, P, I, P, P, P, P, P, P, P, P],
+    "mmt_seq_assemble_bwd": [I, I, I, P, P, P, I, P, I, P, P, P, P, P, P],
+    "mmt_rows_mean_fwd": [P, L, L, I, I, P, I, P, L, P],
+    "mmt_rows_mean_bwd": [P, L, I, I, I, P, I, P, P],
+    "mmt_diffusion_prep": [P, I, I, I, L, P, P, P, I, P, P, P, P, P, L, P, P],
+    "mmt_fourier_bwd": [P, I, I, P, P, P, P],
+    "mmt_diffusion_loss": [P, L, P, I, I, F, P, P, P],
+    "mmt_rmsnorm_fwd": [P, L, I, P, F, P, P],
+    "mmt_embedding_gather": [P, L, I, P, I, P, P],
+    "mmt_adamw": [P, P, P, P, P, L, P, F, F, F, F, F, F, P],
+    "mmt_cast_f32_bf16": [P, P, L, P],
+    "mmt_step_advance": [P, P],
 }
 _VOID = {"mmt_tome_set_match_path"}
 

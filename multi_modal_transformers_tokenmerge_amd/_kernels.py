@@ -122,6 +122,7 @@ def _epi(bias=None, act=ACT_NONE, rng=None, drop_layer=0, drop_site=0, keep_prob
     e.gate_scale = gate_scale
     e.residual = ptr(residual)
     e.ld_res = residual.stride(0) if residual is not None else 0
+    e.res_dtype = _dtype_code(residual) if residual is not None else 1
     e.alpha, e.beta = alpha, beta
     return e
 
@@ -145,10 +146,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
             (M, N), dtype=odt, device=a.device)
     if out.dtype != odt or tuple(out.shape) != (M, N) or out.stride(-1) != 1:
         raise ValueError("bad gemm output tensor")
-    for name in ("gate", "residual"):
+    for name, dts in (("gate", (torch.bfloat16,)), ("residual", (torch.bfloat16, torch.float32))):
         t = epi.get(name)
-        if t is not None and (tuple(t.shape) != (M, N) or t.dtype != torch.bfloat16 or t.stride(-1) != 1):
-            raise ValueError(f"gemm {name} must be bf16 (M, N) with unit inner stride")
+        if t is not None and (tuple(t.shape) != (M, N) or t.dtype not in dts or t.stride(-1) != 1):
+            raise ValueError(f"gemm {name} must be {dts} (M, N) with unit inner stride")
     bias = epi.get("bias")
     if bias is not None and (bias.numel() != N or bias.dtype != torch.float32):
         raise ValueError("gemm bias must be fp32 [N]")
@@ -236,42 +237,159 @@ def attn_bwd(qkv, o, dout, lse, H: int, scale: float, table: SetTable | None = N
 # ------------------------------------------------------------------------ seq LayerNorm etc.
 def seqnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float,
                 out: torch.Tensor | None = None):
+    """x (B, L, D) bf16 or fp32 (the residual stream) -> y bf16, mean, rstd (B, D) fp32."""
     _dev(x, gamma, beta, out)
     B, L, D = x.shape
     if out is None:
         out = torch.empty((B, L, D), dtype=torch.bfloat16, device=x.device)
     mean = torch.empty((B, D), dtype=torch.float32, device=x.device)
     rstd = torch.empty((B, D), dtype=torch.float32, device=x.device)
-    _C.call("mmt_seqnorm_fwd", ptr(x), x.stride(0), x.stride(1), B, L, D, ptr(gamma), ptr(beta),
-            eps, ptr(out), out.stride(0), out.stride(1), ptr(mean), ptr(rstd), _C.stream_ptr())
+    _C.call("mmt_seqnorm_fwd", ptr(x), _dtype_code(x), x.stride(0), x.stride(1), B, L, D,
+            ptr(gamma), ptr(beta), eps, ptr(out), out.stride(0), out.stride(1), ptr(mean),
+            ptr(rstd), _C.stream_ptr())
     return out, mean, rstd
 
 
 def seqnorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, addend=None, out=None):
+    """dx (dtype of x) = LN backward (+ addend, dtype of x); dy bf16 or fp32."""
     _dev(dy, x, mean, rstd, gamma, dgamma, dbeta, addend, out)
     B, L, D = x.shape
+    if addend is not None and addend.dtype != x.dtype:
+        raise TypeError("addend must have the residual (x) dtype")
     if out is None:
-        out = torch.empty((B, L, D), dtype=torch.bfloat16, device=x.device)
+        out = torch.empty((B, L, D), dtype=x.dtype, device=x.device)
     a_sb, a_st = (addend.stride(0), addend.stride(1)) if addend is not None else (0, 0)
-    _C.call("mmt_seqnorm_bwd", ptr(dy), dy.stride(0), dy.stride(1), ptr(x), x.stride(0),
-            x.stride(1), B, L, D, ptr(mean), ptr(rstd), ptr(gamma), ptr(addend), a_sb, a_st,
-            ptr(out), out.stride(0), out.stride(1), ptr(dgamma), ptr(dbeta), _C.stream_ptr())
+    _C.call("mmt_seqnorm_bwd", ptr(dy), _dtype_code(dy), dy.stride(0), dy.stride(1), ptr(x),
+            _dtype_code(x), x.stride(0), x.stride(1), B, L, D, ptr(mean), ptr(rstd), ptr(gamma),
+            ptr(addend), a_sb, a_st, ptr(out), out.stride(0), out.stride(1), ptr(dgamma),
+            ptr(dbeta), _C.stream_ptr())
     return out
 
 
 def colsum(x2d: torch.Tensor, out: torch.Tensor):
     _dev(x2d, out)
     M, N = x2d.shape
-    _C.call("mmt_colsum", ptr(x2d), x2d.stride(0), M, N, ptr(out), _C.stream_ptr())
+    _C.call("mmt_colsum", ptr(x2d), _dtype_code(x2d), x2d.stride(0), M, N, ptr(out), _C.stream_ptr())
     return out
 
 
 def dropout_bwd(dy2d: torch.Tensor, rng, layer: int, site: int, keep_prob: float,
                 row_offset: int = 0, out: torch.Tensor | None = None, colsum_out=None):
+    """dz (bf16) = dy * keep / keep_prob; rng None: plain cast. colsum_out += column sums."""
     _dev(dy2d, rng, out, colsum_out)
     M, N = dy2d.shape
     if out is None:
-        out = torch.empty_like(dy2d)
-    _C.call("mmt_dropout_bwd", ptr(dy2d), dy2d.stride(0), M, N, ptr(rng), layer, site, keep_prob,
-            row_offset, ptr(out), out.stride(0), ptr(colsum_out), _C.stream_ptr())
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=dy2d.device)
+    _C.call("mmt_dropout_bwd", ptr(dy2d), _dtype_code(dy2d), dy2d.stride(0), M, N, ptr(rng), layer,
+            site, keep_prob, row_offset, ptr(out), out.stride(0), ptr(colsum_out), _C.stream_ptr())
+    return out
+
+
+# ------------------------------------------------------------------------------- image stem
+IMG_F32, IMG_U8 = 0, 2
+
+
+def patch_im2col(img: torch.Tensor, patch: int, kh: int, kw: int, stride: int, normalize: bool = True,
+                 out: torch.Tensor | None = None):
+    """img (B, I, H, H, C) fp32 or uint8 -> bf16 [B*I*NP*OH*OW][kh*kw*C]."""
+    _dev(img, out)
+    if img.dim() != 5 or img.shape[2] != img.shape[3] or not img.is_contiguous():
+        raise ValueError("image must be contiguous (B, I, H, H, C) (square, image_tokenizer.py:49-50)")
+    B, I, H, _, C = img.shape
+    if H % patch:
+        raise ValueError(f"image size {H} not divisible by patch {patch}")
+    code = {torch.float32: IMG_F32, torch.uint8: IMG_U8}.get(img.dtype)
+    if code is None:
+        raise TypeError("image dtype must be float32 or uint8")
+    oh, ow = (patch - kh) // stride + 1, (patch - kw) // stride + 1
+    rows = B * I * (H // patch) ** 2 * oh * ow
+    if out is None:
+        out = torch.empty((rows, kh * kw * C), dtype=torch.bfloat16, device=img.device)
+    _C.call("mmt_patch_im2col", ptr(img), code, B, I, H, C, patch, kh, kw, stride, int(normalize),
+            ptr(out), _C.stream_ptr())
+    return out
+
+
+def _f32(t, what):
+    if t.dtype != torch.float32 or not t.is_contiguous():
+        raise TypeError(f"{what} must be contiguous fp32")
+
+
+def maxpool_patch(conv: torch.Tensor, win: int):
+    """conv fp32 (npatch*win, C) -> pooled fp32 (npatch, C), first-max argmax uint8."""
+    _f32(conv, "conv output")
+    rows, C = conv.shape
+    npatch = rows // win
+    pooled = torch.empty((npatch, C), dtype=torch.float32, device=conv.device)
+    arg = torch.empty((npatch, C), dtype=torch.uint8, device=conv.device)
+    _C.call("mmt_maxpool_patch", ptr(conv), npatch, win, C, ptr(pooled), ptr(arg), _C.stream_ptr())
+    return pooled, arg
+
+
+def maxpool_patch_bwd(dpooled: torch.Tensor, arg: torch.Tensor, win: int, out=None):
+    _f32(dpooled, "dpooled")
+    npatch, C = dpooled.shape
+    if out is None:
+        out = torch.empty((npatch * win, C), dtype=torch.bfloat16, device=dpooled.device)
+    _C.call("mmt_maxpool_patch_bwd", ptr(dpooled), ptr(arg), npatch, win, C, ptr(out), _C.stream_ptr())
+    return out
+
+
+def groupnorm_gelu_fwd(x: torch.Tensor, groups: int, gamma, beta, eps: float, out=None):
+    """x (B, R, C) fp32 contiguous -> gelu(GroupNorm(x)) bf16."""
+    _f32(x, "groupnorm input")
+    B, R, C = x.shape
+    if out is None:
+        out = torch.empty((B, R, C), dtype=torch.bfloat16, device=x.device)
+    mean = torch.empty((B, groups), dtype=torch.float32, device=x.device)
+    rstd = torch.empty((B, groups), dtype=torch.float32, device=x.device)
+    _C.call("mmt_groupnorm_gelu_fwd", ptr(x), B, R, C, groups, eps, ptr(gamma), ptr(beta), ptr(out),
+            ptr(mean), ptr(rstd), _C.stream_ptr())
+    return out, mean, rstd
+
+
+def groupnorm_gelu_bwd(dy, x, groups, gamma, beta, mean, rstd, dgamma, dbeta, dx=None,
+                       accumulate=False):
+    """dy, x, dx fp32 (B, R, C); accumulate: dx += result."""
+    _f32(dy, "dy")
+    _f32(x, "x")
+    B, R, C = x.shape
+    if dx is None:
+        dx = torch.empty_like(x)
+    _C.call("mmt_groupnorm_gelu_bwd", ptr(dy), ptr(x), B, R, C, groups, ptr(gamma), ptr(beta),
+            ptr(mean), ptr(rstd), ptr(dx), int(accumulate), ptr(dgamma), ptr(dbeta), _C.stream_ptr())
+    return dx
+
+
+def patch_positions(B: int, I: int, H: int, patch: int, Q: int, train: bool, rng=None, site: int = 0,
+                    sample_offset: int = 0, device=None):
+    npatch = (H // patch) ** 2
+    dev = device if device is not None else rng.device
+    rt = torch.empty((B, I * npatch), dtype=torch.int32, device=dev)
+    ct = torch.empty((B, I * npatch), dtype=torch.int32, device=dev)
+    _C.call("mmt_patch_positions", ptr(rng), site, B, I, H, patch, Q, int(train), sample_offset,
+            ptr(rt), ptr(ct), _C.stream_ptr())
+    return rt, ct
+
+
+# ---------------------------------------------------------------------------------- glue
+def rmsnorm(x2d: torch.Tensor, w: torch.Tensor, eps: float, out=None):
+    rows, D = x2d.shape
+    if out is None:
+        out = torch.empty_like(x2d)
+    _C.call("mmt_rmsnorm_fwd", ptr(x2d), rows, D, ptr(w), eps, ptr(out), _C.stream_ptr())
+    return out
+
+
+def embedding_gather(ids: torch.Tensor, table: torch.Tensor, out=None):
+    n = ids.numel()
+    vocab, D = table.shape
+    if out is None:
+        out = torch.empty((n, D), dtype=table.dtype, device=table.device)
+    _C.call("mmt_embedding_gather", ptr(ids), n, D, ptr(table), vocab, ptr(out), _C.stream_ptr())
+    return out
+
+
+def cast_f32_bf16(a: torch.Tensor, out: torch.Tensor):
+    _C.call("mmt_cast_f32_bf16", ptr(a), ptr(out), a.numel(), _C.stream_ptr())
     return out

@@ -1,0 +1,114 @@
+"""DDPM action head, mirroring the reference's ``multi_modal_transformers/action_heads/diffusion.py``:
+``cosine_beta_schedule`` (:17-27), ``FourierFeatures`` (:30-51), ``OctoDenoise`` (:53-65) and
+``DiffusionActionHead`` (:68-209: ``denoise_loss`` :110-143, ``predict_denoise_term`` :88-107,
+``predict_action`` :146-209).
+
+Training path on MI355X: one fused kernel draws (t, eps), noises the actions and emits the Fourier
+features straight into the denoiser's concatenated input buffer; the time-encoder MLP writes its
+output into that same buffer (GEMM with a column-offset output), the readout mean is written into
+its last columns, so ``concatenate([noisy, time_emb, readout])`` (:61) never materialises
+separately. MLPBlocks here run with dropout disabled, as in the reference (they are called without
+``train``, attention.py:29 default False).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from .. import _C, _kernels as K
+from ..layers import Dense
+from ..params import ParamStore, he_normal
+
+
+def cosine_beta_schedule(timesteps: int, s: float = 0.008) -> np.ndarray:
+    """Reference :17-27 (float32 like jnp)."""
+    steps = timesteps + 1
+    t = (np.linspace(0, timesteps, steps, dtype=np.float32) / np.float32(timesteps)).astype(np.float32)
+    ac = np.cos((t + np.float32(s)) / np.float32(1 + s) * np.float32(np.pi) * np.float32(0.5)) ** 2
+    ac = (ac / ac[0]).astype(np.float32)
+    betas = (1 - (ac[1:] / ac[:-1])).astype(np.float32)
+    return np.clip(betas, 0, 0.999).astype(np.float32)
+
+
+def alpha_hats_of(betas: np.ndarray) -> np.ndarray:
+    """Reference :84-86: prod(alphas[:i+1]) for each i (float32)."""
+    alphas = (1 - betas).astype(np.float32)
+    return np.array([np.prod(alphas[: i + 1], dtype=np.float32) for i in range(len(betas))],
+                    dtype=np.float32)
+
+
+class DiffusionActionHead:
+    def __init__(self, store: ParamStore, name: str, embedding_dim: int, action_dim: int = 8,
+                 diffusion_steps: int = 32, time_dim: int | None = None, hidden: int | None = None):
+        D = embedding_dim
+        self.D, self.A, self.steps = D, action_dim, diffusion_steps
+        self.F = (time_dim or D) // 2
+        T = 2 * self.F
+        self.time_dim = T
+        self.hidden = hidden or D
+        p = f"{name}/OctoDenoise_0"
+        self.fourier = store.add(f"{p}/FourierFeatures_0/fourier_kernel", (self.F, 1),
+                                 he_normal((self.F, 1)))
+        self.t1 = Dense(store, f"{p}/FourierFeatures_0/MLPBlock_0/Dense_0", T, T)
+        self.t2 = Dense(store, f"{p}/FourierFeatures_0/MLPBlock_0/Dense_1", T, T)
+        self.cat_dim = action_dim + T + D
+        self.d1 = Dense(store, f"{p}/MLPBlock_0/Dense_0", self.cat_dim, self.hidden)
+        self.d2 = Dense(store, f"{p}/MLPBlock_0/Dense_1", self.hidden, action_dim)
+        betas = cosine_beta_schedule(diffusion_steps)
+        self.betas_np = betas
+        self.alpha_hats_np = alpha_hats_of(betas)
+        self._dev_consts = {}
+        if self.cat_dim % 8:
+            raise ValueError("action_dim + time_dim + D must be a multiple of 8 (16-B rows)")
+
+    def consts(self, device):
+        if device not in self._dev_consts:
+            self._dev_consts[device] = torch.from_numpy(self.alpha_hats_np).to(device)
+        return self._dev_consts[device]
+
+    def new_cat(self, B, device):
+        return torch.empty((B, self.cat_dim), dtype=torch.bfloat16, device=device)
+
+    def readout_slot(self, cat: torch.Tensor) -> torch.Tensor:
+        return cat[:, self.A + self.time_dim:]
+
+    # ------------------------------------------------------------------------- denoise_loss
+    def loss_forward(self, cat: torch.Tensor, actions: torch.Tensor, rng, sample_offset: int = 0,
+                     t_in=None, eps_in=None):
+        """cat: (B, A+T+D) bf16 whose readout slot is already filled. Returns (loss (1,) fp32,
+        saved). Mirrors denoise_loss (:110-143)."""
+        B = cat.shape[0]
+        dev = cat.device
+        t = torch.empty(B, dtype=torch.int32, device=dev)
+        eps = torch.empty((B, self.A), dtype=torch.float32, device=dev)
+        feats = torch.empty((B, self.time_dim), dtype=torch.bfloat16, device=dev)
+        _C.call("mmt_diffusion_prep", _C.ptr(rng), B, self.A, self.steps, sample_offset,
+                _C.ptr(actions), _C.ptr(self.consts(dev)), _C.ptr(self.fourier.data), self.F,
+                _C.ptr(t_in), _C.ptr(eps_in), _C.ptr(t), _C.ptr(eps), _C.ptr(cat), cat.stride(0),
+                _C.ptr(feats), _C.stream_ptr())
+        ht = self.t1.fwd(feats, act=K.ACT_RELU)
+        self.t2.fwd(ht, out=cat[:, self.A:self.A + self.time_dim])
+        hd = self.d1.fwd(cat, act=K.ACT_RELU)
+        pred = self.d2.fwd(hd, out_mode=K.OUT_F32)
+        loss = torch.empty(1, dtype=torch.float32, device=dev)
+        dpred = torch.empty((B, self.A), dtype=torch.bfloat16, device=dev)
+        _C.call("mmt_diffusion_loss", _C.ptr(pred), pred.stride(0), _C.ptr(eps), B, self.A, 1.0,
+                _C.ptr(loss), _C.ptr(dpred), _C.stream_ptr())
+        return loss, dict(cat=cat, feats=feats, ht=ht, hd=hd, dpred=dpred, t=t, eps=eps, pred=pred)
+
+    def loss_backward(self, sv: dict) -> torch.Tensor:
+        """Returns d(readout mean) (B, D) bf16 view."""
+        B = sv["cat"].shape[0]
+        dzd = self.d2.bwd(sv["dpred"], sv["hd"], gate=sv["hd"], gate_scale=1.0)
+        dcat = self.d1.bwd(dzd, sv["cat"])
+        dtemb = dcat[:, self.A:self.A + self.time_dim]
+        dzt = self.t2.bwd(dtemb, sv["ht"], gate=sv["ht"], gate_scale=1.0)
+        dfeats = self.t1.bwd(dzt, sv["feats"])
+        _C.call("mmt_fourier_bwd", _C.ptr(dfeats), B, self.F, _C.ptr(sv["t"]),
+                _C.ptr(self.fourier.data), _C.ptr(self.fourier.grad), _C.stream_ptr())
+        return dcat[:, self.A + self.time_dim:]
+
+    def predict_action(self, *a, **k):  # SURVEY §8(f) row 2 (inference sampler): next
+        raise NotImplementedError("the 32-step DDPM sampler (diffusion.py:146-209) is §8(f) 'next'")

@@ -1,0 +1,160 @@
+"""Transformer blocks, mirroring the reference's
+``multi_modal_transformers/attention_blocks/attention.py`` (MLPBlock :20-39, Encoder1DBlock
+:41-69, AddPositionEmbedding :71-85, StackedEncoder1DBlock :87-119) with ToMe inserted the way
+``tome_attention.py:249-256`` intends (after the attention residual, before the MLP LayerNorm).
+
+Semantics kept from the reference:
+  * pre-LN block: y = LN0(x); y = MHA(y); y = Dropout(y); x = x + y; z = LN1(x); MLP; x + z,
+    with LayerNorm over the SEQUENCE axis (reduction_axes=[1]);
+  * Flax SelfAttention: q/sqrt(Dh), finfo.min masking, fp32 softmax, dropout(0.1) with one (L, L)
+    mask broadcast over batch and heads; q/k/v/out DenseGeneral with bias (fused QKV here);
+  * MLPBlock: Dense -> relu -> Dropout -> Dense -> Dropout (the YAML key ``norm`` is the Dropout);
+  * ToMe metric = sum over heads of the key projection of the image token set, merged with
+    merge_wavg and the set's token sizes carried across layers (no proportional attention).
+Every op is a libmmt_hip kernel (see layers.py); backward is explicit.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+
+from .. import _kernels as K
+from ..layers import (DROP_ATTN, DROP_ATTN_OUT, DROP_MLP_HIDDEN, DROP_MLP_OUT, Dense,
+                      SeqLayerNorm)
+from ..params import ParamStore, he_normal, normal
+from ..tokenizers.token_sequencer import LayerSets
+
+
+@dataclass
+class LayerCtx:
+    """Static (capture-time) description of one block's sequence plus the step's RNG state."""
+    layer: int
+    sets: LayerSets                # token-set table entering the block
+    table: K.SetTable
+    tome_set: int = -1             # index of the merged token set, -1 = no merge
+    r: int = 0
+    train: bool = True
+    rng: Optional[torch.Tensor] = None
+    sample_offset: int = 0         # global index of this rank's first sample (RNG counters)
+
+
+class MLPBlock:
+    """attention.py:20-39."""
+
+    def __init__(self, store: ParamStore, name: str, in_f: int, hidden: int, out_f: int,
+                 dropout_rate: float = 0.1):
+        self.dense = Dense(store, f"{name}/Dense_0", in_f, hidden)
+        self.dense_out = Dense(store, f"{name}/Dense_1", hidden, out_f)
+        self.rate = dropout_rate
+
+
+class Encoder1DBlock:
+    """attention.py:41-69 (+ ToMe between the attention residual and LN1)."""
+
+    def __init__(self, store: ParamStore, name: str, D: int, num_heads: int, mlp_dim: int,
+                 eps: float = 1e-6, dropout_rate: float = 0.1, attn_dropout_rate: float = 0.1):
+        if D % num_heads:
+            raise ValueError("qkv_features must be divisible by num_heads")
+        self.D, self.H, self.Dh, self.M = D, num_heads, D // num_heads, mlp_dim
+        self.ln0 = SeqLayerNorm(store, f"{name}/LayerNorm_0", D, eps)
+        self.qkv = Dense(store, f"{name}/SelfAttention_0/qkv", D, 3 * D, kernel_init=he_normal((D, D)))
+        self.out = Dense(store, f"{name}/SelfAttention_0/out", D, D, kernel_init=he_normal((D, D)))
+        self.ln1 = SeqLayerNorm(store, f"{name}/LayerNorm_1", D, eps)
+        self.mlp = MLPBlock(store, f"{name}/MLPBlock_0", D, mlp_dim, D, dropout_rate)
+        self.rate = dropout_rate
+        self.attn_rate = attn_dropout_rate
+        self.scale = self.Dh ** -0.5
+
+    # ------------------------------------------------------------------------------ forward
+    def forward(self, x: torch.Tensor, ctx: LayerCtx, size: Optional[torch.Tensor]):
+        B, L, D = x.shape
+        H, Dh = self.H, self.Dh
+        train = ctx.train
+        kp = 1.0 - self.rate if train else 1.0
+        kpa = 1.0 - self.attn_rate if train else 1.0
+
+        def drop(site, rows_per_sample):
+            if not train or kp >= 1.0:
+                return {}
+            return dict(rng=ctx.rng, drop_layer=ctx.layer, drop_site=site, keep_prob=kp,
+                        drop_row_offset=ctx.sample_offset * rows_per_sample)
+
+        y0, mu0, rs0 = self.ln0.fwd(x)
+        qkv = self.qkv.fwd(y0.view(B * L, D)).view(B, L, 3 * D)
+        bits = K.dropout_bits(ctx.rng, ctx.layer, DROP_ATTN, L, L, kpa) if (train and kpa < 1) else None
+        o, lse = K.attn_fwd(qkv, H, self.scale, ctx.table, bits, kpa)
+        # residual stream stays fp32 (sequence-axis LayerNorm conditioning, csrc/norm.hip)
+        x1 = self.out.fwd(o.view(B * L, D), residual=x.view(B * L, D), out_mode=K.OUT_F32,
+                          **drop(DROP_ATTN_OUT, L))
+        x1 = x1.view(B, L, D)
+        tome = None
+        new_size = size
+        if ctx.r > 0:
+            s0, t = ctx.sets.starts[ctx.tome_set], ctx.sets.lens[ctx.tome_set]
+            metric = qkv.view(B, L, 3, H, Dh)[:, s0:s0 + t, 1]     # (B, t, H, Dh): sum_h K
+            unm, src, dst = K.tome_match(metric, ctx.r)
+            x1, new_size, pos = K.tome_merge_fwd(x1, s0, t, ctx.r, unm, src, dst, size_in=size)
+            tome = (s0, t, ctx.r, pos, size, new_size, unm, src, dst)
+        L2 = x1.shape[1]
+        y1, mu1, rs1 = self.ln1.fwd(x1)
+        h = self.mlp.dense.fwd(y1.view(B * L2, D), act=K.ACT_RELU, **drop(DROP_MLP_HIDDEN, L2))
+        x2 = self.mlp.dense_out.fwd(h, residual=x1.view(B * L2, D), out_mode=K.OUT_F32,
+                                    **drop(DROP_MLP_OUT, L2))
+        saved = dict(x=x, y0=y0, mu0=mu0, rs0=rs0, qkv=qkv, o=o, lse=lse, bits=bits, x1=x1, y1=y1,
+                     mu1=mu1, rs1=rs1, h=h, tome=tome, kp=kp, kpa=kpa)
+        return x2.view(B, L2, D), saved, new_size
+
+    # ----------------------------------------------------------------------------- backward
+    def backward(self, dx2: torch.Tensor, sv: dict, ctx: LayerCtx) -> torch.Tensor:
+        B, L2, D = dx2.shape
+        L = sv["x"].shape[1]
+        kp, kpa, train = sv["kp"], sv["kpa"], ctx.train
+        dropping = train and kp < 1.0
+        dx2f = dx2.reshape(B * L2, D)                      # fp32 residual-stream gradient
+        rng = ctx.rng if dropping else None
+        # MLP out: x2 = x1 + drop3(h W2^T + b2); dropout backward = mask/scale + cast to bf16,
+        # fused with the bias gradient (column sum)
+        dz2 = K.dropout_bwd(dx2f, rng, ctx.layer, DROP_MLP_OUT, kp, row_offset=ctx.sample_offset * L2,
+                            colsum_out=self.mlp.dense_out.b.grad)
+        # dh gated by (h > 0): relu + hidden-dropout backward fused into the dX GEMM epilogue
+        dz1 = self.mlp.dense_out.bwd(dz2, sv["h"], bias_grad_done=True, gate=sv["h"],
+                                     gate_scale=(1.0 / kp) if dropping else 1.0)
+        dy1 = self.mlp.dense.bwd(dz1, sv["y1"].view(B * L2, D), out_mode=K.OUT_F32)
+        dx1 = self.ln1.bwd(dy1.view(B, L2, D), sv["x1"], sv["mu1"], sv["rs1"], addend=dx2)
+        if sv["tome"] is not None:
+            s0, t, r, pos, size_in, size_out = sv["tome"][:6]
+            dx1 = K.tome_merge_bwd(dx1, s0, t, r, pos, size_in, size_out)
+        dx1f = dx1.view(B * L, D)
+        dzo = K.dropout_bwd(dx1f, rng, ctx.layer, DROP_ATTN_OUT, kp, row_offset=ctx.sample_offset * L,
+                            colsum_out=self.out.b.grad)
+        do = self.out.bwd(dzo, sv["o"].view(B * L, D), bias_grad_done=True)
+        dqkv = K.attn_bwd(sv["qkv"], sv["o"], do.view(B, L, D), sv["lse"], self.H, self.scale,
+                          ctx.table, sv["bits"], kpa)
+        dy0 = self.qkv.bwd(dqkv.view(B * L, 3 * D), sv["y0"].view(B * L, D), out_mode=K.OUT_F32)
+        return self.ln0.bwd(dy0.view(B, L, D), sv["x"], sv["mu0"], sv["rs0"], addend=dx1)
+
+
+class StackedEncoder1DBlock:
+    """attention.py:87-119 (nn.scan over identical blocks). With ToMe the sequence shrinks per
+    block, so the stack is a Python loop over per-block parameter sets (names Block_{i})."""
+
+    def __init__(self, store: ParamStore, name: str, num_blocks: int, D: int, num_heads: int,
+                 mlp_dim: int, eps: float = 1e-6, dropout_rate: float = 0.1,
+                 attn_dropout_rate: float = 0.1):
+        self.blocks = [Encoder1DBlock(store, f"{name}/Block_{i}", D, num_heads, mlp_dim, eps,
+                                      dropout_rate, attn_dropout_rate) for i in range(num_blocks)]
+
+    def forward(self, x, ctxs: List[LayerCtx]):
+        saved = []
+        size = None
+        for blk, ctx in zip(self.blocks, ctxs):
+            x, sv, size = blk.forward(x, ctx, size)
+            saved.append(sv)
+        return x, saved
+
+    def backward(self, dx, saved, ctxs):
+        for blk, sv, ctx in zip(reversed(self.blocks), reversed(saved), reversed(ctxs)):
+            dx = blk.backward(dx, sv, ctx)
+        return dx

@@ -37,7 +37,8 @@ struct Epi {
   const bf16_t* gate;
   int64_t ld_gate;
   float gate_scale;
-  const bf16_t* residual;
+  const void* residual;
+  int res_f32;
   int64_t ld_res;
   float alpha, beta;
 };
@@ -192,7 +193,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(
           const uint32_t ctr = (uint32_t)((epi.drop_row_offset + gr) * (int64_t)N + gc);
           v = keep_draw(key, ctr, epi.keep_thresh) ? v * epi.drop_scale : 0.f;
         }
-        if (epi.residual) v += bf2f(epi.residual[(int64_t)gr * epi.ld_res + gc]);
+        if (epi.residual) {
+          const int64_t ro = (int64_t)gr * epi.ld_res + gc;
+          v += epi.res_f32 ? reinterpret_cast<const float*>(epi.residual)[ro]
+                           : bf2f(reinterpret_cast<const bf16_t*>(epi.residual)[ro]);
+        }
         if (OUT == 0) {
           reinterpret_cast<bf16_t*>(Cv)[bz * sC + (int64_t)gr * ldc + gc] = f2bf(v);
         } else {
@@ -235,7 +240,8 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     epi.gate = (const bf16_t*)e->gate;
     epi.ld_gate = e->ld_gate;
     epi.gate_scale = e->gate_scale;
-    epi.residual = (const bf16_t*)e->residual;
+    epi.residual = e->residual;
+    epi.res_f32 = e->res_dtype == MMT_F32;
     epi.ld_res = e->ld_res;
     epi.alpha = e->alpha;
     epi.beta = e->beta;

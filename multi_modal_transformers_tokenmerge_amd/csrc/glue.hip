@@ -1,0 +1,420 @@
+// Small fused kernels around the hot path (gfx950): sequence assembly (token_sequencer.py
+// :255-269 + readout.py:18-33 + attention.py:71-85 position embedding + image_tokenizer.py:300-307
+// row/col embeddings), readout mean (diffusion.py:102), diffusion noising / Fourier features /
+// loss (diffusion.py:17-143), T5 RMS-norm and embedding gather, fused AdamW over the flat
+// parameter buffer, and the device-side step counter that keys every random stream.
+#include <math.h>
+
+#include "common.h"
+
+using namespace mmt;
+
+namespace {
+
+__device__ __forceinline__ void unpack8(const uint4& u, float* f) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f[2 * q] = __uint_as_float(w[q] << 16);
+    f[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint32_t w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) w[q] = (uint32_t)f2bf(f[2 * q]) | ((uint32_t)f2bf(f[2 * q + 1]) << 16);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// row descriptor: kind << 24 | index   (kind 0 text row, 1 image row, 2 readout row)
+constexpr int KIND_TEXT = 0, KIND_IMAGE = 1, KIND_READOUT = 2;
+
+__global__ void seq_assemble_fwd_kernel(int B, int L, int D, const int32_t* __restrict__ row_src,
+                                        const bf16_t* __restrict__ text, int T,
+                                        const bf16_t* __restrict__ img, int NI,
+                                        const int32_t* __restrict__ rtok,
+                                        const int32_t* __restrict__ ctok,
+                                        const float* __restrict__ row_emb,
+                                        const float* __restrict__ col_emb,
+                                        const float* __restrict__ readout_pe,
+                                        const float* __restrict__ pe, float* __restrict__ x0) {
+  const int cpr = D / 8;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)B * L * cpr) return;
+  const int ch = idx % cpr;
+  const int l = (idx / cpr) % L;
+  const int b = idx / ((int64_t)cpr * L);
+  const int d0 = ch * 8;
+  const int desc = row_src[l];
+  const int kind = desc >> 24, j = desc & 0xffffff;
+  float v[8];
+  if (kind == KIND_TEXT) {
+    unpack8(*reinterpret_cast<const uint4*>(text + ((int64_t)b * T + j) * D + d0), v);
+  } else if (kind == KIND_IMAGE) {
+    unpack8(*reinterpret_cast<const uint4*>(img + ((int64_t)b * NI + j) * D + d0), v);
+    const int rt = rtok[(int64_t)b * NI + j], ct = ctok[(int64_t)b * NI + j];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += row_emb[(int64_t)rt * D + d0 + e] + col_emb[(int64_t)ct * D + d0 + e];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = readout_pe[(int64_t)j * D + d0 + e];  // zeros + embedding
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] += pe[(int64_t)l * D + d0 + e];
+  float* xo = x0 + ((int64_t)b * L + l) * D + d0;
+  *reinterpret_cast<float4*>(xo) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(xo + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+__global__ void seq_assemble_bwd_kernel(int B, int L, int D, const int32_t* __restrict__ row_src,
+                                        const float* __restrict__ dx0, bf16_t* __restrict__ dtext,
+                                        int T, bf16_t* __restrict__ dimg, int NI,
+                                        const int32_t* __restrict__ rtok,
+                                        const int32_t* __restrict__ ctok,
+                                        float* __restrict__ drow_emb, float* __restrict__ dcol_emb,
+                                        float* __restrict__ dreadout_pe) {
+  const int cpr = D / 8;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)B * L * cpr) return;
+  const int ch = idx % cpr;
+  const int l = (idx / cpr) % L;
+  const int b = idx / ((int64_t)cpr * L);
+  const int d0 = ch * 8;
+  const int desc = row_src[l];
+  const int kind = desc >> 24, j = desc & 0xffffff;
+  float v[8];
+  {
+    const float* gp = dx0 + ((int64_t)b * L + l) * D + d0;
+    const float4 a = *reinterpret_cast<const float4*>(gp), c = *reinterpret_cast<const float4*>(gp + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
+  }
+  if (kind == KIND_TEXT) {
+    if (dtext) *reinterpret_cast<uint4*>(dtext + ((int64_t)b * T + j) * D + d0) = pack8(v);
+  } else if (kind == KIND_IMAGE) {
+    *reinterpret_cast<uint4*>(dimg + ((int64_t)b * NI + j) * D + d0) = pack8(v);
+    const int rt = rtok[(int64_t)b * NI + j], ct = ctok[(int64_t)b * NI + j];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      atomicAdd(drow_emb + (int64_t)rt * D + d0 + e, v[e]);
+      atomicAdd(dcol_emb + (int64_t)ct * D + d0 + e, v[e]);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) atomicAdd(dreadout_pe + (int64_t)j * D + d0 + e, v[e]);
+  }
+}
+
+// e[b, :] = mean over the listed rows of x[b] ; written as bf16 into out (row stride ld_out)
+__global__ void rows_mean_fwd_kernel(const float* __restrict__ x, int64_t xs_b, int64_t xs_t,
+                                     int D, const int32_t* __restrict__ rows, int nrows,
+                                     bf16_t* __restrict__ out, int64_t ld_out) {
+  const int b = blockIdx.x;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = 0.f;
+    for (int i = 0; i < nrows; ++i) s += x[b * xs_b + (int64_t)rows[i] * xs_t + d];
+    out[b * ld_out + d] = f2bf(s / nrows);
+  }
+}
+
+// dx[b, l, :] = de[b, :] / n for listed rows (row_flag[l] >= 0), 0 otherwise (whole buffer)
+__global__ void rows_mean_bwd_kernel(const bf16_t* __restrict__ de, int64_t ld_de, int B, int L,
+                                     int D, const int32_t* __restrict__ row_flag, int nrows,
+                                     float* __restrict__ dx) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)B * L * D) return;
+  const int d = idx % D;
+  const int l = (idx / D) % L;
+  const int b = idx / ((int64_t)D * L);
+  dx[idx] = row_flag[l] >= 0 ? bf2f(de[b * ld_de + d]) / nrows : 0.f;
+}
+
+// Diffusion noising + Fourier features (diffusion.py:41-51, 110-131):
+//   t ~ U{0..steps-1}, eps ~ N(0, 1) (Box-Muller on the counter stream) unless injected;
+//   noisy = sqrt(abar_t) a + sqrt(1 - abar_t) eps  -> cat[:, 0:A]  (bf16)
+//   h = 2 pi t W^T (W: (F,) = fourier kernel (F, 1)), feats = [cos h, sin h] (bf16, 2F)
+__global__ void diffusion_prep_kernel(const uint32_t* __restrict__ rng, int B, int A, int steps,
+                                      int64_t sample_offset, const float* __restrict__ actions,
+                                      const float* __restrict__ alpha_hats,
+                                      const float* __restrict__ fw, int F,
+                                      const int32_t* __restrict__ t_in,
+                                      const float* __restrict__ eps_in, int32_t* __restrict__ t_out,
+                                      float* __restrict__ eps_out, bf16_t* __restrict__ cat,
+                                      int64_t ld_cat, bf16_t* __restrict__ feats) {
+  const int b = blockIdx.x;
+  __shared__ int s_t;
+  if (threadIdx.x == 0) {
+    int t;
+    if (t_in) {
+      t = t_in[b];
+    } else {
+      const uint32_t key = stream_key(rng[0], rng[1], 0xFFFEu, 1);
+      t = (int)(((uint64_t)draw_u32(key, (uint32_t)(sample_offset + b)) * (uint32_t)steps) >> 32);
+    }
+    s_t = t;
+    t_out[b] = t;
+  }
+  __syncthreads();
+  const int t = s_t;
+  const float ah = alpha_hats[t];
+  const float a1 = sqrtf(ah), a2 = sqrtf(1.f - ah);
+  for (int j = threadIdx.x; j < A; j += blockDim.x) {
+    float e;
+    if (eps_in) {
+      e = eps_in[b * A + j];
+    } else {
+      const uint32_t key = stream_key(rng[0], rng[1], 0xFFFEu, 2);
+      const uint32_t c = (uint32_t)((sample_offset + b) * A + j);
+      const float u1 = ((draw_u32(key, 2 * c) >> 8) + 1) * (1.f / 16777216.f);  // (0, 1]
+      const float u2 = (draw_u32(key, 2 * c + 1) >> 8) * (1.f / 16777216.f);
+      e = sqrtf(-2.f * logf(u1)) * cosf(6.283185307179586f * u2);
+    }
+    eps_out[b * A + j] = e;
+    cat[b * ld_cat + j] = f2bf(a1 * actions[b * A + j] + a2 * e);
+  }
+  const float tf = (float)t;
+  for (int k = threadIdx.x; k < F; k += blockDim.x) {
+    const float h = 2.f * 3.141592653589793f * tf * fw[k];
+    feats[(int64_t)b * 2 * F + k] = f2bf(cosf(h));
+    feats[(int64_t)b * 2 * F + F + k] = f2bf(sinf(h));
+  }
+}
+
+// dW[k] += sum_b 2 pi t_b (cos(h) dsin - sin(h) dcos)
+__global__ void fourier_bwd_kernel(const bf16_t* __restrict__ dfeats, int B, int F,
+                                   const int32_t* __restrict__ t, const float* __restrict__ fw,
+                                   float* __restrict__ dw) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= F) return;
+  float acc = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float tt = 2.f * 3.141592653589793f * (float)t[b];
+    const float h = tt * fw[k];
+    const float dc = bf2f(dfeats[(int64_t)b * 2 * F + k]), ds = bf2f(dfeats[(int64_t)b * 2 * F + F + k]);
+    acc += tt * (cosf(h) * ds - sinf(h) * dc);
+  }
+  dw[k] += acc;
+}
+
+// loss = mean_b sum_j 0.5 (pred - eps)^2 (optax.l2_loss, diffusion.py:141-142);
+// dpred = (pred - eps) * grad_scale / B  (bf16). One workgroup.
+__global__ void diffusion_loss_kernel(const float* __restrict__ pred, int64_t ld_pred,
+                                      const float* __restrict__ eps, int B, int A,
+                                      float grad_scale, float* __restrict__ loss,
+                                      bf16_t* __restrict__ dpred) {
+  __shared__ float red[1024 / 64];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < B * A; i += blockDim.x) {
+    const int b = i / A, j = i % A;
+    const float d = pred[b * ld_pred + j] - eps[i];
+    s += 0.5f * d * d;
+    dpred[i] = f2bf(d * grad_scale / B);
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+    loss[0] = t / B;
+  }
+}
+
+// T5LayerNorm: y = x * rsqrt(mean(x^2) + eps) * w   (one wave per row, D % 8 == 0)
+__global__ void rmsnorm_fwd_kernel(const bf16_t* __restrict__ x, int64_t rows, int D,
+                                   const bf16_t* __restrict__ w, float eps, bf16_t* __restrict__ y) {
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const bf16_t* xr = x + row * D;
+  float s = 0.f;
+  for (int c = lane * 8; c < D; c += 512) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(xr + c), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += f[e] * f[e];
+  }
+  s = wave_sum(s);
+  const float rs = rsqrtf(s / D + eps);
+  for (int c = lane * 8; c < D; c += 512) {
+    float f[8], g[8];
+    unpack8(*reinterpret_cast<const uint4*>(xr + c), f);
+    unpack8(*reinterpret_cast<const uint4*>(w + c), g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = f[e] * rs * g[e];
+    *reinterpret_cast<uint4*>(y + row * D + c) = pack8(f);
+  }
+}
+
+__global__ void embedding_gather_kernel(const int32_t* __restrict__ ids, int64_t n, int D,
+                                        const bf16_t* __restrict__ table, int vocab,
+                                        bf16_t* __restrict__ out) {
+  const int cpr = D / 8;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * cpr) return;
+  const int64_t r = idx / cpr;
+  const int c = (idx % cpr) * 8;
+  int id = ids[r];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+  *reinterpret_cast<uint4*>(out + r * D + c) = *reinterpret_cast<const uint4*>(table + (int64_t)id * D + c);
+}
+
+// AdamW (optax.adamw semantics, decoupled weight decay on every parameter, bias-corrected
+// moments) over the flat fp32 master buffer; writes the bf16 shadow used by the GEMMs.
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                             float* __restrict__ m, float* __restrict__ v,
+                             bf16_t* __restrict__ shadow, int64_t n, const int32_t* __restrict__ state,
+                             float lr, float b1, float b2, float eps, float wd, float grad_scale) {
+  const int step = state[1] + 1;
+  const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i] * grad_scale;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float upd = (mi / bc1) / (sqrtf(vi / bc2) + eps) + wd * p[i];
+    const float pn = p[i] - lr * upd;
+    p[i] = pn;
+    if (shadow) shadow[i] = f2bf(pn);
+  }
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ a, bf16_t* __restrict__ b, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    b[i] = f2bf(a[i]);
+}
+
+__global__ void step_advance_kernel(int32_t* state) { state[1] += 1; }
+
+}  // namespace
+
+extern "C" int mmt_seq_assemble_fwd(int B, int L, int D, const int32_t* row_src, const void* text,
+                                    int T, const void* img, int NI, const int32_t* rtok,
+                                    const int32_t* ctok, const float* row_emb, const float* col_emb,
+                                    const float* readout_pe, const float* pe, void* x0,
+                                    mmt_stream_t stream) {
+  MMT_CHECK_ARG(row_src && x0 && pe && D % 8 == 0 && B > 0 && L > 0, "mmt_seq_assemble_fwd: args");
+  const int64_t n = (int64_t)B * L * (D / 8);
+  hipLaunchKernelGGL(seq_assemble_fwd_kernel, dim3((n + 255) / 256), dim3(256), 0,
+                     as_stream(stream), B, L, D, row_src, (const bf16_t*)text, T,
+                     (const bf16_t*)img, NI, rtok, ctok, row_emb, col_emb, readout_pe, pe,
+                     (float*)x0);
+  MMT_CHECK_LAUNCH("mmt_seq_assemble_fwd");
+  return MMT_OK;
+}
+
+extern "C" int mmt_seq_assemble_bwd(int B, int L, int D, const int32_t* row_src, const void* dx0,
+                                    void* dtext, int T, void* dimg, int NI, const int32_t* rtok,
+                                    const int32_t* ctok, float* drow_emb, float* dcol_emb,
+                                    float* dreadout_pe, mmt_stream_t stream) {
+  MMT_CHECK_ARG(row_src && dx0 && D % 8 == 0 && B > 0 && L > 0, "mmt_seq_assemble_bwd: args");
+  const int64_t n = (int64_t)B * L * (D / 8);
+  hipLaunchKernelGGL(seq_assemble_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0,
+                     as_stream(stream), B, L, D, row_src, (const float*)dx0, (bf16_t*)dtext, T,
+                     (bf16_t*)dimg, NI, rtok, ctok, drow_emb, dcol_emb, dreadout_pe);
+  MMT_CHECK_LAUNCH("mmt_seq_assemble_bwd");
+  return MMT_OK;
+}
+
+extern "C" int mmt_rows_mean_fwd(const void* x, int64_t xs_b, int64_t xs_t, int B, int D,
+                                 const int32_t* rows, int nrows, void* out, int64_t ld_out,
+                                 mmt_stream_t stream) {
+  MMT_CHECK_ARG(x && rows && out && B > 0 && nrows > 0, "mmt_rows_mean_fwd: args");
+  hipLaunchKernelGGL(rows_mean_fwd_kernel, dim3(B), dim3(256), 0, as_stream(stream),
+                     (const float*)x, xs_b, xs_t, D, rows, nrows, (bf16_t*)out, ld_out);
+  MMT_CHECK_LAUNCH("mmt_rows_mean_fwd");
+  return MMT_OK;
+}
+
+extern "C" int mmt_rows_mean_bwd(const void* de, int64_t ld_de, int B, int L, int D,
+                                 const int32_t* row_flag, int nrows, void* dx, mmt_stream_t stream) {
+  MMT_CHECK_ARG(de && row_flag && dx && B > 0 && nrows > 0, "mmt_rows_mean_bwd: args");
+  const int64_t n = (int64_t)B * L * D;
+  hipLaunchKernelGGL(rows_mean_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream),
+                     (const bf16_t*)de, ld_de, B, L, D, row_flag, nrows, (float*)dx);
+  MMT_CHECK_LAUNCH("mmt_rows_mean_bwd");
+  return MMT_OK;
+}
+
+extern "C" int mmt_diffusion_prep(const uint32_t* rng, int B, int A, int steps,
+                                  int64_t sample_offset, const float* actions,
+                                  const float* alpha_hats, const float* fourier_w, int F,
+                                  const int32_t* t_in, const float* eps_in, int32_t* t_out,
+                                  float* eps_out, void* cat, int64_t ld_cat, void* feats,
+                                  mmt_stream_t stream) {
+  MMT_CHECK_ARG(actions && alpha_hats && fourier_w && t_out && eps_out && cat && feats && B > 0,
+                "mmt_diffusion_prep: args");
+  MMT_CHECK_ARG((t_in && eps_in) || rng, "mmt_diffusion_prep: need rng or injected (t, eps)");
+  hipLaunchKernelGGL(diffusion_prep_kernel, dim3(B), dim3(256), 0, as_stream(stream), rng, B, A,
+                     steps, sample_offset, actions, alpha_hats, fourier_w, F, t_in, eps_in, t_out,
+                     eps_out, (bf16_t*)cat, ld_cat, (bf16_t*)feats);
+  MMT_CHECK_LAUNCH("mmt_diffusion_prep");
+  return MMT_OK;
+}
+
+extern "C" int mmt_fourier_bwd(const void* dfeats, int B, int F, const int32_t* t,
+                               const float* fourier_w, float* dw, mmt_stream_t stream) {
+  MMT_CHECK_ARG(dfeats && t && fourier_w && dw && B > 0 && F > 0, "mmt_fourier_bwd: args");
+  hipLaunchKernelGGL(fourier_bwd_kernel, dim3((F + 255) / 256), dim3(256), 0, as_stream(stream),
+                     (const bf16_t*)dfeats, B, F, t, fourier_w, dw);
+  MMT_CHECK_LAUNCH("mmt_fourier_bwd");
+  return MMT_OK;
+}
+
+extern "C" int mmt_diffusion_loss(const float* pred, int64_t ld_pred, const float* eps, int B,
+                                  int A, float grad_scale, float* loss, void* dpred,
+                                  mmt_stream_t stream) {
+  MMT_CHECK_ARG(pred && eps && loss && dpred && B > 0 && A > 0, "mmt_diffusion_loss: args");
+  hipLaunchKernelGGL(diffusion_loss_kernel, dim3(1), dim3(1024), 0, as_stream(stream), pred,
+                     ld_pred, eps, B, A, grad_scale, loss, (bf16_t*)dpred);
+  MMT_CHECK_LAUNCH("mmt_diffusion_loss");
+  return MMT_OK;
+}
+
+extern "C" int mmt_rmsnorm_fwd(const void* x, int64_t rows, int D, const void* w, float eps,
+                               void* y, mmt_stream_t stream) {
+  MMT_CHECK_ARG(x && w && y && rows > 0 && D % 8 == 0, "mmt_rmsnorm_fwd: args");
+  hipLaunchKernelGGL(rmsnorm_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, as_stream(stream),
+                     (const bf16_t*)x, rows, D, (const bf16_t*)w, eps, (bf16_t*)y);
+  MMT_CHECK_LAUNCH("mmt_rmsnorm_fwd");
+  return MMT_OK;
+}
+
+extern "C" int mmt_embedding_gather(const int32_t* ids, int64_t n, int D, const void* table,
+                                    int vocab, void* out, mmt_stream_t stream) {
+  MMT_CHECK_ARG(ids && table && out && n > 0 && D % 8 == 0 && vocab > 0, "mmt_embedding_gather: args");
+  const int64_t t = n * (D / 8);
+  hipLaunchKernelGGL(embedding_gather_kernel, dim3((t + 255) / 256), dim3(256), 0,
+                     as_stream(stream), ids, n, D, (const bf16_t*)table, vocab, (bf16_t*)out);
+  MMT_CHECK_LAUNCH("mmt_embedding_gather");
+  return MMT_OK;
+}
+
+extern "C" int mmt_adamw(float* p, const float* g, float* m, float* v, void* shadow_bf16,
+                         int64_t n, const int32_t* state, float lr, float b1, float b2, float eps,
+                         float wd, float grad_scale, mmt_stream_t stream) {
+  MMT_CHECK_ARG(p && g && m && v && state && n > 0, "mmt_adamw: args");
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 256 * 8);
+  hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), p, g, m, v,
+                     (bf16_t*)shadow_bf16, n, state, lr, b1, b2, eps, wd, grad_scale);
+  MMT_CHECK_LAUNCH("mmt_adamw");
+  return MMT_OK;
+}
+
+extern "C" int mmt_cast_f32_bf16(const float* a, void* b, int64_t n, mmt_stream_t stream) {
+  MMT_CHECK_ARG(a && b && n > 0, "mmt_cast_f32_bf16: args");
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 256 * 8);
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), a,
+                     (bf16_t*)b, n);
+  MMT_CHECK_LAUNCH("mmt_cast_f32_bf16");
+  return MMT_OK;
+}
+
+extern "C" int mmt_step_advance(int32_t* state, mmt_stream_t stream) {
+  MMT_CHECK_ARG(state, "mmt_step_advance: null");
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(1), 0, as_stream(stream), state);
+  MMT_CHECK_LAUNCH("mmt_step_advance");
+  return MMT_OK;
+}

@@ -5,8 +5,13 @@
 // attention.py:58,66): statistics over the SEQUENCE axis per (batch, feature), fast variance
 // max(0, E[x^2] - E[x]^2), y = (x - mean) * (rsqrt(var + eps) * scale) + bias.
 // x is (B, L, D) token-major, so a column reduction over L: each workgroup owns 64 features of
-// one sample; 8 lanes x 16 B cover the 64 columns, 32 row groups stride over L (coalesced 128-B
-// row segments), partial sums meet in LDS. The second pass re-reads the 64-column panel (L2-hot).
+// one sample; 8 lanes x 8 elements cover the 64 columns, 32 row groups stride over L (coalesced
+// row segments), partial sums meet in LDS. The second pass re-reads the panel (L2-hot).
+//
+// Precision: a sequence-axis LayerNorm subtracts each feature's mean over the tokens, which in
+// this architecture is large next to the per-token deviations (attention outputs are averages
+// over the sequence). The residual stream x and its gradient are therefore fp32 (x_dtype /
+// res_dtype = MMT_F32 on the training path); y is emitted in bf16 for the MFMA GEMMs.
 #include "common.h"
 
 using namespace mmt;
@@ -17,7 +22,8 @@ constexpr int CW = 64;   // columns per workgroup
 constexpr int RG = 32;   // row groups
 constexpr int NT = 256;  // = 8 column vectors x RG
 
-__device__ __forceinline__ void unpack8(const uint4& u, float* f) {
+__device__ __forceinline__ void load8(const bf16_t* p, float* f) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
   const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -25,15 +31,23 @@ __device__ __forceinline__ void unpack8(const uint4& u, float* f) {
     f[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
   }
 }
-__device__ __forceinline__ uint4 pack8(const float* f) {
+__device__ __forceinline__ void load8(const float* p, float* f) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+  f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+__device__ __forceinline__ void store8(bf16_t* p, const float* f) {
   uint32_t w[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) w[q] = (uint32_t)f2bf(f[2 * q]) | ((uint32_t)f2bf(f[2 * q + 1]) << 16);
-  return make_uint4(w[0], w[1], w[2], w[3]);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ void store8(float* p, const float* f) {
+  *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
 }
 
-// Reduce NV per-thread vectors of 8 column partials over the RG row groups (LDS), result for
-// column (cv*8 + e) of quantity v in red[v][cv*8+e] after the call (row group 0 slot).
 template <int NV>
 __device__ __forceinline__ void reduce_rows(float (*part)[8], float* red /*[NV][RG][CW]*/) {
   const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;
@@ -51,8 +65,9 @@ __device__ __forceinline__ void reduce_rows(float (*part)[8], float* red /*[NV][
   __syncthreads();
 }
 
+template <typename TX>
 __global__ __launch_bounds__(NT) void seqnorm_fwd_kernel(
-    const bf16_t* __restrict__ x, int64_t xs_b, int64_t xs_t, int L, int D,
+    const TX* __restrict__ x, int64_t xs_b, int64_t xs_t, int L, int D,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     bf16_t* __restrict__ y, int64_t ys_b, int64_t ys_t, float* __restrict__ mean_out,
     float* __restrict__ rstd_out) {
@@ -62,12 +77,12 @@ __global__ __launch_bounds__(NT) void seqnorm_fwd_kernel(
   const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;
   const int col = c0 + cv * 8;
   const bool cok = col < D;
-  const bf16_t* xb = x + (int64_t)b * xs_b + col;
+  const TX* xb = x + (int64_t)b * xs_b + col;
   float part[2][8] = {};
   if (cok)
     for (int l = rg; l < L; l += RG) {
       float f[8];
-      unpack8(*reinterpret_cast<const uint4*>(xb + (int64_t)l * xs_t), f);
+      load8(xb + (int64_t)l * xs_t, f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         part[0][e] += f[e];
@@ -82,7 +97,7 @@ __global__ __launch_bounds__(NT) void seqnorm_fwd_kernel(
     const float rs = rsqrtf(var + eps);
     const float mul = rs * gamma[c];
     s_mul[threadIdx.x] = mul;
-    s_add[threadIdx.x] = beta[c] - mu * mul;  // (x - mu) * mul + beta
+    s_add[threadIdx.x] = beta[c] - mu * mul;
     mean_out[(int64_t)b * D + c] = mu;
     rstd_out[(int64_t)b * D + c] = rs;
   }
@@ -97,20 +112,22 @@ __global__ __launch_bounds__(NT) void seqnorm_fwd_kernel(
   bf16_t* yb = y + (int64_t)b * ys_b + col;
   for (int l = rg; l < L; l += RG) {
     float f[8];
-    unpack8(*reinterpret_cast<const uint4*>(xb + (int64_t)l * xs_t), f);
+    load8(xb + (int64_t)l * xs_t, f);
 #pragma unroll
     for (int e = 0; e < 8; ++e) f[e] = f[e] * mul[e] + add[e];
-    *reinterpret_cast<uint4*>(yb + (int64_t)l * ys_t) = pack8(f);
+    store8(yb + (int64_t)l * ys_t, f);
   }
 }
 
 // dx = rstd * (g - mean_L(g) - xhat * mean_L(g * xhat)),  g = dy * gamma  (+ optional addend)
 // dgamma += sum_{b,l} dy * xhat ; dbeta += sum_{b,l} dy   (fp32 atomics, one per column per block)
+// x, addend and dx share the residual dtype TX; dy has its own (TDY).
+template <typename TDY, typename TX>
 __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
-    const bf16_t* __restrict__ dy, int64_t ds_b, int64_t ds_t, const bf16_t* __restrict__ x,
+    const TDY* __restrict__ dy, int64_t ds_b, int64_t ds_t, const TX* __restrict__ x,
     int64_t xs_b, int64_t xs_t, int L, int D, const float* __restrict__ mean,
-    const float* __restrict__ rstd, const float* __restrict__ gamma, const bf16_t* addend,
-    int64_t as_b, int64_t as_t, bf16_t* dx, int64_t dxs_b, int64_t dxs_t,
+    const float* __restrict__ rstd, const float* __restrict__ gamma, const TX* addend,
+    int64_t as_b, int64_t as_t, TX* dx, int64_t dxs_b, int64_t dxs_t,
     float* __restrict__ dgamma, float* __restrict__ dbeta) {
   __shared__ float red[4 * RG * CW];
   const int b = blockIdx.x, c0 = blockIdx.y * CW;
@@ -124,14 +141,14 @@ __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
     rs[e] = cok ? rstd[(int64_t)b * D + col + e] : 0.f;
     ga[e] = cok ? gamma[col + e] : 0.f;
   }
-  const bf16_t* xb = x + (int64_t)b * xs_b + col;
-  const bf16_t* db = dy + (int64_t)b * ds_b + col;
+  const TX* xb = x + (int64_t)b * xs_b + col;
+  const TDY* db = dy + (int64_t)b * ds_b + col;
   float part[4][8] = {};  // sum g, sum g*xhat, sum dy*xhat, sum dy
   if (cok)
     for (int l = rg; l < L; l += RG) {
       float fx[8], fd[8];
-      unpack8(*reinterpret_cast<const uint4*>(xb + (int64_t)l * xs_t), fx);
-      unpack8(*reinterpret_cast<const uint4*>(db + (int64_t)l * ds_t), fd);
+      load8(xb + (int64_t)l * xs_t, fx);
+      load8(db + (int64_t)l * ds_t, fd);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float xh = (fx[e] - mu[e]) * rs[e];
@@ -154,27 +171,29 @@ __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
     mg[e] = red[cv * 8 + e] / L;
     mgx[e] = red[RG * CW + cv * 8 + e] / L;
   }
-  bf16_t* dxb = dx + (int64_t)b * dxs_b + col;
-  const bf16_t* ab = addend ? addend + (int64_t)b * as_b + col : nullptr;
+  TX* dxb = dx + (int64_t)b * dxs_b + col;
+  const TX* ab = addend ? addend + (int64_t)b * as_b + col : nullptr;
   for (int l = rg; l < L; l += RG) {
     float fx[8], fd[8], fa[8];
-    unpack8(*reinterpret_cast<const uint4*>(xb + (int64_t)l * xs_t), fx);
-    unpack8(*reinterpret_cast<const uint4*>(db + (int64_t)l * ds_t), fd);
-    if (ab) unpack8(*reinterpret_cast<const uint4*>(ab + (int64_t)l * as_t), fa);
+    load8(xb + (int64_t)l * xs_t, fx);
+    load8(db + (int64_t)l * ds_t, fd);
+    if (ab) load8(ab + (int64_t)l * as_t, fa);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float xh = (fx[e] - mu[e]) * rs[e];
       const float g = fd[e] * ga[e];
       fx[e] = rs[e] * (g - mg[e] - xh * mgx[e]) + (ab ? fa[e] : 0.f);
     }
-    *reinterpret_cast<uint4*>(dxb + (int64_t)l * dxs_t) = pack8(fx);
+    store8(dxb + (int64_t)l * dxs_t, fx);
   }
 }
 
-// out[n] += sum_m x[m][n]  and, with rng, dz = x * keep / keep_prob written to z first
-// (dropout backward of a GEMM-epilogue dropout; the column sum is then the bias gradient).
+// out[n] += sum_m x[m][n]  and, with z != NULL, z = x * keep / keep_prob (keep = 1 when rng is
+// NULL: a cast to bf16) written first — the dropout backward of a GEMM-epilogue dropout, whose
+// column sum is the bias gradient.
 constexpr int CS_ROWS = 256;
-__global__ __launch_bounds__(NT) void colsum_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+template <typename T>
+__global__ __launch_bounds__(NT) void colsum_kernel(const T* __restrict__ x, int64_t ldx,
                                                     int M, int N, float* __restrict__ out,
                                                     const uint32_t* __restrict__ rng,
                                                     uint32_t layer, uint32_t site, uint32_t thresh,
@@ -191,15 +210,15 @@ __global__ __launch_bounds__(NT) void colsum_kernel(const bf16_t* __restrict__ x
   if (cok)
     for (int m = r0 + rg; m < min(M, r0 + CS_ROWS); m += RG) {
       float f[8];
-      unpack8(*reinterpret_cast<const uint4*>(x + (int64_t)m * ldx + col), f);
+      load8(x + (int64_t)m * ldx + col, f);
       if (rng) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const uint32_t ctr = (uint32_t)((row_offset + m) * (int64_t)N + col + e);
           f[e] = keep_draw(key, ctr, thresh) ? f[e] * scale : 0.f;
         }
-        *reinterpret_cast<uint4*>(z + (int64_t)m * ldz + col) = pack8(f);
       }
+      if (z) store8(z + (int64_t)m * ldz + col, f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) part[0][e] += f[e];
     }
@@ -208,62 +227,93 @@ __global__ __launch_bounds__(NT) void colsum_kernel(const bf16_t* __restrict__ x
   if (threadIdx.x < CW && c0 + threadIdx.x < N) atomicAdd(out + c0 + threadIdx.x, red[threadIdx.x]);
 }
 
+inline bool is_dt(int d) { return d == MMT_F32 || d == MMT_BF16; }
+
 }  // namespace
 
-extern "C" int mmt_seqnorm_fwd(const void* x, int64_t xs_b, int64_t xs_t, int B, int L, int D,
-                               const float* gamma, const float* beta, float eps, void* y,
-                               int64_t ys_b, int64_t ys_t, float* mean, float* rstd,
+extern "C" int mmt_seqnorm_fwd(const void* x, int x_dtype, int64_t xs_b, int64_t xs_t, int B,
+                               int L, int D, const float* gamma, const float* beta, float eps,
+                               void* y, int64_t ys_b, int64_t ys_t, float* mean, float* rstd,
                                mmt_stream_t stream) {
   MMT_CHECK_ARG(x && y && gamma && beta && mean && rstd, "mmt_seqnorm_fwd: null pointer");
+  MMT_CHECK_ARG(is_dt(x_dtype), "mmt_seqnorm_fwd: x_dtype");
   MMT_CHECK_ARG(B > 0 && L > 0 && D > 0 && D % 8 == 0 && xs_t % 8 == 0 && ys_t % 8 == 0 &&
                     xs_b % 8 == 0 && ys_b % 8 == 0,
                 "mmt_seqnorm_fwd: D and strides must be multiples of 8");
   dim3 grid(B, (D + CW - 1) / CW);
-  hipLaunchKernelGGL(seqnorm_fwd_kernel, grid, dim3(NT), 0, as_stream(stream), (const bf16_t*)x,
-                     xs_b, xs_t, L, D, gamma, beta, eps, (bf16_t*)y, ys_b, ys_t, mean, rstd);
+  if (x_dtype == MMT_F32)
+    hipLaunchKernelGGL(seqnorm_fwd_kernel<float>, grid, dim3(NT), 0, as_stream(stream),
+                       (const float*)x, xs_b, xs_t, L, D, gamma, beta, eps, (bf16_t*)y, ys_b, ys_t,
+                       mean, rstd);
+  else
+    hipLaunchKernelGGL(seqnorm_fwd_kernel<bf16_t>, grid, dim3(NT), 0, as_stream(stream),
+                       (const bf16_t*)x, xs_b, xs_t, L, D, gamma, beta, eps, (bf16_t*)y, ys_b, ys_t,
+                       mean, rstd);
   MMT_CHECK_LAUNCH("mmt_seqnorm_fwd");
   return MMT_OK;
 }
 
-extern "C" int mmt_seqnorm_bwd(const void* dy, int64_t ds_b, int64_t ds_t, const void* x,
-                               int64_t xs_b, int64_t xs_t, int B, int L, int D, const float* mean,
-                               const float* rstd, const float* gamma, const void* addend,
-                               int64_t as_b, int64_t as_t, void* dx, int64_t dxs_b, int64_t dxs_t,
-                               float* dgamma, float* dbeta, mmt_stream_t stream) {
+extern "C" int mmt_seqnorm_bwd(const void* dy, int dy_dtype, int64_t ds_b, int64_t ds_t,
+                               const void* x, int x_dtype, int64_t xs_b, int64_t xs_t, int B,
+                               int L, int D, const float* mean, const float* rstd,
+                               const float* gamma, const void* addend, int64_t as_b, int64_t as_t,
+                               void* dx, int64_t dxs_b, int64_t dxs_t, float* dgamma, float* dbeta,
+                               mmt_stream_t stream) {
   MMT_CHECK_ARG(dy && x && mean && rstd && gamma && dx && dgamma && dbeta,
                 "mmt_seqnorm_bwd: null pointer");
+  MMT_CHECK_ARG(is_dt(dy_dtype) && is_dt(x_dtype), "mmt_seqnorm_bwd: dtypes");
   MMT_CHECK_ARG(B > 0 && L > 0 && D > 0 && D % 8 == 0 && ds_t % 8 == 0 && xs_t % 8 == 0 &&
                     dxs_t % 8 == 0 && (!addend || as_t % 8 == 0),
                 "mmt_seqnorm_bwd: D and strides must be multiples of 8");
   dim3 grid(B, (D + CW - 1) / CW);
-  hipLaunchKernelGGL(seqnorm_bwd_kernel, grid, dim3(NT), 0, as_stream(stream), (const bf16_t*)dy,
-                     ds_b, ds_t, (const bf16_t*)x, xs_b, xs_t, L, D, mean, rstd, gamma,
-                     (const bf16_t*)addend, as_b, as_t, (bf16_t*)dx, dxs_b, dxs_t, dgamma, dbeta);
+  hipStream_t s = as_stream(stream);
+#define SNB(TDY, TX)                                                                             \
+  hipLaunchKernelGGL((seqnorm_bwd_kernel<TDY, TX>), grid, dim3(NT), 0, s, (const TDY*)dy, ds_b, \
+                     ds_t, (const TX*)x, xs_b, xs_t, L, D, mean, rstd, gamma, (const TX*)addend,  \
+                     as_b, as_t, (TX*)dx, dxs_b, dxs_t, dgamma, dbeta)
+  if (dy_dtype == MMT_F32 && x_dtype == MMT_F32) SNB(float, float);
+  else if (dy_dtype == MMT_BF16 && x_dtype == MMT_F32) SNB(bf16_t, float);
+  else if (dy_dtype == MMT_F32 && x_dtype == MMT_BF16) SNB(float, bf16_t);
+  else SNB(bf16_t, bf16_t);
+#undef SNB
   MMT_CHECK_LAUNCH("mmt_seqnorm_bwd");
   return MMT_OK;
 }
 
-extern "C" int mmt_colsum(const void* x, int64_t ldx, int M, int N, float* out,
+extern "C" int mmt_colsum(const void* x, int dtype, int64_t ldx, int M, int N, float* out,
                           mmt_stream_t stream) {
-  MMT_CHECK_ARG(x && out && M > 0 && N > 0 && N % 8 == 0 && ldx % 8 == 0, "mmt_colsum: bad args");
+  MMT_CHECK_ARG(x && out && M > 0 && N > 0 && N % 8 == 0 && ldx % 8 == 0 && is_dt(dtype),
+                "mmt_colsum: bad args");
   dim3 grid((N + CW - 1) / CW, (M + CS_ROWS - 1) / CS_ROWS);
-  hipLaunchKernelGGL(colsum_kernel, grid, dim3(NT), 0, as_stream(stream), (const bf16_t*)x, ldx, M,
-                     N, out, nullptr, 0u, 0u, 0u, 1.f, (int64_t)0, nullptr, (int64_t)0);
+  if (dtype == MMT_F32)
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(NT), 0, as_stream(stream), (const float*)x,
+                       ldx, M, N, out, nullptr, 0u, 0u, 0u, 1.f, (int64_t)0, nullptr, (int64_t)0);
+  else
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(NT), 0, as_stream(stream),
+                       (const bf16_t*)x, ldx, M, N, out, nullptr, 0u, 0u, 0u, 1.f, (int64_t)0,
+                       nullptr, (int64_t)0);
   MMT_CHECK_LAUNCH("mmt_colsum");
   return MMT_OK;
 }
 
-extern "C" int mmt_dropout_bwd(const void* dy, int64_t ldy, int M, int N, const uint32_t* rng,
-                               uint32_t layer, uint32_t site, float keep_prob,
+extern "C" int mmt_dropout_bwd(const void* dy, int dtype, int64_t ldy, int M, int N,
+                               const uint32_t* rng, uint32_t layer, uint32_t site, float keep_prob,
                                int64_t row_offset, void* dz, int64_t ldz, float* colsum,
                                mmt_stream_t stream) {
-  MMT_CHECK_ARG(dy && dz && rng && M > 0 && N > 0 && N % 8 == 0 && ldy % 8 == 0 && ldz % 8 == 0,
+  MMT_CHECK_ARG(dy && dz && M > 0 && N > 0 && N % 8 == 0 && ldy % 8 == 0 && ldz % 8 == 0 &&
+                    is_dt(dtype),
                 "mmt_dropout_bwd: bad args");
   MMT_CHECK_ARG(keep_prob > 0.f && keep_prob <= 1.f, "mmt_dropout_bwd: keep_prob");
   dim3 grid((N + CW - 1) / CW, (M + CS_ROWS - 1) / CS_ROWS);
-  hipLaunchKernelGGL(colsum_kernel, grid, dim3(NT), 0, as_stream(stream), (const bf16_t*)dy, ldy, M,
-                     N, colsum, rng, layer, site, keep_threshold(keep_prob), 1.f / keep_prob,
-                     row_offset, (bf16_t*)dz, ldz);
+  const uint32_t th = rng ? keep_threshold(keep_prob) : 0u;
+  const float sc = rng ? 1.f / keep_prob : 1.f;
+  if (dtype == MMT_F32)
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(NT), 0, as_stream(stream), (const float*)dy,
+                       ldy, M, N, colsum, rng, layer, site, th, sc, row_offset, (bf16_t*)dz, ldz);
+  else
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(NT), 0, as_stream(stream),
+                       (const bf16_t*)dy, ldy, M, N, colsum, rng, layer, site, th, sc, row_offset,
+                       (bf16_t*)dz, ldz);
   MMT_CHECK_LAUNCH("mmt_dropout_bwd");
   return MMT_OK;
 }

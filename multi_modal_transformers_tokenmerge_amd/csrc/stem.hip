@@ -1,0 +1,339 @@
+// Gato-style image tokenizer (reference tokenizers/images/image_tokenizer.py) for gfx950:
+//   image_to_patches (:35-71) + normalisation 2*(x/255)-1        -> fused into patch_im2col
+//   encode_patch_position (:74-132)                              -> patch_positions
+//   ResNetV2Block stem (:140-178, model_configs/.../gato_resnet.yaml:41-104):
+//     Conv 12x12 s2 VALID (im2col here + MFMA GEMM) -> max_pool 3x3 s1 VALID (maxpool_patch)
+//     -> 2 x [GroupNorm(32, eps 1e-6) -> gelu(tanh) -> Conv 3x3 SAME] (groupnorm_gelu + GEMM)
+// At patch 16 the pooled map is 1 x 1, so each 3x3 SAME conv reduces to its centre tap (a
+// 64 x 64 Dense) and flatten is the identity; GroupNorm statistics span all images x patches x
+// (C / G) channels of a sample (flax GroupNorm reduces every non-batch axis).
+#include <math.h>
+
+#include "common.h"
+
+using namespace mmt;
+
+namespace {
+
+// One thread per (row, 8-element chunk) of the im2col matrix [rows][K], rows =
+// ((b*I + i)*NP + p)*OH*OW + oy*OW + ox, K = KH*KW*C in (ky, kx, c) order (Flax HWIO kernels).
+template <typename T>
+__global__ void patch_im2col_kernel(const T* __restrict__ img, int64_t s_img, int Himg, int C,
+                                    int P, int KH, int KW, int S, int OH, int OW, int64_t rows,
+                                    int K, bf16_t* __restrict__ out, float in_scale, float in_bias) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int kchunks = K / 8;
+  if (idx >= rows * kchunks) return;
+  const int64_t row = idx / kchunks;
+  const int k0 = (int)(idx - row * kchunks) * 8;
+  const int ox = row % OW, oy = (row / OW) % OH;
+  const int64_t pimg = row / ((int64_t)OH * OW);  // (b*I + i)*NP + p
+  const int PPD = Himg / P, NP = PPD * PPD;
+  const int p = pimg % NP;
+  const int64_t bi = pimg / NP;
+  const int py = p / PPD, px = p % PPD;  // raster order "(h p1) (w p2) -> (h w)"
+  const T* base = img + bi * s_img;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = k0 + e;
+    const int c = k % C, kx = (k / C) % KW, ky = k / (C * KW);
+    const int yy = py * P + oy * S + ky, xx = px * P + ox * S + kx;
+    const float raw = (float)base[((int64_t)yy * Himg + xx) * C + c];
+    v[e] = raw * in_scale + in_bias;
+  }
+  uint32_t w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) w[q] = (uint32_t)f2bf(v[2 * q]) | ((uint32_t)f2bf(v[2 * q + 1]) << 16);
+  *reinterpret_cast<uint4*>(out + row * K + k0) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// max over the `win` conv positions of each patch (3x3 window on a 3x3 map -> 1x1), per channel.
+__global__ void maxpool_patch_kernel(const float* __restrict__ conv, int64_t npatch, int win,
+                                     int C, float* __restrict__ pooled, uint8_t* __restrict__ arg) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= npatch * C) return;
+  const int64_t p = idx / C;
+  const int c = idx % C;
+  const float* src = conv + p * win * C + c;
+  float best = src[0];
+  int bi = 0;
+  for (int s = 1; s < win; ++s) {
+    const float v = src[(int64_t)s * C];
+    if (v > best) {  // first maximum wins (lax.reduce_window max: gradient to one input)
+      best = v;
+      bi = s;
+    }
+  }
+  pooled[idx] = best;
+  arg[idx] = (uint8_t)bi;
+}
+
+// G[p, s, c] = dpooled[p, c] if s == argmax(p, c) else 0 (bf16) -> dW_conv = G^T . im2col
+__global__ void maxpool_patch_bwd_kernel(const float* __restrict__ dpooled,
+                                         const uint8_t* __restrict__ arg, int64_t npatch, int win,
+                                         int C, bf16_t* __restrict__ G) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= npatch * win * C) return;
+  const int c = idx % C;
+  const int s = (idx / C) % win;
+  const int64_t p = idx / ((int64_t)C * win);
+  G[idx] = (arg[p * C + c] == s) ? f2bf(dpooled[p * C + c]) : (bf16_t)0;
+}
+
+__device__ __forceinline__ float gelu_tanh(float z) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * z * (1.f + tanhf(k0 * (z + k1 * z * z * z)));
+}
+__device__ __forceinline__ float gelu_tanh_grad(float z) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (z + k1 * z * z * z);
+  const float th = tanhf(u);
+  return 0.5f * (1.f + th) + 0.5f * z * (1.f - th * th) * k0 * (1.f + 3.f * k1 * z * z);
+}
+
+// GroupNorm + gelu forward over x (B, R, C) bf16: one workgroup per sample; stats per group of
+// C/G adjacent channels over all R rows. y = gelu((x - mu) * rstd * gamma + beta).
+constexpr int GN_NT = 256;
+__global__ __launch_bounds__(GN_NT) void groupnorm_gelu_fwd_kernel(
+    const float* __restrict__ x, int R, int C, int G, float eps, const float* __restrict__ gamma,
+    const float* __restrict__ beta, bf16_t* __restrict__ y, float* __restrict__ mean,
+    float* __restrict__ rstd) {
+  extern __shared__ float sh[];  // [2][GN_NT/64 waves][C] partials, then mu/rs per group
+  const int b = blockIdx.x;
+  const float* xb = x + (int64_t)b * R * C;
+  const int c = threadIdx.x % C;             // C divides GN_NT
+  const int rstep = GN_NT / C;
+  float s1 = 0.f, s2 = 0.f;
+  for (int r = threadIdx.x / C; r < R; r += rstep) {
+    const float v = xb[(int64_t)r * C + c];
+    s1 += v;
+    s2 += v * v;
+  }
+  float* p1 = sh;
+  float* p2 = sh + GN_NT;
+  p1[threadIdx.x] = s1;
+  p2[threadIdx.x] = s2;
+  __syncthreads();
+  float* gmu = sh + 2 * GN_NT;
+  float* grs = gmu + G;
+  if (threadIdx.x < G) {
+    const int cpg = C / G;
+    float a = 0.f, q = 0.f;
+    for (int t = 0; t < rstep; ++t)
+      for (int j = 0; j < cpg; ++j) {
+        a += p1[t * C + threadIdx.x * cpg + j];
+        q += p2[t * C + threadIdx.x * cpg + j];
+      }
+    const float n = (float)R * cpg;
+    const float mu = a / n;
+    const float var = fmaxf(0.f, q / n - mu * mu);
+    gmu[threadIdx.x] = mu;
+    grs[threadIdx.x] = rsqrtf(var + eps);
+    mean[b * G + threadIdx.x] = mu;
+    rstd[b * G + threadIdx.x] = grs[threadIdx.x];
+  }
+  __syncthreads();
+  const int g = c / (C / G);
+  const float mu = gmu[g], rs = grs[g], ga = gamma[c], be = beta[c];
+  bf16_t* yb = y + (int64_t)b * R * C;
+  for (int r = threadIdx.x / C; r < R; r += rstep) {
+    const float v = xb[(int64_t)r * C + c];
+    yb[(int64_t)r * C + c] = f2bf(gelu_tanh((v - mu) * rs * ga + be));
+  }
+}
+
+// Backward: dz = dy * gelu'(z); dxhat = dz * gamma; dx = rstd*(dxhat - mean(dxhat) -
+// xhat*mean(dxhat*xhat)) over the group; dgamma += sum dz*xhat; dbeta += sum dz. dx is ADDED
+// to `dx_accum` when accumulate != 0 (the residual branch of the stem).
+__global__ __launch_bounds__(GN_NT) void groupnorm_gelu_bwd_kernel(
+    const float* __restrict__ dy, const float* __restrict__ x, int R, int C, int G,
+    const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ mean, const float* __restrict__ rstd, float* dx, int accumulate,
+    float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  extern __shared__ float sh[];
+  const int b = blockIdx.x;
+  const float* xb = x + (int64_t)b * R * C;
+  const float* db = dy + (int64_t)b * R * C;
+  const int c = threadIdx.x % C;
+  const int rstep = GN_NT / C;
+  const int g = c / (C / G);
+  const float mu = mean[b * G + g], rs = rstd[b * G + g], ga = gamma[c], be = beta[c];
+  float a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f;  // sum dxhat, sum dxhat*xhat, sum dz*xhat, sum dz
+  for (int r = threadIdx.x / C; r < R; r += rstep) {
+    const float xh = (xb[(int64_t)r * C + c] - mu) * rs;
+    const float dz = db[(int64_t)r * C + c] * gelu_tanh_grad(xh * ga + be);
+    const float dxh = dz * ga;
+    a1 += dxh;
+    a2 += dxh * xh;
+    a3 += dz * xh;
+    a4 += dz;
+  }
+  float* p = sh;  // [4][GN_NT]
+  p[threadIdx.x] = a1;
+  p[GN_NT + threadIdx.x] = a2;
+  p[2 * GN_NT + threadIdx.x] = a3;
+  p[3 * GN_NT + threadIdx.x] = a4;
+  __syncthreads();
+  float* gm1 = sh + 4 * GN_NT;
+  float* gm2 = gm1 + G;
+  const int cpg = C / G;
+  if (threadIdx.x < G) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int t = 0; t < rstep; ++t)
+      for (int j = 0; j < cpg; ++j) {
+        s1 += p[t * C + threadIdx.x * cpg + j];
+        s2 += p[GN_NT + t * C + threadIdx.x * cpg + j];
+      }
+    const float n = (float)R * cpg;
+    gm1[threadIdx.x] = s1 / n;
+    gm2[threadIdx.x] = s2 / n;
+  }
+  if (threadIdx.x < C) {
+    float s3 = 0.f, s4 = 0.f;
+    for (int t = 0; t < rstep; ++t) {
+      s3 += p[2 * GN_NT + t * C + threadIdx.x];
+      s4 += p[3 * GN_NT + t * C + threadIdx.x];
+    }
+    atomicAdd(dgamma + threadIdx.x, s3);
+    atomicAdd(dbeta + threadIdx.x, s4);
+  }
+  __syncthreads();
+  const float m1 = gm1[g], m2 = gm2[g];
+  float* dxb = dx + (int64_t)b * R * C;
+  for (int r = threadIdx.x / C; r < R; r += rstep) {
+    const int64_t o = (int64_t)r * C + c;
+    const float xh = (xb[o] - mu) * rs;
+    const float dz = db[o] * gelu_tanh_grad(xh * ga + be);
+    float v = rs * (dz * ga - m1 - xh * m2);
+    if (accumulate) v += dxb[o];
+    dxb[o] = v;
+  }
+}
+
+// encode_patch_position (image_tokenizer.py:74-132) for every (b, i, p):
+// interval [k*P, (k+1)*P) -> floor(idx / Himg * (Q - 1)) in fp32; "row" token from interval
+// p % PPD, "col" from p // PPD (the reference's transposed convention, :91-92, pinned by
+// tests/test_image_tokenizer.py:53). train: uniform integer in [start, stop) (randint; stop <=
+// start -> start), eval: (start + stop) // 2.
+__global__ void patch_positions_kernel(const uint32_t* __restrict__ rng, uint32_t site, int B,
+                                       int I, int Himg, int P, int Q, int train,
+                                       int64_t sample_offset, int32_t* __restrict__ row_tok,
+                                       int32_t* __restrict__ col_tok) {
+  const int PPD = Himg / P, NP = PPD * PPD;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)B * I * NP) return;
+  const int p = idx % NP;
+  const int64_t bi = idx / NP;
+  auto q = [&](int v) { return (int)floorf(((float)v / (float)Himg) * (float)(Q - 1)); };
+  const int ri = p % PPD, ci = p / PPD;
+  const int rs = q(ri * P), re = q((ri + 1) * P), cs = q(ci * P), ce = q((ci + 1) * P);
+  int rt, ct;
+  if (train) {
+    const uint32_t key = stream_key(rng[0], rng[1], 0xFFFFu, site);
+    const uint64_t g = (uint64_t)(sample_offset * I) * NP + idx;  // global (sample, image, patch)
+    const uint32_t u1 = draw_u32(key, (uint32_t)(2 * g)), u2 = draw_u32(key, (uint32_t)(2 * g + 1));
+    rt = re > rs ? rs + (int)(((uint64_t)u1 * (uint32_t)(re - rs)) >> 32) : rs;
+    ct = ce > cs ? cs + (int)(((uint64_t)u2 * (uint32_t)(ce - cs)) >> 32) : cs;
+  } else {
+    rt = (rs + re) / 2;
+    ct = (cs + ce) / 2;
+  }
+  row_tok[idx] = rt;
+  col_tok[idx] = ct;
+}
+
+}  // namespace
+
+extern "C" int mmt_patch_im2col(const void* img, int in_dtype, int B, int I, int Himg, int C,
+                                int P, int KH, int KW, int S, int normalize, void* out,
+                                mmt_stream_t stream) {
+  MMT_CHECK_ARG(img && out && B > 0 && I > 0 && Himg > 0 && C > 0 && P > 0, "mmt_patch_im2col: args");
+  MMT_CHECK_ARG(Himg % P == 0, "mmt_patch_im2col: image %d not divisible by patch %d (the "
+                "reference's resize branch image_tokenizer.py:54-59 is broken; rejected)", Himg, P);
+  MMT_CHECK_ARG(KH <= P && KW <= P && S > 0, "mmt_patch_im2col: kernel larger than patch");
+  const int OH = (P - KH) / S + 1, OW = (P - KW) / S + 1;
+  const int K = KH * KW * C;
+  MMT_CHECK_ARG(K % 8 == 0, "mmt_patch_im2col: KH*KW*C must be a multiple of 8");
+  const int NP = (Himg / P) * (Himg / P);
+  const int64_t rows = (int64_t)B * I * NP * OH * OW;
+  const int64_t n = rows * (K / 8);
+  const float sc = normalize ? 2.f / 255.f : 1.f, bi = normalize ? -1.f : 0.f;
+  const int64_t s_img = (int64_t)Himg * Himg * C;
+  if (in_dtype == 2)  // uint8
+    hipLaunchKernelGGL(patch_im2col_kernel<uint8_t>, dim3((n + 255) / 256), dim3(256), 0,
+                       as_stream(stream), (const uint8_t*)img, s_img, Himg, C, P, KH, KW, S, OH,
+                       OW, rows, K, (bf16_t*)out, sc, bi);
+  else if (in_dtype == MMT_F32)
+    hipLaunchKernelGGL(patch_im2col_kernel<float>, dim3((n + 255) / 256), dim3(256), 0,
+                       as_stream(stream), (const float*)img, s_img, Himg, C, P, KH, KW, S, OH, OW,
+                       rows, K, (bf16_t*)out, sc, bi);
+  else
+    MMT_CHECK_ARG(false, "mmt_patch_im2col: dtype must be fp32 (0) or uint8 (2)");
+  MMT_CHECK_LAUNCH("mmt_patch_im2col");
+  return MMT_OK;
+}
+
+extern "C" int mmt_maxpool_patch(const void* conv, int64_t npatch, int win, int C, void* pooled,
+                                 uint8_t* argmax, mmt_stream_t stream) {
+  MMT_CHECK_ARG(conv && pooled && argmax && npatch > 0 && win > 0 && win <= 255 && C > 0,
+                "mmt_maxpool_patch: args");
+  const int64_t n = npatch * C;
+  hipLaunchKernelGGL(maxpool_patch_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream),
+                     (const float*)conv, npatch, win, C, (float*)pooled, argmax);
+  MMT_CHECK_LAUNCH("mmt_maxpool_patch");
+  return MMT_OK;
+}
+
+extern "C" int mmt_maxpool_patch_bwd(const void* dpooled, const uint8_t* argmax, int64_t npatch,
+                                     int win, int C, void* G, mmt_stream_t stream) {
+  MMT_CHECK_ARG(dpooled && argmax && G && npatch > 0 && win > 0 && C > 0, "mmt_maxpool_patch_bwd: args");
+  const int64_t n = npatch * win * C;
+  hipLaunchKernelGGL(maxpool_patch_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0,
+                     as_stream(stream), (const float*)dpooled, argmax, npatch, win, C, (bf16_t*)G);
+  MMT_CHECK_LAUNCH("mmt_maxpool_patch_bwd");
+  return MMT_OK;
+}
+
+extern "C" int mmt_groupnorm_gelu_fwd(const void* x, int B, int R, int C, int G, float eps,
+                                      const float* gamma, const float* beta, void* y, float* mean,
+                                      float* rstd, mmt_stream_t stream) {
+  MMT_CHECK_ARG(x && y && gamma && beta && mean && rstd && B > 0 && R > 0,
+                "mmt_groupnorm_gelu_fwd: args");
+  MMT_CHECK_ARG(C > 0 && GN_NT % C == 0 && G > 0 && C % G == 0, "mmt_groupnorm_gelu_fwd: C=%d G=%d", C, G);
+  const size_t sh = sizeof(float) * (2 * GN_NT + 2 * G);
+  hipLaunchKernelGGL(groupnorm_gelu_fwd_kernel, dim3(B), dim3(GN_NT), sh, as_stream(stream),
+                     (const float*)x, R, C, G, eps, gamma, beta, (bf16_t*)y, mean, rstd);
+  MMT_CHECK_LAUNCH("mmt_groupnorm_gelu_fwd");
+  return MMT_OK;
+}
+
+extern "C" int mmt_groupnorm_gelu_bwd(const void* dy, const void* x, int B, int R, int C, int G,
+                                      const float* gamma, const float* beta, const float* mean,
+                                      const float* rstd, void* dx, int accumulate, float* dgamma,
+                                      float* dbeta, mmt_stream_t stream) {
+  MMT_CHECK_ARG(dy && x && dx && gamma && beta && mean && rstd && dgamma && dbeta && B > 0,
+                "mmt_groupnorm_gelu_bwd: args");
+  MMT_CHECK_ARG(C > 0 && GN_NT % C == 0 && G > 0 && C % G == 0, "mmt_groupnorm_gelu_bwd: C/G");
+  const size_t sh = sizeof(float) * (4 * GN_NT + 2 * G);
+  hipLaunchKernelGGL(groupnorm_gelu_bwd_kernel, dim3(B), dim3(GN_NT), sh, as_stream(stream),
+                     (const float*)dy, (const float*)x, R, C, G, gamma, beta, mean, rstd,
+                     (float*)dx, accumulate, dgamma, dbeta);
+  MMT_CHECK_LAUNCH("mmt_groupnorm_gelu_bwd");
+  return MMT_OK;
+}
+
+extern "C" int mmt_patch_positions(const uint32_t* rng, uint32_t site, int B, int I, int Himg,
+                                   int P, int Q, int train, int64_t sample_offset, int32_t* row_tok,
+                                   int32_t* col_tok, mmt_stream_t stream) {
+  MMT_CHECK_ARG(row_tok && col_tok && B > 0 && I > 0 && P > 0 && Himg % P == 0 && Q > 1,
+                "mmt_patch_positions: args");
+  MMT_CHECK_ARG(!train || rng, "mmt_patch_positions: train mode needs the rng state");
+  const int NP = (Himg / P) * (Himg / P);
+  const int64_t n = (int64_t)B * I * NP;
+  hipLaunchKernelGGL(patch_positions_kernel, dim3((n + 255) / 256), dim3(256), 0,
+                     as_stream(stream), rng, site, B, I, Himg, P, Q, train, sample_offset, row_tok,
+                     col_tok);
+  MMT_CHECK_LAUNCH("mmt_patch_positions");
+  return MMT_OK;
+}

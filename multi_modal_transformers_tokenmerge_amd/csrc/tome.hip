@@ -424,7 +424,10 @@ extern "C" int mmt_tome_match(const void* metric, int dtype, int n, int t, int h
 #define LAUNCH(T, M)                                                                         \
   do {                                                                                       \
     auto kfn = tome_match_kernel<T, M>;                                                      \
-    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem); \
+    static const bool attr_set_ = (hipFuncSetAttribute((const void*)kfn,                    \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024), \
+                                   true);                                                    \
+    (void)attr_set_;                                                                         \
     hipLaunchKernelGGL(kfn, dim3(n), dim3(256), smem, s, (const T*)metric, t, heads, c, s_n, s_t, \
                        s_h, r, flags, unm_idx, src_idx, dst_idx, node_max);                  \
   } while (0)

@@ -1,0 +1,67 @@
+"""Dense and sequence-LayerNorm building blocks with explicit forward / backward on libmmt_hip.
+
+The training step is an explicit forward + reverse schedule of C-ABI kernels (no torch autograd
+tape, no per-op Python allocation of gradients): each layer object declares its parameters in
+the flat ParamStore, ``fwd`` returns activations plus what its ``bwd`` needs, and ``bwd`` writes
+parameter gradients straight into the flat gradient buffer (split-K fp32 atomics for dW, column
+sums for biases) and returns the input gradient.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _kernels as K
+from .params import ParamStore, const, he_normal, normal
+
+DROP_ATTN, DROP_ATTN_OUT, DROP_MLP_HIDDEN, DROP_MLP_OUT = 0, 1, 2, 3  # dropout "sites" per layer
+
+
+def split_k_for(n_out: int, k_out: int, m_red: int) -> int:
+    """Split of the M-reduction of a weight-gradient GEMM so the launch fills the 256 CUs."""
+    tiles = math.ceil(n_out / 128) * math.ceil(k_out / 128)
+    want = max(1, math.ceil(512 / tiles))
+    return int(max(1, min(want, m_red // 256, 64)))
+
+
+class Dense:
+    """flax.linen.Dense (kernel (in, out) in Flax; stored here as W[out][in] so the forward is
+    the NT GEMM y = x W^T and the GEMM reads both operands along the reduction)."""
+
+    def __init__(self, store: ParamStore, name: str, in_f: int, out_f: int, use_bias: bool = True,
+                 kernel_init=None, bias_init=None):
+        self.in_f, self.out_f = in_f, out_f
+        self.w = store.add(f"{name}/kernel", (out_f, in_f), kernel_init or he_normal((in_f, out_f)))
+        self.b = store.add(f"{name}/bias", (out_f,), bias_init or normal(0.01)) if use_bias else None
+
+    def fwd(self, x2d: torch.Tensor, out=None, out_mode=K.OUT_BF16, **epi) -> torch.Tensor:
+        return K.gemm(x2d, self.w.bf16, trans_b=True, bias=self.b.data if self.b else None,
+                      out=out, out_mode=out_mode, **epi)
+
+    def bwd(self, dy2d: torch.Tensor, x2d: torch.Tensor, need_dx: bool = True,
+            bias_grad_done: bool = False, dx_out=None, **dx_epi):
+        M = dy2d.shape[0]
+        K.gemm(dy2d, x2d, trans_a=True, out=self.w.grad, out_mode=K.OUT_F32_ATOMIC,
+               split_k=split_k_for(self.out_f, self.in_f, M))
+        if self.b is not None and not bias_grad_done:
+            K.colsum(dy2d, self.b.grad)
+        if need_dx:
+            return K.gemm(dy2d, self.w.bf16, trans_b=False, out=dx_out, **dx_epi)
+        return None
+
+
+class SeqLayerNorm:
+    """flax.linen.LayerNorm(reduction_axes=[1], feature_axes=[-1]) (vanilla_decoder.yaml:5-13)."""
+
+    def __init__(self, store: ParamStore, name: str, D: int, eps: float = 1e-6):
+        self.eps = eps
+        self.scale = store.add(f"{name}/scale", (D,), const(1.0))
+        self.bias = store.add(f"{name}/bias", (D,), const(0.0))
+
+    def fwd(self, x):
+        return K.seqnorm_fwd(x, self.scale.data, self.bias.data, self.eps)
+
+    def bwd(self, dy, x, mean, rstd, addend=None, out=None):
+        return K.seqnorm_bwd(dy, x, mean, rstd, self.scale.data, self.scale.grad, self.bias.grad,
+                             addend=addend, out=out)

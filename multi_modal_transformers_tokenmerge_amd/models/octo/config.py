@@ -1,0 +1,73 @@
+"""OCTO configurations.
+
+The reference pins only ``model_configs/octo_base.yaml`` (D 768, 3 heads, 1 block, 280^2 images,
+patch 56) and reads keys its YAMLs do not define. BASELINE names OCTO-tiny/small/base,
+which the reference does not define; the sizes below are SURVEY §8.0's (upstream Octo ViT-t/s/b
+widths with the reference architecture and quirks).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field, replace
+from typing import Optional
+
+from ...tokenizers.text.t5_base import T5Config
+
+
+@dataclass
+class OctoConfig:
+    name: str = "octo-small"
+    token_embedding_dim: int = 384
+    num_heads: int = 6
+    mlp_dim: int = 1536
+    num_blocks: int = 12
+    image_size: tuple = (256, 256, 3)
+    patch_size: int = 16
+    position_interval: int = 128
+    input_sequence: str = "[TaskDescriptionPrefix{32}] [Image{256};Readout{4}]"
+    token_compression_sequence: Optional[str] = None
+    tokens_per_readout: int = 4
+    num_observation_blocks: int = 1
+    action_space_dim: int = 8
+    diffusion_steps: int = 32
+    dropout_rate: float = 0.1
+    attention_dropout_rate: float = 0.1
+    layer_norm_eps: float = 1e-6
+    t5: T5Config = field(default_factory=T5Config)
+    text_tokens: int = 32
+
+    @property
+    def tome_r(self) -> int:
+        if not self.token_compression_sequence:
+            return 0
+        import re
+        return max(int(x) for x in re.findall(r"\{(\d+)\}", self.token_compression_sequence))
+
+
+TOME16 = "[TaskDescriptionPrefix{0}] [Image{16};Readout{0}]"
+
+PRESETS = {
+    # configs[0]: CPU plumbing case (no text, 64^2, 1 step)
+    "octo-tiny": OctoConfig(name="octo-tiny", token_embedding_dim=192, num_heads=3, mlp_dim=768,
+                            image_size=(64, 64, 3), input_sequence="[Image{16};Readout{4}]",
+                            text_tokens=0),
+    # configs[1]: small, ToMe off
+    "octo-small": OctoConfig(),
+    # configs[2]: small, ToMe r=16 per block (BASELINE metric config)
+    "octo-small-tome16": OctoConfig(name="octo-small-tome16", token_compression_sequence=TOME16),
+    # configs[3]: base, 2 cameras, 2-step history
+    "octo-base-2cam": OctoConfig(
+        name="octo-base-2cam", token_embedding_dim=768, num_heads=12, mlp_dim=3072,
+        input_sequence="[TaskDescriptionPrefix{32}] [Image{256};Image{256};Readout{4}]*2",
+        num_observation_blocks=2),
+    # configs[4]: base hi-res 512^2, ToMe r=32 (bf16 here; the fp8 weight path is not built)
+    "octo-base-hires-tome32": OctoConfig(
+        name="octo-base-hires-tome32", token_embedding_dim=768, num_heads=12, mlp_dim=3072,
+        image_size=(512, 512, 3), input_sequence="[TaskDescriptionPrefix{32}] [Image{1024};Readout{4}]",
+        token_compression_sequence="[TaskDescriptionPrefix{0}] [Image{32};Readout{0}]"),
+}
+
+
+def get_config(name: str, **overrides) -> OctoConfig:
+    if name not in PRESETS:
+        raise KeyError(f"unknown config {name!r}; known: {sorted(PRESETS)}")
+    return replace(PRESETS[name], **overrides)

@@ -1,0 +1,271 @@
+"""OCTO model and diffusion training step, mirroring the reference's
+``multi_modal_transformers/models/octo/octo.py`` (Octo :55-198, generate_readouts :91-126,
+compute_diffusion_denoise_loss :139-145, diffusion_train_step :204-240, OCTOTrainState :326-332,
+create_octo_train_state :334-386).
+
+MI355X design of the step (SURVEY §3.1 call stack):
+  tokenizers  : frozen T5 (bf16 GEMM/attention kernels) -> Dense(768->D) [build addition for D!=768];
+                image stem kernels; device-drawn patch positions
+  sequence    : ONE fused kernel writes the token sequence (text | image + row/col emb | readout
+                embedding) + the learned position embedding; the blockwise mask is a token-set
+                table evaluated inside the attention kernel, never an (B, H, L, L) tensor
+  backbone    : StackedEncoder1DBlock with ToMe, explicit fwd/bwd (attention_blocks/attention.py)
+  head        : diffusion denoise loss (action_heads/diffusion.py)
+  optimizer   : one fused AdamW launch over the flat parameter buffer; device step counter
+Everything after the input upload is stream-ordered device work with no host sync, so the whole
+step is captured into a HIP graph and replayed (see OCTOTrainState.graphed_step).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ... import _C, _kernels as K
+from ...action_heads.diffusion import DiffusionActionHead
+from ...attention_blocks.attention import LayerCtx, StackedEncoder1DBlock
+from ...layers import Dense
+from ...params import ParamStore, he_normal, normal
+from ...tokenizers.images.image_tokenizer import ImageTokenizer
+from ...tokenizers.text.t5_base import T5Tokenizer
+from ...tokenizers.token_sequencer import Image, Readout, Text, TokenSequence
+from .config import OctoConfig, get_config
+
+KIND_TEXT, KIND_IMAGE, KIND_READOUT = 0, 1, 2
+
+
+class Octo:
+    """Reference octo.py:55-198. ``Octo(config, device)`` declares, initialises (seeded, Flax
+    initialisers) and uploads every parameter."""
+
+    def __init__(self, config: OctoConfig | str = "octo-small", device="cuda", seed: int = 0):
+        self.cfg = cfg = get_config(config) if isinstance(config, str) else config
+        self.device = torch.device(device)
+        D = cfg.token_embedding_dim
+        self.D = D
+        self.seq = TokenSequence(cfg.input_sequence, cfg.token_compression_sequence)
+        sets0 = self.seq.token_sequence
+        self.L0 = sum(ts.num_tokens for ts in sets0)
+        self.n_images = sum(isinstance(ts, Image) for ts in sets0)
+        self.n_text = sum(ts.num_tokens for ts in sets0 if isinstance(ts, Text))
+        self.n_readout = sum(ts.num_tokens for ts in sets0 if isinstance(ts, Readout))
+        self.has_text = self.n_text > 0
+        if self.has_text and cfg.text_tokens != self.n_text:
+            raise ValueError("text_tokens must equal the text set sizes of input_sequence")
+        store = self.store = ParamStore()
+        # ---- tokenizers
+        self.image_tokenizer = ImageTokenizer(store, "ImageTokenizer_0", cfg.image_size,
+                                              cfg.patch_size, True, cfg.position_interval, D)
+        NP = self.image_tokenizer.num_patches
+        for ts in sets0:
+            if isinstance(ts, Image) and ts.num_tokens != NP:
+                raise ValueError(f"Image set of {ts.num_tokens} tokens != {NP} patches")
+        self.text_proj = None
+        if self.has_text and cfg.t5.d_model != D:
+            self.text_proj = Dense(store, "TextProjection_0", cfg.t5.d_model, D)
+        self.readout_pe = store.add("AddPositionEmbedding_0/pos_embedding", (self.n_readout, D),
+                                    he_normal((1, self.n_readout, D)))
+        # ---- backbone (posembed_input of StackedEncoder1DBlock, attention.py:97-100)
+        self.pos_embed = store.add("StackedEncoder1DBlock_0/posembed_input/pos_embedding",
+                                   (self.L0, D), normal(0.02))
+        self.stack = StackedEncoder1DBlock(store, "StackedEncoder1DBlock_0", cfg.num_blocks, D,
+                                           cfg.num_heads, cfg.mlp_dim, cfg.layer_norm_eps,
+                                           cfg.dropout_rate, cfg.attention_dropout_rate)
+        # ---- head
+        self.head = DiffusionActionHead(store, "diffusion_action_head", D, cfg.action_space_dim,
+                                        cfg.diffusion_steps)
+        store.materialize(self.device, seed)
+        self.t5 = T5Tokenizer(cfg.t5).materialize(self.device, seed + 1) if self.has_text else None
+        self._build_tables()
+
+    # ------------------------------------------------------------------ static tables
+    def _build_tables(self):
+        cfg = self.cfg
+        NP = self.image_tokenizer.num_patches
+        row_src = []
+        ti = ii = ri = 0
+        for ts in self.seq.token_sequence:
+            for j in range(ts.num_tokens):
+                if isinstance(ts, Text):
+                    row_src.append((KIND_TEXT << 24) | (ti + j))
+                elif isinstance(ts, Image):
+                    row_src.append((KIND_IMAGE << 24) | (ii * NP + j))
+                else:
+                    row_src.append((KIND_READOUT << 24) | (ri + j))
+            if isinstance(ts, Text):
+                ti += ts.num_tokens
+            elif isinstance(ts, Image):
+                ii += 1
+            else:
+                ri += ts.num_tokens
+        self.row_src = torch.tensor(row_src, dtype=torch.int32, device=self.device)
+        # per-layer token-set tables (square masks) + ToMe set / r
+        self.layer_sets = []
+        for layer in range(cfg.num_blocks):
+            sets = self.seq.set_table(layer)
+            merged = [i for i, ts in enumerate(self.seq._parse(layer) if cfg.token_compression_sequence
+                                                else self.seq.token_sequence)
+                      if ts.tokens_compressed_per_layer > 0]
+            if len(merged) > 1:
+                raise NotImplementedError("ToMe on more than one token set per layer")
+            tome_set = merged[0] if merged else -1
+            r = 0
+            if tome_set >= 0:
+                r = self.seq._parse(layer)[tome_set].tokens_compressed_per_layer
+                t = sets.lens[tome_set]
+                if r > t // 2:
+                    raise ValueError(f"layer {layer}: ToMe r={r} exceeds t//2={t // 2}")
+            if any(sets.causal):
+                raise NotImplementedError("causal Text sets are not supported by the attention kernel yet")
+            self.layer_sets.append((sets, K.SetTable(sets.starts, sets.lens, sets.vis), tome_set, r))
+        final = self.seq.set_table(cfg.num_blocks) if cfg.token_compression_sequence else self.seq.set_table(0)
+        self.L_final = final.L
+        rows = [s + j for s, n, m in zip(final.starts, final.lens, final.modalities) if m == "readouts"
+                for j in range(n)]
+        self.readout_rows = torch.tensor(rows, dtype=torch.int32, device=self.device)
+        flag = np.full(self.L_final, -1, np.int32)
+        flag[rows] = np.arange(len(rows))
+        self.readout_flag = torch.from_numpy(flag).to(self.device)
+
+    def layer_ctxs(self, train: bool, rng, sample_offset: int) -> List[LayerCtx]:
+        return [LayerCtx(layer=i, sets=s, table=t, tome_set=ts, r=r, train=train, rng=rng,
+                         sample_offset=sample_offset)
+                for i, (s, t, ts, r) in enumerate(self.layer_sets)]
+
+    # ------------------------------------------------------------------ forward / backward
+    def generate_readouts(self, text_tokens, images, train=True, rng=None, sample_offset=0,
+                          positions=None):
+        """Reference :91-126. Returns the final sequence (B, L_final, D) and the saved state."""
+        B = images.shape[0]
+        D = self.D
+        st: Dict = dict(B=B, train=train, rng=rng, sample_offset=sample_offset)
+        txt, T = None, max(self.n_text, 1)
+        if self.has_text:
+            t5_out = self.t5(text_tokens)                                   # stop_gradient
+            st["t5_out"] = t5_out
+            if self.text_proj is not None:
+                txt = self.text_proj.fwd(t5_out.view(B * self.n_text, -1)).view(B, self.n_text, D)
+            else:
+                txt = t5_out
+        img_tok, (rt, ct), isv = self.image_tokenizer.forward(images, train, rng, sample_offset,
+                                                              positions)
+        st.update(img_sv=isv, rt=rt, ct=ct)
+        x0 = torch.empty((B, self.L0, D), dtype=torch.float32, device=images.device)  # fp32 residual
+        NI = img_tok.shape[1]
+        _C.call("mmt_seq_assemble_fwd", B, self.L0, D, _C.ptr(self.row_src), _C.ptr(txt), T,
+                _C.ptr(img_tok), NI, _C.ptr(rt), _C.ptr(ct), _C.ptr(self.image_tokenizer.row_emb.data),
+                _C.ptr(self.image_tokenizer.col_emb.data), _C.ptr(self.readout_pe.data),
+                _C.ptr(self.pos_embed.data), _C.ptr(x0), _C.stream_ptr())
+        ctxs = self.layer_ctxs(train, rng, sample_offset)
+        xL, ssv = self.stack.forward(x0, ctxs)
+        st.update(ctxs=ctxs, stack_sv=ssv, NI=NI, T=T)
+        return xL, st
+
+    def compute_diffusion_denoise_loss(self, text_tokens, images, actions, train=True, rng=None,
+                                       sample_offset=0, inject: Optional[dict] = None):
+        """Reference :139-145. Returns (loss (1,) fp32 device tensor, saved state)."""
+        inject = inject or {}
+        xL, st = self.generate_readouts(text_tokens, images, train, rng, sample_offset,
+                                        inject.get("positions"))
+        B = xL.shape[0]
+        cat = self.head.new_cat(B, xL.device)
+        _C.call("mmt_rows_mean_fwd", _C.ptr(xL), xL.stride(0), xL.stride(1), B, self.D,
+                _C.ptr(self.readout_rows), self.readout_rows.numel(),
+                _C.ptr(self.head.readout_slot(cat)), cat.stride(0), _C.stream_ptr())
+        loss, hsv = self.head.loss_forward(cat, actions, rng, sample_offset, inject.get("t"),
+                                           inject.get("eps"))
+        st.update(head_sv=hsv, xL_shape=tuple(xL.shape))
+        return loss, st
+
+    def backward(self, st: Dict):
+        """Reverse schedule of compute_diffusion_denoise_loss; writes every parameter gradient
+        into the flat gradient buffer (which must be zeroed before the forward)."""
+        B = st["B"]
+        D = self.D
+        de = self.head.loss_backward(st["head_sv"])
+        dxL = torch.empty(st["xL_shape"], dtype=torch.float32, device=de.device)
+        _C.call("mmt_rows_mean_bwd", _C.ptr(de), de.stride(0), B, self.L_final, D,
+                _C.ptr(self.readout_flag), self.readout_rows.numel(), _C.ptr(dxL), _C.stream_ptr())
+        dx0 = self.stack.backward(dxL, st["stack_sv"], st["ctxs"])
+        NI, T = st["NI"], st["T"]
+        dimg = torch.empty((B, NI, D), dtype=torch.bfloat16, device=de.device)
+        dtxt = torch.empty((B, T, D), dtype=torch.bfloat16, device=de.device) if self.text_proj else None
+        it = self.image_tokenizer
+        _C.call("mmt_seq_assemble_bwd", B, self.L0, D, _C.ptr(self.row_src), _C.ptr(dx0),
+                _C.ptr(dtxt), T, _C.ptr(dimg), NI, _C.ptr(st["rt"]), _C.ptr(st["ct"]),
+                _C.ptr(it.row_emb.grad), _C.ptr(it.col_emb.grad), _C.ptr(self.readout_pe.grad),
+                _C.stream_ptr())
+        K.colsum(dx0.view(B, self.L0 * D), self.pos_embed.grad.view(-1))
+        it.backward(dimg, st["img_sv"])
+        if self.text_proj is not None:
+            self.text_proj.bwd(dtxt.view(B * T, D), st["t5_out"].view(B * T, -1), need_dx=False)
+
+    def num_params(self) -> int:
+        return self.store.num_params()
+
+
+# ---------------------------------------------------------------------- train state / step
+@dataclass
+class AdamW:
+    """The reference takes an optax tx from its caller (octo.py:341); this is optax.adamw with
+    these defaults (decoupled weight decay applied to every parameter, as optax without a mask)."""
+    learning_rate: float = 3e-4
+    b1: float = 0.9
+    b2: float = 0.999
+    eps: float = 1e-8
+    weight_decay: float = 1e-4
+
+
+@dataclass
+class OCTOTrainState:
+    """Reference octo.py:326-332: params (flat store), optimizer, rngs (device {seed, step}),
+    step, metrics (running loss average, clu.metrics.Average equivalent)."""
+    model: Octo
+    tx: AdamW
+    rng: torch.Tensor
+    allreduce: Optional[Callable] = None        # DDP gradient all-reduce (distributed.py)
+    sample_offset: int = 0
+    loss_sum: float = 0.0
+    loss_count: int = 0
+
+    @property
+    def params(self):
+        return self.model.store.state_dict()
+
+    @property
+    def step(self) -> int:
+        return int(self.rng[1].item())
+
+    def apply_gradients(self):
+        s = self.model.store
+        tx = self.tx
+        _C.call("mmt_adamw", _C.ptr(s.flat), _C.ptr(s.flat_grad), _C.ptr(s.m), _C.ptr(s.v),
+                _C.ptr(s.flat_bf16), s.flat.numel(), _C.ptr(self.rng), tx.learning_rate, tx.b1,
+                tx.b2, tx.eps, tx.weight_decay, getattr(self.allreduce, "grad_scale", 1.0),
+                _C.stream_ptr())
+        _C.call("mmt_step_advance", _C.ptr(self.rng), _C.stream_ptr())
+
+
+def create_octo_train_state(model: Octo, tx: AdamW | None = None, seed: int = 1234,
+                            allreduce=None, sample_offset: int = 0) -> OCTOTrainState:
+    """Reference octo.py:334-386 (parameters were initialised by Octo(...))."""
+    rng = torch.tensor([seed, 0], dtype=torch.int32, device=model.device)
+    return OCTOTrainState(model, tx or AdamW(), rng, allreduce, sample_offset)
+
+
+def diffusion_train_step(model: Octo, train_state: OCTOTrainState, text_tokens, images, actions,
+                         inject: Optional[dict] = None):
+    """Reference octo.py:204-240: value_and_grad of the denoise loss, then apply_gradients.
+    Returns (train_state, loss_tensor); gradients stay in model.store.flat_grad (views:
+    ``p.grad`` of every model.store parameter)."""
+    model.store.zero_grad()
+    loss, st = model.compute_diffusion_denoise_loss(text_tokens, images, actions, True,
+                                                    train_state.rng, train_state.sample_offset,
+                                                    inject)
+    model.backward(st)
+    if train_state.allreduce is not None:
+        train_state.allreduce(model.store.flat_grad)
+    train_state.apply_gradients()
+    return train_state, loss

@@ -1,0 +1,175 @@
+"""Flat parameter storage for the training path.
+
+Every trainable tensor is a view into ONE fp32 master buffer, with parallel flat buffers for its
+bf16 shadow (what the MFMA GEMMs read), its fp32 gradient (what the backward kernels accumulate
+into, zeroed by one memset per step) and the AdamW moments. Consequences on MI355X:
+  * the optimizer is one fused kernel launch over the whole model (mmt_adamw);
+  * the data-parallel gradient all-reduce runs on a few large contiguous buckets (RCCL over
+    xGMI) instead of hundreds of small tensors;
+  * no per-parameter allocation or autograd accumulation kernels exist on the hot path.
+Views are 64-element aligned (256 B) so every GEMM operand base is 16-B aligned.
+
+Frozen parameters (the T5 encoder, t5_base.py:14 stop_gradient) live in a separate bf16-only
+store: they have no master copy, no gradient and no optimizer state.
+
+Initialisers restate the Flax ones the reference's YAML names (he_normal = variance_scaling(2,
+fan_in, truncated_normal), normal(0.01) biases, LayerNorm ones/zeros, ...).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Tuple
+
+import torch
+
+ALIGN = 64
+
+
+def _fans(shape, in_axis=-2, out_axis=-1):
+    """flax.linen.initializers._compute_fans for a Flax-layout shape (..., in, out)."""
+    if len(shape) < 2:
+        return shape[0], shape[0]
+    rf = 1
+    for i, s in enumerate(shape):
+        if i not in (len(shape) + in_axis, len(shape) + out_axis):
+            rf *= s
+    return shape[in_axis] * rf, shape[out_axis] * rf
+
+
+def he_normal(flax_shape):
+    """variance_scaling(2.0, 'fan_in', 'truncated_normal') on the Flax kernel shape."""
+    fan_in, _ = _fans(flax_shape)
+    std = math.sqrt(2.0 / fan_in) / 0.87962566103423978
+
+    def init(t: torch.Tensor, g: torch.Generator):
+        with torch.no_grad():
+            t.copy_(torch.fmod(torch.randn(t.shape, generator=g), 2.0) * std)  # approx trunc at 2 sd
+        return t
+    return init
+
+
+def normal(std):
+    def init(t, g):
+        with torch.no_grad():
+            t.copy_(torch.randn(t.shape, generator=g) * std)
+        return t
+    return init
+
+
+def variance_scaling_normal(scale, flax_shape):
+    fan_in, _ = _fans(flax_shape)
+    return normal(math.sqrt(scale / fan_in))
+
+
+def const(v):
+    def init(t, g):
+        with torch.no_grad():
+            t.fill_(v)
+        return t
+    return init
+
+
+@dataclass
+class Param:
+    name: str
+    shape: Tuple[int, ...]
+    init: Callable
+    offset: int = -1
+    data: torch.Tensor | None = None      # fp32 master view
+    bf16: torch.Tensor | None = None      # bf16 shadow view
+    grad: torch.Tensor | None = None      # fp32 grad view
+
+    @property
+    def numel(self):
+        return math.prod(self.shape)
+
+
+class ParamStore:
+    def __init__(self):
+        self.params: List[Param] = []
+        self.by_name: Dict[str, Param] = {}
+        self.n = 0
+        self.flat = self.flat_bf16 = self.flat_grad = self.m = self.v = None
+
+    def add(self, name: str, shape, init) -> Param:
+        if name in self.by_name:
+            raise KeyError(f"duplicate parameter {name}")
+        p = Param(name, tuple(int(s) for s in shape), init)
+        p.offset = self.n
+        self.n += (p.numel + ALIGN - 1) // ALIGN * ALIGN
+        self.params.append(p)
+        self.by_name[name] = p
+        return p
+
+    def materialize(self, device, seed: int = 0):
+        """Allocate the flat buffers, initialise every parameter deterministically on the host
+        (torch.Generator(seed), in declaration order) and upload once."""
+        g = torch.Generator().manual_seed(seed)
+        host = torch.zeros(self.n, dtype=torch.float32)
+        for p in self.params:
+            view = host[p.offset:p.offset + p.numel].view(p.shape)
+            p.init(view, g)
+        self.flat = host.to(device)
+        self.flat_bf16 = self.flat.to(torch.bfloat16)
+        self.flat_grad = torch.zeros_like(self.flat)
+        self.m = torch.zeros_like(self.flat)
+        self.v = torch.zeros_like(self.flat)
+        self._bind()
+        return self
+
+    def _bind(self):
+        for p in self.params:
+            sl = slice(p.offset, p.offset + p.numel)
+            p.data = self.flat[sl].view(p.shape)
+            p.bf16 = self.flat_bf16[sl].view(p.shape)
+            p.grad = self.flat_grad[sl].view(p.shape)
+
+    def zero_grad(self):
+        self.flat_grad.zero_()
+
+    def sync_shadow(self):
+        """Re-derive the bf16 shadow after the master was modified outside AdamW."""
+        self.flat_bf16.copy_(self.flat.to(torch.bfloat16))
+
+    def num_params(self) -> int:
+        return sum(p.numel for p in self.params)
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        return {p.name: p.data for p in self.params}
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor]):
+        for p in self.params:
+            p.data.copy_(sd[p.name].to(p.data.device, torch.float32).view(p.shape))
+        self.sync_shadow()
+
+
+class FrozenStore:
+    """bf16-only parameters (no grad, no optimizer state)."""
+
+    def __init__(self):
+        self.params: List[Param] = []
+        self.by_name: Dict[str, Param] = {}
+        self.n = 0
+        self.flat_bf16 = None
+
+    def add(self, name, shape, init) -> Param:
+        p = Param(name, tuple(int(s) for s in shape), init)
+        p.offset = self.n
+        self.n += (p.numel + ALIGN - 1) // ALIGN * ALIGN
+        self.params.append(p)
+        self.by_name[name] = p
+        return p
+
+    def materialize(self, device, seed: int = 0):
+        g = torch.Generator().manual_seed(seed)
+        host = torch.zeros(self.n, dtype=torch.float32)
+        for p in self.params:
+            p.init(host[p.offset:p.offset + p.numel].view(p.shape), g)
+        self.flat_bf16 = host.to(torch.bfloat16).to(device)
+        for p in self.params:
+            p.bf16 = self.flat_bf16[p.offset:p.offset + p.numel].view(p.shape)
+        return self
+
+    def num_params(self) -> int:
+        return sum(p.numel for p in self.params)
