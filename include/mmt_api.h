@@ -96,16 +96,20 @@ int mmt_tome_merge_wavg_bwd(const void* g_out, int dtype, int n, int L, int D, i
  *   transA = 0: A is [M][K] (lda >= K);  transA = 1: A is stored [K][M] (lda >= M)
  *   transB = 0: B is [K][N] (ldb >= N);  transB = 1: B is stored [N][K] (ldb >= K)
  * A, B bf16; contiguous dims and strides multiples of 8 elements, base pointers 16-B aligned.
- * c_mode: MMT_OUT_BF16 (store), MMT_OUT_F32 (C = epi + beta*C), MMT_OUT_F32_ATOMIC (C += alpha*acc,
- * the split-K / gradient-accumulation form; no other epilogue).
+ * c_mode: MMT_OUT_BF16 (store), MMT_OUT_F32 (C = epi + beta*C), MMT_OUT_F32_ACCUM (C += alpha*acc,
+ * the weight-gradient form; no other epilogue; with split_k > 1 the K range is split over
+ * workgroups writing fp32 partial slabs into `workspace` (>= split_k*M*N floats, 16-B aligned)
+ * which a second kernel sums into C — deterministic, no atomics).
  * Batched: blockIdx.z = batch index, with element strides sA, sB, sC.
+ * N, ldc and sC must be multiples of 8 (8-column vector epilogue); A, B, C 16-B aligned.
  * Epilogue order: v = alpha*acc + bias[n]; act; v *= (gate[m][n] > 0 ? gate_scale : 0);
- * dropout (keep iff mix32(key ^ mix32(ctr)) < keep_prob*2^32, ctr = (drop_row_offset + m)*N + n,
- * key = stream_key(rng[0], rng[1], drop_layer, drop_site); kept values scaled by 1/keep_prob —
- * flax.linen.Dropout semantics with a counter-based stream); v += residual[m][n].
+ * dropout (flax.linen.Dropout with a counter-based stream: element idx = (drop_row_offset + m)*N
+ * + n keeps iff the 16-bit half (idx & 1) of mix32(key ^ (idx >> 1)) < floor(keep_prob * 65536),
+ * key = stream_key(rng[0], rng[1], drop_layer, drop_site); kept values scaled by 1/keep_prob);
+ * v += residual[m][n] (bf16 or fp32 per res_dtype).
  */
 enum { MMT_ACT_NONE = 0, MMT_ACT_RELU = 1 };
-enum { MMT_OUT_BF16 = 0, MMT_OUT_F32 = 1, MMT_OUT_F32_ATOMIC = 2 };
+enum { MMT_OUT_BF16 = 0, MMT_OUT_F32 = 1, MMT_OUT_F32_ACCUM = 2 };
 
 typedef struct {
   const float* bias;          /* [N] fp32 or NULL */
@@ -125,7 +129,8 @@ typedef struct {
 
 int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t lda, const void* B,
              int transB, int64_t ldb, void* C, int c_mode, int64_t ldc, int batch, int64_t sA,
-             int64_t sB, int64_t sC, int split_k, const mmt_epilogue_t* epi, mmt_stream_t stream);
+             int64_t sB, int64_t sC, int split_k, const mmt_epilogue_t* epi, float* workspace,
+             int64_t ws_elems, mmt_stream_t stream);
 
 /* ------------------------------------------------------------------ attention
  * Blockwise-causal MHA replacing flax.linen.SelfAttention / dot_product_attention as the

@@ -104,7 +104,7 @@ def tome_merge_bwd(g_out: torch.Tensor, set_start: int, t: int, r: int, pos_map:
 
 
 # ------------------------------------------------------------------------------------ GEMM
-OUT_BF16, OUT_F32, OUT_F32_ATOMIC = 0, 1, 2
+OUT_BF16, OUT_F32, OUT_F32_ACCUM = 0, 1, 2
 ACT_NONE, ACT_RELU = 0, 1
 
 
@@ -142,7 +142,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
         raise ValueError(f"gemm inner dims differ: {K} vs {Kb}")
     odt = torch.bfloat16 if out_mode == OUT_BF16 else torch.float32
     if out is None:
-        out = (torch.zeros if out_mode == OUT_F32_ATOMIC else torch.empty)(
+        out = (torch.zeros if out_mode == OUT_F32_ACCUM else torch.empty)(
             (M, N), dtype=odt, device=a.device)
     if out.dtype != odt or tuple(out.shape) != (M, N) or out.stride(-1) != 1:
         raise ValueError("bad gemm output tensor")
@@ -154,9 +154,12 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
     if bias is not None and (bias.numel() != N or bias.dtype != torch.float32):
         raise ValueError("gemm bias must be fp32 [N]")
     e = _epi(**epi)
+    ws = None
+    if split_k > 1:  # fp32 partial slabs, summed into `out` by the library's reduce kernel
+        ws = torch.empty(split_k * M * N, dtype=torch.float32, device=a.device)
     _C.call("mmt_gemm", M, N, K, ptr(a), int(trans_a), a.stride(0), ptr(b), int(trans_b),
             b.stride(0), ptr(out), out_mode, out.stride(0), 1, 0, 0, 0, split_k,
-            _C.ctypes.byref(e), _C.stream_ptr())
+            _C.ctypes.byref(e), ptr(ws), 0 if ws is None else ws.numel(), _C.stream_ptr())
     return out
 
 

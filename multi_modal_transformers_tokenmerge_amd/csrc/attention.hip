@@ -519,7 +519,7 @@ __global__ void dropout_bits_kernel(const uint32_t* __restrict__ rng, uint32_t l
   uint32_t bits = 0;
   for (int j = 0; j < 32; ++j) {
     const int c = w * 32 + j;
-    if (c < cols && keep_draw(key, (uint32_t)((int64_t)r * cols + c), thresh)) bits |= 1u << j;
+    if (c < cols && keep_elem(key, (uint32_t)((int64_t)r * cols + c), thresh)) bits |= 1u << j;
   }
   out[idx] = bits;
 }
@@ -568,7 +568,7 @@ extern "C" int mmt_dropout_bits(const uint32_t* rng, uint32_t layer, uint32_t si
   const int words = (cols + 31) / 32;
   const int64_t n = (int64_t)rows * words;
   hipLaunchKernelGGL(dropout_bits_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream),
-                     rng, layer, site, rows, cols, words, keep_threshold(keep_prob), out);
+                     rng, layer, site, rows, cols, words, keep_threshold16(keep_prob), out);
   MMT_CHECK_LAUNCH("mmt_dropout_bits");
   return MMT_OK;
 }

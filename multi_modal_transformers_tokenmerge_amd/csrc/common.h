@@ -86,6 +86,21 @@ inline uint32_t keep_threshold(float keep_prob) {
   return t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
 }
 
+// Dropout keep decisions (every flax.linen.Dropout site of the path): element idx of a stream
+// keeps iff the 16-bit half (idx & 1) of mix32(key ^ (idx >> 1)) is < thresh16 =
+// floor(keep_prob * 65536). One mixer evaluation serves two elements (half the multiplies of
+// draw_u32); keep probability is exact to 2^-16.
+inline uint32_t keep_threshold16(float keep_prob) {
+  double t = (double)keep_prob * 65536.0;
+  return t >= 65536.0 ? 65536u : (uint32_t)t;
+}
+__host__ __device__ __forceinline__ uint32_t pair_draw(uint32_t key, uint32_t pair) {
+  return mix32(key ^ pair);
+}
+__host__ __device__ __forceinline__ bool keep_elem(uint32_t key, uint32_t idx, uint32_t thresh16) {
+  return ((pair_draw(key, idx >> 1) >> ((idx & 1u) << 4)) & 0xffffu) < thresh16;
+}
+
 // ---------------------------------------------------------------- wave helpers (wave64)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -11,6 +11,10 @@
 // M/N-contiguous tiles (the transposed operands of the backward GEMMs) are staged as they come
 // from HBM and read with the gfx950 transpose read ds_read_b64_tr_b16 — no transpose pass in HBM.
 // Register-staged double buffer (global loads of tile k+1 issued before the MFMAs of tile k).
+// Workgroups are remapped so the tiles sharing an A row-panel run on one XCD (shared L2).
+// Epilogue: the fp32 accumulator tile is staged through LDS and processed row-major, 8 columns
+// per thread, so bias / gate / residual loads and the C store are 16-32 B vector accesses.
+// Split-K writes fp32 partial slabs (plain stores) reduced by a second kernel — no atomics.
 #include "common.h"
 
 using namespace mmt;
@@ -26,11 +30,13 @@ constexpr int KC_STRIDE = BK + 8;   // K-contiguous tile [128][72] bf16 (144 B r
 constexpr int MC_STRIDE = BM + 8;   // M/N-contiguous tile [64][136] bf16 (272 B rows)
 constexpr int TILE_ELEMS = 128 * KC_STRIDE;  // >= 64 * MC_STRIDE
 constexpr int NTHREADS = 256;
+constexpr int CT_STRIDE = BN + 4;   // fp32 epilogue staging tile [128][132]
+static_assert(BM * CT_STRIDE * 4 <= 4 * TILE_ELEMS * 2, "epilogue tile must fit the LDS");
 
 struct Epi {
   const float* bias;
   int act;
-  uint32_t drop_layer, drop_site, keep_thresh;
+  uint32_t drop_layer, drop_site, keep_thresh16;
   float drop_scale;
   const uint32_t* rng;
   int64_t drop_row_offset;
@@ -102,14 +108,36 @@ __device__ __forceinline__ bf16x8 load_frag(const bf16_t* S, int rbase, int ks, 
   }
 }
 
-template <bool TA, bool TB, int OUT>  // OUT: 0 bf16 store, 1 fp32 store (beta), 2 fp32 atomic add
+__device__ __forceinline__ void ld8(const bf16_t* p, float* f) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f[2 * q] = __uint_as_float(w[q] << 16);
+    f[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void ld8(const float* p, float* f) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+// XCD-aware bijective remap: blocks b and b+8 share an XCD (round-robin dispatch), so give each
+// XCD a contiguous range of tile ids (guide §5.5 T1, bijective form). Speed only.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <bool TA, bool TB, int OUT>  // OUT: 0 bf16, 1 fp32 (C = epi + beta*C), 2 fp32 split-K slab
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
     const bf16_t* __restrict__ B, int64_t ldb, int64_t sB, void* __restrict__ Cv, int64_t ldc,
     int64_t sC, int split_k, int k_chunk, int tiles_n, Epi epi) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE_ELEMS];
   const int bz = blockIdx.z / split_k, ks_id = blockIdx.z - bz * split_k;
-  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x - tm * tiles_n;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = wg / tiles_n, tn = wg - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = ks_id * k_chunk, kend = min(K, kbeg + k_chunk);
   A += bz * sA;
@@ -167,45 +195,111 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(
     __syncthreads();
   }
 
-  // ---------------- epilogue
-  uint32_t key = 0;
-  if (epi.rng) key = stream_key(epi.rng[0], epi.rng[1], epi.drop_layer, epi.drop_site);
+  // ---------------- epilogue: stage the fp32 tile through LDS, then 8 columns per thread
+  float* Ct = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int a = 0; a < 2; ++a) {
+  for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int gc = n0 + wn * 64 + b * 32 + (lane & 31);
-      if (gc >= N) continue;
-      const float bias = epi.bias ? epi.bias[gc] : 0.f;
+    for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int gr = m0 + wm * 64 + a * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
-        if (gr >= M) continue;
-        float v = acc[a][b][q] * epi.alpha;
-        if (OUT == 2) {
-          atomicAdd(reinterpret_cast<float*>(Cv) + bz * sC + (int64_t)gr * ldc + gc, v);
-          continue;
-        }
-        v += bias;
-        if (epi.act == MMT_ACT_RELU) v = fmaxf(v, 0.f);
-        if (epi.gate) v *= (bf2f(epi.gate[(int64_t)gr * epi.ld_gate + gc]) > 0.f) ? epi.gate_scale : 0.f;
-        if (epi.rng) {
-          const uint32_t ctr = (uint32_t)((epi.drop_row_offset + gr) * (int64_t)N + gc);
-          v = keep_draw(key, ctr, epi.keep_thresh) ? v * epi.drop_scale : 0.f;
-        }
-        if (epi.residual) {
-          const int64_t ro = (int64_t)gr * epi.ld_res + gc;
-          v += epi.res_f32 ? reinterpret_cast<const float*>(epi.residual)[ro]
-                           : bf2f(reinterpret_cast<const bf16_t*>(epi.residual)[ro]);
-        }
-        if (OUT == 0) {
-          reinterpret_cast<bf16_t*>(Cv)[bz * sC + (int64_t)gr * ldc + gc] = f2bf(v);
-        } else {
-          float* cp = reinterpret_cast<float*>(Cv) + bz * sC + (int64_t)gr * ldc + gc;
-          *cp = epi.beta != 0.f ? v + epi.beta * *cp : v;
-        }
+        const int r = wm * 64 + a * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+        Ct[r * CT_STRIDE + wn * 64 + b * 32 + (lane & 31)] = acc[a][b][q];
+      }
+  __syncthreads();
+  uint32_t key = 0;
+  if (OUT != 2 && epi.rng) key = stream_key(epi.rng[0], epi.rng[1], epi.drop_layer, epi.drop_site);
+  const int c8 = (threadIdx.x & 15) * 8;
+  const int gc = n0 + c8;
+  if (gc >= N) return;  // N % 8 == 0: whole 8-column groups are in or out
+  float bias[8];
+  if (OUT != 2 && epi.bias) ld8(epi.bias + gc, bias);
+#pragma unroll 2
+  for (int r = threadIdx.x >> 4; r < BM; r += NTHREADS / 16) {
+    const int gr = m0 + r;
+    if (gr >= M) break;
+    float v[8];
+    {
+      const float4 p0 = *reinterpret_cast<const float4*>(Ct + r * CT_STRIDE + c8);
+      const float4 p1 = *reinterpret_cast<const float4*>(Ct + r * CT_STRIDE + c8 + 4);
+      v[0] = p0.x; v[1] = p0.y; v[2] = p0.z; v[3] = p0.w;
+      v[4] = p1.x; v[5] = p1.y; v[6] = p1.z; v[7] = p1.w;
+    }
+    if (OUT == 2) {  // split-K partial slab
+      float* cp = reinterpret_cast<float*>(Cv) + ks_id * sC + (int64_t)gr * ldc + gc;
+      *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      continue;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= epi.alpha;
+    if (epi.bias)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bias[e];
+    if (epi.act == MMT_ACT_RELU)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    if (epi.gate) {
+      float g[8];
+      ld8(epi.gate + (int64_t)gr * epi.ld_gate + gc, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= (g[e] > 0.f) ? epi.gate_scale : 0.f;
+    }
+    if (epi.rng) {
+      const uint32_t base = (uint32_t)((epi.drop_row_offset + gr) * (int64_t)N + gc);  // even
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const uint32_t d = pair_draw(key, (base + e) >> 1);
+        v[e] = ((d & 0xffffu) < epi.keep_thresh16) ? v[e] * epi.drop_scale : 0.f;
+        v[e + 1] = ((d >> 16) < epi.keep_thresh16) ? v[e + 1] * epi.drop_scale : 0.f;
       }
     }
+    if (epi.residual) {
+      float rr[8];
+      const int64_t ro = (int64_t)gr * epi.ld_res + gc;
+      if (epi.res_f32) ld8(reinterpret_cast<const float*>(epi.residual) + ro, rr);
+      else ld8(reinterpret_cast<const bf16_t*>(epi.residual) + ro, rr);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += rr[e];
+    }
+    if (OUT == 0) {
+      uint32_t w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[q] = (uint32_t)f2bf(v[2 * q]) | ((uint32_t)f2bf(v[2 * q + 1]) << 16);
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(Cv) + bz * sC + (int64_t)gr * ldc + gc) =
+          make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      float* cp = reinterpret_cast<float*>(Cv) + bz * sC + (int64_t)gr * ldc + gc;
+      if (epi.beta != 0.f) {
+        float o[8];
+        ld8(cp, o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += epi.beta * o[e];
+      }
+      *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+  }
+}
+
+// out[m][n] = beta * out[m][n] + alpha * sum_s slab[s][m][n]  (fp32, 4 columns per thread)
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int split, int M, int N,
+                                     float* __restrict__ out, int64_t ldo, float alpha, float beta) {
+  const int64_t n4 = (int64_t)M * N / 4;
+  const int64_t slab = (int64_t)M * N;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i * 4;
+    const int m = e / N, n = e % N;
+    float4 s = *reinterpret_cast<const float4*>(ws + e);
+    for (int k = 1; k < split; ++k) {
+      const float4 t = *reinterpret_cast<const float4*>(ws + k * slab + e);
+      s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    }
+    float4* op = reinterpret_cast<float4*>(out + (int64_t)m * ldo + n);
+    const float4 o = beta != 0.f ? *op : make_float4(0, 0, 0, 0);
+    *op = make_float4(beta * o.x + alpha * s.x, beta * o.y + alpha * s.y, beta * o.z + alpha * s.z,
+                      beta * o.w + alpha * s.w);
   }
 }
 
@@ -214,15 +308,19 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(
 extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t lda,
                         const void* B, int transB, int64_t ldb, void* C, int c_mode, int64_t ldc,
                         int batch, int64_t sA, int64_t sB, int64_t sC, int split_k,
-                        const mmt_epilogue_t* e, mmt_stream_t stream) {
+                        const mmt_epilogue_t* e, float* workspace, int64_t ws_elems,
+                        mmt_stream_t stream) {
   MMT_CHECK_ARG(A && B && C, "mmt_gemm: null pointer");
   MMT_CHECK_ARG(M > 0 && N > 0 && K > 0 && batch > 0 && split_k > 0, "mmt_gemm: bad shape");
-  MMT_CHECK_ARG(c_mode >= MMT_OUT_BF16 && c_mode <= MMT_OUT_F32_ATOMIC, "mmt_gemm: c_mode");
-  // 16-byte vector loads along the contiguous dimension of each operand
+  MMT_CHECK_ARG(c_mode >= MMT_OUT_BF16 && c_mode <= MMT_OUT_F32_ACCUM, "mmt_gemm: c_mode");
+  // 16-byte vector loads along the contiguous dimension of each operand; 8-column epilogue
   MMT_CHECK_ARG(((transA ? M : K) % 8 == 0) && lda % 8 == 0 && ((transB ? K : N) % 8 == 0) &&
-                    ldb % 8 == 0 && sA % 8 == 0 && sB % 8 == 0,
-                "mmt_gemm: contiguous dims/strides must be multiples of 8 (M=%d N=%d K=%d)", M, N, K);
-  MMT_CHECK_ARG(((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0), "mmt_gemm: A/B not 16B aligned");
+                    ldb % 8 == 0 && sA % 8 == 0 && sB % 8 == 0 && N % 8 == 0 && ldc % 8 == 0 &&
+                    sC % 8 == 0,
+                "mmt_gemm: N, contiguous dims and strides must be multiples of 8 (M=%d N=%d K=%d)",
+                M, N, K);
+  MMT_CHECK_ARG(((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && ((uintptr_t)C % 16 == 0),
+                "mmt_gemm: A/B/C not 16-byte aligned");
   MMT_CHECK_ARG(lda >= (transA ? M : K) && ldb >= (transB ? K : N) && ldc >= N,
                 "mmt_gemm: leading dimension too small");
   Epi epi{};
@@ -234,7 +332,7 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     epi.drop_layer = e->drop_layer;
     epi.drop_site = e->drop_site;
     MMT_CHECK_ARG(!e->rng || (e->keep_prob > 0.f && e->keep_prob <= 1.f), "mmt_gemm: keep_prob");
-    epi.keep_thresh = e->rng ? keep_threshold(e->keep_prob) : 0u;
+    epi.keep_thresh16 = e->rng ? keep_threshold16(e->keep_prob) : 65536u;
     epi.drop_scale = e->rng ? 1.f / e->keep_prob : 1.f;
     epi.drop_row_offset = e->drop_row_offset;
     epi.gate = (const bf16_t*)e->gate;
@@ -245,24 +343,43 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     epi.ld_res = e->ld_res;
     epi.alpha = e->alpha;
     epi.beta = e->beta;
-    MMT_CHECK_ARG(c_mode != MMT_OUT_F32_ATOMIC || (!e->bias && !e->act && !e->rng && !e->gate &&
-                                                   !e->residual),
-                  "mmt_gemm: atomic (split-K) output takes no epilogue besides alpha");
+    MMT_CHECK_ARG((!e->gate || (e->ld_gate % 8 == 0 && (uintptr_t)e->gate % 16 == 0)) &&
+                      (!e->residual || (e->ld_res % 8 == 0 && (uintptr_t)e->residual % 16 == 0)),
+                  "mmt_gemm: gate/residual must be 16-byte aligned with ld % 8 == 0");
+    MMT_CHECK_ARG(c_mode != MMT_OUT_F32_ACCUM || (!e->bias && !e->act && !e->rng && !e->gate &&
+                                                  !e->residual),
+                  "mmt_gemm: accumulate mode takes no epilogue besides alpha");
   }
-  MMT_CHECK_ARG(split_k == 1 || c_mode == MMT_OUT_F32_ATOMIC, "mmt_gemm: split_k needs atomic output");
+  hipStream_t s = as_stream(stream);
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  int out_kind = c_mode == MMT_OUT_BF16 ? 0 : 1;
+  if (c_mode == MMT_OUT_F32_ACCUM) {
+    if (split_k == 1) {  // C += alpha * acc directly in the epilogue
+      epi.beta = 1.f;
+    } else {
+      MMT_CHECK_ARG(batch == 1, "mmt_gemm: split-K needs batch == 1");
+      MMT_CHECK_ARG(workspace && ws_elems >= (int64_t)split_k * M * N &&
+                        (uintptr_t)workspace % 16 == 0,
+                    "mmt_gemm: split-K needs a 16-B aligned workspace of split_k*M*N floats");
+      out_kind = 2;
+    }
+  } else {
+    MMT_CHECK_ARG(split_k == 1, "mmt_gemm: split_k > 1 needs MMT_OUT_F32_ACCUM");
+  }
   int k_chunk = ((K + split_k - 1) / split_k + BK - 1) / BK * BK;
   dim3 grid(tiles_m * tiles_n, 1, batch * split_k);
-  hipStream_t s = as_stream(stream);
+  void* Cdst = out_kind == 2 ? (void*)workspace : C;
+  const int64_t ldd = out_kind == 2 ? (int64_t)N : ldc;
+  const int64_t sdd = out_kind == 2 ? (int64_t)M * N : sC;
 #define GL(TA, TB, OUT)                                                                            \
   hipLaunchKernelGGL((gemm_kernel<TA, TB, OUT>), grid, dim3(NTHREADS), 0, s, M, N, K,             \
-                     (const bf16_t*)A, lda, sA, (const bf16_t*)B, ldb, sB, C, ldc, sC, split_k, \
-                     k_chunk, tiles_n, epi)
-#define GL_OUT(TA, TB)                            \
-  do {                                            \
-    if (c_mode == MMT_OUT_BF16) GL(TA, TB, 0);    \
-    else if (c_mode == MMT_OUT_F32) GL(TA, TB, 1); \
-    else GL(TA, TB, 2);                           \
+                     (const bf16_t*)A, lda, sA, (const bf16_t*)B, ldb, sB, Cdst, ldd, sdd,        \
+                     split_k, k_chunk, tiles_n, epi)
+#define GL_OUT(TA, TB)                          \
+  do {                                          \
+    if (out_kind == 0) GL(TA, TB, 0);           \
+    else if (out_kind == 1) GL(TA, TB, 1);      \
+    else GL(TA, TB, 2);                         \
   } while (0)
   if (!transA && transB) GL_OUT(false, true);
   else if (!transA && !transB) GL_OUT(false, false);
@@ -271,5 +388,12 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
 #undef GL_OUT
 #undef GL
   MMT_CHECK_LAUNCH("mmt_gemm");
+  if (out_kind == 2) {
+    const int64_t n4 = (int64_t)M * N / 4;
+    const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, workspace, split_k, M,
+                       N, (float*)C, ldc, epi.alpha, 1.f);
+    MMT_CHECK_LAUNCH("mmt_gemm(split-K reduce)");
+  }
   return MMT_OK;
 }

@@ -215,7 +215,7 @@ __global__ __launch_bounds__(NT) void colsum_kernel(const T* __restrict__ x, int
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const uint32_t ctr = (uint32_t)((row_offset + m) * (int64_t)N + col + e);
-          f[e] = keep_draw(key, ctr, thresh) ? f[e] * scale : 0.f;
+          f[e] = keep_elem(key, ctr, thresh) ? f[e] * scale : 0.f;
         }
       }
       if (z) store8(z + (int64_t)m * ldz + col, f);
@@ -305,7 +305,7 @@ extern "C" int mmt_dropout_bwd(const void* dy, int dtype, int64_t ldy, int M, in
                 "mmt_dropout_bwd: bad args");
   MMT_CHECK_ARG(keep_prob > 0.f && keep_prob <= 1.f, "mmt_dropout_bwd: keep_prob");
   dim3 grid((N + CW - 1) / CW, (M + CS_ROWS - 1) / CS_ROWS);
-  const uint32_t th = rng ? keep_threshold(keep_prob) : 0u;
+  const uint32_t th = rng ? keep_threshold16(keep_prob) : 0u;
   const float sc = rng ? 1.f / keep_prob : 1.f;
   if (dtype == MMT_F32)
     hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(NT), 0, as_stream(stream), (const float*)dy,

@@ -42,7 +42,7 @@ class Dense:
     def bwd(self, dy2d: torch.Tensor, x2d: torch.Tensor, need_dx: bool = True,
             bias_grad_done: bool = False, dx_out=None, **dx_epi):
         M = dy2d.shape[0]
-        K.gemm(dy2d, x2d, trans_a=True, out=self.w.grad, out_mode=K.OUT_F32_ATOMIC,
+        K.gemm(dy2d, x2d, trans_a=True, out=self.w.grad, out_mode=K.OUT_F32_ACCUM,
                split_k=split_k_for(self.out_f, self.in_f, M))
         if self.b is not None and not bias_grad_done:
             K.colsum(dy2d, self.b.grad)

@@ -38,8 +38,17 @@ def keep_thresh(keep_prob: float) -> int:
     return 0xFFFFFFFF if t >= 4294967295.0 else int(t)
 
 
-def keep_mask(key: int, ctr, keep_prob: float) -> np.ndarray:
-    return draw_u32(key, ctr) < np.uint64(keep_thresh(keep_prob))
+def keep_thresh16(keep_prob: float) -> int:
+    t = float(np.float32(keep_prob)) * 65536.0
+    return 65536 if t >= 65536.0 else int(t)
+
+
+def keep_mask(key: int, idx, keep_prob: float) -> np.ndarray:
+    """csrc/common.h keep_elem: 16-bit half (idx & 1) of mix32(key ^ (idx >> 1)) < thresh16."""
+    idx = np.asarray(idx, dtype=np.uint64) & M32
+    d = mix32(np.uint64(key) ^ (idx >> np.uint64(1)))
+    half = (d >> ((idx & np.uint64(1)) << np.uint64(4))) & np.uint64(0xFFFF)
+    return half < np.uint64(keep_thresh16(keep_prob))
 
 
 def dropout_mask_2d(seed, step, layer, site, rows: int, cols: int, row_offset: int, keep_prob: float):

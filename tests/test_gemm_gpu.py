@@ -83,7 +83,7 @@ def test_gemm_gate_and_beta_and_atomic_splitk(dev):
     # dW-style: A^T . B with split-K atomics over a long reduction
     x, dy = _mk((4096, 96), dev, g), _mk((4096, 160), dev, g)
     dw = torch.zeros(160, 96, device=dev)
-    Kn.gemm(dy, x, trans_a=True, out=dw, out_mode=Kn.OUT_F32_ATOMIC, split_k=8)
+    Kn.gemm(dy, x, trans_a=True, out=dw, out_mode=Kn.OUT_F32_ACCUM, split_k=8)
     ref = dy.float().t() @ x.float()
     torch.testing.assert_close(dw, ref, rtol=1e-4, atol=1e-3)
 

@@ -1,0 +1,62 @@
+"""Micro-benchmark of libmmt_hip's MFMA GEMM at the OCTO-small training-step shapes (B=64).
+Times each variant with HIP events on the launching stream; prints TFLOP/s."""
+import sys
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from multi_modal_transformers_tokenmerge_amd import _kernels as K
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(reps):
+        fn()
+    b.record(s)
+    b.synchronize()
+    return a.elapsed_time(b) / reps * 1e3  # us
+
+
+def main():
+    dev = torch.device("cuda")
+    rng = torch.tensor([7, 1], dtype=torch.int32, device=dev)
+    M1 = 64 * 276
+    cases = []
+    # (name, M, N, K, ta, tb, out_mode, epi)
+    for (M, N, Kd) in [(M1, 1536, 384), (M1, 384, 1536), (64 * 292, 1152, 384), (64 * 292, 384, 384),
+                       (4096, 4096, 4096)]:
+        cases.append(("fwd NT plain", M, N, Kd, False, True, K.OUT_BF16, {}))
+    cases.append(("fwd NT bias+relu+drop", M1, 1536, 384, False, True, K.OUT_BF16,
+                  dict(act=K.ACT_RELU, rng=rng, keep_prob=0.9)))
+    cases.append(("fwd NT f32 out + residual f32 + drop", M1, 384, 1536, False, True, K.OUT_F32,
+                  dict(rng=rng, keep_prob=0.9, residual="f32")))
+    cases.append(("dX NN plain", M1, 384, 1536, False, False, K.OUT_BF16, {}))
+    cases.append(("dX NN gate", M1, 1536, 384, False, False, K.OUT_BF16, dict(gate="bf16")))
+    cases.append(("dX NN f32", M1, 384, 1536, False, False, K.OUT_F32, {}))
+    cases.append(("dW TN splitK", 1536, 384, M1, True, False, K.OUT_F32_ACCUM, {}))
+    cases.append(("dW TN splitK", 384, 1536, M1, True, False, K.OUT_F32_ACCUM, {}))
+    cases.append(("dW TN splitK", 1152, 384, 64 * 292, True, False, K.OUT_F32_ACCUM, {}))
+    for name, M, N, Kd, ta, tb, om, epi in cases:
+        a = torch.randn((Kd, M) if ta else (M, Kd), device=dev).bfloat16()
+        b = torch.randn((N, Kd) if tb else (Kd, N), device=dev).bfloat16()
+        e = dict(epi)
+        if e.get("residual") == "f32":
+            e["residual"] = torch.randn((M, N), device=dev)
+        if e.get("gate") == "bf16":
+            e["gate"] = torch.randn((M, N), device=dev).bfloat16()
+        out = torch.zeros((M, N), device=dev, dtype=torch.bfloat16 if om == K.OUT_BF16 else torch.float32)
+        sk = 1
+        if om == K.OUT_F32_ACCUM:
+            from multi_modal_transformers_tokenmerge_amd.layers import split_k_for
+            sk = split_k_for(M, N, Kd)
+        us = timeit(lambda: K.gemm(a, b, ta, tb, out=out, out_mode=om, split_k=sk, **e))
+        print(f"{name:40s} M={M:6d} N={N:5d} K={Kd:6d} split={sk:2d}: {us:8.1f} us  {2*M*N*Kd/us/1e6:7.1f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
