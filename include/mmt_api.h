@@ -234,12 +234,14 @@ int mmt_seq_assemble_fwd(int B, int L, int D, const int32_t* row_src, const void
                          const void* img, int NI, const int32_t* rtok, const int32_t* ctok,
                          const float* row_emb, const float* col_emb, const float* readout_pe,
                          const float* pe, void* x0, mmt_stream_t stream);
-/* backward: gathers d(text), d(img) (bf16), accumulates d(row_emb), d(col_emb), d(readout_pe)
- * (fp32 atomics). d(pe) is mmt_colsum over the batch. */
+/* backward: gathers d(text), d(img) (bf16) from the fp32 dx0, accumulates d(readout_pe) and the
+ * (Q, D) row/col embedding gradients (LDS histograms per 64-column slice, then one global
+ * atomic per table entry). img_rows[j] = sequence row of image token j. d(pe) is mmt_colsum
+ * over the batch. */
 int mmt_seq_assemble_bwd(int B, int L, int D, const int32_t* row_src, const void* dx0,
                          void* dtext, int T, void* dimg, int NI, const int32_t* rtok,
-                         const int32_t* ctok, float* drow_emb, float* dcol_emb,
-                         float* dreadout_pe, mmt_stream_t stream);
+                         const int32_t* ctok, const int32_t* img_rows, int Q, float* drow_emb,
+                         float* dcol_emb, float* dreadout_pe, mmt_stream_t stream);
 /* readout gather + mean (octo.py:122-124, diffusion.py:102): out[b] = mean_i x[b, rows[i]]. */
 int mmt_rows_mean_fwd(const void* x, int64_t xs_b, int64_t xs_t, int B, int D,
                       const int32_t* rows, int nrows, void* out, int64_t ld_out,

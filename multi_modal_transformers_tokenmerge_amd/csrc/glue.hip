@@ -92,15 +92,52 @@ __global__ void seq_assemble_bwd_kernel(int B, int L, int D, const int32_t* __re
     if (dtext) *reinterpret_cast<uint4*>(dtext + ((int64_t)b * T + j) * D + d0) = pack8(v);
   } else if (kind == KIND_IMAGE) {
     *reinterpret_cast<uint4*>(dimg + ((int64_t)b * NI + j) * D + d0) = pack8(v);
-    const int rt = rtok[(int64_t)b * NI + j], ct = ctok[(int64_t)b * NI + j];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      atomicAdd(drow_emb + (int64_t)rt * D + d0 + e, v[e]);
-      atomicAdd(dcol_emb + (int64_t)ct * D + d0 + e, v[e]);
-    }
   } else {
 #pragma unroll
     for (int e = 0; e < 8; ++e) atomicAdd(dreadout_pe + (int64_t)j * D + d0 + e, v[e]);
+  }
+}
+
+// d(row_emb)[tok] += dx0[b, l(j)] over every image token (b, j) with rtok == tok (same for col).
+// One workgroup = 64 columns x a slice of the image tokens; the two (Q x 64) partial tables are
+// accumulated with LDS atomics and flushed with one global atomic per table entry.
+constexpr int EMB_COLS = 64, EMB_SPLIT = 128;
+__global__ __launch_bounds__(256) void embed_grad_kernel(int B, int L, int D, int NI, int Q,
+                                                         const int32_t* __restrict__ img_rows,
+                                                         const float* __restrict__ dx0,
+                                                         const int32_t* __restrict__ rtok,
+                                                         const int32_t* __restrict__ ctok,
+                                                         float* __restrict__ drow_emb,
+                                                         float* __restrict__ dcol_emb) {
+  extern __shared__ float tab[];  // [2][Q][EMB_COLS]
+  const int c0 = blockIdx.x * EMB_COLS;
+  for (int i = threadIdx.x; i < 2 * Q * EMB_COLS; i += blockDim.x) tab[i] = 0.f;
+  __syncthreads();
+  const int64_t total = (int64_t)B * NI;
+  const int64_t per = (total + gridDim.y - 1) / gridDim.y;
+  const int64_t r0 = blockIdx.y * per, r1 = min(total, r0 + per);
+  const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;  // 8 x 8 columns, 32 row groups
+  const int col = c0 + cv * 8;
+  if (col < D) {
+    for (int64_t rr = r0 + rg; rr < r1; rr += 32) {
+      const int b = rr / NI, j = rr % NI;
+      const float* gp = dx0 + ((int64_t)b * L + img_rows[j]) * D + col;
+      const float4 a = *reinterpret_cast<const float4*>(gp), c = *reinterpret_cast<const float4*>(gp + 4);
+      const float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+      const int rt = rtok[rr], ct = ctok[rr];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        atomicAdd(&tab[rt * EMB_COLS + cv * 8 + e], v[e]);
+        atomicAdd(&tab[(Q + ct) * EMB_COLS + cv * 8 + e], v[e]);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * Q * EMB_COLS; i += blockDim.x) {
+    const int which = i / (Q * EMB_COLS), rem = i % (Q * EMB_COLS);
+    const int tok = rem / EMB_COLS, cc = c0 + rem % EMB_COLS;
+    const float val = tab[i];
+    if (cc < D && val != 0.f) atomicAdd((which ? dcol_emb : drow_emb) + (int64_t)tok * D + cc, val);
   }
 }
 
@@ -307,14 +344,30 @@ extern "C" int mmt_seq_assemble_fwd(int B, int L, int D, const int32_t* row_src,
 
 extern "C" int mmt_seq_assemble_bwd(int B, int L, int D, const int32_t* row_src, const void* dx0,
                                     void* dtext, int T, void* dimg, int NI, const int32_t* rtok,
-                                    const int32_t* ctok, float* drow_emb, float* dcol_emb,
-                                    float* dreadout_pe, mmt_stream_t stream) {
+                                    const int32_t* ctok, const int32_t* img_rows, int Q,
+                                    float* drow_emb, float* dcol_emb, float* dreadout_pe,
+                                    mmt_stream_t stream) {
   MMT_CHECK_ARG(row_src && dx0 && D % 8 == 0 && B > 0 && L > 0, "mmt_seq_assemble_bwd: args");
+  MMT_CHECK_ARG(NI == 0 || (img_rows && rtok && ctok && drow_emb && dcol_emb && Q > 0 &&
+                            2 * Q * EMB_COLS * 4 <= 160 * 1024),
+                "mmt_seq_assemble_bwd: image embedding arguments");
   const int64_t n = (int64_t)B * L * (D / 8);
-  hipLaunchKernelGGL(seq_assemble_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0,
-                     as_stream(stream), B, L, D, row_src, (const float*)dx0, (bf16_t*)dtext, T,
-                     (bf16_t*)dimg, NI, rtok, ctok, drow_emb, dcol_emb, dreadout_pe);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(seq_assemble_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0, s, B, L, D,
+                     row_src, (const float*)dx0, (bf16_t*)dtext, T, (bf16_t*)dimg, NI, rtok, ctok,
+                     drow_emb, dcol_emb, dreadout_pe);
   MMT_CHECK_LAUNCH("mmt_seq_assemble_bwd");
+  if (NI > 0) {
+    const size_t sh = sizeof(float) * 2 * Q * EMB_COLS;
+    static const bool attr_ = (hipFuncSetAttribute((const void*)embed_grad_kernel,
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   160 * 1024), true);
+    (void)attr_;
+    hipLaunchKernelGGL(embed_grad_kernel, dim3((D + EMB_COLS - 1) / EMB_COLS, EMB_SPLIT), dim3(256),
+                       sh, s, B, L, D, NI, Q, img_rows, (const float*)dx0, rtok, ctok, drow_emb,
+                       dcol_emb);
+    MMT_CHECK_LAUNCH("mmt_seq_assemble_bwd(embedding grads)");
+  }
   return MMT_OK;
 }
 

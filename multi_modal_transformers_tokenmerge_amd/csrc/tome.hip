@@ -37,36 +37,60 @@ struct MatchSmem {
   int ta, tb, ta_pad, tb_pad, cs;
 };
 
-// One workgroup per batch row. LDS: a^ [ta_pad][c+1], b^ [tb_pad][c+1] fp32 + per-a-row arrays.
+constexpr int MATCH_NT = 512;  // 8 waves per batch row
+
+__device__ __forceinline__ void ld8f(const bf16_t* p, float* f) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f[2 * q] = __uint_as_float(w[q] << 16);
+    f[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void ld8f(const float* p, float* f) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+// One workgroup (8 waves) per batch row. LDS: a^ [ta_pad][c+1], b^ [tb_pad][c+1] fp32, per-a-row
+// node arrays and per-(b tile, a row) argmax partials [PJ][ta_pad].
 template <typename T, bool MFMA>
-__global__ __launch_bounds__(256) void tome_match_kernel(const T* __restrict__ metric, int t,
-                                                         int heads, int c, int64_t s_n,
-                                                         int64_t s_t, int64_t s_h, int r,
-                                                         int flags, int32_t* __restrict__ unm_idx,
-                                                         int32_t* __restrict__ src_idx,
-                                                         int32_t* __restrict__ dst_idx,
-                                                         float* __restrict__ node_max_out) {
+__global__ __launch_bounds__(MATCH_NT) void tome_match_kernel(const T* __restrict__ metric, int t,
+                                                              int heads, int c, int64_t s_n,
+                                                              int64_t s_t, int64_t s_h, int r,
+                                                              int flags, int vec,
+                                                              int32_t* __restrict__ unm_idx,
+                                                              int32_t* __restrict__ src_idx,
+                                                              int32_t* __restrict__ dst_idx,
+                                                              float* __restrict__ node_max_out) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int n = blockIdx.x;
   const int ta = (t + 1) / 2, tb = t / 2;
   const int ta_pad = (ta + 31) & ~31, tb_pad = (tb + 31) & ~31;
+  const int n_it = ta_pad / 32, n_jt = tb_pad / 32;
+  const int PJ = n_jt > 4 ? n_jt : 4;
   const int cs = c + 1;
   float* A = smem;                    // normalised even tokens (the reference's a = m[::2])
   float* Bm = A + ta_pad * cs;        // normalised odd tokens  (b = m[1::2])
   float* nmax = Bm + tb_pad * cs;     // node_max [ta_pad]
   int* nidx = (int*)(nmax + ta_pad);  // node_idx [ta_pad]
   int* edge = nidx + ta_pad;          // edge_idx [ta_pad]
-  float* pbest = (float*)(edge + ta_pad);  // VALU path partials [4][ta_pad]
-  int* pidx = (int*)(pbest + 4 * ta_pad);
+  float* pbest = (float*)(edge + ta_pad);  // argmax partials [PJ][ta_pad]
+  int* pidx = (int*)(pbest + PJ * ta_pad);
 
   const T* base = metric + (int64_t)n * s_n;
   const bool cls = flags & MMT_TOME_CLASS_TOKEN;
   const bool dis = flags & MMT_TOME_DISTILL_TOKEN;
   const int rows_total = ta_pad + tb_pad;
 
-  // Phase 1a: metric = sum over heads (fp32, h ascending), coalesced along c. Pad rows = 0.
-  for (int e = threadIdx.x; e < rows_total * c; e += blockDim.x) {
-    const int row = e / c, k = e - row * c;
+  // Phase 1a: metric = sum over heads (fp32, h ascending). Pad rows = 0. Vector path: 8
+  // contiguous c per work item, 16-B loads per head.
+  for (int i = threadIdx.x; i < PJ * ta_pad; i += blockDim.x) pidx[i] = -1;
+  const int cw = vec ? 8 : 1;
+  const int cchunks = c / cw;
+  for (int e = threadIdx.x; e < rows_total * cchunks; e += blockDim.x) {
+    const int row = e / cchunks, k = (e - row * cchunks) * cw;
     int tok;
     float* dstp;
     if (row < ta_pad) {
@@ -77,12 +101,27 @@ __global__ __launch_bounds__(256) void tome_match_kernel(const T* __restrict__ m
       tok = (j < tb) ? 2 * j + 1 : -1;
       dstp = Bm + j * cs + k;
     }
-    float acc = 0.f;
-    if (tok >= 0) {
-      const T* p = base + (int64_t)tok * s_t + k;
-      for (int h = 0; h < heads; ++h) acc = acc + ld_f32(p + (int64_t)h * s_h);
+    if (vec) {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (tok >= 0) {
+        const T* p = base + (int64_t)tok * s_t + k;
+        for (int h = 0; h < heads; ++h) {
+          float f[8];
+          ld8f(p + (int64_t)h * s_h, f);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc[q] = acc[q] + f[q];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) dstp[q] = acc[q];
+    } else {
+      float acc = 0.f;
+      if (tok >= 0) {
+        const T* p = base + (int64_t)tok * s_t + k;
+        for (int h = 0; h < heads; ++h) acc = acc + ld_f32(p + (int64_t)h * s_h);
+      }
+      *dstp = acc;
     }
-    *dstp = acc;
   }
   __syncthreads();
 
@@ -100,35 +139,34 @@ __global__ __launch_bounds__(256) void tome_match_kernel(const T* __restrict__ m
   }
   __syncthreads();
 
-  // Phase 2: scores = a^ b^T (fmaf chain over c ascending), node_max / node_idx per a row.
+  // Phase 2: scores = a^ b^T (fmaf chain over c ascending); per (b tile, a row) argmax partials.
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   if (MFMA) {
     // S^T tile (32 b rows x 32 a cols) = b^ . a^T with v_mfma_f32_32x32x2_f32, whose result is a
     // k-ordered fmaf chain (f32 in / f32 accumulate, one rounding per step). a row i is on the
-    // lane, b rows in the 16 accumulator registers: the argmax over j is lane-local.
-    const int n_it = ta_pad / 32, n_jt = tb_pad / 32;
-    for (int it = wave; it < n_it; it += nwaves) {
+    // lane, b rows in the 16 accumulator registers: the argmax over j is lane-local. The
+    // (a tile, b tile) pairs are spread over the 8 waves.
+    for (int pr = wave; pr < n_it * n_jt; pr += nwaves) {
+      const int it = pr / n_jt, jt = pr - it * n_jt;
       const int i = it * 32 + (lane & 31);
+      const float* bp = A + (it * 32 + (lane & 31)) * cs + (lane >> 5);
+      const float* ap = Bm + (jt * 32 + (lane & 31)) * cs + (lane >> 5);
+      floatx16 acc;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+      for (int s = 0; s < c / 2; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[2 * s], bp[2 * s], acc, 0, 0, 0);
       float best = 0.f;
       int bidx = -1;
-      const float* bp = A + (it * 32 + (lane & 31)) * cs + (lane >> 5);
-      for (int jt = 0; jt < n_jt; ++jt) {
-        floatx16 acc;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-        const float* ap = Bm + (jt * 32 + (lane & 31)) * cs + (lane >> 5);
-        for (int s = 0; s < c / 2; ++s)
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[2 * s], bp[2 * s], acc, 0, 0, 0);
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int jj = jt * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
-          if (jj >= tb) continue;
-          float v = acc[q];
-          if ((cls && i == 0) || (dis && jj == 0)) v = -INFINITY;
-          if (bidx < 0 || argmax_better(v, jj, best, bidx)) {
-            best = v;
-            bidx = jj;
-          }
+      for (int q = 0; q < 16; ++q) {
+        const int jj = jt * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+        if (jj >= tb) continue;
+        float v = acc[q];
+        if ((cls && i == 0) || (dis && jj == 0)) v = -INFINITY;
+        if (bidx < 0 || argmax_better(v, jj, best, bidx)) {
+          best = v;
+          bidx = jj;
         }
       }
       const float ov = __shfl_xor(best, 32, 64);
@@ -138,21 +176,20 @@ __global__ __launch_bounds__(256) void tome_match_kernel(const T* __restrict__ m
         bidx = oi;
       }
       if (lane < 32 && i < ta) {
-        nmax[i] = best;
-        nidx[i] = bidx;
+        pbest[jt * ta_pad + i] = best;
+        pidx[jt * ta_pad + i] = bidx;
       }
     }
   } else {
-    // VALU path: (a row, quarter of the b rows) per thread, sequential __fmaf_rn over c.
-    const int JC = 4;
-    const int cw = (tb + JC - 1) / JC;
-    for (int e = threadIdx.x; e < ta * JC; e += blockDim.x) {
-      const int i = e / JC, jc = e - i * JC;
+    // VALU path: (a row, one of PJ slices of the b rows) per thread, sequential __fmaf_rn.
+    const int cwj = (tb + PJ - 1) / PJ;
+    for (int e = threadIdx.x; e < ta * PJ; e += blockDim.x) {
+      const int i = e / PJ, jc = e - i * PJ;
       const float* ap = A + i * cs;
       float best = 0.f;
       int bidx = -1;
-      const int j1 = min(tb, (jc + 1) * cw);
-      for (int j = jc * cw; j < j1; ++j) {
+      const int j1 = min(tb, (jc + 1) * cwj);
+      for (int j = jc * cwj; j < j1; ++j) {
         const float* bq = Bm + j * cs;
         float acc = 0.f;
         for (int k = 0; k < c; ++k) acc = __fmaf_rn(ap[k], bq[k], acc);
@@ -165,21 +202,21 @@ __global__ __launch_bounds__(256) void tome_match_kernel(const T* __restrict__ m
       pbest[jc * ta_pad + i] = best;
       pidx[jc * ta_pad + i] = bidx;
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < ta; i += blockDim.x) {
-      float best = 0.f;
-      int bidx = -1;
-      for (int jc = 0; jc < JC; ++jc) {
-        const int oi = pidx[jc * ta_pad + i];
-        const float ov = pbest[jc * ta_pad + i];
-        if (oi >= 0 && (bidx < 0 || argmax_better(ov, oi, best, bidx))) {
-          best = ov;
-          bidx = oi;
-        }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < ta; i += blockDim.x) {  // combine the partials (order-free)
+    float best = 0.f;
+    int bidx = -1;
+    for (int jc = 0; jc < PJ; ++jc) {
+      const int oi = pidx[jc * ta_pad + i];
+      const float ov = pbest[jc * ta_pad + i];
+      if (oi >= 0 && (bidx < 0 || argmax_better(ov, oi, best, bidx))) {
+        best = ov;
+        bidx = oi;
       }
-      nmax[i] = best;
-      nidx[i] = bidx;
     }
+    nmax[i] = best;
+    nidx[i] = bidx;
   }
   __syncthreads();
 
@@ -397,7 +434,8 @@ __global__ __launch_bounds__(256) void tome_merge_bwd_kernel(
 size_t match_smem_bytes(int t, int c) {
   const int ta = (t + 1) / 2, tb = t / 2;
   const int ta_pad = (ta + 31) & ~31, tb_pad = (tb + 31) & ~31;
-  return sizeof(float) * ((size_t)(ta_pad + tb_pad) * (c + 1) + ta_pad * 3 + 8 * ta_pad);
+  const int PJ = tb_pad / 32 > 4 ? tb_pad / 32 : 4;
+  return sizeof(float) * ((size_t)(ta_pad + tb_pad) * (c + 1) + ta_pad * 3 + 2 * PJ * ta_pad);
 }
 
 bool g_match_use_mfma = true;
@@ -420,6 +458,9 @@ extern "C" int mmt_tome_match(const void* metric, int dtype, int n, int t, int h
   MMT_CHECK_ARG(smem <= 160 * 1024, "mmt_tome_match: t=%d c=%d needs %zu B of LDS (> 160 KiB)",
                 t, c, smem);
   const bool mfma = g_match_use_mfma && (c % 2 == 0);
+  const int vw = dtype == MMT_BF16 ? 8 : 4;  // elements per 16 B
+  const int vec = (c % 8 == 0) && (s_n % vw == 0) && (s_t % vw == 0) && (s_h % vw == 0) &&
+                  ((uintptr_t)metric % 16 == 0);
   hipStream_t s = as_stream(stream);
 #define LAUNCH(T, M)                                                                         \
   do {                                                                                       \
@@ -428,8 +469,8 @@ extern "C" int mmt_tome_match(const void* metric, int dtype, int n, int t, int h
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024), \
                                    true);                                                    \
     (void)attr_set_;                                                                         \
-    hipLaunchKernelGGL(kfn, dim3(n), dim3(256), smem, s, (const T*)metric, t, heads, c, s_n, s_t, \
-                       s_h, r, flags, unm_idx, src_idx, dst_idx, node_max);                  \
+    hipLaunchKernelGGL(kfn, dim3(n), dim3(MATCH_NT), smem, s, (const T*)metric, t, heads, c, s_n, \
+                       s_t, s_h, r, flags, vec, unm_idx, src_idx, dst_idx, node_max);       \
   } while (0)
   if (dtype == MMT_F32) {
     if (mfma) LAUNCH(float, true); else LAUNCH(float, false);

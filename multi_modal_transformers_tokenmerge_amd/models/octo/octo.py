@@ -101,6 +101,11 @@ class Octo:
             else:
                 ri += ts.num_tokens
         self.row_src = torch.tensor(row_src, dtype=torch.int32, device=self.device)
+        img_rows = np.zeros(ii * NP, np.int32)                 # image token -> sequence row
+        for row, v in enumerate(row_src):
+            if v >> 24 == KIND_IMAGE:
+                img_rows[v & 0xFFFFFF] = row
+        self.img_rows = torch.from_numpy(img_rows).to(self.device)
         # per-layer token-set tables (square masks) + ToMe set / r
         self.layer_sets = []
         for layer in range(cfg.num_blocks):
@@ -195,7 +200,7 @@ class Octo:
         it = self.image_tokenizer
         _C.call("mmt_seq_assemble_bwd", B, self.L0, D, _C.ptr(self.row_src), _C.ptr(dx0),
                 _C.ptr(dtxt), T, _C.ptr(dimg), NI, _C.ptr(st["rt"]), _C.ptr(st["ct"]),
-                _C.ptr(it.row_emb.grad), _C.ptr(it.col_emb.grad), _C.ptr(self.readout_pe.grad),
+                _C.ptr(self.img_rows), it.row_emb.grad.shape[0], _C.ptr(it.row_emb.grad), _C.ptr(it.col_emb.grad), _C.ptr(self.readout_pe.grad),
                 _C.stream_ptr())
         K.colsum(dx0.view(B, self.L0 * D), self.pos_embed.grad.view(-1))
         it.backward(dimg, st["img_sv"])
