@@ -107,6 +107,19 @@ def probe_dominant_gemm(model, B, reps=20):
                 tflops=flops / (avg_ms * 1e-3) / 1e12)
 
 
+def gemm_traffic(shape):
+    """HBM bytes per launch of the probe GEMM from the committed rocprofv3 PMC passes
+    (profiles/*_gemm_pmc.json, written by tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE,
+    the gfx950 correction of MI355X_MICROARCH.md "HBM"), or None when no pass matches."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_gemm_pmc.json")), reverse=True):
+        with open(f) as fh:
+            d = json.load(fh)
+        if list(d.get("shape_MNK", [])) == list(shape):
+            return d["hbm_bytes_per_launch"]
+    return None
+
+
 def cpu_baseline(cfg_name, model, budget_s=15.0, B=2):
     """fp32 CPU restatement (oracle/octo_ref.py) forward+backward+AdamW on a bounded sample."""
     from oracle.octo_ref import OctoRef, sequence_spec
@@ -157,6 +170,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--probe-only", action="store_true",
+                    help="only launch the dominant GEMM (for rocprofv3 --pmc traffic passes)")
     args = ap.parse_args()
 
     di = init_from_env()
@@ -168,6 +183,10 @@ def main():
     cfg = get_config(args.config)
     B = args.batch
     model = Octo(cfg, dev, seed=0)
+    if args.probe_only:
+        probe = probe_dominant_gemm(model, B, reps=50)
+        print(json.dumps(dict(probe_only=True, **probe)), flush=True)
+        return
     if di.enabled:  # identical initial parameters on every rank (broadcast from rank 0)
         dist.broadcast(model.store.flat, 0)
         model.store.sync_shadow()
@@ -249,9 +268,13 @@ def main():
         probe = probe_dominant_gemm(model, B)
         roof = dict(bound="mfma", achieved=round(probe["tflops"], 2), peak=MFMA_BF16_PEAK_TFLOPS,
                     unit="TFLOP/s", frac=round(probe["tflops"] / MFMA_BF16_PEAK_TFLOPS, 4),
-                    traffic=None, kernel=probe["kernel"], shape_MNK=probe["shape"],
+                    traffic=gemm_traffic(probe["shape"]), kernel=probe["kernel"], shape_MNK=probe["shape"],
                     avg_launch_us=round(probe["avg_us"], 2),
-                    flops_per_launch=probe["flops"])
+                    flops_per_launch=probe["flops"],
+                    algorithmic_bytes_per_launch=2 * (probe["shape"][0] * probe["shape"][2]
+                                                      + probe["shape"][1] * probe["shape"][2]
+                                                      + probe["shape"][0] * probe["shape"][1])
+                    + 4 * probe["shape"][1])
         fps = algorithmic_flops_per_sample(model)
         cpu = None
         if N == 1 and not args.no_cpu_baseline:
