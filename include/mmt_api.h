@@ -202,17 +202,19 @@ int mmt_dropout_bwd(const void* dy, int dtype, int64_t ldy, int M, int N, const 
 int mmt_patch_im2col(const void* img, int in_dtype, int B, int I, int Himg, int C, int P, int KH,
                      int KW, int S, int normalize, void* out, mmt_stream_t stream);
 /* max_pool over the `win` conv outputs of each patch (3x3 s1 VALID on the 3x3 map, :159) with
- * first-max argmax for the backward (bf16 conv [npatch][win][C] -> pooled [npatch][C]). */
+ * first-max argmax for the backward (fp32 conv [npatch][win][C] -> fp32 pooled [npatch][C]);
+ * the backward scatters fp32 dpooled into the bf16 conv-output gradient G [npatch][win][C]. */
 int mmt_maxpool_patch(const void* conv, int64_t npatch, int win, int C, void* pooled,
                       uint8_t* argmax, mmt_stream_t stream);
 int mmt_maxpool_patch_bwd(const void* dpooled, const uint8_t* argmax, int64_t npatch, int win,
                           int C, void* G, mmt_stream_t stream);
 /* flax GroupNorm(num_groups=G, eps) over every non-batch axis + gelu(tanh approx)
- * (gato_resnet.yaml:77-86, image_tokenizer.py:165-167): x (B, R, C) bf16. */
+ * (gato_resnet.yaml:77-86, image_tokenizer.py:165-167): x (B, R, C) fp32 -> y bf16 (the next
+ * conv's GEMM operand); statistics in fp32. */
 int mmt_groupnorm_gelu_fwd(const void* x, int B, int R, int C, int G, float eps,
                            const float* gamma, const float* beta, void* y, float* mean,
                            float* rstd, mmt_stream_t stream);
-/* backward; dx += result when accumulate != 0; dgamma/dbeta accumulated. */
+/* backward (dy, x, dx fp32); dx += result when accumulate != 0; dgamma/dbeta accumulated. */
 int mmt_groupnorm_gelu_bwd(const void* dy, const void* x, int B, int R, int C, int G,
                            const float* gamma, const float* beta, const float* mean,
                            const float* rstd, void* dx, int accumulate, float* dgamma,

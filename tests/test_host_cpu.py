@@ -1,0 +1,146 @@
+"""CPU tests of the host-side logic and the oracle's known-answer tests (no GPU needed).
+
+KAT-3 / KAT-4 restate the reference's own tests (tokenizers/images/tests/test_image_tokenizer.py
+:22-36 raster round trip, :41-53 eval position tokens); KAT-5 is the block mask of SURVEY §8c
+derived from token_sequencer.py:94-183.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import octo_ref as OR
+from oracle import rng as R
+
+
+# ----------------------------------------------------------------------------- KAT-4 patches
+def test_kat4_image_to_patches_raster_round_trip():
+    # 16 constant patches of 70x70x3 with values 1..16 assigned in raster order
+    patches = np.ones((16, 70, 70, 3), np.float32) * (np.arange(16, dtype=np.float32) + 1)[:, None, None, None]
+    image = patches.reshape(4, 4, 70, 70, 3).transpose(0, 2, 1, 3, 4).reshape(280, 280, 3)
+    out = OR.image_to_patches(image, 70, normalize=False)
+    assert out.shape == (16, 70, 70, 3)
+    np.testing.assert_array_equal(out, patches)
+    norm = OR.image_to_patches(np.full((32, 32, 3), 255.0, np.float32), 16, normalize=True)
+    np.testing.assert_allclose(norm, 1.0)
+
+
+# ----------------------------------------------------------------------------- KAT-3 positions
+def test_kat3_encode_patch_position_reference_case():
+    row, col = OR.encode_patch_position_eval(128, 1, 128)
+    assert row.shape == (128 * 128,) and col.shape == (128 * 128,)
+    assert row[123] == 122                      # test_image_tokenizer.py:53
+    # transposed convention (image_tokenizer.py:91-92): row token follows p % P, col p // P
+    p = np.arange(128 * 128)
+    np.testing.assert_array_equal(col, row[p // 128])
+    np.testing.assert_array_equal(row, row[p % 128])
+
+
+def test_kat3_encode_patch_position_small_geometry():
+    row, col = OR.encode_patch_position_eval(256, 16, 128)
+    p = np.arange(256)
+    np.testing.assert_array_equal(row, 3 + 8 * (p % 16))
+    np.testing.assert_array_equal(col, 3 + 8 * (p // 16))
+
+
+# ----------------------------------------------------------------------------- KAT-5 masks
+def _dense_from_table(sets):
+    L = sets.L
+    m = np.zeros((L, L), bool)
+    for i, (si, li) in enumerate(zip(sets.starts, sets.lens)):
+        for j, (sj, lj) in enumerate(zip(sets.starts, sets.lens)):
+            if sets.vis[i] >> j & 1:
+                m[si:si + li, sj:sj + lj] = True
+    return m
+
+
+def test_kat5_small_block_mask():
+    from multi_modal_transformers_tokenmerge_amd.tokenizers.token_sequencer import TokenSequence
+    seq = TokenSequence("[TaskDescriptionPrefix{32}] [Image{256};Readout{4}]")
+    sets = seq.set_table(0)
+    assert sets.lens == [32, 256, 4]
+    vis = [[sets.vis[i] >> j & 1 for j in range(3)] for i in range(3)]
+    assert vis == [[1, 0, 0], [1, 1, 0], [1, 1, 1]]
+    m = seq.generate_attention_mask(repeats=2)
+    assert m.shape == (2, 292, 292)
+    assert m[0].sum(1).min() > 0                  # no fully masked row
+
+
+CASES = [
+    ("[TaskDescriptionPrefix{32}] [Image{256};Readout{4}]", None, [0]),
+    ("[TaskDescriptionPrefix{32}] [Image{256};Readout{4}]",
+     "[TaskDescriptionPrefix{0}] [Image{16};Readout{0}]", [0, 1, 5, 11]),
+    ("[TaskDescriptionPrefix{32}] [Image{256};Image{256};Readout{4}]*2", None, [0]),
+    ("[Image{16};Readout{4}]", None, [0]),
+    ("[TaskDescriptionPrefix{16}] [Image{25};Readout{4}]*2", None, [0]),
+]
+
+
+@pytest.mark.parametrize("seq_str,comp,layers", CASES)
+def test_set_table_matches_literal_mask(seq_str, comp, layers):
+    from multi_modal_transformers_tokenmerge_amd.tokenizers.token_sequencer import TokenSequence
+    seq = TokenSequence(seq_str, comp)
+    spec = OR.sequence_spec(seq_str, comp)
+    for layer in layers:
+        sets = seq.set_table(layer)
+        lit = OR.literal_mask([(k, n - layer * c, t) for k, n, t, c in spec])
+        np.testing.assert_array_equal(_dense_from_table(sets), lit)
+        np.testing.assert_array_equal(seq.generate_attention_mask(layer=layer if comp else None,
+                                                                  square=True)[0], lit)
+
+
+def test_modality_idx_and_slices():
+    from multi_modal_transformers_tokenmerge_amd.tokenizers.token_sequencer import TokenSequence
+    seq = TokenSequence("[TaskDescriptionPrefix{32}] [Image{256};Readout{4}]*2")
+    np.testing.assert_array_equal(seq.get_modality_idx("readouts"),
+                                  np.r_[288:292, 548:552])
+    assert seq.slice_idx == [(0, 32), (0, 256), (0, 4), (256, 256), (4, 4)]
+
+
+# ----------------------------------------------------------------------------- diffusion
+def test_cosine_schedule_matches_oracle():
+    from multi_modal_transformers_tokenmerge_amd.action_heads.diffusion import (
+        alpha_hats_of, cosine_beta_schedule)
+    b = cosine_beta_schedule(32)
+    np.testing.assert_array_equal(b, OR.cosine_beta_schedule(32))
+    ah = alpha_hats_of(b)
+    assert ah.shape == (32,) and np.all(np.diff(ah) < 0) and 0 < ah[-1] < ah[0] <= 1
+    np.testing.assert_allclose(ah, np.cumprod(1 - b.astype(np.float64)), rtol=1e-6)
+
+
+# ----------------------------------------------------------------------------- RNG / sharding
+def test_dropout_streams_shard_by_global_sample():
+    """N ranks x B samples draw exactly the keep-masks of 1 rank x N*B (row offsets are global)."""
+    B, L, D, N = 3, 20, 64, 4
+    full = R.dropout_mask_2d(1234, 7, 2, 2, N * B * L, D, 0, 0.9)
+    for r in range(N):
+        part = R.dropout_mask_2d(1234, 7, 2, 2, B * L, D, r * B * L, 0.9)
+        np.testing.assert_array_equal(part, full[r * B * L:(r + 1) * B * L])
+    assert abs(full.mean() - 0.9) < 0.01
+
+
+def test_keep_threshold_edges():
+    assert R.keep_thresh16(1.0) == 65536 and R.keep_thresh16(0.0) == 0
+    assert R.keep_mask(R.stream_key(1, 0, 0, 0), np.arange(1000), 1.0).all()
+    assert not R.keep_mask(R.stream_key(1, 0, 0, 0), np.arange(1000), 0.0).any()
+
+
+# ----------------------------------------------------------------------------- fail loudly
+def test_product_ops_refuse_host_tensors():
+    from multi_modal_transformers_tokenmerge_amd.tokenizers.token_compression import (
+        bipartite_soft_matching)
+    with pytest.raises((ValueError, ImportError)):
+        bipartite_soft_matching(torch.randn(2, 16, 8), 4)
+    # r <= 0 is the reference's do-nothing tuple (token_compression.py:69-70), no kernel call
+    a, b = bipartite_soft_matching(torch.randn(2, 16, 8), 0)
+    x = torch.randn(2, 16, 8)
+    assert a(x) is x and b(x) is x
+
+
+# ----------------------------------------------------------------------------- T5 oracle pin
+def test_t5_oracle_matches_transformers_golden():
+    """oracle t5_encoder vs transformers.T5EncoderModel (tests/golden/make_t5_golden.py)."""
+    from pathlib import Path
+    g = np.load(Path(__file__).parent / "golden" / "t5_small_golden.npz")
+    tp = {k: torch.from_numpy(g[k]) for k in g.files if k.startswith("T5Tokenizer_0")}
+    out = OR.t5_encoder(tp, torch.from_numpy(g["ids"]), num_layers=2, H=4, d_kv=8)
+    np.testing.assert_allclose(out.numpy(), g["out"], rtol=1e-4, atol=1e-4 * np.abs(g["out"]).max())

@@ -1,0 +1,71 @@
+"""GPU: the frozen T5 encoder (HIP GEMMs + rmsnorm + bias-mode attention) against the
+transformers.T5EncoderModel golden fixture (tests/golden/make_t5_golden.py, d_kv = 64), and the
+patch-position tokens (a2) against the oracle's restatement of image_tokenizer.py:74-132.
+
+T5 tolerance: the HIP path multiplies bf16 weights with bf16 activations (fp32 accumulation), so
+the bar is against the oracle run on the same bf16-rounded weights: cosine >= 0.999 and max abs
+error <= 3e-2 x max|out|; against the fp32 golden itself cosine >= 0.995.
+"""
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import octo_ref as OR
+
+pytestmark = pytest.mark.gpu
+GOLD = Path(__file__).parent / "golden" / "t5_dkv64_golden.npz"
+
+
+def _cos(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float(a @ b / (a.norm() * b.norm()))
+
+
+def test_t5_encoder_vs_transformers_golden(dev):
+    from multi_modal_transformers_tokenmerge_amd.tokenizers.text.t5_base import T5Config, T5Tokenizer
+    g = np.load(GOLD)
+    cfg = T5Config(vocab_size=96, d_model=64, d_kv=64, d_ff=128, num_layers=2, num_heads=2)
+    t5 = T5Tokenizer(cfg).materialize(dev, seed=0)
+    for p in t5.store.params:
+        p.bf16.copy_(torch.from_numpy(g[p.name]).to(torch.bfloat16))
+    ids = torch.from_numpy(g["ids"]).to(dev)
+    out = t5(ids).float().cpu()
+    tp = {p.name: p.bf16.float().cpu() for p in t5.store.params}
+    ref_bf = OR.t5_encoder(tp, torch.from_numpy(g["ids"]), num_layers=2, H=2, d_kv=64)
+    gold = torch.from_numpy(g["out"])
+    assert _cos(out, ref_bf) >= 0.999
+    assert (out - ref_bf).abs().max() <= 3e-2 * ref_bf.abs().max()
+    assert _cos(out, gold) >= 0.995
+
+
+@pytest.mark.parametrize("H,P,Q", [(256, 16, 128), (128, 1, 128), (64, 16, 128), (280, 56, 128)])
+def test_patch_positions_eval_match_oracle(dev, H, P, Q):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    rt, ct = K.patch_positions(3, 2, H, P, Q, train=False, device=dev)
+    row, col = OR.encode_patch_position_eval(H, P, Q)
+    np.testing.assert_array_equal(rt.cpu().numpy(), np.tile(row, (3, 2)))
+    np.testing.assert_array_equal(ct.cpu().numpy(), np.tile(col, (3, 2)))
+    if (H, P) == (128, 1):
+        assert int(rt[0, 123]) == 122           # test_image_tokenizer.py:53
+
+
+def test_patch_positions_train_in_interval(dev):
+    """Train draws lie in [q(start), q(stop)) of their interval (image_tokenizer.py:103-108) and
+    are keyed by the global sample index: rank shards reproduce the single-batch draws."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    H, P, Q, B = 256, 16, 128, 8
+    rng = torch.tensor([1234, 3], dtype=torch.int32, device=dev)
+    rt, ct = K.patch_positions(B, 1, H, P, Q, train=True, rng=rng)
+    n = H // P
+    edges = np.floor(np.arange(0, H + P, P, dtype=np.float32) / np.float32(H) * np.float32(Q - 1)).astype(int)
+    p = np.arange(n * n)
+    lo_r, hi_r = edges[p % n], edges[p % n + 1]
+    lo_c, hi_c = edges[p // n], edges[p // n + 1]
+    r, c = rt.cpu().numpy(), ct.cpu().numpy()
+    assert ((r >= lo_r) & (r < hi_r)).all() and ((c >= lo_c) & (c < hi_c)).all()
+    assert len(np.unique(r)) > n                  # actually random within intervals
+    r2, c2 = K.patch_positions(B // 2, 1, H, P, Q, train=True, rng=rng, sample_offset=B // 2)
+    np.testing.assert_array_equal(r2.cpu().numpy(), r[B // 2:])
+    np.testing.assert_array_equal(c2.cpu().numpy(), c[B // 2:])

@@ -56,6 +56,17 @@ def main():
             sk = split_k_for(M, N, Kd)
         us = timeit(lambda: K.gemm(a, b, ta, tb, out=out, out_mode=om, split_k=sk, **e))
         print(f"{name:40s} M={M:6d} N={N:5d} K={Kd:6d} split={sk:2d}: {us:8.1f} us  {2*M*N*Kd/us/1e6:7.1f} TF/s", flush=True)
+    # library reference point (hipBLASLt through torch.matmul), plain bf16 output, same shapes
+    if "--torch" in sys.argv:
+        for (M, N, Kd, ta, tb) in [(M1, 1536, 384, False, True), (M1, 384, 1536, False, True),
+                                   (M1, 384, 1536, False, False), (1536, 384, M1, True, False),
+                                   (4096, 4096, 4096, False, True)]:
+            a = torch.randn((Kd, M) if ta else (M, Kd), device=dev).bfloat16()
+            b = torch.randn((N, Kd) if tb else (Kd, N), device=dev).bfloat16()
+            A = a.t() if ta else a
+            Bm = b.t() if tb else b
+            us = timeit(lambda: torch.matmul(A, Bm))
+            print(f"torch.matmul ta={ta:d} tb={tb:d}               M={M:6d} N={N:5d} K={Kd:6d}         : {us:8.1f} us  {2*M*N*Kd/us/1e6:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
