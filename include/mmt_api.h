@@ -151,17 +151,21 @@ int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, int L, int H,
                  const float* bias, void* o, int64_t o_s_b, int64_t o_s_t, float* lse,
                  mmt_stream_t stream);
 /* Backward: writes dq, dk, dv into dqkv (same row layout as qkv). delta: fp32 (B, H, L)
- * workspace (rowsum(dO * O)). */
+ * workspace (rowsum(dO * O)). drop_bits_t: the transposed keep mask (mmt_dropout_bits out_t);
+ * both or neither of drop_bits / drop_bits_t. */
 int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, int L, int H, int Dh,
                  float scale, int n_sets, const int32_t* set_start, const int32_t* set_len,
-                 const uint32_t* set_vis, const uint32_t* drop_bits, float keep_prob,
-                 const void* o, int64_t o_s_b, int64_t o_s_t, const void* dout, int64_t d_s_b,
-                 int64_t d_s_t, const float* lse, float* delta, void* dqkv, int64_t dq_s_b,
-                 int64_t dq_s_t, mmt_stream_t stream);
-/* Keep bitmask (rows, ceil(cols/32)) of a dropout stream: bit c of word (r, c/32) set iff
- * draw(key(rng, layer, site), r*cols + c) < keep_prob * 2^32. */
+                 const uint32_t* set_vis, const uint32_t* drop_bits, const uint32_t* drop_bits_t,
+                 float keep_prob, const void* o, int64_t o_s_b, int64_t o_s_t, const void* dout,
+                 int64_t d_s_b, int64_t d_s_t, const float* lse, float* delta, void* dqkv,
+                 int64_t dq_s_b, int64_t dq_s_t, mmt_stream_t stream);
+/* Keep bitmask (rows, ceil(cols/32)) of a dropout stream (flax Dropout keep-mask, broadcast over
+ * batch and heads for attention): bit c of word (r, c/32) set iff keep_elem(key(rng, layer,
+ * site), r*cols + c), i.e. the 16-bit half (idx & 1) of mix32(key ^ (idx >> 1)) is below
+ * floor(keep_prob * 65536). out_t (optional, rows == cols): the transposed mask, bit r of word
+ * (c, r/32). */
 int mmt_dropout_bits(const uint32_t* rng, uint32_t layer, uint32_t site, int rows, int cols,
-                     float keep_prob, uint32_t* out, mmt_stream_t stream);
+                     float keep_prob, uint32_t* out, uint32_t* out_t, mmt_stream_t stream);
 
 /* ------------------------------------------------------------------ sequence LayerNorm
  * flax.linen.LayerNorm(reduction_axes=[1], feature_axes=[-1], epsilon) as used in

@@ -185,10 +185,16 @@ class SetTable:
 
 def dropout_bits(rng: torch.Tensor, layer: int, site: int, rows: int, cols: int, keep_prob: float,
                  out: torch.Tensor | None = None):
+    """Keep bitmask words (rows, ceil(cols/32)) int32; for a square (attention) mask the result
+    is (2, L, W): [0] row-major, [1] transposed (what the dK/dV kernel reads)."""
     words = (cols + 31) // 32
+    square = rows == cols
     if out is None:
-        out = torch.empty((rows, words), dtype=torch.int32, device=rng.device)
-    _C.call("mmt_dropout_bits", ptr(rng), layer, site, rows, cols, keep_prob, ptr(out), _C.stream_ptr())
+        shape = (2, rows, words) if square else (rows, words)
+        out = torch.empty(shape, dtype=torch.int32, device=rng.device)
+    out_t = ptr(out[1]) if square else None
+    _C.call("mmt_dropout_bits", ptr(rng), layer, site, rows, cols, keep_prob,
+            ptr(out[0] if square else out), out_t, _C.stream_ptr())
     return out
 
 
@@ -214,6 +220,8 @@ def attn_fwd(qkv: torch.Tensor, H: int, scale: float, table: SetTable | None = N
     if out is None:
         out = torch.empty((B, L, H * Dh), dtype=torch.bfloat16, device=qkv.device)
     lse = torch.empty((B, H, L), dtype=torch.float32, device=qkv.device)
+    if drop_bits is not None and drop_bits.dim() == 3:
+        drop_bits = drop_bits[0]
     _C.call("mmt_attn_fwd", ptr(qkv), qkv.stride(0), qkv.stride(1), B, L, H, Dh, scale, t.n,
             t.starts, t.lens, t.vis, ptr(drop_bits), keep_prob, ptr(bias), ptr(out), out.stride(0),
             out.stride(1), ptr(lse), _C.stream_ptr())
@@ -230,8 +238,11 @@ def attn_bwd(qkv, o, dout, lse, H: int, scale: float, table: SetTable | None = N
     if dqkv is None:
         dqkv = torch.empty_like(qkv)
     delta = torch.empty((B, H, L), dtype=torch.float32, device=qkv.device)
+    if drop_bits is not None and (drop_bits.dim() != 3 or drop_bits.shape[0] != 2):
+        raise ValueError("attn_bwd needs the (2, L, W) mask of dropout_bits (row-major + transposed)")
+    bits, bits_t = (None, None) if drop_bits is None else (drop_bits[0], drop_bits[1])
     _C.call("mmt_attn_bwd", ptr(qkv), qkv.stride(0), qkv.stride(1), B, L, H, Dh, scale, t.n,
-            t.starts, t.lens, t.vis, ptr(drop_bits), keep_prob, ptr(o), o.stride(0), o.stride(1),
+            t.starts, t.lens, t.vis, ptr(bits), ptr(bits_t), keep_prob, ptr(o), o.stride(0), o.stride(1),
             ptr(dout), dout.stride(0), dout.stride(1), ptr(lse), ptr(delta), ptr(dqkv),
             dqkv.stride(0), dqkv.stride(1), _C.stream_ptr())
     return dqkv

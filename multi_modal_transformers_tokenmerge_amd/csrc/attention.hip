@@ -6,18 +6,23 @@
 //   logits = (q / sqrt(Dh)) . k ; where(mask, logits, finfo.min) ; softmax (fp32) ;
 //   attention dropout with ONE (L, L) keep-mask broadcast over batch and heads ; . v
 // The (B, H, L, L) logits are never materialised. The mask is not a tensor either: it is the
-// token-set table of the layer (set ranges + a bitmask of the key sets each query set sees), so
-// fully invisible key tiles are skipped. T5 mode: an additive fp32 (H, L, L) bias, scale 1.
+// token-set table of the layer (set ranges + a bitmask of the key sets each query set sees). Per
+// 64-wide tile every lane turns it into a 64-bit visibility word (a few range ops per set), so
+// masking costs two bit operations per score, and tiles no query of the block sees are skipped;
+// waves whose 32 rows lie past L skip the math. T5 mode: an additive fp32 (H, L, L) bias, scale 1.
 //
 // Layout: qkv rows (b, t) hold [q(H, Dh) | k(H, Dh) | v(H, Dh)] (the fused QKV GEMM output);
-// o rows (b, t) hold (H, Dh); lse / delta are (B, H, L) fp32.
+// o rows (b, t) hold (H, Dh); lse / delta are (B, H, L) fp32. Dropout keep bits: (L, W) words,
+// bit k of word (q, k/32); the backward also takes the transposed (L, W) words (bit q of
+// word (k, q/32)) so the key-on-lane dK/dV kernel reads one word per 32 queries.
 //
 // Forward and dQ: one wave = 32 queries ON THE LANES; S^T = K . Q^T so every score of a query is
 // lane-local (registers) and the row max / sum need one cross-half exchange; the S^T accumulator
 // is used directly as the B operand of O^T += V^T . P^T (no LDS round trip for P).
 // dK/dV: one wave = 32 keys on the lanes; S = Q . K^T and dP = dO . V^T accumulators feed
 // dV^T += dO^T . P and dK^T += Q^T . dS directly. V^T, dO^T, Q^T, K^T operands come from
-// row-major LDS tiles through ds_read_b64_tr_b16.
+// row-major LDS tiles through ds_read_b64_tr_b16. K/V (resp. Q/dO) tiles are double-buffered in
+// LDS and prefetched through registers one tile ahead: one barrier per tile.
 #include <math.h>
 
 #include "common.h"
@@ -34,7 +39,9 @@ namespace {
 constexpr int MAX_SETS = 16;
 constexpr int KT = 64;      // keys (or queries) per LDS tile
 constexpr int NT = 256;     // threads per workgroup (4 waves x 32 rows)
-constexpr int MAXL = 4096;  // LDS set-id table size
+constexpr int MAXL = 4096;
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
 
 struct AttnMask {
   int n_sets;
@@ -61,6 +68,37 @@ __device__ __forceinline__ bool tile_visible(const AttnMask& m, int q0, int q1, 
       return true;
   return false;
 }
+
+// first key tile >= k0 that queries [q0, q1) see (L if none)
+__device__ __forceinline__ int next_key_tile(const AttnMask& m, int q0, int q1, int k0, int L) {
+  for (; k0 < L; k0 += KT)
+    if (tile_visible(m, q0, q1, k0, min(L, k0 + KT))) return k0;
+  return L;
+}
+__device__ __forceinline__ int next_query_tile(const AttnMask& m, int k0, int k1, int q0, int L) {
+  for (; q0 < L; q0 += KT)
+    if (tile_visible(m, q0, min(L, q0 + KT), k0, k1)) return q0;
+  return L;
+}
+
+// Bits [t0, t0 + 64) of the positions covered by the sets selected in `sel`.
+__device__ __forceinline__ uint64_t sets_bits(const AttnMask& m, uint32_t sel, int t0) {
+  uint64_t r = 0;
+  for (int i = 0; i < m.n_sets; ++i) {
+    const int a = max(m.start[i] - t0, 0), e = min(m.start[i] + m.len[i] - t0, KT);
+    if (((sel >> i) & 1u) && a < e) {
+      const uint64_t hi = e >= 64 ? ~0ull : ((1ull << e) - 1ull);
+      r |= hi & ~((1ull << a) - 1ull);
+    }
+  }
+  return r;
+}
+
+// Bit of accumulator register r of this lane inside a 32-row word pre-shifted by 4*(lane>>5):
+// acc row(r) = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
+__device__ __forceinline__ constexpr int rbit(int r) { return (r & 3) + 8 * (r >> 2); }
+// all-ones if the bit is set, else 0
+__device__ __forceinline__ int bitmask_of(uint32_t w, int b) { return (int)(w << (31 - b)) >> 31; }
 
 __device__ __forceinline__ short4v tr_read(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -103,22 +141,33 @@ __device__ __forceinline__ bf16x8 pack_frag(const floatx16& x, int s) {
   return r;
 }
 
-__device__ __forceinline__ int acc_row(int reg, int lane) {
-  return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
-}
-
-// Cooperative copy of a KT x DH bf16 tile (rows r0.., clipped at L) into LDS [KT][DH+8].
+// Register-staged copy of two KT x DH bf16 tiles (rows r0.., zero past L) -> LDS [KT][DH+8].
 template <int DH>
-__device__ __forceinline__ void load_rows_to_lds(bf16_t* lds, const bf16_t* base, int64_t s_t,
-                                                 int r0, int L) {
-  constexpr int CPR = DH / 8;  // 16-B chunks per row
-  for (int c = threadIdx.x; c < KT * CPR; c += NT) {
-    const int row = c / CPR, ch = c % CPR;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r0 + row < L) v = *reinterpret_cast<const uint4*>(base + (int64_t)(r0 + row) * s_t + ch * 8);
-    *reinterpret_cast<uint4*>(lds + row * (DH + 8) + ch * 8) = v;
+struct TilePair {
+  static constexpr int CPR = DH / 8;            // 16-B chunks per row
+  static constexpr int PER = KT * CPR / NT;     // chunks per thread per tile
+  uint4 a[PER], b[PER];
+  __device__ __forceinline__ void load(const bf16_t* pa, int64_t sa, const bf16_t* pb, int64_t sb,
+                                       int r0, int L) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + i * NT, row = c / CPR, ch = c % CPR;
+      const bool ok = r0 + row < L;
+      a[i] = ok ? *reinterpret_cast<const uint4*>(pa + (int64_t)(r0 + row) * sa + ch * 8)
+                : make_uint4(0, 0, 0, 0);
+      b[i] = ok ? *reinterpret_cast<const uint4*>(pb + (int64_t)(r0 + row) * sb + ch * 8)
+                : make_uint4(0, 0, 0, 0);
+    }
   }
-}
+  __device__ __forceinline__ void store(bf16_t* la, bf16_t* lb) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + i * NT, row = c / CPR, ch = c % CPR;
+      *reinterpret_cast<uint4*>(la + row * (DH + 8) + ch * 8) = a[i];
+      *reinterpret_cast<uint4*>(lb + row * (DH + 8) + ch * 8) = b[i];
+    }
+  }
+};
 
 struct Geo {
   const bf16_t* qkv;
@@ -138,26 +187,26 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(Geo g, AttnMask mask,
   constexpr int STR = DH + 8;
   constexpr int NS = DH / 16;   // k-steps over the head dim
   constexpr int ND = DH / 32;   // 32-row d sub-tiles of O^T
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[KT * STR];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[KT * STR];
-  __shared__ uint8_t kset[MAXL];
+  constexpr int TILE = KT * STR;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE];  // [buf][K | V]
   const int b = blockIdx.z, h = blockIdx.y;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
   const int L = g.L, D = g.H * DH;
   const int q0 = blockIdx.x * 128, q1 = min(L, q0 + 128);
   const int q = q0 + wave * 32 + (lane & 31);
   const bool qv = q < L;
+  const bool wave_live = q0 + wave * 32 < L;
   const bf16_t* base = g.qkv + (int64_t)b * g.s_b;
   const bf16_t* kbase = base + D + h * DH;
   const bf16_t* vbase = base + 2 * D + h * DH;
-  for (int t = threadIdx.x; t < L; t += NT) kset[t] = (uint8_t)set_of(mask, t);
 
   bf16x8 qf[NS];
   const bf16_t* qrow = base + (int64_t)(qv ? q : 0) * g.s_t + h * DH;
 #pragma unroll
   for (int s = 0; s < NS; ++s) qf[s] = row_frag_global(qrow, qv, s, lane);
-  const uint32_t visq = mask.vis[set_of(mask, qv ? q : 0)];
+  const uint32_t visq = qv ? mask.vis[set_of(mask, q)] : 0u;
   const float* brow = bias ? bias + ((int64_t)h * L + (qv ? q : 0)) * L : nullptr;
+  const float c = bias ? 1.f : g.scale * LOG2E;  // score -> log2 units (bias mode converts first)
 
   floatx16 oacc[ND];
 #pragma unroll
@@ -165,90 +214,117 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(Geo g, AttnMask mask,
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
   float m = -INFINITY, l = 0.f;
-  const float sl2 = g.scale * 1.4426950408889634f;
-  __syncthreads();
 
-  for (int k0 = 0; k0 < L; k0 += KT) {
-    if (!tile_visible(mask, q0, q1, k0, min(L, k0 + KT))) continue;
-    load_rows_to_lds<DH>(Ks, kbase, g.s_t, k0, L);
-    load_rows_to_lds<DH>(Vs, vbase, g.s_t, k0, L);
-    __syncthreads();
-    floatx16 sacc[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[u][r] = 0.f;
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-        sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<STR>(Ks, 32 * u, s, lane),
-                                                          qf[s], sacc[u], 0, 0, 0);
-    }
-    uint32_t dw0 = 0xffffffffu, dw1 = 0xffffffffu;
-    if (drop_bits && qv) {
-      dw0 = drop_bits[(int64_t)q * drop_words + (k0 >> 5)];
-      if ((k0 >> 5) + 1 < drop_words) dw1 = drop_bits[(int64_t)q * drop_words + (k0 >> 5) + 1];
-    }
-    // scores (log2 domain), mask, running max
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kk = k0 + 32 * u + acc_row(r, lane);
-        float v = sacc[u][r] * sl2;
-        if (brow && kk < L) v += brow[kk] * 1.4426950408889634f;
-        const bool ok = kk < L && ((visq >> kset[kk < L ? kk : 0]) & 1u);
-        v = ok ? v : -INFINITY;
-        sacc[u][r] = v;
-        tmax = fmaxf(tmax, v);
+  TilePair<DH> pf;
+  int kt = next_key_tile(mask, q0, q1, 0, L);
+  if (kt < L) {
+    pf.load(kbase, g.s_t, vbase, g.s_t, kt, L);
+    pf.store(smem, smem + TILE);
+  }
+  __syncthreads();
+  int buf = 0;
+  while (kt < L) {
+    const int kn = next_key_tile(mask, q0, q1, kt + KT, L);
+    if (kn < L) pf.load(kbase, g.s_t, vbase, g.s_t, kn, L);
+    const bf16_t* Ks = smem + buf * 2 * TILE;
+    const bf16_t* Vs = Ks + TILE;
+    if (wave_live) {
+      uint32_t dw[2] = {0xffffffffu, 0xffffffffu};
+      if (drop_bits && qv) {
+        dw[0] = drop_bits[(int64_t)q * drop_words + (kt >> 5)];
+        if ((kt >> 5) + 1 < drop_words) dw[1] = drop_bits[(int64_t)q * drop_words + (kt >> 5) + 1];
       }
-    }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mn = fmaxf(m, tmax);
-    const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
-    float rs = 0.f;
+      floatx16 sacc[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const uint32_t dw = u ? dw1 : dw0;
+      for (int u = 0; u < 2; ++u) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = (mn == -INFINITY) ? 0.f : exp2f(sacc[u][r] - mn);
-        rs += p;
-        const bool keep = (dw >> acc_row(r, lane)) & 1u;
-        sacc[u][r] = keep ? p * drop_scale : 0.f;
+        for (int r = 0; r < 16; ++r) sacc[u][r] = 0.f;
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+          sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<STR>(Ks, 32 * u, s, lane),
+                                                            qf[s], sacc[u], 0, 0, 0);
       }
-    }
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = mn;
+      const uint64_t vm = sets_bits(mask, visq, kt);
+      if (brow) {
 #pragma unroll
-    for (int d = 0; d < ND; ++d) {
+        for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+          for (int r = 0; r < 16; ++r) {
+            const int kk = kt + 32 * u + rbit(r) + 4 * hh;
+            sacc[u][r] = sacc[u][r] * (g.scale * LOG2E) + (kk < L ? brow[kk] * LOG2E : 0.f);
+          }
+      }
+      if (!__all(vm == ~0ull)) {  // partially visible tile: masked scores -> -inf
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const uint32_t w = (uint32_t)(vm >> (32 * u)) >> (4 * hh);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int mk = bitmask_of(w, rbit(r));
+            sacc[u][r] = __int_as_float((__float_as_int(sacc[u][r]) & mk) | (~mk & (int)0xff800000u));
+          }
+        }
+      }
+      float tmax = -INFINITY;
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sacc[u][r]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mn = fmaxf(m, tmax);
+      const float mnc = mn == -INFINITY ? 0.f : mn * c;
+      const float alpha = exp2f(m * c - mnc);  // m = -inf -> 0 (nothing accumulated yet)
+      float rs = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t w = dw[u] >> (4 * hh);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = exp2f(fmaf(sacc[u][r], c, -mnc));
+          rs += p;
+          sacc[u][r] = __int_as_float(__float_as_int(p) & bitmask_of(w, rbit(r)));
+        }
+      }
+      rs += __shfl_xor(rs, 32, 64);
+      l = l * alpha + rs;
+      m = mn;
+      if (!__all(alpha == 1.f)) {
+#pragma unroll
+        for (int d = 0; d < ND; ++d)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bf16x8 p0 = pack_frag(sacc[u], 0), p1 = pack_frag(sacc[u], 1);
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+          oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trans_frag<STR>(Vs, 32 * u, 32 * d, lane),
+                                                            p0, oacc[d], 0, 0, 0);
           oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              trans_frag<STR>(Vs, 32 * u + 16 * s, 32 * d, lane), pack_frag(sacc[u], s), oacc[d],
-              0, 0, 0);
+              trans_frag<STR>(Vs, 32 * u + 16, 32 * d, lane), p1, oacc[d], 0, 0, 0);
+        }
+      }
     }
+    if (kn < L) pf.store(smem + (buf ^ 1) * 2 * TILE, smem + (buf ^ 1) * 2 * TILE + TILE);
     __syncthreads();
+    buf ^= 1;
+    kt = kn;
   }
   if (qv) {
-    const float inv = 1.f / l;
+    const float inv = l > 0.f ? drop_scale / l : 0.f;
     bf16_t* orow = o + (int64_t)b * o_s_b + (int64_t)q * o_s_t + h * DH;
 #pragma unroll
     for (int d = 0; d < ND; ++d)
 #pragma unroll
       for (int r4 = 0; r4 < 4; ++r4) {
-        const int dd = 32 * d + 8 * r4 + 4 * (lane >> 5);
+        const int dd = 32 * d + 8 * r4 + 4 * hh;
         uint2 w;
         w.x = (uint32_t)f2bf(oacc[d][4 * r4] * inv) | ((uint32_t)f2bf(oacc[d][4 * r4 + 1] * inv) << 16);
         w.y = (uint32_t)f2bf(oacc[d][4 * r4 + 2] * inv) | ((uint32_t)f2bf(oacc[d][4 * r4 + 3] * inv) << 16);
         *reinterpret_cast<uint2*>(orow + dd) = w;
       }
-    if (lane < 32) lse[((int64_t)b * g.H + h) * L + q] = m * 0.6931471805599453f + logf(l);
+    if (lane < 32) lse[((int64_t)b * g.H + h) * L + q] = l > 0.f ? m * c * LN2 + logf(l) : -INFINITY;
   }
 }
 
@@ -293,17 +369,18 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(Geo g, AttnMask mask,
   constexpr int STR = DH + 8;
   constexpr int NS = DH / 16;
   constexpr int ND = DH / 32;
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[KT * STR];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[KT * STR];
-  __shared__ uint8_t kset[MAXL];
+  constexpr int TILE = KT * STR;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE];  // [buf][K | V]
   const int b = blockIdx.z, h = blockIdx.y;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
   const int L = g.L, D = g.H * DH;
   const int q0 = blockIdx.x * 128, q1 = min(L, q0 + 128);
   const int q = q0 + wave * 32 + (lane & 31);
   const bool qv = q < L;
+  const bool wave_live = q0 + wave * 32 < L;
   const bf16_t* base = g.qkv + (int64_t)b * g.s_b;
-  for (int t = threadIdx.x; t < L; t += NT) kset[t] = (uint8_t)set_of(mask, t);
+  const bf16_t* kbase = base + D + h * DH;
+  const bf16_t* vbase = base + 2 * D + h * DH;
   bf16x8 qf[NS], df[NS];
   const bf16_t* qrow = base + (int64_t)(qv ? q : 0) * g.s_t + h * DH;
   const bf16_t* drow = dout + (int64_t)b * d_s_b + (int64_t)(qv ? q : 0) * d_s_t + h * DH;
@@ -312,64 +389,79 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(Geo g, AttnMask mask,
     qf[s] = row_frag_global(qrow, qv, s, lane);
     df[s] = row_frag_global(drow, qv, s, lane);
   }
-  const uint32_t visq = mask.vis[set_of(mask, qv ? q : 0)];
+  const uint32_t visq = qv ? mask.vis[set_of(mask, q)] : 0u;
   const int64_t row_bh = ((int64_t)b * g.H + h) * L;
-  const float lse2 = qv ? lse[row_bh + q] * 1.4426950408889634f : INFINITY;
+  const float lse2 = qv ? lse[row_bh + q] * LOG2E : INFINITY;
   const float dlt = qv ? delta[row_bh + q] : 0.f;
-  const float sl2 = g.scale * 1.4426950408889634f;
+  const float sl2 = g.scale * LOG2E;
   floatx16 dqacc[ND];
 #pragma unroll
   for (int d = 0; d < ND; ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dqacc[d][r] = 0.f;
+
+  TilePair<DH> pf;
+  int kt = next_key_tile(mask, q0, q1, 0, L);
+  if (kt < L) {
+    pf.load(kbase, g.s_t, vbase, g.s_t, kt, L);
+    pf.store(smem, smem + TILE);
+  }
   __syncthreads();
-  for (int k0 = 0; k0 < L; k0 += KT) {
-    if (!tile_visible(mask, q0, q1, k0, min(L, k0 + KT))) continue;
-    load_rows_to_lds<DH>(Ks, base + D + h * DH, g.s_t, k0, L);
-    load_rows_to_lds<DH>(Vs, base + 2 * D + h * DH, g.s_t, k0, L);
-    __syncthreads();
-    uint32_t dw0 = 0xffffffffu, dw1 = 0xffffffffu;
-    if (drop_bits && qv) {
-      dw0 = drop_bits[(int64_t)q * drop_words + (k0 >> 5)];
-      if ((k0 >> 5) + 1 < drop_words) dw1 = drop_bits[(int64_t)q * drop_words + (k0 >> 5) + 1];
-    }
-    floatx16 ds[2];
+  int buf = 0;
+  while (kt < L) {
+    const int kn = next_key_tile(mask, q0, q1, kt + KT, L);
+    if (kn < L) pf.load(kbase, g.s_t, vbase, g.s_t, kn, L);
+    const bf16_t* Ks = smem + buf * 2 * TILE;
+    const bf16_t* Vs = Ks + TILE;
+    if (wave_live) {
+      uint32_t dw[2] = {0xffffffffu, 0xffffffffu};
+      if (drop_bits && qv) {
+        dw[0] = drop_bits[(int64_t)q * drop_words + (kt >> 5)];
+        if ((kt >> 5) + 1 < drop_words) dw[1] = drop_bits[(int64_t)q * drop_words + (kt >> 5) + 1];
+      }
+      const uint64_t vm = sets_bits(mask, visq, kt);
+      floatx16 ds[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      floatx16 sacc, pacc;
+      for (int u = 0; u < 2; ++u) {
+        floatx16 sacc, pacc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sacc[r] = 0.f;
-        pacc[r] = 0.f;
+        for (int r = 0; r < 16; ++r) {
+          sacc[r] = 0.f;
+          pacc[r] = 0.f;
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<STR>(Ks, 32 * u, s, lane), qf[s],
+                                                         sacc, 0, 0, 0);
+          pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<STR>(Vs, 32 * u, s, lane), df[s],
+                                                         pacc, 0, 0, 0);
+        }
+        const uint32_t wv = (uint32_t)(vm >> (32 * u)) >> (4 * hh);
+        const uint32_t wd = dw[u] >> (4 * hh);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __int_as_float(__float_as_int(exp2f(fmaf(sacc[r], sl2, -lse2))) &
+                                         bitmask_of(wv, rbit(r)));
+          const float t = __int_as_float(__float_as_int(pacc[r] * drop_scale) & bitmask_of(wd, rbit(r)));
+          ds[u][r] = p * (t - dlt);
+        }
       }
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<STR>(Ks, 32 * u, s, lane), qf[s],
-                                                       sacc, 0, 0, 0);
-        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<STR>(Vs, 32 * u, s, lane), df[s],
-                                                       pacc, 0, 0, 0);
-      }
-      const uint32_t dw = u ? dw1 : dw0;
+      for (int u = 0; u < 2; ++u) {
+        const bf16x8 p0 = pack_frag(ds[u], 0), p1 = pack_frag(ds[u], 1);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kr = 32 * u + acc_row(r, lane);
-        const int kk = k0 + kr;
-        const bool ok = kk < L && ((visq >> kset[kk < L ? kk : 0]) & 1u);
-        const float p = ok ? exp2f(sacc[r] * sl2 - lse2) : 0.f;
-        const float md = ((dw >> acc_row(r, lane)) & 1u) ? drop_scale : 0.f;
-        ds[u][r] = p * (pacc[r] * md - dlt);
-      }
-    }
-#pragma unroll
-    for (int d = 0; d < ND; ++d)
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
+        for (int d = 0; d < ND; ++d) {
           dqacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              trans_frag<STR>(Ks, 32 * u + 16 * s, 32 * d, lane), pack_frag(ds[u], s), dqacc[d],
-              0, 0, 0);
+              trans_frag<STR>(Ks, 32 * u, 32 * d, lane), p0, dqacc[d], 0, 0, 0);
+          dqacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              trans_frag<STR>(Ks, 32 * u + 16, 32 * d, lane), p1, dqacc[d], 0, 0, 0);
+        }
+      }
+    }
+    if (kn < L) pf.store(smem + (buf ^ 1) * 2 * TILE, smem + (buf ^ 1) * 2 * TILE + TILE);
     __syncthreads();
+    buf ^= 1;
+    kt = kn;
   }
   if (qv) {
     bf16_t* orow = dqkv + (int64_t)b * dq_s_b + (int64_t)q * dq_s_t + h * DH;
@@ -377,7 +469,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(Geo g, AttnMask mask,
     for (int d = 0; d < ND; ++d)
 #pragma unroll
       for (int r4 = 0; r4 < 4; ++r4) {
-        const int dd = 32 * d + 8 * r4 + 4 * (lane >> 5);
+        const int dd = 32 * d + 8 * r4 + 4 * hh;
         uint2 w;
         w.x = (uint32_t)f2bf(dqacc[d][4 * r4] * g.scale) |
               ((uint32_t)f2bf(dqacc[d][4 * r4 + 1] * g.scale) << 16);
@@ -391,7 +483,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(Geo g, AttnMask mask,
 // =============================================================================== bwd: dK, dV
 template <int DH>
 __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(Geo g, AttnMask mask,
-                                                           const uint32_t* __restrict__ drop_bits,
+                                                           const uint32_t* __restrict__ drop_bits_t,
                                                            int drop_words, float drop_scale,
                                                            const bf16_t* __restrict__ dout,
                                                            int64_t d_s_b, int64_t d_s_t,
@@ -402,18 +494,19 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(Geo g, AttnMask mask,
   constexpr int STR = DH + 8;
   constexpr int NS = DH / 16;
   constexpr int ND = DH / 32;
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[KT * STR];
-  __shared__ __attribute__((aligned(16))) bf16_t Ds[KT * STR];
-  __shared__ float s_lse[KT], s_dlt[KT];
-  __shared__ uint32_t s_vis[KT];
-  __shared__ uint32_t s_bits[KT][4];
+  constexpr int TILE = KT * STR;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE];  // [buf][Q | dO]
+  __shared__ __attribute__((aligned(16))) float s_rows[2][2][KT];  // [buf][lse*log2e | delta]
   const int b = blockIdx.z, h = blockIdx.y;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
   const int L = g.L, D = g.H * DH;
   const int kb0 = blockIdx.x * 128, kb1 = min(L, kb0 + 128);
   const int key = kb0 + wave * 32 + (lane & 31);
   const bool kv = key < L;
+  const bool wave_live = kb0 + wave * 32 < L;
   const bf16_t* base = g.qkv + (int64_t)b * g.s_b;
+  const bf16_t* qbase = base + h * DH;
+  const bf16_t* dbase = dout + (int64_t)b * d_s_b + h * DH;
   bf16x8 kf[NS], vf[NS];
   const bf16_t* krow = base + (int64_t)(kv ? key : 0) * g.s_t + D + h * DH;
 #pragma unroll
@@ -421,9 +514,14 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(Geo g, AttnMask mask,
     kf[s] = row_frag_global(krow, kv, s, lane);
     vf[s] = row_frag_global(krow + D, kv, s, lane);
   }
-  const int kset_l = set_of(mask, kv ? key : 0);
+  // query sets that see this key's set
+  uint32_t selq = 0;
+  if (kv) {
+    const int ks = set_of(mask, key);
+    for (int i = 0; i < mask.n_sets; ++i) selq |= ((mask.vis[i] >> ks) & 1u) << i;
+  }
   const int64_t row_bh = ((int64_t)b * g.H + h) * L;
-  const float sl2 = g.scale * 1.4426950408889634f;
+  const float sl2 = g.scale * LOG2E;
   floatx16 dk[ND], dv[ND];
 #pragma unroll
   for (int d = 0; d < ND; ++d)
@@ -432,63 +530,101 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(Geo g, AttnMask mask,
       dk[d][r] = 0.f;
       dv[d][r] = 0.f;
     }
-  const int wbase = kb0 >> 5;  // first 32-key word of this block
-  for (int q0 = 0; q0 < L; q0 += KT) {
-    if (!tile_visible(mask, q0, min(L, q0 + KT), kb0, kb1)) continue;
-    load_rows_to_lds<DH>(Qs, base + h * DH, g.s_t, q0, L);
-    load_rows_to_lds<DH>(Ds, dout + (int64_t)b * d_s_b + h * DH, d_s_t, q0, L);
-    for (int i = threadIdx.x; i < KT; i += NT) {
-      const int qq = q0 + i;
-      const bool ok = qq < L;
-      s_lse[i] = ok ? lse[row_bh + qq] * 1.4426950408889634f : INFINITY;
-      s_dlt[i] = ok ? delta[row_bh + qq] : 0.f;
-      s_vis[i] = ok ? mask.vis[set_of(mask, qq)] : 0u;
+
+  TilePair<DH> pf;
+  float rowv = 0.f;  // thread t < 128 stages lse (t < 64) or delta (64 <= t < 128) of one row
+  auto load_rows = [&](int q0) {
+    if (threadIdx.x < 2 * KT) {
+      const int qq = q0 + (threadIdx.x & (KT - 1));
+      rowv = threadIdx.x < KT ? (qq < L ? lse[row_bh + qq] * LOG2E : INFINITY)
+                              : (qq < L ? delta[row_bh + qq] : 0.f);
     }
-    for (int i = threadIdx.x; i < KT * 4; i += NT) {
-      const int qi = i >> 2, w = i & 3, qq = q0 + qi;
-      uint32_t bits = 0xffffffffu;
-      if (drop_bits && qq < L && wbase + w < drop_words) bits = drop_bits[(int64_t)qq * drop_words + wbase + w];
-      s_bits[qi][w] = bits;
+  };
+  auto store_rows = [&](int bi) {
+    if (threadIdx.x < 2 * KT) s_rows[bi][threadIdx.x >> 6][threadIdx.x & (KT - 1)] = rowv;
+  };
+  int qt = next_query_tile(mask, kb0, kb1, 0, L);
+  if (qt < L) {
+    pf.load(qbase, g.s_t, dbase, d_s_t, qt, L);
+    load_rows(qt);
+    pf.store(smem, smem + TILE);
+    store_rows(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  while (qt < L) {
+    const int qn = next_query_tile(mask, kb0, kb1, qt + KT, L);
+    if (qn < L) {
+      pf.load(qbase, g.s_t, dbase, d_s_t, qn, L);
+      load_rows(qn);
     }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {  // 32-query sub-tiles
-      floatx16 sacc, pacc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sacc[r] = 0.f;
-        pacc[r] = 0.f;
+    const bf16_t* Qs = smem + buf * 2 * TILE;
+    const bf16_t* Ds = Qs + TILE;
+    if (wave_live) {
+      uint32_t dw[2] = {0xffffffffu, 0xffffffffu};
+      if (drop_bits_t && kv) {
+        dw[0] = drop_bits_t[(int64_t)key * drop_words + (qt >> 5)];
+        if ((qt >> 5) + 1 < drop_words) dw[1] = drop_bits_t[(int64_t)key * drop_words + (qt >> 5) + 1];
       }
+      const uint64_t qm = sets_bits(mask, selq, qt);
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<STR>(Qs, 32 * u, s, lane), kf[s],
-                                                       sacc, 0, 0, 0);
-        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<STR>(Ds, 32 * u, s, lane), vf[s],
-                                                       pacc, 0, 0, 0);
-      }
-      floatx16 pd, dsv;
-      const int kw = (wave * 32 + (lane & 31)) >> 5;   // word index within the block
-      const int kb = (wave * 32 + (lane & 31)) & 31;   // bit within the word
+      for (int u = 0; u < 2; ++u) {  // 32-query sub-tiles
+        floatx16 sacc, pacc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qi = 32 * u + acc_row(r, lane);
-        const bool ok = kv && ((s_vis[qi] >> kset_l) & 1u);
-        const float p = ok ? exp2f(sacc[r] * sl2 - s_lse[qi]) : 0.f;
-        const float md = ((s_bits[qi][kw] >> kb) & 1u) ? drop_scale : 0.f;
-        pd[r] = p * md;
-        dsv[r] = p * (pacc[r] * md - s_dlt[qi]);
-      }
-#pragma unroll
-      for (int d = 0; d < ND; ++d)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              trans_frag<STR>(Ds, 32 * u + 16 * s, 32 * d, lane), pack_frag(pd, s), dv[d], 0, 0, 0);
-          dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              trans_frag<STR>(Qs, 32 * u + 16 * s, 32 * d, lane), pack_frag(dsv, s), dk[d], 0, 0, 0);
+        for (int r = 0; r < 16; ++r) {
+          sacc[r] = 0.f;
+          pacc[r] = 0.f;
         }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<STR>(Qs, 32 * u, s, lane), kf[s],
+                                                         sacc, 0, 0, 0);
+          pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<STR>(Ds, 32 * u, s, lane), vf[s],
+                                                         pacc, 0, 0, 0);
+        }
+        // per-row lse / delta: rows 32u + 8j + 4hh + {0..3} are float4 j
+        float lr[16], dr[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 a = *reinterpret_cast<const float4*>(&s_rows[buf][0][32 * u + 8 * j + 4 * hh]);
+          const float4 d = *reinterpret_cast<const float4*>(&s_rows[buf][1][32 * u + 8 * j + 4 * hh]);
+          lr[4 * j] = a.x; lr[4 * j + 1] = a.y; lr[4 * j + 2] = a.z; lr[4 * j + 3] = a.w;
+          dr[4 * j] = d.x; dr[4 * j + 1] = d.y; dr[4 * j + 2] = d.z; dr[4 * j + 3] = d.w;
+        }
+        const uint32_t wv = (uint32_t)(qm >> (32 * u)) >> (4 * hh);
+        const uint32_t wd = dw[u] >> (4 * hh);
+        floatx16 pd, dsv;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __int_as_float(__float_as_int(exp2f(fmaf(sacc[r], sl2, -lr[r]))) &
+                                         bitmask_of(wv, rbit(r)));
+          const int keep = bitmask_of(wd, rbit(r));
+          pd[r] = __int_as_float(__float_as_int(p) & keep);  // drop_scale applied to dV at the end
+          const float t = __int_as_float(__float_as_int(pacc[r] * drop_scale) & keep);
+          dsv[r] = p * (t - dr[r]);
+        }
+        const bf16x8 pd0 = pack_frag(pd, 0), pd1 = pack_frag(pd, 1);
+        const bf16x8 ds0 = pack_frag(dsv, 0), ds1 = pack_frag(dsv, 1);
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+          dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trans_frag<STR>(Ds, 32 * u, 32 * d, lane),
+                                                          pd0, dv[d], 0, 0, 0);
+          dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              trans_frag<STR>(Ds, 32 * u + 16, 32 * d, lane), pd1, dv[d], 0, 0, 0);
+          dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trans_frag<STR>(Qs, 32 * u, 32 * d, lane),
+                                                          ds0, dk[d], 0, 0, 0);
+          dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              trans_frag<STR>(Qs, 32 * u + 16, 32 * d, lane), ds1, dk[d], 0, 0, 0);
+        }
+      }
+    }
+    if (qn < L) {
+      pf.store(smem + (buf ^ 1) * 2 * TILE, smem + (buf ^ 1) * 2 * TILE + TILE);
+      store_rows(buf ^ 1);
     }
     __syncthreads();
+    buf ^= 1;
+    qt = qn;
   }
   if (kv) {
     bf16_t* krow_o = dqkv + (int64_t)b * dq_s_b + (int64_t)key * dq_s_t + D + h * DH;
@@ -496,12 +632,14 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(Geo g, AttnMask mask,
     for (int d = 0; d < ND; ++d)
 #pragma unroll
       for (int r4 = 0; r4 < 4; ++r4) {
-        const int dd = 32 * d + 8 * r4 + 4 * (lane >> 5);
+        const int dd = 32 * d + 8 * r4 + 4 * hh;
         uint2 wk, wv;
         wk.x = (uint32_t)f2bf(dk[d][4 * r4] * g.scale) | ((uint32_t)f2bf(dk[d][4 * r4 + 1] * g.scale) << 16);
         wk.y = (uint32_t)f2bf(dk[d][4 * r4 + 2] * g.scale) | ((uint32_t)f2bf(dk[d][4 * r4 + 3] * g.scale) << 16);
-        wv.x = (uint32_t)f2bf(dv[d][4 * r4]) | ((uint32_t)f2bf(dv[d][4 * r4 + 1]) << 16);
-        wv.y = (uint32_t)f2bf(dv[d][4 * r4 + 2]) | ((uint32_t)f2bf(dv[d][4 * r4 + 3]) << 16);
+        wv.x = (uint32_t)f2bf(dv[d][4 * r4] * drop_scale) |
+               ((uint32_t)f2bf(dv[d][4 * r4 + 1] * drop_scale) << 16);
+        wv.y = (uint32_t)f2bf(dv[d][4 * r4 + 2] * drop_scale) |
+               ((uint32_t)f2bf(dv[d][4 * r4 + 3] * drop_scale) << 16);
         *reinterpret_cast<uint2*>(krow_o + dd) = wk;
         *reinterpret_cast<uint2*>(krow_o + D + dd) = wv;
       }
@@ -509,19 +647,32 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(Geo g, AttnMask mask,
 }
 
 // =============================================================================== dropout bits
+// idx < rows*words: word (r, w) of the row-major mask; idx >= rows*words (square masks, out_t
+// given): word (c, w) of the transposed mask, bit j = keep(r = 32w + j, c).
 __global__ void dropout_bits_kernel(const uint32_t* __restrict__ rng, uint32_t layer, uint32_t site,
                                     int rows, int cols, int words, uint32_t thresh,
-                                    uint32_t* __restrict__ out) {
+                                    uint32_t* __restrict__ out, uint32_t* __restrict__ out_t) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)rows * words) return;
-  const int r = idx / words, w = idx % words;
+  const int64_t n = (int64_t)rows * words;
+  if (idx >= (out_t ? 2 * n : n)) return;
   const uint32_t key = stream_key(rng[0], rng[1], layer, site);
   uint32_t bits = 0;
-  for (int j = 0; j < 32; ++j) {
-    const int c = w * 32 + j;
-    if (c < cols && keep_elem(key, (uint32_t)((int64_t)r * cols + c), thresh)) bits |= 1u << j;
+  if (idx < n) {
+    const int r = idx / words, w = idx % words;
+    for (int j = 0; j < 32; ++j) {
+      const int c = w * 32 + j;
+      if (c < cols && keep_elem(key, (uint32_t)((int64_t)r * cols + c), thresh)) bits |= 1u << j;
+    }
+    out[idx] = bits;
+  } else {
+    const int64_t t = idx - n;
+    const int c = t / words, w = t % words;
+    for (int j = 0; j < 32; ++j) {
+      const int r = w * 32 + j;
+      if (r < rows && keep_elem(key, (uint32_t)((int64_t)r * cols + c), thresh)) bits |= 1u << j;
+    }
+    out_t[t] = bits;
   }
-  out[idx] = bits;
 }
 
 int fill_mask(AttnMask& m, int n_sets, const int32_t* starts, const int32_t* lens,
@@ -531,6 +682,11 @@ int fill_mask(AttnMask& m, int n_sets, const int32_t* starts, const int32_t* len
     m.start[0] = 0;
     m.len[0] = L;
     m.vis[0] = 1u;
+    for (int i = 1; i < MAX_SETS; ++i) {
+      m.start[i] = 1 << 30;
+      m.len[i] = 0;
+      m.vis[i] = 0;
+    }
     return MMT_OK;
   }
   MMT_CHECK_ARG(n_sets <= MAX_SETS && starts && lens && vis, "attention: bad token-set table");
@@ -562,13 +718,15 @@ int fill_mask(AttnMask& m, int n_sets, const int32_t* starts, const int32_t* len
   } while (0)
 
 extern "C" int mmt_dropout_bits(const uint32_t* rng, uint32_t layer, uint32_t site, int rows,
-                                int cols, float keep_prob, uint32_t* out, mmt_stream_t stream) {
+                                int cols, float keep_prob, uint32_t* out, uint32_t* out_t,
+                                mmt_stream_t stream) {
   MMT_CHECK_ARG(rng && out && rows > 0 && cols > 0 && keep_prob > 0.f && keep_prob <= 1.f,
                 "mmt_dropout_bits: bad args");
+  MMT_CHECK_ARG(!out_t || rows == cols, "mmt_dropout_bits: the transposed mask needs rows == cols");
   const int words = (cols + 31) / 32;
-  const int64_t n = (int64_t)rows * words;
+  const int64_t n = (int64_t)rows * words * (out_t ? 2 : 1);
   hipLaunchKernelGGL(dropout_bits_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream),
-                     rng, layer, site, rows, cols, words, keep_threshold16(keep_prob), out);
+                     rng, layer, site, rows, cols, words, keep_threshold16(keep_prob), out, out_t);
   MMT_CHECK_LAUNCH("mmt_dropout_bits");
   return MMT_OK;
 }
@@ -590,8 +748,9 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   Geo g{(const bf16_t*)qkv, s_b, s_t, L, H, scale};
   const int words = (L + 31) / 32;
   dim3 grid((L + 127) / 128, H, B);
+  const float dscale = drop_bits ? 1.f / keep_prob : 1.f;
   ATTN_DISPATCH(DH, hipLaunchKernelGGL(attn_fwd_kernel<DH>, grid, dim3(NT), 0, as_stream(stream),
-                                       g, m, drop_bits, words, 1.f / keep_prob, bias, (bf16_t*)o,
+                                       g, m, drop_bits, words, dscale, bias, (bf16_t*)o,
                                        o_s_b, o_s_t, lse));
   MMT_CHECK_LAUNCH("mmt_attn_fwd");
   return MMT_OK;
@@ -600,20 +759,24 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
 extern "C" int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, int L, int H, int Dh,
                             float scale, int n_sets, const int32_t* set_start,
                             const int32_t* set_len, const uint32_t* set_vis,
-                            const uint32_t* drop_bits, float keep_prob, const void* o,
-                            int64_t o_s_b, int64_t o_s_t, const void* dout, int64_t d_s_b,
-                            int64_t d_s_t, const float* lse, float* delta, void* dqkv,
-                            int64_t dq_s_b, int64_t dq_s_t, mmt_stream_t stream) {
+                            const uint32_t* drop_bits, const uint32_t* drop_bits_t,
+                            float keep_prob, const void* o, int64_t o_s_b, int64_t o_s_t,
+                            const void* dout, int64_t d_s_b, int64_t d_s_t, const float* lse,
+                            float* delta, void* dqkv, int64_t dq_s_b, int64_t dq_s_t,
+                            mmt_stream_t stream) {
   MMT_CHECK_ARG(qkv && o && dout && lse && delta && dqkv, "mmt_attn_bwd: null pointer");
   MMT_CHECK_ARG(B > 0 && L > 0 && H > 0 && L <= MAXL, "mmt_attn_bwd: bad shape");
   MMT_CHECK_ARG(s_t % 8 == 0 && d_s_t % 8 == 0 && dq_s_t % 4 == 0 && o_s_t % 8 == 0,
                 "mmt_attn_bwd: strides must keep 16-B rows");
   MMT_CHECK_ARG(keep_prob > 0.f && keep_prob <= 1.f, "mmt_attn_bwd: keep_prob");
+  MMT_CHECK_ARG(!drop_bits == !drop_bits_t,
+                "mmt_attn_bwd: dropout needs both the mask and its transpose (mmt_dropout_bits)");
   AttnMask m;
   int rc = fill_mask(m, n_sets, set_start, set_len, set_vis, L);
   if (rc) return rc;
   Geo g{(const bf16_t*)qkv, s_b, s_t, L, H, scale};
   const int words = (L + 31) / 32;
+  const float dscale = drop_bits ? 1.f / keep_prob : 1.f;
   hipStream_t s = as_stream(stream);
   const int64_t nd = (int64_t)B * H * L;
   ATTN_DISPATCH(DH, hipLaunchKernelGGL(attn_bwd_delta_kernel<DH>, dim3((nd + 255) / 256), dim3(256),
@@ -621,10 +784,10 @@ extern "C" int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
                                        d_s_b, d_s_t, B, L, H, delta));
   dim3 grid((L + 127) / 128, H, B);
   ATTN_DISPATCH(DH, hipLaunchKernelGGL(attn_bwd_dq_kernel<DH>, grid, dim3(NT), 0, s, g, m, drop_bits,
-                                       words, 1.f / keep_prob, (const bf16_t*)dout, d_s_b, d_s_t,
+                                       words, dscale, (const bf16_t*)dout, d_s_b, d_s_t,
                                        lse, delta, (bf16_t*)dqkv, dq_s_b, dq_s_t));
   ATTN_DISPATCH(DH, hipLaunchKernelGGL(attn_bwd_dkdv_kernel<DH>, grid, dim3(NT), 0, s, g, m,
-                                       drop_bits, words, 1.f / keep_prob, (const bf16_t*)dout,
+                                       drop_bits_t, words, dscale, (const bf16_t*)dout,
                                        d_s_b, d_s_t, lse, delta, (bf16_t*)dqkv, dq_s_b, dq_s_t));
   MMT_CHECK_LAUNCH("mmt_attn_bwd");
   return MMT_OK;

@@ -74,10 +74,11 @@ def test_attention_fwd_bwd(dev, B, L, H, Dh, masked, drop):
     keep_prob = 0.9 if drop else 1.0
     rng = torch.tensor([77, 5], dtype=torch.int32, device=dev)
     bits = K.dropout_bits(rng, 3, 7, L, L, keep_prob) if drop else None
-    keep = bits_to_keep(bits, L).to(dev) if drop else None
-    if drop:  # the bitmask is the oracle's stream
+    keep = bits_to_keep(bits[0], L).to(dev) if drop else None
+    if drop:  # the bitmask is the oracle's stream; [1] is its transpose
         ref_keep = R.dropout_mask_2d(77, 5, 3, 7, L, L, 0, 0.9)
         assert (keep.cpu().numpy() == ref_keep).all()
+        assert (bits_to_keep(bits[1], L).numpy() == ref_keep.T).all()
     o, lse = K.attn_fwd(qkv, H, scale, table, bits, keep_prob)
     qf = qkv.float().requires_grad_()
     ref = ref_attention(qf, H, scale, mask, keep, keep_prob)
