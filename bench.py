@@ -91,18 +91,30 @@ def probe_dominant_gemm(model, B, reps=20):
     def launch():
         blk.mlp.dense.fwd(x, out=out, act=K.ACT_RELU, rng=rng, drop_layer=0, drop_site=2,
                           keep_prob=0.9)
-    for _ in range(3):
-        launch()
+    # reps launches captured in one HIP graph (as in the training step: no host launch gaps),
+    # timed with HIP events recorded on the stream the graph replays on
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            launch()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            launch()
+    g.replay()
+    torch.cuda.synchronize()
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
-    for _ in range(reps):
-        launch()
+    g.replay()
     e1.record(s)
     e1.synchronize()
     avg_ms = e0.elapsed_time(e1) / reps
     flops = 2.0 * M * cfg.mlp_dim * D
-    return dict(kernel="gemm_kernel<false,true,0> (MLP Dense_0 fwd, bias+relu+dropout epilogue)",
+    return dict(kernel="gemm_kernel<false, true, 0, PIPE> (MLP Dense_0 fwd, bias+relu+dropout epilogue)",
                 shape=[M, cfg.mlp_dim, D], avg_us=avg_ms * 1e3, flops=flops,
                 tflops=flops / (avg_ms * 1e-3) / 1e12)
 

@@ -30,6 +30,7 @@ SIGNATURES: dict[str, list] = {
     "mmt_tome_match": [P, I, I, I, I, I, L, L, L, I, I, P, P, P, P, P],
     "mmt_tome_merge_wavg_fwd": [P, I, I, I, I, L, L, I, I, I, I, P, P, P, P, P, L, L, P, P, P],
     "mmt_tome_merge_wavg_bwd": [P, I, I, I, I, L, L, I, I, I, P, P, P, P, L, L, P],
+    "mmt_gemm_set_variant": [I],
     "mmt_gemm": [I, I, I, P, I, L, P, I, L, P, I, L, I, L, L, L, I, P, P, L, P],
     "mmt_attn_fwd": [P, L, L, I, I, I, I, F, I, P, P, P, P, F, P, P, L, L, P, P],
     "mmt_attn_bwd": [P, L, L, I, I, I, I, F, I, P, P, P, P, P, F, P, L, L, P, L, L, P, P, P, L, L, P],
@@ -57,7 +58,7 @@ SIGNATURES: dict[str, list] = {
     "mmt_cast_f32_bf16": [P, P, L, P],
     "mmt_step_advance": [P, P],
 }
-_VOID = {"mmt_tome_set_match_path"}
+_VOID = {"mmt_tome_set_match_path", "mmt_gemm_set_variant"}
 
 
 class MMTError(RuntimeError):
@@ -79,6 +80,9 @@ def lib():
             fn.argtypes = args
             fn.restype = None if name in _VOID else I
         _lib = h
+        import os
+        if os.environ.get("MMT_GEMM_VARIANT"):  # benchmarking knob (include/mmt_api.h)
+            h.mmt_gemm_set_variant(int(os.environ["MMT_GEMM_VARIANT"]))
     return _lib
 
 

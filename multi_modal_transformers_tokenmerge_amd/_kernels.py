@@ -127,10 +127,21 @@ def _epi(bias=None, act=ACT_NONE, rng=None, drop_layer=0, drop_site=0, keep_prob
     return e
 
 
+def auto_split_k(M: int, N: int, K: int) -> int:
+    """Split of the reduction for launches with too few 128x128 tiles to fill 256 CUs (e.g. the
+    T5 projections at M = B*32): fp32 slabs + a combine kernel that applies the epilogue."""
+    tiles = -(-M // 128) * -(-N // 128)
+    if tiles >= 192 or K < 512:
+        return 1
+    return int(max(1, min(-(-384 // tiles), K // 256, 8)))
+
+
 def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool = False,
-         out: torch.Tensor | None = None, out_mode: int = OUT_BF16, split_k: int = 1, **epi):
+         out: torch.Tensor | None = None, out_mode: int = OUT_BF16, split_k: int | None = None,
+         **epi):
     """2-D GEMM: op(a) (M x K) . op(b) (K x N). a/b bf16 with unit inner stride.
-    trans_a: a is stored (K, M); trans_b: b is stored (N, K) (a weight W[N][K])."""
+    trans_a: a is stored (K, M); trans_b: b is stored (N, K) (a weight W[N][K]).
+    split_k None: auto_split_k."""
     _dev(a, b, out)
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
         raise TypeError("gemm operands must be bfloat16")
@@ -154,6 +165,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
     if bias is not None and (bias.numel() != N or bias.dtype != torch.float32):
         raise ValueError("gemm bias must be fp32 [N]")
     e = _epi(**epi)
+    if split_k is None:
+        split_k = auto_split_k(M, N, K)
     ws = None
     if split_k > 1:  # fp32 partial slabs, summed into `out` by the library's reduce kernel
         ws = torch.empty(split_k * M * N, dtype=torch.float32, device=a.device)

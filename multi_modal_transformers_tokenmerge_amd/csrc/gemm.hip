@@ -12,8 +12,9 @@
 // from HBM and read with the gfx950 transpose read ds_read_b64_tr_b16 — no transpose pass in HBM.
 // Register-staged double buffer (global loads of tile k+1 issued before the MFMAs of tile k).
 // Workgroups are remapped so the tiles sharing an A row-panel run on one XCD (shared L2).
-// Epilogue: the fp32 accumulator tile is staged through LDS and processed row-major, 8 columns
-// per thread, so bias / gate / residual loads and the C store are 16-32 B vector accesses.
+// Epilogue straight from registers: the MFMA operands are swapped so the accumulator holds C^T
+// and every lane owns runs of 4 consecutive columns of one row (8-16 B vector bias / gate /
+// residual loads and C stores, no LDS round trip).
 // Split-K writes fp32 partial slabs (plain stores) reduced by a second kernel — no atomics.
 #include "common.h"
 
@@ -30,8 +31,9 @@ constexpr int KC_STRIDE = BK + 8;   // K-contiguous tile [128][72] bf16 (144 B r
 constexpr int MC_STRIDE = BM + 8;   // M/N-contiguous tile [64][136] bf16 (272 B rows)
 constexpr int TILE_ELEMS = 128 * KC_STRIDE;  // >= 64 * MC_STRIDE
 constexpr int NTHREADS = 256;
-constexpr int CT_STRIDE = BN + 4;   // fp32 epilogue staging tile [128][132]
-static_assert(BM * CT_STRIDE * 4 <= 4 * TILE_ELEMS * 2, "epilogue tile must fit the LDS");
+
+// tuning knob: 0 / 1 = force PIPE 0 / 1; -1 or 3 = by K-steps per work item (PIPE 1 up to 24)
+int g_variant = -1;
 
 struct Epi {
   const float* bias;
@@ -49,39 +51,47 @@ struct Epi {
   float alpha, beta;
 };
 
-// global -> registers for one 128 x 64 (K-contig) or 64 x 128 (MN-contig) operand tile
+// global -> registers for one 128 x 64 (K-contig) or 64 x 128 (MN-contig) operand tile.
+// Branch-free: every chunk loads from an address clamped into range (needs the contiguous
+// extent to be a multiple of 8, checked by mmt_gemm); store_tile zeroes the out-of-range chunks
+// when it writes LDS. Keeping the mask out of the load lets the compiler count vmcnt waits (a
+// predicated load forces vmcnt(0)) and leaves the loads in flight until the store.
+template <bool KCONTIG>
+__device__ __forceinline__ void chunk_of(int c, int r0, int k0, int& row, int& kk) {
+  if (KCONTIG) {  // [row][k]: 8 chunks of 8 per row
+    row = r0 + (c >> 3);
+    kk = k0 + (c & 7) * 8;
+  } else {        // [k][row]: 16 chunks of 8 per k-row
+    kk = k0 + (c >> 4);
+    row = r0 + (c & 15) * 8;
+  }
+}
+
 template <bool KCONTIG>
 __device__ __forceinline__ void load_tile(const bf16_t* __restrict__ P, int64_t ld, int rows_lim,
                                           int k_lim, int r0, int k0, uint4 (&reg)[4]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int c = threadIdx.x + q * NTHREADS;
     int row, kk;
-    if (KCONTIG) {  // [row][k]: 8 chunks of 8 per row
-      row = c >> 3;
-      kk = (c & 7) * 8;
-      const bool ok = (r0 + row < rows_lim) && (k0 + kk < k_lim);
-      reg[q] = ok ? *reinterpret_cast<const uint4*>(P + (int64_t)(r0 + row) * ld + k0 + kk)
-                  : make_uint4(0, 0, 0, 0);
-    } else {        // [k][row]: 16 chunks of 8 per k-row
-      kk = c >> 4;
-      row = (c & 15) * 8;
-      const bool ok = (k0 + kk < k_lim) && (r0 + row < rows_lim);
-      reg[q] = ok ? *reinterpret_cast<const uint4*>(P + (int64_t)(k0 + kk) * ld + r0 + row)
-                  : make_uint4(0, 0, 0, 0);
-    }
+    chunk_of<KCONTIG>(threadIdx.x + q * NTHREADS, r0, k0, row, kk);
+    const bf16_t* p = KCONTIG ? P + (int64_t)min(row, rows_lim - 1) * ld + min(kk, k_lim - 8)
+                              : P + (int64_t)min(kk, k_lim - 1) * ld + min(row, rows_lim - 8);
+    reg[q] = *reinterpret_cast<const uint4*>(p);
   }
 }
 
 template <bool KCONTIG>
-__device__ __forceinline__ void store_tile(bf16_t* __restrict__ S, const uint4 (&reg)[4]) {
+__device__ __forceinline__ void store_tile(bf16_t* __restrict__ S, const uint4 (&reg)[4],
+                                           int rows_lim, int k_lim, int r0, int k0) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int c = threadIdx.x + q * NTHREADS;
-    int off;
-    if (KCONTIG) off = (c >> 3) * KC_STRIDE + (c & 7) * 8;
-    else off = (c >> 4) * MC_STRIDE + (c & 15) * 8;
-    *reinterpret_cast<uint4*>(S + off) = reg[q];
+    int row, kk;
+    chunk_of<KCONTIG>(c, r0, k0, row, kk);
+    const uint32_t m = (row < rows_lim && kk < k_lim) ? 0xffffffffu : 0u;
+    const int off = KCONTIG ? (c >> 3) * KC_STRIDE + (c & 7) * 8 : (c >> 4) * MC_STRIDE + (c & 15) * 8;
+    *reinterpret_cast<uint4*>(S + off) =
+        make_uint4(reg[q].x & m, reg[q].y & m, reg[q].z & m, reg[q].w & m);
   }
 }
 
@@ -108,18 +118,98 @@ __device__ __forceinline__ bf16x8 load_frag(const bf16_t* S, int rbase, int ks, 
   }
 }
 
-__device__ __forceinline__ void ld8(const bf16_t* p, float* f) {
-  const uint4 u = *reinterpret_cast<const uint4*>(p);
-  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+// W consecutive elements (W = 4 or 8, 8*W/... byte aligned) -> fp32
+template <int W>
+__device__ __forceinline__ void ldw(const bf16_t* p, float* f) {
+  uint32_t w[W / 2];
+  if constexpr (W == 8) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    w[0] = u.x; w[1] = u.y; w[2] = u.z; w[3] = u.w;
+  } else {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    w[0] = u.x; w[1] = u.y;
+  }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < W / 2; ++q) {
     f[2 * q] = __uint_as_float(w[q] << 16);
     f[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
   }
 }
-__device__ __forceinline__ void ld8(const float* p, float* f) {
-  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+template <int W>
+__device__ __forceinline__ void ldw(const float* p, float* f) {
+#pragma unroll
+  for (int q = 0; q < W / 4; ++q) {
+    const float4 a = *reinterpret_cast<const float4*>(p + 4 * q);
+    f[4 * q] = a.x; f[4 * q + 1] = a.y; f[4 * q + 2] = a.z; f[4 * q + 3] = a.w;
+  }
+}
+
+// Epilogue on W consecutive columns (gc .. gc+W-1, gc even) of output row gr, in place on v[W]:
+// alpha, bias, relu, gate, counter-RNG dropout (pairs of 16-bit draws), residual.
+template <int W>
+__device__ __forceinline__ void epilogue_w(const Epi& epi, uint32_t key, int N, int gr, int gc,
+                                           float* v) {
+#pragma unroll
+  for (int e = 0; e < W; ++e) v[e] *= epi.alpha;
+  if (epi.bias) {
+    float bb[W];
+    ldw<W>(epi.bias + gc, bb);
+#pragma unroll
+    for (int e = 0; e < W; ++e) v[e] += bb[e];
+  }
+  if (epi.act == MMT_ACT_RELU)
+#pragma unroll
+    for (int e = 0; e < W; ++e) v[e] = fmaxf(v[e], 0.f);
+  if (epi.gate) {
+    float g[W];
+    ldw<W>(epi.gate + (int64_t)gr * epi.ld_gate + gc, g);
+#pragma unroll
+    for (int e = 0; e < W; ++e) v[e] *= (g[e] > 0.f) ? epi.gate_scale : 0.f;
+  }
+  if (epi.rng) {
+    const uint32_t base = (uint32_t)((epi.drop_row_offset + gr) * (int64_t)N + gc);  // even
+#pragma unroll
+    for (int e = 0; e < W; e += 2) {
+      const uint32_t d = pair_draw(key, (base + e) >> 1);
+      v[e] = ((d & 0xffffu) < epi.keep_thresh16) ? v[e] * epi.drop_scale : 0.f;
+      v[e + 1] = ((d >> 16) < epi.keep_thresh16) ? v[e + 1] * epi.drop_scale : 0.f;
+    }
+  }
+  if (epi.residual) {
+    float rr[W];
+    const int64_t ro = (int64_t)gr * epi.ld_res + gc;
+    if (epi.res_f32) ldw<W>(reinterpret_cast<const float*>(epi.residual) + ro, rr);
+    else ldw<W>(reinterpret_cast<const bf16_t*>(epi.residual) + ro, rr);
+#pragma unroll
+    for (int e = 0; e < W; ++e) v[e] += rr[e];
+  }
+}
+
+// Store W columns: bf16 (OUT 0) or fp32 with C = v + beta * C (OUT 1, or 2 = plain fp32 slab).
+template <int OUT, int W>
+__device__ __forceinline__ void store_w(void* Cv, int64_t off, float beta, const float* v) {
+  if (OUT == 0) {
+    uint32_t w[W / 2];
+#pragma unroll
+    for (int q = 0; q < W / 2; ++q) w[q] = (uint32_t)f2bf(v[2 * q]) | ((uint32_t)f2bf(v[2 * q + 1]) << 16);
+    bf16_t* cp = reinterpret_cast<bf16_t*>(Cv) + off;
+    if constexpr (W == 8) *reinterpret_cast<uint4*>(cp) = make_uint4(w[0], w[1], w[2], w[3]);
+    else *reinterpret_cast<uint2*>(cp) = make_uint2(w[0], w[1]);
+  } else {
+    float* cp = reinterpret_cast<float*>(Cv) + off;
+    float o[W];
+    if (OUT == 1 && beta != 0.f) {
+      ldw<W>(cp, o);
+#pragma unroll
+      for (int e = 0; e < W; ++e) o[e] = v[e] + beta * o[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < W; ++e) o[e] = v[e];
+    }
+#pragma unroll
+    for (int q = 0; q < W / 4; ++q)
+      *reinterpret_cast<float4*>(cp + 4 * q) = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  }
 }
 
 // XCD-aware bijective remap: blocks b and b+8 share an XCD (round-robin dispatch), so give each
@@ -129,51 +219,61 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-template <bool TA, bool TB, int OUT>  // OUT: 0 bf16, 1 fp32 (C = epi + beta*C), 2 fp32 split-K slab
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(
-    int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, int64_t sA,
-    const bf16_t* __restrict__ B, int64_t ldb, int64_t sB, void* __restrict__ Cv, int64_t ldc,
-    int64_t sC, int split_k, int k_chunk, int tiles_n, Epi epi) {
-  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE_ELEMS];
-  const int bz = blockIdx.z / split_k, ks_id = blockIdx.z - bz * split_k;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = wg / tiles_n, tn = wg - tm * tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = ks_id * k_chunk, kend = min(K, kbeg + k_chunk);
-  A += bz * sA;
-  B += bz * sB;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+// One output tile of one batch entry / K-split ("work item").
+struct Work {
+  int bz, ks, m0, n0, kbeg, kend, nk;
+};
+__device__ __forceinline__ Work decode_work(int w, int tiles_n, int tiles, int split_k, int K,
+                                            int k_chunk) {
+  Work r;
+  const int z = w / tiles, t = w - z * tiles;
+  r.bz = z / split_k;
+  r.ks = z - r.bz * split_k;
+  const int tm = t / tiles_n;
+  r.m0 = tm * BM;
+  r.n0 = (t - tm * tiles_n) * BN;
+  r.kbeg = r.ks * k_chunk;
+  r.kend = min(K, r.kbeg + k_chunk);
+  r.nk = max(0, (r.kend - r.kbeg + BK - 1) / BK);
+  return r;
+}
 
+// OUT: 0 bf16, 1 fp32 (C = epi + beta*C), 2 fp32 split-K slab.
+// One work item per workgroup; workgroups are remapped so each XCD runs a contiguous range of
+// items (tiles sharing an A row-panel share that XCD's L2).
+// PIPE 0: double-buffered LDS, operands prefetched one K-step ahead through registers (one
+//         barrier per K-step, 2 workgroups/CU) — long K loops.
+// PIPE 1: a single LDS stage (write-after-barrier, two barriers per K-step), 36 KB so 3
+//         workgroups/CU — short K loops (measured better up to ~24 K-steps). A persistent
+//         variant of it (next tile's loads issued before the epilogue) measured slower.
+// Epilogue (OUT 0/1): the transposed accumulator runs go to an LDS row-major fp32 tile (16-B
+// writes), then 16 threads per row apply the epilogue on 8 columns each (256-B coalesced row
+// segments for C / gate / residual). Split-K slabs (OUT 2) are stored straight from registers.
+template <bool TA, bool TB, int OUT, int PIPE>
+__global__ __launch_bounds__(NTHREADS, PIPE == 1 ? 3 : 2) void gemm_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A0, int64_t lda, int64_t sA,
+    const bf16_t* __restrict__ B0, int64_t ldb, int64_t sB, void* __restrict__ Cv, int64_t ldc,
+    int64_t sC, int split_k, int k_chunk, int tiles_n, int n_work, Epi epi) {
+  constexpr bool DB = PIPE == 0;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[(DB ? 4 : 2) * TILE_ELEMS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1, hl = lane >> 5;
+  const int tiles = ((M + BM - 1) / BM) * tiles_n;
   constexpr bool A_KC = !TA;  // A [M][K]
   constexpr bool B_KC = TB;   // B [N][K]
-  floatx16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[a][b][q] = 0.f;
+  uint32_t key = 0;
+  if (OUT != 2 && epi.rng) key = stream_key(epi.rng[0], epi.rng[1], epi.drop_layer, epi.drop_site);
 
-  uint4 ra[4], rb[4];
-  const int nk = (kend - kbeg + BK - 1) / BK;
-  if (nk > 0) {
-    load_tile<A_KC>(A, lda, M, kend, m0, kbeg, ra);
-    load_tile<B_KC>(B, ldb, N, kend, n0, kbeg, rb);
-    store_tile<A_KC>(smem, ra);
-    store_tile<B_KC>(smem + TILE_ELEMS, rb);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      const int k0 = kbeg + (kt + 1) * BK;
-      load_tile<A_KC>(A, lda, M, kend, m0, k0, ra);
-      load_tile<B_KC>(B, ldb, N, kend, n0, k0, rb);
-    }
-    const bf16_t* As = smem + cur * 2 * TILE_ELEMS;
-    const bf16_t* Bs = As + TILE_ELEMS;
+  floatx16 acc[2][2];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[a][b][q] = 0.f;
+  };
+  auto mma_tile = [&](const bf16_t* As, const bf16_t* Bs) {
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8 af[2], bfr[2];
@@ -184,126 +284,139 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_kernel(
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < 2; ++b)  // operands swapped: the accumulator holds C^T
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
     }
-    if (more) {
-      bf16_t* Ns = smem + (cur ^ 1) * 2 * TILE_ELEMS;
-      store_tile<A_KC>(Ns, ra);
-      store_tile<B_KC>(Ns + TILE_ELEMS, rb);
+  };
+  uint4 ra[4], rb[4];
+  auto load_step = [&](const Work& w, int kt) {
+    const int k0 = w.kbeg + kt * BK;
+    load_tile<A_KC>(A0 + w.bz * sA, lda, M, w.kend, w.m0, k0, ra);
+    load_tile<B_KC>(B0 + w.bz * sB, ldb, N, w.kend, w.n0, k0, rb);
+  };
+  auto store_step = [&](const Work& w, int kt, bf16_t* S) {
+    const int k0 = w.kbeg + kt * BK;
+    store_tile<A_KC>(S, ra, M, w.kend, w.m0, k0);
+    store_tile<B_KC>(S + TILE_ELEMS, rb, N, w.kend, w.n0, k0);
+  };
+
+  // lane (m = lane & 31, h) of accumulator block (a, b) holds row m, columns 8g + 4h + {0..3}
+  auto epilogue = [&](const Work& w) {
+    if (OUT == 2) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int gr = w.m0 + wm * 64 + a * 32 + (lane & 31);
+        if (gr >= M) continue;
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int gc = w.n0 + wn * 64 + b * 32 + 8 * g + 4 * hl;
+            if (gc >= N) continue;  // N % 8 == 0: a 4-column run is entirely in or out
+            float v[4] = {acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2],
+                          acc[a][b][4 * g + 3]};
+            store_w<2, 4>(Cv, w.ks * sC + (int64_t)gr * ldc + gc, 0.f, v);
+          }
+      }
+      return;
+    }
+    constexpr int CTS = BN + 4;         // staging row stride (floats): conflict-free 16-B writes
+    constexpr int HALVES = DB ? 1 : 2;  // one LDS stage holds 64 of the 128 rows at a time
+    constexpr int ROWS = BM / HALVES;
+    static_assert(ROWS * CTS * 4 <= (DB ? 4 : 2) * TILE_ELEMS * 2, "staging tile exceeds the LDS");
+    float* Ct = reinterpret_cast<float*>(smem);
+    const int c8 = (threadIdx.x & 15) * 8;
+    const int gc = w.n0 + c8;
+#pragma unroll 1
+    for (int hf = 0; hf < HALVES; ++hf) {
+      __syncthreads();  // operand tile (hf 0) / the previous half (hf 1) consumed
+      if (DB || wm == hf) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const int r = (DB ? wm * 64 : 0) + a * 32 + (lane & 31);
+              *reinterpret_cast<float4*>(Ct + r * CTS + wn * 64 + b * 32 + 8 * g + 4 * hl) =
+                  make_float4(acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2],
+                              acc[a][b][4 * g + 3]);
+            }
+      }
+      __syncthreads();
+      if (gc >= N) continue;
+#pragma unroll 2
+      for (int r = threadIdx.x >> 4; r < ROWS; r += NTHREADS / 16) {
+        const int gr = w.m0 + hf * ROWS + r;
+        if (gr >= M) break;
+        float v[8];
+        ldw<8>(Ct + r * CTS + c8, v);
+        epilogue_w<8>(epi, key, N, gr, gc, v);
+        store_w<OUT, 8>(Cv, w.bz * sC + (int64_t)gr * ldc + gc, epi.beta, v);
+      }
+    }
+  };
+
+  zero_acc();
+  if (DB) {
+    const Work w = decode_work(xcd_remap(blockIdx.x, gridDim.x), tiles_n, tiles, split_k, K, k_chunk);
+    if (w.nk > 0) {
+      load_step(w, 0);
+      store_step(w, 0, smem);
     }
     __syncthreads();
-  }
-
-  // ---------------- epilogue: stage the fp32 tile through LDS, then 8 columns per thread
-  float* Ct = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int r = wm * 64 + a * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
-        Ct[r * CT_STRIDE + wn * 64 + b * 32 + (lane & 31)] = acc[a][b][q];
-      }
-  __syncthreads();
-  uint32_t key = 0;
-  if (OUT != 2 && epi.rng) key = stream_key(epi.rng[0], epi.rng[1], epi.drop_layer, epi.drop_site);
-  const int c8 = (threadIdx.x & 15) * 8;
-  const int gc = n0 + c8;
-  if (gc >= N) return;  // N % 8 == 0: whole 8-column groups are in or out
-  float bias[8];
-  if (OUT != 2 && epi.bias) ld8(epi.bias + gc, bias);
-#pragma unroll 2
-  for (int r = threadIdx.x >> 4; r < BM; r += NTHREADS / 16) {
-    const int gr = m0 + r;
-    if (gr >= M) break;
-    float v[8];
-    {
-      const float4 p0 = *reinterpret_cast<const float4*>(Ct + r * CT_STRIDE + c8);
-      const float4 p1 = *reinterpret_cast<const float4*>(Ct + r * CT_STRIDE + c8 + 4);
-      v[0] = p0.x; v[1] = p0.y; v[2] = p0.z; v[3] = p0.w;
-      v[4] = p1.x; v[5] = p1.y; v[6] = p1.z; v[7] = p1.w;
+    for (int kt = 0; kt < w.nk; ++kt) {
+      const int cur = kt & 1;
+      const bool more = kt + 1 < w.nk;
+      if (more) load_step(w, kt + 1);
+      mma_tile(smem + cur * 2 * TILE_ELEMS, smem + cur * 2 * TILE_ELEMS + TILE_ELEMS);
+      if (more) store_step(w, kt + 1, smem + (cur ^ 1) * 2 * TILE_ELEMS);
+      __syncthreads();
     }
-    if (OUT == 2) {  // split-K partial slab
-      float* cp = reinterpret_cast<float*>(Cv) + ks_id * sC + (int64_t)gr * ldc + gc;
-      *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
-      *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
-      continue;
+    epilogue(w);
+  } else {
+    const Work w = decode_work(xcd_remap(blockIdx.x, gridDim.x), tiles_n, tiles, split_k, K, k_chunk);
+    if (w.nk > 0) load_step(w, 0);
+    for (int kt = 0; kt < w.nk; ++kt) {
+      if (kt > 0) __syncthreads();  // every wave is done reading the previous K-step
+      store_step(w, kt, smem);
+      __syncthreads();
+      if (kt + 1 < w.nk) load_step(w, kt + 1);  // in flight during this K-step's MFMAs
+      mma_tile(smem, smem + TILE_ELEMS);
     }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] *= epi.alpha;
-    if (epi.bias)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += bias[e];
-    if (epi.act == MMT_ACT_RELU)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-    if (epi.gate) {
-      float g[8];
-      ld8(epi.gate + (int64_t)gr * epi.ld_gate + gc, g);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= (g[e] > 0.f) ? epi.gate_scale : 0.f;
-    }
-    if (epi.rng) {
-      const uint32_t base = (uint32_t)((epi.drop_row_offset + gr) * (int64_t)N + gc);  // even
-#pragma unroll
-      for (int e = 0; e < 8; e += 2) {
-        const uint32_t d = pair_draw(key, (base + e) >> 1);
-        v[e] = ((d & 0xffffu) < epi.keep_thresh16) ? v[e] * epi.drop_scale : 0.f;
-        v[e + 1] = ((d >> 16) < epi.keep_thresh16) ? v[e + 1] * epi.drop_scale : 0.f;
-      }
-    }
-    if (epi.residual) {
-      float rr[8];
-      const int64_t ro = (int64_t)gr * epi.ld_res + gc;
-      if (epi.res_f32) ld8(reinterpret_cast<const float*>(epi.residual) + ro, rr);
-      else ld8(reinterpret_cast<const bf16_t*>(epi.residual) + ro, rr);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += rr[e];
-    }
-    if (OUT == 0) {
-      uint32_t w[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) w[q] = (uint32_t)f2bf(v[2 * q]) | ((uint32_t)f2bf(v[2 * q + 1]) << 16);
-      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(Cv) + bz * sC + (int64_t)gr * ldc + gc) =
-          make_uint4(w[0], w[1], w[2], w[3]);
-    } else {
-      float* cp = reinterpret_cast<float*>(Cv) + bz * sC + (int64_t)gr * ldc + gc;
-      if (epi.beta != 0.f) {
-        float o[8];
-        ld8(cp, o);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += epi.beta * o[e];
-      }
-      *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
-      *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
-    }
+    epilogue(w);
   }
 }
 
-// out[m][n] = beta * out[m][n] + alpha * sum_s slab[s][m][n]  (fp32, 4 columns per thread)
-__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int split, int M, int N,
-                                     float* __restrict__ out, int64_t ldo, float alpha, float beta) {
-  const int64_t n4 = (int64_t)M * N / 4;
+// Split-K combine: v = sum_s slab[s][m][n] (fp32), then the GEMM epilogue, 8 columns per thread.
+template <int OUT>
+__global__ void splitk_epilogue_kernel(const float* __restrict__ ws, int split, int M, int N,
+                                       void* __restrict__ Cv, int64_t ldc, Epi epi) {
+  const int n8 = N / 8;
+  const int64_t total = (int64_t)M * n8;
   const int64_t slab = (int64_t)M * N;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+  uint32_t key = 0;
+  if (epi.rng) key = stream_key(epi.rng[0], epi.rng[1], epi.drop_layer, epi.drop_site);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = i * 4;
-    const int m = e / N, n = e % N;
-    float4 s = *reinterpret_cast<const float4*>(ws + e);
+    const int gr = i / n8, gc = (i % n8) * 8;
+    const float* p = ws + (int64_t)gr * N + gc;
+    float v[8];
+    ldw<8>(p, v);
     for (int k = 1; k < split; ++k) {
-      const float4 t = *reinterpret_cast<const float4*>(ws + k * slab + e);
-      s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+      float t[8];
+      ldw<8>(p + k * slab, t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += t[e];
     }
-    float4* op = reinterpret_cast<float4*>(out + (int64_t)m * ldo + n);
-    const float4 o = beta != 0.f ? *op : make_float4(0, 0, 0, 0);
-    *op = make_float4(beta * o.x + alpha * s.x, beta * o.y + alpha * s.y, beta * o.z + alpha * s.z,
-                      beta * o.w + alpha * s.w);
+    epilogue_w<8>(epi, key, N, gr, gc, v);
+    store_w<OUT, 8>(Cv, (int64_t)gr * ldc + gc, epi.beta, v);
   }
 }
 
 }  // namespace
+
+extern "C" void mmt_gemm_set_variant(int v) { g_variant = v; }
 
 extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t lda,
                         const void* B, int transB, int64_t ldb, void* C, int c_mode, int64_t ldc,
@@ -352,29 +465,34 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
   }
   hipStream_t s = as_stream(stream);
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
-  int out_kind = c_mode == MMT_OUT_BF16 ? 0 : 1;
-  if (c_mode == MMT_OUT_F32_ACCUM) {
-    if (split_k == 1) {  // C += alpha * acc directly in the epilogue
-      epi.beta = 1.f;
-    } else {
-      MMT_CHECK_ARG(batch == 1, "mmt_gemm: split-K needs batch == 1");
-      MMT_CHECK_ARG(workspace && ws_elems >= (int64_t)split_k * M * N &&
-                        (uintptr_t)workspace % 16 == 0,
-                    "mmt_gemm: split-K needs a 16-B aligned workspace of split_k*M*N floats");
-      out_kind = 2;
-    }
-  } else {
-    MMT_CHECK_ARG(split_k == 1, "mmt_gemm: split_k > 1 needs MMT_OUT_F32_ACCUM");
+  const int final_kind = c_mode == MMT_OUT_BF16 ? 0 : 1;
+  if (c_mode == MMT_OUT_F32_ACCUM) epi.beta = 1.f;  // C += alpha * acc
+  int out_kind = final_kind;
+  if (split_k > 1) {  // fp32 partial slabs + a combine kernel that applies the epilogue
+    MMT_CHECK_ARG(batch == 1, "mmt_gemm: split-K needs batch == 1");
+    MMT_CHECK_ARG(workspace && ws_elems >= (int64_t)split_k * M * N &&
+                      (uintptr_t)workspace % 16 == 0,
+                  "mmt_gemm: split-K needs a 16-B aligned workspace of split_k*M*N floats");
+    out_kind = 2;
   }
-  int k_chunk = ((K + split_k - 1) / split_k + BK - 1) / BK * BK;
-  dim3 grid(tiles_m * tiles_n, 1, batch * split_k);
+  const int k_chunk = ((K + split_k - 1) / split_k + BK - 1) / BK * BK;
+  if (out_kind == 2) split_k = (K + k_chunk - 1) / k_chunk;  // no empty K-splits
+  const int n_work = tiles_m * tiles_n * batch * split_k;
+  const int pipe = (g_variant >= 0 && (g_variant & 3) != 3) ? (g_variant & 1)
+                                                            : (k_chunk / BK > 24 ? 0 : 1);
+  const int grid_x = n_work;
   void* Cdst = out_kind == 2 ? (void*)workspace : C;
   const int64_t ldd = out_kind == 2 ? (int64_t)N : ldc;
   const int64_t sdd = out_kind == 2 ? (int64_t)M * N : sC;
-#define GL(TA, TB, OUT)                                                                            \
-  hipLaunchKernelGGL((gemm_kernel<TA, TB, OUT>), grid, dim3(NTHREADS), 0, s, M, N, K,             \
+#define GL1(TA, TB, OUT, P)                                                                        \
+  hipLaunchKernelGGL((gemm_kernel<TA, TB, OUT, P>), dim3(grid_x), dim3(NTHREADS), 0, s, M, N, K,   \
                      (const bf16_t*)A, lda, sA, (const bf16_t*)B, ldb, sB, Cdst, ldd, sdd,        \
-                     split_k, k_chunk, tiles_n, epi)
+                     split_k, k_chunk, tiles_n, n_work, epi)
+#define GL(TA, TB, OUT)                         \
+  do {                                          \
+    if (pipe == 0) GL1(TA, TB, OUT, 0);         \
+    else GL1(TA, TB, OUT, 1);                   \
+  } while (0)
 #define GL_OUT(TA, TB)                          \
   do {                                          \
     if (out_kind == 0) GL(TA, TB, 0);           \
@@ -387,13 +505,18 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
   else GL_OUT(true, true);
 #undef GL_OUT
 #undef GL
+#undef GL1
   MMT_CHECK_LAUNCH("mmt_gemm");
   if (out_kind == 2) {
-    const int64_t n4 = (int64_t)M * N / 4;
-    const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, workspace, split_k, M,
-                       N, (float*)C, ldc, epi.alpha, 1.f);
-    MMT_CHECK_LAUNCH("mmt_gemm(split-K reduce)");
+    const int64_t n8 = (int64_t)M * N / 8;
+    const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 4096);
+    if (final_kind == 0)
+      hipLaunchKernelGGL(splitk_epilogue_kernel<0>, dim3(blocks), dim3(256), 0, s, workspace,
+                         split_k, M, N, C, ldc, epi);
+    else
+      hipLaunchKernelGGL(splitk_epilogue_kernel<1>, dim3(blocks), dim3(256), 0, s, workspace,
+                         split_k, M, N, C, ldc, epi);
+    MMT_CHECK_LAUNCH("mmt_gemm(split-K combine)");
   }
   return MMT_OK;
 }

@@ -94,3 +94,40 @@ def test_gemm_rejects_bad_shapes(dev):
     b = torch.zeros((12, 16), dtype=torch.bfloat16, device=dev)
     with pytest.raises(_C.MMTError):
         Kn.gemm(a, b)  # K = 12 not a multiple of 8
+
+
+@pytest.mark.parametrize("split", [2, 3, 5])
+def test_gemm_splitk_applies_epilogue(dev, split):
+    """Split-K slabs + combine kernel: bias / relu / dropout / residual (bf16 out) and gate."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    g = torch.Generator().manual_seed(10 + split)
+    M, N, K = 200, 256, 1024
+    a, w = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    bias = torch.randn(N, generator=g).to(dev)
+    res = torch.randn((M, N), generator=g).to(dev)
+    rng = torch.tensor([99, 3], dtype=torch.int32, device=dev)
+    out = Kn.gemm(a, w, False, True, bias=bias, act=Kn.ACT_RELU, rng=rng, drop_layer=1,
+                  drop_site=3, keep_prob=0.8, drop_row_offset=7, residual=res, split_k=split)
+    keep = torch.from_numpy(R.dropout_mask_2d(99, 3, 1, 3, M, N, 7, 0.8)).to(dev)
+    ref = torch.relu(a.float() @ w.float().t() + bias)
+    ref = torch.where(keep, ref / 0.8, torch.zeros_like(ref)) + res
+    _close_bf16(out, ref)
+    gate = _mk((M, N), dev, g)
+    b2 = _mk((K, N), dev, g)
+    o2 = Kn.gemm(a, b2, gate=gate, gate_scale=2.0, split_k=split, out_mode=Kn.OUT_F32)
+    ref2 = (a.float() @ b2.float()) * (gate.float() > 0).float() * 2.0
+    torch.testing.assert_close(o2, ref2, rtol=1e-4, atol=1e-3)
+
+
+def test_auto_split_small_m(dev):
+    """T5-like projection (M = 2048, N = 768): auto split-K path vs the unsplit kernel."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    assert Kn.auto_split_k(2048, 768, 3072) > 1 and Kn.auto_split_k(17664, 1536, 384) == 1
+    g = torch.Generator().manual_seed(5)
+    a, w = _mk((2048, 3072), dev, g), _mk((768, 3072), dev, g)
+    res = _mk((2048, 768), dev, g)
+    o_auto = Kn.gemm(a, w, trans_b=True, residual=res)
+    o_one = Kn.gemm(a, w, trans_b=True, residual=res, split_k=1)
+    ref = a.float() @ w.float().t() + res.float()
+    _close_bf16(o_auto, ref)
+    _close_bf16(o_one, ref)

@@ -10,21 +10,48 @@ from multi_modal_transformers_tokenmerge_amd import _kernels as K
 
 
 def timeit(fn, reps=20):
-    for _ in range(3):
-        fn()
-    s = torch.cuda.current_stream()
+    """Average kernel time of fn: reps launches captured in one HIP graph and replayed, so host
+    launch overhead (Python + ctypes, ~10 us per call) is excluded, as in the training step."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    cur = torch.cuda.current_stream()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record(s)
-    for _ in range(reps):
-        fn()
-    b.record(s)
+    a.record(cur)
+    for _ in range(3):
+        g.replay()
+    b.record(cur)
     b.synchronize()
-    return a.elapsed_time(b) / reps * 1e3  # us
+    return a.elapsed_time(b) / (3 * reps) * 1e3  # us
 
 
 def main():
+    from multi_modal_transformers_tokenmerge_amd import _C
+    for a in sys.argv[1:]:
+        if a.startswith("--variant="):
+            _C.call("mmt_gemm_set_variant", int(a.split("=")[1]))
+            print("variant", a, flush=True)
     dev = torch.device("cuda")
     rng = torch.tensor([7, 1], dtype=torch.int32, device=dev)
+    if "--sweep" in sys.argv:  # fixed cost vs per-K-step cost of one launch shape
+        for (M, N) in [(18688, 384), (18688, 1536)]:
+            for Kd in [64, 128, 256, 384, 768, 1536]:
+                a = torch.randn((M, Kd), device=dev).bfloat16()
+                b = torch.randn((N, Kd), device=dev).bfloat16()
+                out = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+                us = timeit(lambda: K.gemm(a, b, False, True, out=out, split_k=1))
+                print(f"sweep M={M} N={N} K={Kd:5d}: {us:8.2f} us  {2*M*N*Kd/us/1e6:7.1f} TF/s", flush=True)
+        return
     M1 = 64 * 276
     cases = []
     # (name, M, N, K, ta, tb, out_mode, epi)
