@@ -87,6 +87,22 @@ int mmt_tome_merge_wavg_bwd(const void* g_out, int dtype, int n, int L, int D, i
                             int64_t gi_s_n, int64_t gi_s_t, mmt_stream_t stream);
 
 
+/* ------------------------------------------------------------------ top-k token pruning
+ * mmt_topk_gather replaces tokenizers/token_compression.py:15-46 (compute_top_k_tokens, vmapped
+ * over the batch, :168): for each token set s (host arrays set_start/set_len/set_k, <= 16 sets,
+ * len <= 4096), the indices of jax.lax.top_k(scores[b, start:start+len], k) (descending, equal
+ * scores keep the lower index first, float total order with NaN largest) + start, concatenated
+ * over the sets in the given order -> idx_out (B, K = sum k) int32, and out[b, i] = x[b, idx].
+ * x/out: (B, L, D) / (B, K, D) rows of fp32 or bf16 (dtype), 16-B aligned rows. */
+int mmt_topk_gather(const void* x, int dtype, int B, int L, int D, int64_t xs_b, int64_t xs_t,
+                    const float* scores, int64_t ss_b, int n_sets, const int32_t* set_start,
+                    const int32_t* set_len, const int32_t* set_k, void* out, int64_t os_b,
+                    int64_t os_t, int32_t* idx_out, mmt_stream_t stream);
+/* Backward of the gather: dx = 0, dx[b, idx[b, i]] = dout[b, i]. */
+int mmt_topk_scatter_bwd(const void* dout, int dtype, int B, int K, int D, int64_t ds_b,
+                         int64_t ds_t, const int32_t* idx, int L, void* dx, int64_t xs_b,
+                         int64_t xs_t, mmt_stream_t stream);
+
 /* ------------------------------------------------------------------ GEMM (MFMA bf16)
  * C = epilogue(op(A) . op(B)), fp32 accumulation, replacing every flax.linen.Dense /
  * DenseGeneral on the path (attention.py:32-37 MLPBlock; Flax SelfAttention q/k/v/out

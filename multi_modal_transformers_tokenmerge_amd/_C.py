@@ -30,6 +30,8 @@ SIGNATURES: dict[str, list] = {
     "mmt_tome_match": [P, I, I, I, I, I, L, L, L, I, I, P, P, P, P, P],
     "mmt_tome_merge_wavg_fwd": [P, I, I, I, I, L, L, I, I, I, I, P, P, P, P, P, L, L, P, P, P],
     "mmt_tome_merge_wavg_bwd": [P, I, I, I, I, L, L, I, I, I, P, P, P, P, L, L, P],
+    "mmt_topk_gather": [P, I, I, I, I, L, L, P, L, I, P, P, P, P, L, L, P, P],
+    "mmt_topk_scatter_bwd": [P, I, I, I, I, L, L, P, I, P, L, L, P],
     "mmt_gemm_set_variant": [I],
     "mmt_gemm": [I, I, I, P, I, L, P, I, L, P, I, L, I, L, L, L, I, P, P, L, P],
     "mmt_attn_fwd": [P, L, L, I, I, I, I, F, I, P, P, P, P, F, P, P, L, L, P, P],

@@ -176,6 +176,38 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
     return out
 
 
+# ----------------------------------------------------------------------------- top-k pruning
+def topk_gather(x: torch.Tensor, scores: torch.Tensor, tokenset_idx, tokenset_k):
+    """x (B, L, D) fp32/bf16, scores (B, L) fp32; tokenset_idx [(start, num)], tokenset_k [k].
+    Returns (out (B, sum k, D), idx (B, sum k) int32)."""
+    _dev(x, scores)
+    B, L, D = x.shape
+    if scores.shape != (B, L) or scores.dtype != torch.float32 or scores.stride(1) != 1:
+        raise ValueError("scores must be fp32 (B, L) with unit inner stride")
+    n = len(tokenset_idx)
+    if n != len(tokenset_k):
+        raise ValueError("tokenset_idx and tokenset_k differ in length")
+    starts = (_C.ctypes.c_int32 * n)(*[int(s) for s, _ in tokenset_idx])
+    lens = (_C.ctypes.c_int32 * n)(*[int(m) for _, m in tokenset_idx])
+    ks = (_C.ctypes.c_int32 * n)(*[int(k) for k in tokenset_k])
+    K = int(sum(int(k) for k in tokenset_k))
+    out = torch.empty((B, K, D), dtype=x.dtype, device=x.device)
+    idx = torch.empty((B, K), dtype=torch.int32, device=x.device)
+    _C.call("mmt_topk_gather", ptr(x), _dtype_code(x), B, L, D, x.stride(0), x.stride(1),
+            ptr(scores), scores.stride(0), n, starts, lens, ks, ptr(out), out.stride(0),
+            out.stride(1), ptr(idx), _C.stream_ptr())
+    return out, idx
+
+
+def topk_scatter_bwd(dout: torch.Tensor, idx: torch.Tensor, L: int):
+    _dev(dout, idx)
+    B, K, D = dout.shape
+    dx = torch.empty((B, L, D), dtype=dout.dtype, device=dout.device)
+    _C.call("mmt_topk_scatter_bwd", ptr(dout), _dtype_code(dout), B, K, D, dout.stride(0),
+            dout.stride(1), ptr(idx), L, ptr(dx), dx.stride(0), dx.stride(1), _C.stream_ptr())
+    return dx
+
+
 # ------------------------------------------------------------------------------- attention
 class SetTable:
     """Host-side token-set table of one layer: contiguous sets tiling [0, L) and, per query set,

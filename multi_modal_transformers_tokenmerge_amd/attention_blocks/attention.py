@@ -40,6 +40,21 @@ class LayerCtx:
     sample_offset: int = 0         # global index of this rank's first sample (RNG counters)
 
 
+_SIDE = {}
+
+
+def side_stream(device) -> torch.cuda.Stream:
+    """Second HIP stream for small independent kernels (attention-dropout bits, ToMe matching)
+    that overlap the main stream's GEMMs and attention. Discipline: every side launch follows a
+    fork (side waits on main), and main waits on the side before consuming its results, so
+    tensors passed between the streams are never reused early (this also holds under HIP-graph
+    capture, where the side stream joins the capture through the fork)."""
+    key = torch.device(device).index
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=device)
+    return _SIDE[key]
+
+
 class MLPBlock:
     """attention.py:20-39."""
 
@@ -81,9 +96,27 @@ class Encoder1DBlock:
             return dict(rng=ctx.rng, drop_layer=ctx.layer, drop_site=site, keep_prob=kp,
                         drop_row_offset=ctx.sample_offset * rows_per_sample)
 
+        main = torch.cuda.current_stream()
+        side = side_stream(x.device)
+        bits = None
+        bits_ready = None
+        if train and kpa < 1:  # the (L, L) attention keep mask depends only on the RNG state
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                bits = K.dropout_bits(ctx.rng, ctx.layer, DROP_ATTN, L, L, kpa)
+                bits_ready = torch.cuda.Event()
+                bits_ready.record(side)
         y0, mu0, rs0 = self.ln0.fwd(x)
         qkv = self.qkv.fwd(y0.view(B * L, D)).view(B, L, 3 * D)
-        bits = K.dropout_bits(ctx.rng, ctx.layer, DROP_ATTN, L, L, kpa) if (train and kpa < 1) else None
+        tome_idx = None
+        if ctx.r > 0:  # ToMe matching needs only K: it runs beside attention + out-projection
+            s0, t = ctx.sets.starts[ctx.tome_set], ctx.sets.lens[ctx.tome_set]
+            metric = qkv.view(B, L, 3, H, Dh)[:, s0:s0 + t, 1]     # (B, t, H, Dh): sum_h K
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                tome_idx = K.tome_match(metric, ctx.r)
+        if bits_ready is not None:
+            main.wait_event(bits_ready)
         o, lse = K.attn_fwd(qkv, H, self.scale, ctx.table, bits, kpa)
         # residual stream stays fp32 (sequence-axis LayerNorm conditioning, csrc/norm.hip)
         x1 = self.out.fwd(o.view(B * L, D), residual=x.view(B * L, D), out_mode=K.OUT_F32,
@@ -92,11 +125,12 @@ class Encoder1DBlock:
         tome = None
         new_size = size
         if ctx.r > 0:
-            s0, t = ctx.sets.starts[ctx.tome_set], ctx.sets.lens[ctx.tome_set]
-            metric = qkv.view(B, L, 3, H, Dh)[:, s0:s0 + t, 1]     # (B, t, H, Dh): sum_h K
-            unm, src, dst = K.tome_match(metric, ctx.r)
+            main.wait_stream(side)
+            unm, src, dst = tome_idx
             x1, new_size, pos = K.tome_merge_fwd(x1, s0, t, ctx.r, unm, src, dst, size_in=size)
             tome = (s0, t, ctx.r, pos, size, new_size, unm, src, dst)
+        elif bits_ready is not None:
+            main.wait_stream(side)
         L2 = x1.shape[1]
         y1, mu1, rs1 = self.ln1.fwd(x1)
         h = self.mlp.dense.fwd(y1.view(B * L2, D), act=K.ACT_RELU, **drop(DROP_MLP_HIDDEN, L2))

@@ -286,8 +286,6 @@ struct Vec<float> {
   }
 };
 
-constexpr int kMergeRowsPerBlock = 16;
-
 // Set-local output row q -> (primary set token, dst index j or -1 for an unmerged a token).
 __device__ __forceinline__ void merged_row_source(int q, int ta, int r, bool dis,
                                                   const int32_t* unm, int* tok, int* j) {
@@ -311,6 +309,14 @@ __device__ __forceinline__ void merged_row_source(int q, int ta, int r, bool dis
   }
 }
 
+// Forward merge, one block = kMergeRows output rows of one sample. Phase 1 resolves every output
+// row (primary source row, size weight, divisor, and the list of src tokens scattered into it,
+// in increasing i = the reference's sequential scatter order) into LDS; phase 2 streams the
+// (row, 16-B chunk) items of the block with all primary loads of a 4-item group issued before
+// any use, so many loads are in flight per thread (HBM-bound gather).
+constexpr int kMergeRows = 8;
+constexpr int kMergeSeg = 8;  // src tokens listed per row in LDS (more: scan the dst list)
+
 template <typename T>
 __global__ __launch_bounds__(256) void tome_merge_fwd_kernel(
     const T* __restrict__ x, int L, int D, int64_t xs_n, int64_t xs_t, int set_start, int t, int r,
@@ -320,6 +326,10 @@ __global__ __launch_bounds__(256) void tome_merge_fwd_kernel(
   __shared__ int32_t s_unm[1024];
   __shared__ int32_t s_src[512];
   __shared__ int32_t s_dst[512];
+  __shared__ int32_t m_prim[kMergeRows], m_cnt[kMergeRows], m_j[kMergeRows];
+  __shared__ float m_sp[kMergeRows], m_S[kMergeRows];
+  __shared__ int32_t m_list[kMergeRows][kMergeSeg];
+  __shared__ float m_ss[kMergeRows][kMergeSeg];
   const int n = blockIdx.x;
   const int ta = (t + 1) / 2;
   const int nu = ta - r;
@@ -332,56 +342,40 @@ __global__ __launch_bounds__(256) void tome_merge_fwd_kernel(
     s_dst[k] = dst_g[(int64_t)n * r + k];
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr int V = Vec<T>::N;
-  const int nchunk = D / V;
-  const T* xb = x + (int64_t)n * xs_n;
-  T* ob = out + (int64_t)n * os_n;
   const float* sb = size_in ? size_in + (int64_t)n * t : nullptr;
   const int Lout = L - r;
-  const int row0 = blockIdx.y * kMergeRowsPerBlock;
-  for (int o = row0 + wave; o < min(Lout, row0 + kMergeRowsPerBlock); o += 4) {
+  const int row0 = blockIdx.y * kMergeRows;
+  const int nrows = min(kMergeRows, Lout - row0);
+  if (threadIdx.x < nrows) {  // phase 1: one thread per output row
+    const int ri = threadIdx.x, o = row0 + ri;
     if (o < set_start || o >= set_start + t - r) {  // plain copy of a non-merged token
-      const int src_row = o < set_start ? o : o + r;
-      const T* ip = xb + (int64_t)src_row * xs_t;
-      T* op = ob + (int64_t)o * os_t;
-      for (int ch = lane; ch < nchunk; ch += 64)
-        *reinterpret_cast<typename Vec<T>::raw*>(op + ch * V) =
-            *reinterpret_cast<const typename Vec<T>::raw*>(ip + ch * V);
-      continue;
-    }
-    const int q = o - set_start;
-    const T* xs = xb + (int64_t)set_start * xs_t;  // the merged token set
-    int tok, j;
-    merged_row_source(q, ta, r, dis, s_unm, &tok, &j);
-    const float sp = (sb && !plain) ? sb[tok] : 1.f;
-    // sizes: S = s_primary + sum_i s_src_i in increasing i (sequential scatter-add, :100-101)
-    float S = sb ? sb[tok] : 1.f;
-    if (j >= 0 && scatter)
-      for (int i = 0; i < r; ++i)
-        if (s_dst[i] == j) S = S + (sb ? sb[2 * s_src[i]] : 1.f);
-    for (int ch = lane; ch < nchunk; ch += 64) {
-      float acc[V], v[V];
-      Vec<T>::load(xs + (int64_t)tok * xs_t + ch * V, v);
-#pragma unroll
-      for (int e = 0; e < V; ++e) acc[e] = v[e] * sp;
+      m_prim[ri] = o < set_start ? o : o + r;
+      m_j[ri] = -2;
+      m_cnt[ri] = 0;
+    } else {
+      const int q = o - set_start;
+      int tok, j;
+      merged_row_source(q, ta, r, dis, s_unm, &tok, &j);
+      m_prim[ri] = set_start + tok;
+      m_sp[ri] = (sb && !plain) ? sb[tok] : 1.f;
+      // sizes: S = s_primary + sum_i s_src_i in increasing i (sequential scatter-add, :100-101)
+      float S = sb ? sb[tok] : 1.f;
+      int cnt = 0;
       if (j >= 0 && scatter) {
         for (int i = 0; i < r; ++i) {
           if (s_dst[i] != j) continue;
           const int st = 2 * s_src[i];
-          const float ss = (sb && !plain) ? sb[st] : 1.f;
-          Vec<T>::load(xs + (int64_t)st * xs_t + ch * V, v);
-#pragma unroll
-          for (int e = 0; e < V; ++e) acc[e] = acc[e] + v[e] * ss;
+          S = S + (sb ? sb[st] : 1.f);
+          if (cnt < kMergeSeg) {
+            m_list[ri][cnt] = set_start + st;
+            m_ss[ri][cnt] = (sb && !plain) ? sb[st] : 1.f;
+          }
+          ++cnt;
         }
       }
-      if (!plain) {
-#pragma unroll
-        for (int e = 0; e < V; ++e) acc[e] = __fdiv_rn(acc[e], S);
-      }
-      Vec<T>::store(ob + (int64_t)o * os_t + ch * V, acc);
-    }
-    if (lane == 0) {
+      m_j[ri] = (j >= 0 && scatter) ? j : -1;
+      m_cnt[ri] = cnt;
+      m_S[ri] = S;
       if (size_out) size_out[(int64_t)n * (t - r) + q] = S;
       if (pos_map) {
         int32_t* pm = pos_map + (int64_t)n * t;
@@ -392,41 +386,122 @@ __global__ __launch_bounds__(256) void tome_merge_fwd_kernel(
       }
     }
   }
+  __syncthreads();
+  constexpr int V = Vec<T>::N;
+  const int nchunk = D / V;
+  const T* xb = x + (int64_t)n * xs_n;
+  T* ob = out + (int64_t)n * os_n;
+  const int total = nrows * nchunk;
+  constexpr int G = 4;  // items per thread whose loads are issued together
+  for (int base = 0; base < total; base += G * 256) {
+    float v[G][V];
+    int ri[G], ch[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {  // clamped (always valid) addresses: loads issue unconditionally
+      const int idx = min(base + u * 256 + (int)threadIdx.x, total - 1);
+      ri[u] = idx / nchunk;
+      ch[u] = idx - ri[u] * nchunk;
+      Vec<T>::load(xb + (int64_t)m_prim[ri[u]] * xs_t + ch[u] * V, v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      if (base + u * 256 + (int)threadIdx.x >= total) break;
+      const int rr = ri[u];
+      const int64_t ooff = (int64_t)(row0 + rr) * os_t + ch[u] * V;
+      const int jr = m_j[rr];
+      if (jr == -2) {  // copy row
+        Vec<T>::store(ob + ooff, v[u]);
+        continue;
+      }
+      float acc[V];
+      const float sp = m_sp[rr];
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] = v[u][e] * sp;
+      const int cnt = m_cnt[rr];
+      if (cnt <= kMergeSeg) {
+        for (int k = 0; k < cnt; ++k) {
+          float w[V];
+          Vec<T>::load(xb + (int64_t)m_list[rr][k] * xs_t + ch[u] * V, w);
+          const float ss = m_ss[rr][k];
+#pragma unroll
+          for (int e = 0; e < V; ++e) acc[e] = acc[e] + w[e] * ss;
+        }
+      } else {
+        for (int i = 0; i < r; ++i) {
+          if (s_dst[i] != jr) continue;
+          const int st = 2 * s_src[i];
+          const float ss = (sb && !plain) ? sb[st] : 1.f;
+          float w[V];
+          Vec<T>::load(xb + (int64_t)(set_start + st) * xs_t + ch[u] * V, w);
+#pragma unroll
+          for (int e = 0; e < V; ++e) acc[e] = acc[e] + w[e] * ss;
+        }
+      }
+      if (!plain) {
+        const float S = m_S[rr];
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] = __fdiv_rn(acc[e], S);
+      }
+      Vec<T>::store(ob + ooff, acc);
+    }
+  }
 }
 
+// Backward merge: g_in[row] = g_out[pos(row)] * s_tok / S_pos for set tokens (a weighted
+// gather), a copy elsewhere. One block = kMergeRows input rows; (row, chunk) items streamed
+// with 4 loads in flight per thread.
 template <typename T>
 __global__ __launch_bounds__(256) void tome_merge_bwd_kernel(
     const T* __restrict__ g_out, int L, int D, int64_t go_s_n, int64_t go_s_t, int set_start,
     int t, int r, const float* __restrict__ size_in, const float* __restrict__ size_out,
     const int32_t* __restrict__ pos_map, T* __restrict__ g_in, int64_t gi_s_n, int64_t gi_s_t) {
+  __shared__ int32_t m_orow[kMergeRows];
+  __shared__ float m_s[kMergeRows], m_S[kMergeRows];
+  __shared__ int32_t m_copy[kMergeRows];
   const int n = blockIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row0 = blockIdx.y * kMergeRows;
+  const int nrows = min(kMergeRows, L - row0);
+  if (threadIdx.x < nrows) {
+    const int ri = threadIdx.x, row = row0 + ri;
+    if (row < set_start || row >= set_start + t) {
+      m_orow[ri] = row < set_start ? row : row - r;
+      m_copy[ri] = 1;
+    } else {
+      const int tok = row - set_start;
+      const int q = pos_map[(int64_t)n * t + tok];
+      m_orow[ri] = set_start + q;
+      m_s[ri] = size_in ? size_in[(int64_t)n * t + tok] : 1.f;
+      m_S[ri] = size_out ? size_out[(int64_t)n * (t - r) + q] : 1.f;  // NULL: plain sum
+      m_copy[ri] = 0;
+    }
+  }
+  __syncthreads();
   constexpr int V = Vec<T>::N;
   const int nchunk = D / V;
   const T* gb = g_out + (int64_t)n * go_s_n;
   T* ib = g_in + (int64_t)n * gi_s_n;
-  const int row0 = blockIdx.y * kMergeRowsPerBlock;
-  for (int row = row0 + wave; row < min(L, row0 + kMergeRowsPerBlock); row += 4) {
-    T* ip = ib + (int64_t)row * gi_s_t;
-    if (row < set_start || row >= set_start + t) {
-      const int orow = row < set_start ? row : row - r;
-      const T* op = gb + (int64_t)orow * go_s_t;
-      for (int ch = lane; ch < nchunk; ch += 64)
-        *reinterpret_cast<typename Vec<T>::raw*>(ip + ch * V) =
-            *reinterpret_cast<const typename Vec<T>::raw*>(op + ch * V);
-      continue;
-    }
-    const int tok = row - set_start;
-    const int q = pos_map[(int64_t)n * t + tok];
-    const float s = size_in ? size_in[(int64_t)n * t + tok] : 1.f;
-    const float S = size_out ? size_out[(int64_t)n * (t - r) + q] : 1.f;  // NULL: plain sum
-    const T* op = gb + (int64_t)(set_start + q) * go_s_t;
-    for (int ch = lane; ch < nchunk; ch += 64) {
-      float v[V];
-      Vec<T>::load(op + ch * V, v);
+  const int total = nrows * nchunk;
+  constexpr int G = 4;
+  for (int base = 0; base < total; base += G * 256) {
+    float v[G][V];
+    int ri[G], ch[G];
 #pragma unroll
-      for (int e = 0; e < V; ++e) v[e] = (v[e] * s) / S;
-      Vec<T>::store(ip + ch * V, v);
+    for (int u = 0; u < G; ++u) {
+      const int idx = min(base + u * 256 + (int)threadIdx.x, total - 1);
+      ri[u] = idx / nchunk;
+      ch[u] = idx - ri[u] * nchunk;
+      Vec<T>::load(gb + (int64_t)m_orow[ri[u]] * go_s_t + ch[u] * V, v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      if (base + u * 256 + (int)threadIdx.x >= total) break;
+      const int rr = ri[u];
+      if (!m_copy[rr]) {
+        const float s = m_s[rr], S = m_S[rr];
+#pragma unroll
+        for (int e = 0; e < V; ++e) v[u][e] = (v[u][e] * s) / S;
+      }
+      Vec<T>::store(ib + (int64_t)(row0 + rr) * gi_s_t + ch[u] * V, v[u]);
     }
   }
 }
@@ -501,7 +576,7 @@ extern "C" int mmt_tome_merge_wavg_fwd(const void* x, int dtype, int n, int L, i
   MMT_CHECK_ARG(dtype == MMT_F32 || dtype == MMT_BF16, "mmt_tome_merge_wavg_fwd: dtype");
   MMT_CHECK_ARG(check_vec(dtype, D, x_s_n, x_s_t, o_s_n, o_s_t),
                 "mmt_tome_merge_wavg_fwd: D and strides must be multiples of 16 bytes");
-  dim3 grid(n, (L - r + kMergeRowsPerBlock - 1) / kMergeRowsPerBlock);
+  dim3 grid(n, (L - r + kMergeRows - 1) / kMergeRows);
   hipStream_t s = as_stream(stream);
   if (dtype == MMT_F32)
     hipLaunchKernelGGL(tome_merge_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)x, L, D,
@@ -527,7 +602,7 @@ extern "C" int mmt_tome_merge_wavg_bwd(const void* g_out, int dtype, int n, int 
   MMT_CHECK_ARG(dtype == MMT_F32 || dtype == MMT_BF16, "mmt_tome_merge_wavg_bwd: dtype");
   MMT_CHECK_ARG(check_vec(dtype, D, go_s_n, go_s_t, gi_s_n, gi_s_t),
                 "mmt_tome_merge_wavg_bwd: D and strides must be multiples of 16 bytes");
-  dim3 grid(n, (L + kMergeRowsPerBlock - 1) / kMergeRowsPerBlock);
+  dim3 grid(n, (L + kMergeRows - 1) / kMergeRows);
   hipStream_t s = as_stream(stream);
   if (dtype == MMT_F32)
     hipLaunchKernelGGL(tome_merge_bwd_kernel<float>, grid, dim3(256), 0, s, (const float*)g_out, L,

@@ -96,5 +96,33 @@ def merge_wavg(merge: Callable, x: torch.Tensor,
     return out, size_out[..., None]
 
 
-def compute_top_k_tokens(*args, **kwargs):  # reference :15-46 (pruning) — SURVEY §8f "next"
-    raise NotImplementedError("top-k token pruning is SURVEY §8(f) row 1 (next), not built yet")
+class _TopKFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, embeddings, scores, tokenset_idx, tokenset_k):
+        out, idx = K.topk_gather(embeddings, scores, tokenset_idx, tokenset_k)
+        ctx.save_for_backward(idx)
+        ctx.L = embeddings.shape[1]
+        ctx.mark_non_differentiable(idx)
+        return out, idx
+
+    @staticmethod
+    def backward(ctx, g_out, _g_idx):
+        (idx,) = ctx.saved_tensors
+        return K.topk_scatter_bwd(g_out.contiguous(), idx, ctx.L), None, None, None
+
+
+def compute_top_k_tokens(embeddings: torch.Tensor, importance_scores: torch.Tensor,
+                         tokenset_idx, tokenset_k, return_indices: bool = False):
+    """Reference token_compression.py:15-46: per token set (start, num_tokens), the tokens with
+    the k largest importance scores (jax.lax.top_k order: descending, ties to the lower index),
+    the sets concatenated in order. Accepts the reference's single-sample (L, D) / (L,) call or
+    the vmapped batch (B, L, D) / (B, L) (:168). Differentiable w.r.t. the embeddings (the
+    indices carry no gradient). One gfx950 kernel (csrc/prune.hip)."""
+    single = embeddings.dim() == 2
+    x = embeddings[None] if single else embeddings
+    sc = importance_scores[None] if single else importance_scores
+    out, idx = _TopKFn.apply(x.contiguous(), sc.float().contiguous(), list(tokenset_idx),
+                             list(tokenset_k))
+    if single:
+        out, idx = out[0], idx[0]
+    return (out, idx) if return_indices else out

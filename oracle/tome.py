@@ -160,3 +160,22 @@ def canon_merge_bwd(g_out: np.ndarray, size_in, size_out, pos_map) -> np.ndarray
     g = np.take_along_axis(g_out, pos_map[..., None].astype(np.int64), axis=1)
     S = np.take_along_axis(size_out, pos_map.astype(np.int64), axis=1)
     return ((g * s[..., None]) / S[..., None]).astype(np.float32)
+
+
+def topk_tokens(embeddings: np.ndarray, scores: np.ndarray, tokenset_idx, tokenset_k):
+    """Literal restatement of token_compression.py:15-46 for one sample: jax.lax.top_k per set
+    (descending; equal values keep the lower index first; lax's float total order, NaN largest),
+    indices + set start, concatenated, then take(embeddings, ids, axis=0)."""
+    def key(v):
+        v = np.float32(v)
+        if np.isnan(v):
+            return (1, 0)
+        return (0, float(v) if v != 0 else (0.0 if not np.signbit(v) else -0.0),
+                0 if np.signbit(v) else 1)
+    ids = []
+    for (start, num), k in zip(tokenset_idx, tokenset_k):
+        sub = scores[start:start + num]
+        order = sorted(range(num), key=lambda i: (tuple(-x for x in key(sub[i])), i))
+        ids.extend(start + i for i in order[:k])
+    ids = np.asarray(ids, dtype=np.int32)
+    return embeddings[ids], ids
