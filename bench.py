@@ -6,6 +6,8 @@ metric, config[2] (the single-GPU line uses the same workload at N=1).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config NAME]
     torchrun --nproc-per-node N bench.py --gpus N ...          (one process per GPU, RCCL)
 
+Per-GPU batch 256 by default (measured 5.7k / 7.4k / 8.6k / 9.1k samples/s at B = 64 / 128 / 256 /
+512 on one MI355X: at B = 64 the launches are too small to fill 256 CUs; see DESIGN.md "Batch").
 One step = zero grads -> forward (frozen T5, image stem, 12 ToMe blocks, diffusion loss) ->
 backward -> [gradient all-reduce over RCCL] -> fused AdamW -> device step counter, on synthetic
 inputs resident in HBM (numpy default_rng(0) shapes of SURVEY §8d). The N=1 step is one HIP graph
@@ -177,7 +179,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=256,
+                    help="per-GPU batch (256: see DESIGN.md 'Batch'; 64 leaves the chip underfilled)")
     ap.add_argument("--config", default="octo-small-tome16")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")

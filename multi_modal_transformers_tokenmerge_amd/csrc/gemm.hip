@@ -24,15 +24,37 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short short4v __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+#ifdef MMT_GEMM_TRACE  // tools/gemm_trace.cpp: per-workgroup phase timestamps (wave 0)
+__device__ unsigned long long g_gemm_trace[1 << 16][5];
+#define GEMM_TRACE(i)                                                                          \
+  do {                                                                                         \
+    __builtin_amdgcn_s_waitcnt(0);                                                             \
+    if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) {                                          \
+      g_gemm_trace[blockIdx.x][i] = wall_clock64();                                            \
+      if ((i) == 0) g_gemm_trace[blockIdx.x][4] = __smid();                                    \
+    }                                                                                          \
+  } while (0)
+#else
+#define GEMM_TRACE(i) \
+  do {                \
+  } while (0)
+#endif
+
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int KC_STRIDE = BK + 8;   // K-contiguous tile [128][72] bf16 (144 B rows)
-constexpr int MC_STRIDE = BM + 8;   // M/N-contiguous tile [64][136] bf16 (272 B rows)
-constexpr int TILE_ELEMS = 128 * KC_STRIDE;  // >= 64 * MC_STRIDE
+constexpr int BM = 128, BN = 128;
 constexpr int NTHREADS = 256;
+constexpr int MC_STRIDE = BM + 8;   // M/N-contiguous tile [BK][136] bf16 (272 B rows)
+// LDS geometry per K-step depth BKT (64 or 128)
+template <int BKT>
+struct Geom {
+  static constexpr int KCS = BKT + 8;                      // K-contiguous tile [128][BKT+8]
+  static constexpr int TILE = 128 * KCS > BKT * MC_STRIDE ? 128 * KCS : BKT * MC_STRIDE;
+  static constexpr int Q = 128 * BKT / 8 / NTHREADS;       // 16-B chunks per thread per operand
+};
 
-// tuning knob: 0 / 1 = force PIPE 0 / 1; -1 or 3 = by K-steps per work item (PIPE 1 up to 24)
+// tuning knob: 0 = PIPE 0 / BK 64, 1 = PIPE 1 / BK 64, 2 = PIPE 1 / BK 128; other = by K-steps
+// per work item (PIPE 1 up to 24 steps of 64)
 int g_variant = -1;
 
 struct Epi {
@@ -56,40 +78,41 @@ struct Epi {
 // extent to be a multiple of 8, checked by mmt_gemm); store_tile zeroes the out-of-range chunks
 // when it writes LDS. Keeping the mask out of the load lets the compiler count vmcnt waits (a
 // predicated load forces vmcnt(0)) and leaves the loads in flight until the store.
-template <bool KCONTIG>
+template <bool KCONTIG, int BKT>
 __device__ __forceinline__ void chunk_of(int c, int r0, int k0, int& row, int& kk) {
-  if (KCONTIG) {  // [row][k]: 8 chunks of 8 per row
-    row = r0 + (c >> 3);
-    kk = k0 + (c & 7) * 8;
+  if (KCONTIG) {  // [row][k]: BKT/8 chunks of 8 per row
+    row = r0 + c / (BKT / 8);
+    kk = k0 + (c % (BKT / 8)) * 8;
   } else {        // [k][row]: 16 chunks of 8 per k-row
     kk = k0 + (c >> 4);
     row = r0 + (c & 15) * 8;
   }
 }
 
-template <bool KCONTIG>
+template <bool KCONTIG, int BKT>
 __device__ __forceinline__ void load_tile(const bf16_t* __restrict__ P, int64_t ld, int rows_lim,
-                                          int k_lim, int r0, int k0, uint4 (&reg)[4]) {
+                                          int k_lim, int r0, int k0, uint4 (&reg)[Geom<BKT>::Q]) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < Geom<BKT>::Q; ++q) {
     int row, kk;
-    chunk_of<KCONTIG>(threadIdx.x + q * NTHREADS, r0, k0, row, kk);
+    chunk_of<KCONTIG, BKT>(threadIdx.x + q * NTHREADS, r0, k0, row, kk);
     const bf16_t* p = KCONTIG ? P + (int64_t)min(row, rows_lim - 1) * ld + min(kk, k_lim - 8)
                               : P + (int64_t)min(kk, k_lim - 1) * ld + min(row, rows_lim - 8);
     reg[q] = *reinterpret_cast<const uint4*>(p);
   }
 }
 
-template <bool KCONTIG>
-__device__ __forceinline__ void store_tile(bf16_t* __restrict__ S, const uint4 (&reg)[4],
+template <bool KCONTIG, int BKT>
+__device__ __forceinline__ void store_tile(bf16_t* __restrict__ S, const uint4 (&reg)[Geom<BKT>::Q],
                                            int rows_lim, int k_lim, int r0, int k0) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < Geom<BKT>::Q; ++q) {
     const int c = threadIdx.x + q * NTHREADS;
     int row, kk;
-    chunk_of<KCONTIG>(c, r0, k0, row, kk);
+    chunk_of<KCONTIG, BKT>(c, r0, k0, row, kk);
     const uint32_t m = (row < rows_lim && kk < k_lim) ? 0xffffffffu : 0u;
-    const int off = KCONTIG ? (c >> 3) * KC_STRIDE + (c & 7) * 8 : (c >> 4) * MC_STRIDE + (c & 15) * 8;
+    const int off = KCONTIG ? (c / (BKT / 8)) * Geom<BKT>::KCS + (c % (BKT / 8)) * 8
+                            : (c >> 4) * MC_STRIDE + (c & 15) * 8;
     *reinterpret_cast<uint4*>(S + off) =
         make_uint4(reg[q].x & m, reg[q].y & m, reg[q].z & m, reg[q].w & m);
   }
@@ -101,10 +124,10 @@ __device__ __forceinline__ short4v tr_read(const bf16_t* p) {
 }
 
 // MFMA 32x32x16 operand fragment: lane (r = lane&31, h = lane>>5) holds X[r][k = 8h + j].
-template <bool KCONTIG>
+template <bool KCONTIG, int KCS>
 __device__ __forceinline__ bf16x8 load_frag(const bf16_t* S, int rbase, int ks, int lane) {
   if (KCONTIG) {
-    const bf16_t* p = S + (rbase + (lane & 31)) * KC_STRIDE + ks * 16 + 8 * (lane >> 5);
+    const bf16_t* p = S + (rbase + (lane & 31)) * KCS + ks * 16 + 8 * (lane >> 5);
     return *reinterpret_cast<const bf16x8*>(p);
   } else {
     const int i = lane & 15, q = i >> 2, p4 = i & 3, g = lane >> 4, h = lane >> 5;
@@ -224,7 +247,7 @@ struct Work {
   int bz, ks, m0, n0, kbeg, kend, nk;
 };
 __device__ __forceinline__ Work decode_work(int w, int tiles_n, int tiles, int split_k, int K,
-                                            int k_chunk) {
+                                            int k_chunk, int bk) {
   Work r;
   const int z = w / tiles, t = w - z * tiles;
   r.bz = z / split_k;
@@ -234,7 +257,7 @@ __device__ __forceinline__ Work decode_work(int w, int tiles_n, int tiles, int s
   r.n0 = (t - tm * tiles_n) * BN;
   r.kbeg = r.ks * k_chunk;
   r.kend = min(K, r.kbeg + k_chunk);
-  r.nk = max(0, (r.kend - r.kbeg + BK - 1) / BK);
+  r.nk = max(0, (r.kend - r.kbeg + bk - 1) / bk);
   return r;
 }
 
@@ -243,19 +266,23 @@ __device__ __forceinline__ Work decode_work(int w, int tiles_n, int tiles, int s
 // items (tiles sharing an A row-panel share that XCD's L2).
 // PIPE 0: double-buffered LDS, operands prefetched one K-step ahead through registers (one
 //         barrier per K-step, 2 workgroups/CU) — long K loops.
-// PIPE 1: a single LDS stage (write-after-barrier, two barriers per K-step), 36 KB so 3
-//         workgroups/CU — short K loops (measured better up to ~24 K-steps). A persistent
-//         variant of it (next tile's loads issued before the epilogue) measured slower.
+// PIPE 1: a single LDS stage (write-after-barrier, two barriers per K-step) — short K loops
+//         (measured better up to ~24 K-steps); BKT 64: 36 KB, 3 workgroups/CU; BKT 128: 70 KB,
+//         2 workgroups/CU, half the latency-bound K-step round trips. A persistent variant
+//         (next tile's loads issued before the epilogue) measured slower.
 // Epilogue (OUT 0/1): the transposed accumulator runs go to an LDS row-major fp32 tile (16-B
 // writes), then 16 threads per row apply the epilogue on 8 columns each (256-B coalesced row
 // segments for C / gate / residual). Split-K slabs (OUT 2) are stored straight from registers.
-template <bool TA, bool TB, int OUT, int PIPE>
-__global__ __launch_bounds__(NTHREADS, PIPE == 1 ? 3 : 2) void gemm_kernel(
+template <bool TA, bool TB, int OUT, int PIPE, int BK>
+__global__ __launch_bounds__(NTHREADS, (PIPE == 1 && BK == 64) ? 3 : 2) void gemm_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A0, int64_t lda, int64_t sA,
     const bf16_t* __restrict__ B0, int64_t ldb, int64_t sB, void* __restrict__ Cv, int64_t ldc,
     int64_t sC, int split_k, int k_chunk, int tiles_n, int n_work, Epi epi) {
   constexpr bool DB = PIPE == 0;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[(DB ? 4 : 2) * TILE_ELEMS];
+  constexpr int TILE_ELEMS = Geom<BK>::TILE;
+  constexpr int KCS = Geom<BK>::KCS;
+  constexpr int SMEM_ELEMS = (DB ? 4 : 2) * TILE_ELEMS;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM_ELEMS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1, hl = lane >> 5;
   const int tiles = ((M + BM - 1) / BM) * tiles_n;
@@ -278,9 +305,9 @@ __global__ __launch_bounds__(NTHREADS, PIPE == 1 ? 3 : 2) void gemm_kernel(
     for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8 af[2], bfr[2];
 #pragma unroll
-      for (int a = 0; a < 2; ++a) af[a] = load_frag<A_KC>(As, wm * 64 + a * 32, ks, lane);
+      for (int a = 0; a < 2; ++a) af[a] = load_frag<A_KC, KCS>(As, wm * 64 + a * 32, ks, lane);
 #pragma unroll
-      for (int b = 0; b < 2; ++b) bfr[b] = load_frag<B_KC>(Bs, wn * 64 + b * 32, ks, lane);
+      for (int b = 0; b < 2; ++b) bfr[b] = load_frag<B_KC, KCS>(Bs, wn * 64 + b * 32, ks, lane);
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -288,16 +315,16 @@ __global__ __launch_bounds__(NTHREADS, PIPE == 1 ? 3 : 2) void gemm_kernel(
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
     }
   };
-  uint4 ra[4], rb[4];
+  uint4 ra[Geom<BK>::Q], rb[Geom<BK>::Q];
   auto load_step = [&](const Work& w, int kt) {
     const int k0 = w.kbeg + kt * BK;
-    load_tile<A_KC>(A0 + w.bz * sA, lda, M, w.kend, w.m0, k0, ra);
-    load_tile<B_KC>(B0 + w.bz * sB, ldb, N, w.kend, w.n0, k0, rb);
+    load_tile<A_KC, BK>(A0 + w.bz * sA, lda, M, w.kend, w.m0, k0, ra);
+    load_tile<B_KC, BK>(B0 + w.bz * sB, ldb, N, w.kend, w.n0, k0, rb);
   };
   auto store_step = [&](const Work& w, int kt, bf16_t* S) {
     const int k0 = w.kbeg + kt * BK;
-    store_tile<A_KC>(S, ra, M, w.kend, w.m0, k0);
-    store_tile<B_KC>(S + TILE_ELEMS, rb, N, w.kend, w.n0, k0);
+    store_tile<A_KC, BK>(S, ra, M, w.kend, w.m0, k0);
+    store_tile<B_KC, BK>(S + TILE_ELEMS, rb, N, w.kend, w.n0, k0);
   };
 
   // lane (m = lane & 31, h) of accumulator block (a, b) holds row m, columns 8g + 4h + {0..3}
@@ -321,23 +348,23 @@ __global__ __launch_bounds__(NTHREADS, PIPE == 1 ? 3 : 2) void gemm_kernel(
       return;
     }
     constexpr int CTS = BN + 4;         // staging row stride (floats): conflict-free 16-B writes
-    constexpr int HALVES = DB ? 1 : 2;  // one LDS stage holds 64 of the 128 rows at a time
+    constexpr int HALVES = BM * CTS * 4 <= SMEM_ELEMS * 2 ? 1 : 2;  // whole tile or 64-row halves
     constexpr int ROWS = BM / HALVES;
-    static_assert(ROWS * CTS * 4 <= (DB ? 4 : 2) * TILE_ELEMS * 2, "staging tile exceeds the LDS");
+    static_assert(ROWS * CTS * 4 <= SMEM_ELEMS * 2, "staging tile exceeds the LDS");
     float* Ct = reinterpret_cast<float*>(smem);
     const int c8 = (threadIdx.x & 15) * 8;
     const int gc = w.n0 + c8;
 #pragma unroll 1
     for (int hf = 0; hf < HALVES; ++hf) {
       __syncthreads();  // operand tile (hf 0) / the previous half (hf 1) consumed
-      if (DB || wm == hf) {
+      if (HALVES == 1 || wm == hf) {
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
           for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-              const int r = (DB ? wm * 64 : 0) + a * 32 + (lane & 31);
+              const int r = (HALVES == 1 ? wm * 64 : 0) + a * 32 + (lane & 31);
               *reinterpret_cast<float4*>(Ct + r * CTS + wn * 64 + b * 32 + 8 * g + 4 * hl) =
                   make_float4(acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2],
                               acc[a][b][4 * g + 3]);
@@ -359,7 +386,7 @@ __global__ __launch_bounds__(NTHREADS, PIPE == 1 ? 3 : 2) void gemm_kernel(
 
   zero_acc();
   if (DB) {
-    const Work w = decode_work(xcd_remap(blockIdx.x, gridDim.x), tiles_n, tiles, split_k, K, k_chunk);
+    const Work w = decode_work(xcd_remap(blockIdx.x, gridDim.x), tiles_n, tiles, split_k, K, k_chunk, BK);
     if (w.nk > 0) {
       load_step(w, 0);
       store_step(w, 0, smem);
@@ -375,16 +402,20 @@ __global__ __launch_bounds__(NTHREADS, PIPE == 1 ? 3 : 2) void gemm_kernel(
     }
     epilogue(w);
   } else {
-    const Work w = decode_work(xcd_remap(blockIdx.x, gridDim.x), tiles_n, tiles, split_k, K, k_chunk);
+    GEMM_TRACE(0);
+    const Work w = decode_work(xcd_remap(blockIdx.x, gridDim.x), tiles_n, tiles, split_k, K, k_chunk, BK);
     if (w.nk > 0) load_step(w, 0);
     for (int kt = 0; kt < w.nk; ++kt) {
       if (kt > 0) __syncthreads();  // every wave is done reading the previous K-step
       store_step(w, kt, smem);
+      if (kt == 0) GEMM_TRACE(1);
       __syncthreads();
       if (kt + 1 < w.nk) load_step(w, kt + 1);  // in flight during this K-step's MFMAs
       mma_tile(smem, smem + TILE_ELEMS);
     }
+    GEMM_TRACE(2);
     epilogue(w);
+    GEMM_TRACE(3);
   }
 }
 
@@ -475,23 +506,24 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
                   "mmt_gemm: split-K needs a 16-B aligned workspace of split_k*M*N floats");
     out_kind = 2;
   }
-  const int k_chunk = ((K + split_k - 1) / split_k + BK - 1) / BK * BK;
+  const int k_chunk = ((K + split_k - 1) / split_k + 63) / 64 * 64;
   if (out_kind == 2) split_k = (K + k_chunk - 1) / k_chunk;  // no empty K-splits
   const int n_work = tiles_m * tiles_n * batch * split_k;
-  const int pipe = (g_variant >= 0 && (g_variant & 3) != 3) ? (g_variant & 1)
-                                                            : (k_chunk / BK > 24 ? 0 : 1);
+  // 0: PIPE 0 / BK 64, 1: PIPE 1 / BK 64, 2: PIPE 1 / BK 128
+  const int pipe = (g_variant >= 0 && g_variant <= 2) ? g_variant : (k_chunk / 64 > 24 ? 0 : 1);
   const int grid_x = n_work;
   void* Cdst = out_kind == 2 ? (void*)workspace : C;
   const int64_t ldd = out_kind == 2 ? (int64_t)N : ldc;
   const int64_t sdd = out_kind == 2 ? (int64_t)M * N : sC;
-#define GL1(TA, TB, OUT, P)                                                                        \
-  hipLaunchKernelGGL((gemm_kernel<TA, TB, OUT, P>), dim3(grid_x), dim3(NTHREADS), 0, s, M, N, K,   \
-                     (const bf16_t*)A, lda, sA, (const bf16_t*)B, ldb, sB, Cdst, ldd, sdd,        \
+#define GL1(TA, TB, OUT, P, BKT)                                                                   \
+  hipLaunchKernelGGL((gemm_kernel<TA, TB, OUT, P, BKT>), dim3(grid_x), dim3(NTHREADS), 0, s, M, N, \
+                     K, (const bf16_t*)A, lda, sA, (const bf16_t*)B, ldb, sB, Cdst, ldd, sdd,     \
                      split_k, k_chunk, tiles_n, n_work, epi)
 #define GL(TA, TB, OUT)                         \
   do {                                          \
-    if (pipe == 0) GL1(TA, TB, OUT, 0);         \
-    else GL1(TA, TB, OUT, 1);                   \
+    if (pipe == 0) GL1(TA, TB, OUT, 0, 64);     \
+    else if (pipe == 1) GL1(TA, TB, OUT, 1, 64); \
+    else GL1(TA, TB, OUT, 1, 128);              \
   } while (0)
 #define GL_OUT(TA, TB)                          \
   do {                                          \
