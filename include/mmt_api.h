@@ -143,10 +143,10 @@ typedef struct {
   int res_dtype;              /* MMT_BF16 / MMT_F32 */
 } mmt_epilogue_t;
 
-/* Tuning knob (benchmarks). bits 0-1: main loop (0 double-buffered LDS, 1 single LDS stage at 3
- * workgroups/CU, 2 double-buffered with loads two K-steps ahead, 3 by K-steps per workgroup);
- * bit 2: epilogue straight from registers instead of through LDS. -1 = defaults. Process-wide,
- * not thread-safe. */
+/* Tuning knob (benchmarks): 0 = 128x128 register-staged, double-buffered LDS; 1 = same, single
+ * LDS stage at 3 workgroups/CU; 2 = single stage with 128-deep K-steps; 3 = 256x192 tiles, 8
+ * waves; 4 = direct-to-LDS (global_load_lds) 128x128 kernel for NT; -1 = automatic (default).
+ * Process-wide, not thread-safe. */
 void mmt_gemm_set_variant(int variant);
 int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t lda, const void* B,
              int transB, int64_t ldb, void* C, int c_mode, int64_t ldc, int batch, int64_t sA,

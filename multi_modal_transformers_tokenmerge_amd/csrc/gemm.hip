@@ -53,8 +53,8 @@ struct Geom {
   static constexpr int Q = 128 * BKT / 8 / NTHREADS;       // 16-B chunks per thread per operand
 };
 
-// tuning knob: 0 = PIPE 0 / BK 64, 1 = PIPE 1 / BK 64, 2 = PIPE 1 / BK 128; other = by K-steps
-// per work item (PIPE 1 up to 24 steps of 64)
+// tuning knob: 0 = PIPE 0 / BK 64, 1 = PIPE 1 / BK 64, 2 = PIPE 1 / BK 128, 3 = 256 x 192 tiles,
+// 4 = direct-to-LDS NT kernel; other = automatic (see mmt_gemm)
 int g_variant = -1;
 
 struct Epi {
@@ -78,41 +78,43 @@ struct Epi {
 // extent to be a multiple of 8, checked by mmt_gemm); store_tile zeroes the out-of-range chunks
 // when it writes LDS. Keeping the mask out of the load lets the compiler count vmcnt waits (a
 // predicated load forces vmcnt(0)) and leaves the loads in flight until the store.
-template <bool KCONTIG, int BKT>
+// Operand tile of R rows (M or N) x BKT (K) held in LDS either K-contiguous [R][BKT+8] or
+// M/N-contiguous [BKT][R+8]; NT threads move it in 16-B chunks, Q = R*BKT/8/NT per thread.
+template <bool KCONTIG, int BKT, int R>
 __device__ __forceinline__ void chunk_of(int c, int r0, int k0, int& row, int& kk) {
   if (KCONTIG) {  // [row][k]: BKT/8 chunks of 8 per row
     row = r0 + c / (BKT / 8);
     kk = k0 + (c % (BKT / 8)) * 8;
-  } else {        // [k][row]: 16 chunks of 8 per k-row
-    kk = k0 + (c >> 4);
-    row = r0 + (c & 15) * 8;
+  } else {        // [k][row]: R/8 chunks of 8 per k-row
+    kk = k0 + c / (R / 8);
+    row = r0 + (c % (R / 8)) * 8;
   }
 }
 
-template <bool KCONTIG, int BKT>
+template <bool KCONTIG, int BKT, int R, int NT>
 __device__ __forceinline__ void load_tile(const bf16_t* __restrict__ P, int64_t ld, int rows_lim,
-                                          int k_lim, int r0, int k0, uint4 (&reg)[Geom<BKT>::Q]) {
+                                          int k_lim, int r0, int k0, uint4 (&reg)[R * BKT / 8 / NT]) {
 #pragma unroll
-  for (int q = 0; q < Geom<BKT>::Q; ++q) {
+  for (int q = 0; q < R * BKT / 8 / NT; ++q) {
     int row, kk;
-    chunk_of<KCONTIG, BKT>(threadIdx.x + q * NTHREADS, r0, k0, row, kk);
+    chunk_of<KCONTIG, BKT, R>(threadIdx.x + q * NT, r0, k0, row, kk);
     const bf16_t* p = KCONTIG ? P + (int64_t)min(row, rows_lim - 1) * ld + min(kk, k_lim - 8)
                               : P + (int64_t)min(kk, k_lim - 1) * ld + min(row, rows_lim - 8);
     reg[q] = *reinterpret_cast<const uint4*>(p);
   }
 }
 
-template <bool KCONTIG, int BKT>
-__device__ __forceinline__ void store_tile(bf16_t* __restrict__ S, const uint4 (&reg)[Geom<BKT>::Q],
+template <bool KCONTIG, int BKT, int R, int NT>
+__device__ __forceinline__ void store_tile(bf16_t* __restrict__ S, const uint4 (&reg)[R * BKT / 8 / NT],
                                            int rows_lim, int k_lim, int r0, int k0) {
 #pragma unroll
-  for (int q = 0; q < Geom<BKT>::Q; ++q) {
-    const int c = threadIdx.x + q * NTHREADS;
+  for (int q = 0; q < R * BKT / 8 / NT; ++q) {
+    const int c = threadIdx.x + q * NT;
     int row, kk;
-    chunk_of<KCONTIG, BKT>(c, r0, k0, row, kk);
+    chunk_of<KCONTIG, BKT, R>(c, r0, k0, row, kk);
     const uint32_t m = (row < rows_lim && kk < k_lim) ? 0xffffffffu : 0u;
-    const int off = KCONTIG ? (c / (BKT / 8)) * Geom<BKT>::KCS + (c % (BKT / 8)) * 8
-                            : (c >> 4) * MC_STRIDE + (c & 15) * 8;
+    const int off = KCONTIG ? (c / (BKT / 8)) * (BKT + 8) + (c % (BKT / 8)) * 8
+                            : (c / (R / 8)) * (R + 8) + (c % (R / 8)) * 8;
     *reinterpret_cast<uint4*>(S + off) =
         make_uint4(reg[q].x & m, reg[q].y & m, reg[q].z & m, reg[q].w & m);
   }
@@ -124,7 +126,7 @@ __device__ __forceinline__ short4v tr_read(const bf16_t* p) {
 }
 
 // MFMA 32x32x16 operand fragment: lane (r = lane&31, h = lane>>5) holds X[r][k = 8h + j].
-template <bool KCONTIG, int KCS>
+template <bool KCONTIG, int KCS, int MCS>
 __device__ __forceinline__ bf16x8 load_frag(const bf16_t* S, int rbase, int ks, int lane) {
   if (KCONTIG) {
     const bf16_t* p = S + (rbase + (lane & 31)) * KCS + ks * 16 + 8 * (lane >> 5);
@@ -133,8 +135,8 @@ __device__ __forceinline__ bf16x8 load_frag(const bf16_t* S, int rbase, int ks, 
     const int i = lane & 15, q = i >> 2, p4 = i & 3, g = lane >> 4, h = lane >> 5;
     const int col = rbase + 16 * (g & 1) + 4 * p4;
     const int k1 = ks * 16 + 8 * h + q;
-    const short4v v1 = tr_read(S + k1 * MC_STRIDE + col);
-    const short4v v2 = tr_read(S + (k1 + 4) * MC_STRIDE + col);
+    const short4v v1 = tr_read(S + k1 * MCS + col);
+    const short4v v2 = tr_read(S + (k1 + 4) * MCS + col);
     short __attribute__((ext_vector_type(8))) v = {v1[0], v1[1], v1[2], v1[3],
                                                    v2[0], v2[1], v2[2], v2[3]};
     return __builtin_bit_cast(bf16x8, v);
@@ -305,9 +307,11 @@ __global__ __launch_bounds__(NTHREADS, (PIPE == 1 && BK == 64) ? 3 : 2) void gem
     for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8 af[2], bfr[2];
 #pragma unroll
-      for (int a = 0; a < 2; ++a) af[a] = load_frag<A_KC, KCS>(As, wm * 64 + a * 32, ks, lane);
+      for (int a = 0; a < 2; ++a)
+        af[a] = load_frag<A_KC, KCS, MC_STRIDE>(As, wm * 64 + a * 32, ks, lane);
 #pragma unroll
-      for (int b = 0; b < 2; ++b) bfr[b] = load_frag<B_KC, KCS>(Bs, wn * 64 + b * 32, ks, lane);
+      for (int b = 0; b < 2; ++b)
+        bfr[b] = load_frag<B_KC, KCS, MC_STRIDE>(Bs, wn * 64 + b * 32, ks, lane);
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -318,13 +322,13 @@ __global__ __launch_bounds__(NTHREADS, (PIPE == 1 && BK == 64) ? 3 : 2) void gem
   uint4 ra[Geom<BK>::Q], rb[Geom<BK>::Q];
   auto load_step = [&](const Work& w, int kt) {
     const int k0 = w.kbeg + kt * BK;
-    load_tile<A_KC, BK>(A0 + w.bz * sA, lda, M, w.kend, w.m0, k0, ra);
-    load_tile<B_KC, BK>(B0 + w.bz * sB, ldb, N, w.kend, w.n0, k0, rb);
+    load_tile<A_KC, BK, 128, NTHREADS>(A0 + w.bz * sA, lda, M, w.kend, w.m0, k0, ra);
+    load_tile<B_KC, BK, 128, NTHREADS>(B0 + w.bz * sB, ldb, N, w.kend, w.n0, k0, rb);
   };
   auto store_step = [&](const Work& w, int kt, bf16_t* S) {
     const int k0 = w.kbeg + kt * BK;
-    store_tile<A_KC, BK>(S, ra, M, w.kend, w.m0, k0);
-    store_tile<B_KC, BK>(S + TILE_ELEMS, rb, N, w.kend, w.n0, k0);
+    store_tile<A_KC, BK, 128, NTHREADS>(S, ra, M, w.kend, w.m0, k0);
+    store_tile<B_KC, BK, 128, NTHREADS>(S + TILE_ELEMS, rb, N, w.kend, w.n0, k0);
   };
 
   // lane (m = lane & 31, h) of accumulator block (a, b) holds row m, columns 8g + 4h + {0..3}
@@ -419,6 +423,310 @@ __global__ __launch_bounds__(NTHREADS, (PIPE == 1 && BK == 64) ? 3 : 2) void gem
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// NT (both operands K-contiguous: the forward Dense layers) with direct global->LDS loads
+// (global_load_lds_dwordx4): no VGPR staging and no ds_write pass — the LDS store path is what
+// bounds the register-staged kernels (a 128x128x64 step stores 32 KB through ds_write_b128 at
+// ~13 cycles/KB, more than the LDS reads and near the MFMA time). Tiles [128][64] bf16 with
+// 128-B rows, no padding; 16-B chunk c of row r sits at chunk c ^ ((r >> 1) & 7) (the swizzle is
+// applied to each lane's SOURCE address, the DMA destination stays lane-linear, and the fragment
+// reads apply the same XOR: conflict-free ds_read_b128). Two stages (64 KB, 2 workgroups/CU);
+// the next stage's DMA stays in flight across the barrier (counted vmcnt, raw s_barrier).
+// A partial last K-step is zero-filled in LDS after its DMA lands.
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+
+template <int OUT>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_glds_nt_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A0, int64_t lda, int64_t sA,
+    const bf16_t* __restrict__ B0, int64_t ldb, int64_t sB, void* __restrict__ Cv, int64_t ldc,
+    int64_t sC, int split_k, int k_chunk, int tiles_n, int n_work, Epi epi) {
+  constexpr int BKG = 64;
+  constexpr int OPE = 128 * BKG;       // elements per operand tile
+  constexpr int STAGE = 2 * OPE;       // A | B
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1, hl = lane >> 5;
+  const int tiles = ((M + BM - 1) / BM) * tiles_n;
+  const Work w = decode_work(xcd_remap(blockIdx.x, gridDim.x), tiles_n, tiles, split_k, K, k_chunk, BKG);
+  const bf16_t* A = A0 + w.bz * sA;
+  const bf16_t* B = B0 + w.bz * sB;
+  uint32_t key = 0;
+  if (OUT != 2 && epi.rng) key = stream_key(epi.rng[0], epi.rng[1], epi.drop_layer, epi.drop_site);
+
+  // DMA of K-step kt into stage st: instruction i of this wave fills rows 8(4 wave + i) .. +7
+  auto issue = [&](int kt, int st) {
+    const int k0 = w.kbeg + kt * BKG;
+    bf16_t* SA = smem + st * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = wave * 4 + i;
+      const int row = 8 * j + (lane >> 3);
+      const int c = (lane & 7) ^ swz(row);
+      const int kk = min(k0 + c * 8, w.kend - 8);
+      const bf16_t* ga = A + (int64_t)min(w.m0 + row, M - 1) * lda + kk;
+      const bf16_t* gb = B + (int64_t)min(w.n0 + row, N - 1) * ldb + kk;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ga,
+                                       (__attribute__((address_space(3))) void*)(SA + j * 512),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gb,
+                                       (__attribute__((address_space(3))) void*)(SA + OPE + j * 512),
+                                       16, 0, 0);
+    }
+  };
+  // zero the chunks of a partial K-step that lie past kend (after its DMA landed)
+  auto zero_tail = [&](int kt, int st) {
+    const int k0 = w.kbeg + kt * BKG;
+    bf16_t* SA = smem + st * STAGE;
+    for (int e = threadIdx.x; e < 2 * 128 * 8; e += NTHREADS) {
+      const int op = e >> 10, row = (e >> 3) & 127, c = e & 7;
+      if (k0 + c * 8 >= w.kend)
+        *reinterpret_cast<uint4*>(SA + op * OPE + row * BKG + ((c ^ swz(row)) * 8)) =
+            make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto frag = [&](const bf16_t* S, int rbase, int ks) {
+    const int r = rbase + (lane & 31);
+    const int c = (ks * 2 + hl) ^ swz(r);
+    return *reinterpret_cast<const bf16x8*>(S + r * BKG + c * 8);
+  };
+
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[a][b][q] = 0.f;
+
+  if (w.nk > 0) issue(0, 0);
+  for (int kt = 0; kt < w.nk; ++kt) {
+    const int st = kt & 1;
+    if (kt + 1 < w.nk) {
+      issue(kt + 1, st ^ 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this K-step's 8 DMAs landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (w.kbeg + (kt + 1) * BKG > w.kend) {
+        asm volatile("s_barrier" ::: "memory");
+        zero_tail(kt, st);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    }
+    asm volatile("s_barrier" ::: "memory");
+    const bf16_t* As = smem + st * STAGE;
+    const bf16_t* Bs = As + OPE;
+#pragma unroll
+    for (int ks = 0; ks < BKG / 16; ++ks) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) af[a] = frag(As, wm * 64 + a * 32, ks);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) bfr[b] = frag(Bs, wn * 64 + b * 32, ks);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // stage st free again
+  }
+
+  // ---------------- epilogue: 64-row halves through the (now idle) LDS
+  if (OUT == 2) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int gr = w.m0 + wm * 64 + a * 32 + (lane & 31);
+      if (gr >= M) continue;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int gc = w.n0 + wn * 64 + b * 32 + 8 * g + 4 * hl;
+          if (gc >= N) continue;
+          float v[4] = {acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2],
+                        acc[a][b][4 * g + 3]};
+          store_w<2, 4>(Cv, w.ks * sC + (int64_t)gr * ldc + gc, 0.f, v);
+        }
+    }
+    return;
+  }
+  constexpr int CTS = BN + 4;
+  static_assert(64 * CTS * 4 <= 2 * STAGE * 2, "staging half exceeds the LDS");
+  float* Ct = reinterpret_cast<float*>(smem);
+  const int c8 = (threadIdx.x & 15) * 8;
+  const int gc = w.n0 + c8;
+#pragma unroll 1
+  for (int hf = 0; hf < 2; ++hf) {
+    __syncthreads();
+    if (wm == hf) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(Ct + (a * 32 + (lane & 31)) * CTS + wn * 64 + b * 32 +
+                                       8 * g + 4 * hl) =
+                make_float4(acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2],
+                            acc[a][b][4 * g + 3]);
+    }
+    __syncthreads();
+    if (gc >= N) continue;
+#pragma unroll 2
+    for (int r = threadIdx.x >> 4; r < 64; r += NTHREADS / 16) {
+      const int gr = w.m0 + hf * 64 + r;
+      if (gr >= M) break;
+      float v[8];
+      ldw<8>(Ct + r * CTS + c8, v);
+      epilogue_w<8>(epi, key, N, gr, gc, v);
+      store_w<OUT, 8>(Cv, w.bz * sC + (int64_t)gr * ldc + gc, epi.beta, v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Large-tile variant for big launches: 256 x 192 output tile, 8 waves (4 along M x 2 along N,
+// 64 x 96 each = 2 x 3 MFMA blocks), K-step 64, double-buffered LDS (2 x 64.5 KB) with operands
+// prefetched one K-step ahead through registers, one workgroup per CU. Against the 128 x 128
+// tile it moves 1/110 instead of 1/64 operand bytes per flop through the per-CU load
+// path, which bounds the small tile (tools/gemm_trace.cpp: per-K-step time grows with the bytes
+// per step, not with occupancy). 192 divides every N of the path (384, 768, 1152, 1536, 2304,
+// 3072), so the last N tile is never partial there.
+constexpr int BM2 = 256, BN2 = 192, BK2 = 64, NT2 = 512;
+
+template <bool TA, bool TB, int OUT>
+__global__ __launch_bounds__(NT2, 1) void gemm_big_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A0, int64_t lda, int64_t sA,
+    const bf16_t* __restrict__ B0, int64_t ldb, int64_t sB, void* __restrict__ Cv, int64_t ldc,
+    int64_t sC, int split_k, int k_chunk, int tiles_n, int n_work, Epi epi) {
+  constexpr bool A_KC = !TA, B_KC = TB;
+  constexpr int A_MCS = BM2 + 8, B_MCS = BN2 + 8, KCS = BK2 + 8;
+  constexpr int TA_E = A_KC ? BM2 * KCS : BK2 * A_MCS;
+  constexpr int TB_E = B_KC ? BN2 * KCS : BK2 * B_MCS;
+  constexpr int STAGE = TA_E + TB_E;
+  constexpr int QA = BM2 * BK2 / 8 / NT2, QB = BN2 * BK2 / 8 / NT2;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1, hl = lane >> 5;
+  const int tiles = ((M + BM2 - 1) / BM2) * tiles_n;
+  uint32_t key = 0;
+  if (OUT != 2 && epi.rng) key = stream_key(epi.rng[0], epi.rng[1], epi.drop_layer, epi.drop_site);
+
+  // work item
+  const int wi = xcd_remap(blockIdx.x, gridDim.x);
+  const int z = wi / tiles, t = wi - z * tiles;
+  const int bz = z / split_k, ks_id = z - bz * split_k;
+  const int tm = t / tiles_n;
+  const int m0 = tm * BM2, n0 = (t - tm * tiles_n) * BN2;
+  const int kbeg = ks_id * k_chunk, kend = min(K, kbeg + k_chunk);
+  const int nk = max(0, (kend - kbeg + BK2 - 1) / BK2);
+  const bf16_t* A = A0 + bz * sA;
+  const bf16_t* B = B0 + bz * sB;
+
+  floatx16 acc[2][3];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[a][b][q] = 0.f;
+
+  uint4 ra[QA], rb[QB];
+  auto load_step = [&](int kt) {
+    const int k0 = kbeg + kt * BK2;
+    load_tile<A_KC, BK2, BM2, NT2>(A, lda, M, kend, m0, k0, ra);
+    load_tile<B_KC, BK2, BN2, NT2>(B, ldb, N, kend, n0, k0, rb);
+  };
+  auto store_step = [&](int kt, bf16_t* S) {
+    const int k0 = kbeg + kt * BK2;
+    store_tile<A_KC, BK2, BM2, NT2>(S, ra, M, kend, m0, k0);
+    store_tile<B_KC, BK2, BN2, NT2>(S + TA_E, rb, N, kend, n0, k0);
+  };
+  auto mma_tile = [&](const bf16_t* As, const bf16_t* Bs) {
+#pragma unroll
+    for (int ks = 0; ks < BK2 / 16; ++ks) {
+      bf16x8 af[2], bfr[3];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+        af[a] = load_frag<A_KC, KCS, A_MCS>(As, wm * 64 + a * 32, ks, lane);
+#pragma unroll
+      for (int b = 0; b < 3; ++b)
+        bfr[b] = load_frag<B_KC, KCS, B_MCS>(Bs, wn * 96 + b * 32, ks, lane);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b)  // operands swapped: the accumulator holds C^T
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+    }
+  };
+
+  if (nk > 0) {
+    load_step(0);
+    store_step(0, smem);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) load_step(kt + 1);
+    mma_tile(smem + cur * STAGE, smem + cur * STAGE + TA_E);
+    if (more) store_step(kt + 1, smem + (cur ^ 1) * STAGE);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue (lane (m = lane & 31, h) of block (a, b): row m, columns 8g+4h+{0..3})
+  if (OUT == 2) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int gr = m0 + wm * 64 + a * 32 + (lane & 31);
+      if (gr >= M) continue;
+#pragma unroll
+      for (int b = 0; b < 3; ++b)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int gc = n0 + wn * 96 + b * 32 + 8 * g + 4 * hl;
+          if (gc >= N) continue;
+          float v[4] = {acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2],
+                        acc[a][b][4 * g + 3]};
+          store_w<2, 4>(Cv, ks_id * sC + (int64_t)gr * ldc + gc, 0.f, v);
+        }
+    }
+    return;
+  }
+  // 64-row chunks through an LDS fp32 tile [64][196]; chunk c comes from the two waves wm == c
+  constexpr int CTS = BN2 + 4;
+  static_assert(64 * CTS * 4 <= 2 * STAGE * 2, "staging chunk exceeds the LDS");
+  float* Ct = reinterpret_cast<float*>(smem);
+  constexpr int GPR = BN2 / 8;  // 8-column groups per row
+#pragma unroll 1
+  for (int c = 0; c < BM2 / 64; ++c) {
+    if (c > 0) __syncthreads();  // previous chunk consumed
+    if (wm == c) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(Ct + (a * 32 + (lane & 31)) * CTS + wn * 96 + b * 32 +
+                                       8 * g + 4 * hl) =
+                make_float4(acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2],
+                            acc[a][b][4 * g + 3]);
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 64 * GPR; e += NT2) {
+      const int r = e / GPR, g8 = (e - r * GPR) * 8;
+      const int gr = m0 + c * 64 + r, gc = n0 + g8;
+      if (gr >= M || gc >= N) continue;
+      float v[8];
+      ldw<8>(Ct + r * CTS + g8, v);
+      epilogue_w<8>(epi, key, N, gr, gc, v);
+      store_w<OUT, 8>(Cv, bz * sC + (int64_t)gr * ldc + gc, epi.beta, v);
+    }
+  }
+}
+
 // Split-K combine: v = sum_s slab[s][m][n] (fp32), then the GEMM epilogue, 8 columns per thread.
 template <int OUT>
 __global__ void splitk_epilogue_kernel(const float* __restrict__ ws, int split, int M, int N,
@@ -509,8 +817,17 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
   const int k_chunk = ((K + split_k - 1) / split_k + 63) / 64 * 64;
   if (out_kind == 2) split_k = (K + k_chunk - 1) / k_chunk;  // no empty K-splits
   const int n_work = tiles_m * tiles_n * batch * split_k;
-  // 0: PIPE 0 / BK 64, 1: PIPE 1 / BK 64, 2: PIPE 1 / BK 128
-  const int pipe = (g_variant >= 0 && g_variant <= 2) ? g_variant : (k_chunk / 64 > 24 ? 0 : 1);
+  // 0: PIPE 0 / BK 64, 1: PIPE 1 / BK 64, 2: PIPE 1 / BK 128, 3: 256 x 192 tiles
+  const int big_work = ((M + BM2 - 1) / BM2) * ((N + BN2 - 1) / BN2) * batch * split_k;
+  // Automatic choice (tools/gemm_bench.py, B = 256 shapes, graph-timed): NT -> direct-to-LDS
+  // kernel (equal or better everywhere: +8 % at K = 1536, +22 % on the T5 projections); TN
+  // (weight gradients, split-K) -> 256 x 192 tiles when they fill the chip (+12-15 %); otherwise
+  // the register-staged 128 x 128 kernel, single stage up to 24 K-steps.
+  int pipe;
+  if (g_variant >= 0 && g_variant <= 4) pipe = g_variant;
+  else if (!transA && transB && K % 8 == 0) pipe = 4;
+  else if (transA && !transB && big_work >= 128) pipe = 3;
+  else pipe = k_chunk / 64 > 24 ? 0 : 1;
   const int grid_x = n_work;
   void* Cdst = out_kind == 2 ? (void*)workspace : C;
   const int64_t ldd = out_kind == 2 ? (int64_t)N : ldc;
@@ -519,11 +836,22 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
   hipLaunchKernelGGL((gemm_kernel<TA, TB, OUT, P, BKT>), dim3(grid_x), dim3(NTHREADS), 0, s, M, N, \
                      K, (const bf16_t*)A, lda, sA, (const bf16_t*)B, ldb, sB, Cdst, ldd, sdd,     \
                      split_k, k_chunk, tiles_n, n_work, epi)
-#define GL(TA, TB, OUT)                         \
-  do {                                          \
-    if (pipe == 0) GL1(TA, TB, OUT, 0, 64);     \
+#define GLB(TA, TB, OUT)                                                                           \
+  hipLaunchKernelGGL((gemm_big_kernel<TA, TB, OUT>), dim3(big_work), dim3(NT2), 0, s, M, N, K,     \
+                     (const bf16_t*)A, lda, sA, (const bf16_t*)B, ldb, sB, Cdst, ldd, sdd,        \
+                     split_k, k_chunk, (N + BN2 - 1) / BN2, big_work, epi)
+#define GLG(OUT)                                                                                   \
+  hipLaunchKernelGGL((gemm_glds_nt_kernel<OUT>), dim3(grid_x), dim3(NTHREADS), 0, s, M, N, K,      \
+                     (const bf16_t*)A, lda, sA, (const bf16_t*)B, ldb, sB, Cdst, ldd, sdd,        \
+                     split_k, k_chunk, tiles_n, n_work, epi)
+  if (pipe == 4 && !(!transA && transB && K % 8 == 0)) pipe = 1;  // glds path: NT only
+#define GL(TA, TB, OUT)                          \
+  do {                                           \
+    if (pipe == 4) GLG(OUT);                     \
+    else if (pipe == 0) GL1(TA, TB, OUT, 0, 64); \
     else if (pipe == 1) GL1(TA, TB, OUT, 1, 64); \
-    else GL1(TA, TB, OUT, 1, 128);              \
+    else if (pipe == 2) GL1(TA, TB, OUT, 1, 128); \
+    else GLB(TA, TB, OUT);                       \
   } while (0)
 #define GL_OUT(TA, TB)                          \
   do {                                          \
@@ -538,6 +866,8 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
 #undef GL_OUT
 #undef GL
 #undef GL1
+#undef GLB
+#undef GLG
   MMT_CHECK_LAUNCH("mmt_gemm");
   if (out_kind == 2) {
     const int64_t n8 = (int64_t)M * N / 8;

@@ -52,10 +52,14 @@ def main():
                 us = timeit(lambda: K.gemm(a, b, False, True, out=out, split_k=1))
                 print(f"sweep M={M} N={N} K={Kd:5d}: {us:8.2f} us  {2*M*N*Kd/us/1e6:7.1f} TF/s", flush=True)
         return
-    M1 = 64 * 276
+    Bsz = 256
+    for a in sys.argv[1:]:
+        if a.startswith("--b="):
+            Bsz = int(a.split("=")[1])
+    M1 = Bsz * 276
     cases = []
     # (name, M, N, K, ta, tb, out_mode, epi)
-    for (M, N, Kd) in [(M1, 1536, 384), (M1, 384, 1536), (64 * 292, 1152, 384), (64 * 292, 384, 384),
+    for (M, N, Kd) in [(M1, 1536, 384), (M1, 384, 1536), (Bsz * 292, 1152, 384), (Bsz * 292, 384, 384), (Bsz * 32, 768, 3072), (Bsz * 32, 2304, 768),
                        (4096, 4096, 4096)]:
         cases.append(("fwd NT plain", M, N, Kd, False, True, K.OUT_BF16, {}))
     cases.append(("fwd NT bias+relu+drop", M1, 1536, 384, False, True, K.OUT_BF16,
@@ -67,7 +71,7 @@ def main():
     cases.append(("dX NN f32", M1, 384, 1536, False, False, K.OUT_F32, {}))
     cases.append(("dW TN splitK", 1536, 384, M1, True, False, K.OUT_F32_ACCUM, {}))
     cases.append(("dW TN splitK", 384, 1536, M1, True, False, K.OUT_F32_ACCUM, {}))
-    cases.append(("dW TN splitK", 1152, 384, 64 * 292, True, False, K.OUT_F32_ACCUM, {}))
+    cases.append(("dW TN splitK", 1152, 384, Bsz * 292, True, False, K.OUT_F32_ACCUM, {}))
     for name, M, N, Kd, ta, tb, om, epi in cases:
         a = torch.randn((Kd, M) if ta else (M, Kd), device=dev).bfloat16()
         b = torch.randn((N, Kd) if tb else (Kd, N), device=dev).bfloat16()
@@ -86,6 +90,7 @@ def main():
     # library reference point (hipBLASLt through torch.matmul), plain bf16 output, same shapes
     if "--torch" in sys.argv:
         for (M, N, Kd, ta, tb) in [(M1, 1536, 384, False, True), (M1, 384, 1536, False, True),
+                                   (Bsz * 292, 1152, 384, False, True), (Bsz * 32, 768, 3072, False, True),
                                    (M1, 384, 1536, False, False), (1536, 384, M1, True, False),
                                    (4096, 4096, 4096, False, True)]:
             a = torch.randn((Kd, M) if ta else (M, Kd), device=dev).bfloat16()
