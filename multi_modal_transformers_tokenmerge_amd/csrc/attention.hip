@@ -142,29 +142,35 @@ __device__ __forceinline__ bf16x8 pack_frag(const floatx16& x, int s) {
 }
 
 // Register-staged copy of two KT x DH bf16 tiles (rows r0.., zero past L) -> LDS [KT][DH+8].
+// Loads are branch-free (rows clamped to L-1, zeroed at the LDS store), so the compiler keeps
+// counted vmcnt waits and the prefetch stays in flight through the MFMAs.
 template <int DH>
 struct TilePair {
   static constexpr int CPR = DH / 8;            // 16-B chunks per row
   static constexpr int PER = KT * CPR / NT;     // chunks per thread per tile
   uint4 a[PER], b[PER];
+  uint32_t ok;
   __device__ __forceinline__ void load(const bf16_t* pa, int64_t sa, const bf16_t* pb, int64_t sb,
                                        int r0, int L) {
+    ok = 0;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = threadIdx.x + i * NT, row = c / CPR, ch = c % CPR;
-      const bool ok = r0 + row < L;
-      a[i] = ok ? *reinterpret_cast<const uint4*>(pa + (int64_t)(r0 + row) * sa + ch * 8)
-                : make_uint4(0, 0, 0, 0);
-      b[i] = ok ? *reinterpret_cast<const uint4*>(pb + (int64_t)(r0 + row) * sb + ch * 8)
-                : make_uint4(0, 0, 0, 0);
+      const int rr = min(r0 + row, L - 1);
+      ok |= (r0 + row < L ? 1u : 0u) << i;
+      a[i] = *reinterpret_cast<const uint4*>(pa + (int64_t)rr * sa + ch * 8);
+      b[i] = *reinterpret_cast<const uint4*>(pb + (int64_t)rr * sb + ch * 8);
     }
   }
   __device__ __forceinline__ void store(bf16_t* la, bf16_t* lb) const {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = threadIdx.x + i * NT, row = c / CPR, ch = c % CPR;
-      *reinterpret_cast<uint4*>(la + row * (DH + 8) + ch * 8) = a[i];
-      *reinterpret_cast<uint4*>(lb + row * (DH + 8) + ch * 8) = b[i];
+      const uint32_t m = ((ok >> i) & 1u) ? 0xffffffffu : 0u;
+      *reinterpret_cast<uint4*>(la + row * (DH + 8) + ch * 8) =
+          make_uint4(a[i].x & m, a[i].y & m, a[i].z & m, a[i].w & m);
+      *reinterpret_cast<uint4*>(lb + row * (DH + 8) + ch * 8) =
+          make_uint4(b[i].x & m, b[i].y & m, b[i].z & m, b[i].w & m);
     }
   }
 };
@@ -178,7 +184,7 @@ struct Geo {
 
 // =============================================================================== forward
 template <int DH>
-__global__ __launch_bounds__(NT) void attn_fwd_kernel(Geo g, AttnMask mask,
+__global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(Geo g, AttnMask mask,
                                                       const uint32_t* __restrict__ drop_bits,
                                                       int drop_words, float drop_scale,
                                                       const float* __restrict__ bias,
@@ -357,7 +363,7 @@ __global__ void attn_bwd_delta_kernel(const bf16_t* __restrict__ o, int64_t o_s_
 
 // =============================================================================== bwd: dQ
 template <int DH>
-__global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(Geo g, AttnMask mask,
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mask,
                                                          const uint32_t* __restrict__ drop_bits,
                                                          int drop_words, float drop_scale,
                                                          const bf16_t* __restrict__ dout,
@@ -482,7 +488,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(Geo g, AttnMask mask,
 
 // =============================================================================== bwd: dK, dV
 template <int DH>
-__global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(Geo g, AttnMask mask,
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask mask,
                                                            const uint32_t* __restrict__ drop_bits_t,
                                                            int drop_words, float drop_scale,
                                                            const bf16_t* __restrict__ dout,
@@ -567,8 +573,8 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(Geo g, AttnMask mask,
         if ((qt >> 5) + 1 < drop_words) dw[1] = drop_bits_t[(int64_t)key * drop_words + (qt >> 5) + 1];
       }
       const uint64_t qm = sets_bits(mask, selq, qt);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {  // 32-query sub-tiles
+#pragma unroll 1
+      for (int u = 0; u < 2; ++u) {  // 32-query sub-tiles (not unrolled: keeps 2 waves/SIMD)
         floatx16 sacc, pacc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
