@@ -15,6 +15,12 @@ using namespace mmt;
 
 namespace {
 
+// image_tokenizer.py:67-68 in the reference's fp32 order: 2 * (x / 255) - 1 (division, exact
+// doubling, subtraction; no fused multiply-add). normalize == 0 passes x through.
+__device__ __forceinline__ float normalize_px(float x, float normalize) {
+  return normalize != 0.f ? __fsub_rn(__fmul_rn(__fdiv_rn(x, 255.f), 2.f), 1.f) : x;
+}
+
 // One thread per (row, 8-element chunk) of the im2col matrix [rows][K], rows =
 // ((b*I + i)*NP + p)*OH*OW + oy*OW + ox, K = KH*KW*C in (ky, kx, c) order (Flax HWIO kernels).
 template <typename T>
@@ -40,12 +46,42 @@ __global__ void patch_im2col_kernel(const T* __restrict__ img, int64_t s_img, in
     const int c = k % C, kx = (k / C) % KW, ky = k / (C * KW);
     const int yy = py * P + oy * S + ky, xx = px * P + ox * S + kx;
     const float raw = (float)base[((int64_t)yy * Himg + xx) * C + c];
-    v[e] = raw * in_scale + in_bias;
+    v[e] = normalize_px(raw, in_scale);
   }
   uint32_t w[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) w[q] = (uint32_t)f2bf(v[2 * q]) | ((uint32_t)f2bf(v[2 * q + 1]) << 16);
   *reinterpret_cast<uint4*>(out + row * K + k0) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Same im2col, one thread per (row, ky): the KW*C values of a kernel row are contiguous in the
+// NHWC image, so a thread reads them in order and writes KW*C bf16 with 8-byte stores (needs
+// KW*C % 4 == 0). The per-element index arithmetic of the generic kernel is gone.
+template <typename T, int SEG>
+__global__ void patch_im2col_rows_kernel(const T* __restrict__ img, int64_t s_img, int Himg, int C,
+                                         int P, int KH, int S, int OH, int OW, int64_t rows, int K,
+                                         bf16_t* __restrict__ out, float in_scale, float in_bias) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * KH) return;
+  const int64_t row = idx / KH;
+  const int ky = (int)(idx - row * KH);
+  const int ox = row % OW, oy = (row / OW) % OH;
+  const int64_t pimg = row / ((int64_t)OH * OW);
+  const int PPD = Himg / P, NP = PPD * PPD;
+  const int p = pimg % NP;
+  const int64_t bi = pimg / NP;
+  const int py = p / PPD, px = p % PPD;
+  const T* src = img + bi * s_img + ((int64_t)(py * P + oy * S + ky) * Himg + px * P + ox * S) * C;
+  bf16_t* dst = out + row * K + ky * SEG;
+#pragma unroll
+  for (int e = 0; e < SEG; e += 4) {
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = normalize_px((float)src[e + q], in_scale);
+    *reinterpret_cast<uint2*>(dst + e) =
+        make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                   (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+  }
 }
 
 // max over the `win` conv positions of each patch (3x3 window on a 3x3 map -> 1x1), per channel.
@@ -258,9 +294,20 @@ extern "C" int mmt_patch_im2col(const void* img, int in_dtype, int B, int I, int
   const int NP = (Himg / P) * (Himg / P);
   const int64_t rows = (int64_t)B * I * NP * OH * OW;
   const int64_t n = rows * (K / 8);
-  const float sc = normalize ? 2.f / 255.f : 1.f, bi = normalize ? -1.f : 0.f;
+  const float sc = normalize ? 1.f : 0.f, bi = 0.f;  // sc: the normalize flag of normalize_px
   const int64_t s_img = (int64_t)Himg * Himg * C;
-  if (in_dtype == 2)  // uint8
+  MMT_CHECK_ARG(in_dtype == 2 || in_dtype == MMT_F32, "mmt_patch_im2col: dtype must be fp32 (0) or uint8 (2)");
+  if (KW * C == 36) {  // the 12x12 RGB stem conv (gato_resnet.yaml:45-60): row-segment kernel
+    const int64_t nr = rows * KH;
+    if (in_dtype == 2)
+      hipLaunchKernelGGL((patch_im2col_rows_kernel<uint8_t, 36>), dim3((nr + 255) / 256), dim3(256),
+                         0, as_stream(stream), (const uint8_t*)img, s_img, Himg, C, P, KH, S, OH,
+                         OW, rows, K, (bf16_t*)out, sc, bi);
+    else
+      hipLaunchKernelGGL((patch_im2col_rows_kernel<float, 36>), dim3((nr + 255) / 256), dim3(256),
+                         0, as_stream(stream), (const float*)img, s_img, Himg, C, P, KH, S, OH, OW,
+                         rows, K, (bf16_t*)out, sc, bi);
+  } else if (in_dtype == 2)  // uint8
     hipLaunchKernelGGL(patch_im2col_kernel<uint8_t>, dim3((n + 255) / 256), dim3(256), 0,
                        as_stream(stream), (const uint8_t*)img, s_img, Himg, C, P, KH, KW, S, OH,
                        OW, rows, K, (bf16_t*)out, sc, bi);

@@ -1,0 +1,39 @@
+"""GPU: the fused patchify + normalise + conv-im2col kernel (image_tokenizer.py:35-71 and the
+stem Conv of gato_resnet.yaml:45-60) vs the oracle's image_to_patches (fp32 2*(x/255)-1, the
+reference's order) followed by a literal im2col in numpy. Bit-exact after the bf16 rounding."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import octo_ref as OR
+
+pytestmark = pytest.mark.gpu
+
+
+def _im2col_ref(images, P, KH, KW, S, normalize):
+    B, I, H, _, C = images.shape
+    OH, OW = (P - KH) // S + 1, (P - KW) // S + 1
+    rows = []
+    for b in range(B):
+        for i in range(I):
+            patches = OR.image_to_patches(images[b, i].astype(np.float32), P, normalize)
+            for pt in patches:
+                for oy in range(OH):
+                    for ox in range(OW):
+                        win = pt[oy * S:oy * S + KH, ox * S:ox * S + KW, :]   # (ky, kx, c)
+                        rows.append(win.reshape(-1))
+    return torch.from_numpy(np.stack(rows)).bfloat16()
+
+
+@pytest.mark.parametrize("dtype,H,P,KH,KW,S,C", [("u8", 64, 16, 12, 12, 2, 3),
+                                               ("f32", 32, 16, 12, 12, 2, 3),
+                                               ("u8", 32, 8, 4, 2, 2, 4)])
+def test_patch_im2col_matches_oracle(dev, dtype, H, P, KH, KW, S, C):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    g = np.random.default_rng(H + KW)
+    img = g.integers(0, 256, (2, 1, H, H, C), dtype=np.uint8)
+    t = torch.from_numpy(img if dtype == "u8" else img.astype(np.float32)).to(dev)
+    out = K.patch_im2col(t, P, KH, KW, S, normalize=True)
+    ref = _im2col_ref(img, P, KH, KW, S, True)
+    assert out.shape == ref.shape
+    torch.testing.assert_close(out.cpu(), ref, rtol=0, atol=0)
