@@ -80,7 +80,8 @@ def algorithmic_flops_per_sample(model) -> float:
 
 def probe_dominant_gemm(model, B, reps=20):
     """Average duration (HIP events on the launching stream) of the MLP up-projection GEMM of
-    block 0 at the step's exact shape: M = B*L1, N = mlp_dim, K = D (bias+relu+dropout fused)."""
+    block 0 at the step's exact shape: M = B*L1, N = mlp_dim, K = D (bias+relu+dropout fused);
+    the library's automatic choice for this NT shape is the direct-to-LDS kernel."""
     cfg = model.cfg
     blk = model.stack.blocks[0]
     sets, _, ts, r = model.layer_sets[0]
@@ -116,7 +117,7 @@ def probe_dominant_gemm(model, B, reps=20):
     e1.synchronize()
     avg_ms = e0.elapsed_time(e1) / reps
     flops = 2.0 * M * cfg.mlp_dim * D
-    return dict(kernel="gemm_kernel<false, true, 0, PIPE> (MLP Dense_0 fwd, bias+relu+dropout epilogue)",
+    return dict(kernel="gemm_glds_nt_kernel<0> (MLP Dense_0 fwd, bias+relu+dropout epilogue)",
                 shape=[M, cfg.mlp_dim, D], avg_us=avg_ms * 1e3, flops=flops,
                 tflops=flops / (avg_ms * 1e-3) / 1e12)
 

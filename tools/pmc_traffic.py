@@ -19,7 +19,7 @@ import json
 import os
 import statistics
 
-KERNEL = "gemm_kernel<false, true, 0,"
+KERNEL = "gemm_glds_nt_kernel<0>"
 
 
 def per_dispatch(d: str, counter: str) -> list[float]:
