@@ -34,9 +34,42 @@ __device__ unsigned long long g_gemm_trace[1 << 16][5];
       if ((i) == 0) g_gemm_trace[blockIdx.x][4] = __smid();                                    \
     }                                                                                          \
   } while (0)
+// nt256: per workgroup, per tile (up to 16): K-step 0 landed, main loop done, epilogue issued
+__device__ unsigned long long g_nt_trace[1024][16][3];
+#define NT_TRACE(ti, slot)                                                                     \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < 1024 && (ti) < 16)                                    \
+      g_nt_trace[blockIdx.x][ti][slot] = wall_clock64();                                       \
+  } while (0)
+// nt256 in-kernel clock: s_memtime / s_memrealtime at the first K-step and after the last epilogue
+__device__ unsigned long long g_nt_clk[1024][4];
+#define NT_CLK(slot)                                                                           \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) {                                               \
+      g_nt_clk[blockIdx.x][2 * (slot)] = __builtin_amdgcn_s_memtime();                         \
+      g_nt_clk[blockIdx.x][2 * (slot) + 1] = __builtin_amdgcn_s_memrealtime();                 \
+    }                                                                                          \
+  } while (0)
+// nt256 per-step timeline of wave 0 and wave 4: after DMA issue, after vmcnt wait, after barrier,
+// after compute, after the closing barrier (steps 0..15)
+__device__ unsigned long long g_nt_step[1024][2][16][5];
+#define NT_STEP(st_, slot)                                                                     \
+  do {                                                                                         \
+    if ((threadIdx.x & 255) == 0 && blockIdx.x < 1024 && (st_) < 16)                           \
+      g_nt_step[blockIdx.x][threadIdx.x >> 8][st_][slot] = wall_clock64();                     \
+  } while (0)
 #else
+#define NT_CLK(slot) \
+  do {               \
+  } while (0)
+#define NT_STEP(st_, slot) \
+  do {                     \
+  } while (0)
 #define GEMM_TRACE(i) \
   do {                \
+  } while (0)
+#define NT_TRACE(ti, slot) \
+  do {                     \
   } while (0)
 #endif
 
@@ -727,6 +760,329 @@ __global__ __launch_bounds__(NT2, 1) void gemm_big_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Persistent 256 x BN NT kernel (forward Dense layers and, with the transposed weight shadow, the
+// input gradients): one 512-thread workgroup per CU walks a strided list of output tiles; the
+// (tile, K-step) sequence is flattened so the first K-step of the NEXT tile is DMA'd while the
+// current tile finishes its last K-step and runs its epilogue (no per-tile prologue bubble, the
+// epilogue's store tail overlaps the next tile's loads).
+//  * 8 waves as 4 (M) x 2 (N); wave tile 64 x W (W = BN/2), v_mfma_f32_16x16x32_bf16 with the
+//    operands swapped (accumulator = C^T: lane holds 4 consecutive columns of one row).
+//  * B fragment rows are permuted so that lane group q = lane>>4 owns the W/4 CONTIGUOUS columns
+//    q*W/4 .. q*W/4+W/4-1 of its row across the W/16 fragments: the epilogue stores 16-B vectors
+//    straight from registers (no LDS round trip, which the next tile's DMA is using).
+//  * operands DMA'd global->LDS (global_load_lds_dwordx4) into unpadded [rows][64] bf16 images
+//    (128-B rows); the 16-B chunk c of row r sits at c ^ f(r), applied to each lane's SOURCE
+//    address (the DMA destination is lane-linear) and to the fragment reads. f_A(r) = r & 6 and
+//    f_B(r) = (r & 2) | bit(r, log2(W/4)) << 2 make every ds_read_b128 of both the plain A rows
+//    and the permuted B rows conflict-free (exhaustive check over the 16-lane groups).
+//  * two LDS stages; one K-step's DMA is in flight during the previous K-step's MFMAs, waited
+//    for by a counted vmcnt (the previous tile's epilogue stores, issued after it, are counted
+//    in the immediate) and a raw s_barrier, never vmcnt(0) in the loop.
+// Requires K % 64 == 0 and N % BN == 0 (checked by mmt_gemm); rows past M are clamped on load
+// and not stored.
+constexpr int NT3 = 512;
+
+// buffer_load_dwordx4 ... lds of 16 B per lane: byte voffset + soffset inside [base, base + bytes)
+// (out-of-range lanes read zeros) into the wave-uniform LDS address lds (+ 16 * lane).
+__device__ __forceinline__ void dma16(const void* base, int64_t bytes, void* lds, int voffset,
+                                      int soffset) {
+#if defined(__HIP_DEVICE_COMPILE__)  // the buffer-resource type exists only in the device pass
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(base), (short)0, (int)min(bytes, (int64_t)0x7ffffff0), 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
+                                           voffset, soffset, 0, 0);
+#endif
+}
+
+template <int BN, int OUT, bool STASH, int NS>
+__global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
+    int64_t ldb, void* __restrict__ Cv, int64_t ldc, int tiles_n, int n_tiles, Epi epi) {
+  constexpr int W = BN / 2, NF = W / 16, Q = W / 4;
+  constexpr int BSH = __builtin_ctz(Q);
+  constexpr int A_BYTES = 256 * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  constexpr int GA = 4, GB = BN / 64, G = GA + GB;  // DMA instructions per wave per K-step
+  // 16-B output chunks per lane per tile (CPM per 16-row fragment); with STASH they are held in
+  // registers and stored SPS per K-step during the next tile (NSTEPS K-steps)
+  constexpr int CPM = OUT == 0 ? Q / 8 : Q / 4, E = 4 * CPM;
+  constexpr int SPS = 4, NSTEPS = E / SPS;
+  static_assert(E % SPS == 0, "stash chunks");
+  static_assert(NS == 2 || (NS == 3 && STASH), "3 stages only with the stash");
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nk = K / 64;
+  const int first = xcd_remap(blockIdx.x, gridDim.x), stride = gridDim.x;
+  const int n_mine = first < n_tiles ? (n_tiles - first + stride - 1) / stride : 0;
+  const int S = n_mine * nk;
+  uint32_t key = 0;
+  if (epi.rng) key = stream_key(epi.rng[0], epi.rng[1], epi.drop_layer, epi.drop_site);
+
+  auto fA = [](int r) { return r & 6; };
+  auto fB = [](int r) { return (r & 2) | (((r >> BSH) & 1) << 2); };
+  // one DMA piece (1 KB per wave) of K-step position (m0, n0, k0) into stage st:
+  // pieces 0..GA-1 are A rows 8j..8j+7 (j = wave*GA + p), the rest B rows. buffer_load ... lds
+  // with the tile's panel as the buffer: the per-lane byte offsets (row, swizzled chunk) are
+  // fixed for the kernel, the panel base and k0 are scalars, so a piece costs no VALU; A rows
+  // past M fall outside the buffer's range and read as zeros.
+  int voff[G];
+#pragma unroll
+  for (int p = 0; p < G; ++p) {
+    const int j = p < GA ? wave * GA + p : wave * GB + (p - GA);
+    const int row = 8 * j + (lane >> 3);
+    const int c = (lane & 7) ^ (p < GA ? fA(row) : fB(row));
+    voff[p] = row * (int)((p < GA ? lda : ldb) * 2) + c * 16;
+  }
+  auto piece = [&](int m0, int n0, int k0, int st, int p) {
+#ifdef NT_NO_LOAD  // tools/nt_trace: time the kernel without its operand DMA (wrong results)
+    return;
+#endif
+    char* S0 = smem + st * STAGE;
+    if (p < GA)
+      dma16(A + (int64_t)m0 * lda, (int64_t)(M - m0) * lda * 2, S0 + (wave * GA + p) * 1024,
+            voff[p], k0 * 2);
+    else
+      dma16(B + (int64_t)n0 * ldb, (int64_t)BN * ldb * 2,
+            S0 + A_BYTES + (wave * GB + (p - GA)) * 1024, voff[p], k0 * 2);
+  };
+  auto position = [&](int s, int& m0, int& n0, int& k0) {
+    const int i = s / nk, kt = s - i * nk;
+    const int tile = first + i * stride;
+    const int tm = tile / tiles_n;
+    m0 = tm * 256;
+    n0 = (tile - tm * tiles_n) * BN;
+    k0 = kt * 64;
+  };
+
+  typedef float floatx4 __attribute__((ext_vector_type(4)));
+  floatx4 acc[4][NF];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < NF; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // per-lane fragment row offsets (bytes) and swizzles, fixed for the kernel
+  const int l15 = lane & 15, lq = lane >> 4;
+  int a_off[4], a_sw[4], b_off[NF], b_sw[NF];
+#pragma unroll
+  for (int mf = 0; mf < 4; ++mf) {
+    const int r = wm * 64 + mf * 16 + l15;
+    a_off[mf] = r * 128;
+    a_sw[mf] = fA(r);
+  }
+#pragma unroll
+  for (int nf = 0; nf < NF; ++nf) {
+    const int r = wn * W + (l15 >> 2) * Q + 4 * nf + (l15 & 3);
+    b_off[nf] = A_BYTES + r * 128;
+    b_sw[nf] = fB(r);
+  }
+
+  // Output stash (STASH): the finished tile's epilogue values, bf16-packed (OUT 0) or fp32, as
+  // 16-B chunks ci = mf * CPM + c; chunk ci covers row srow + 16 mf, columns sgc + 8c (bf16) /
+  // sgc + 4c (fp32).
+  uint32_t stash[E][4];
+  int sk = NSTEPS;            // next K-step's store group (NSTEPS: nothing left to store)
+  int srow = 0, sgc = 0;      // this lane's first row / first column of the stashed tile
+  auto stash_store = [&](int ci) {
+    const int mf = ci / CPM, c = ci - mf * CPM;
+    const int gr = srow + 16 * mf;
+    if (gr < M) {
+      const int64_t off = (int64_t)gr * ldc + sgc + (OUT == 0 ? 8 : 4) * c;
+      const uint4 u = make_uint4(stash[ci][0], stash[ci][1], stash[ci][2], stash[ci][3]);
+#ifdef NT_NO_STORE
+      if (u.x == 0x12345u)
+#endif
+      {
+        if (OUT == 0) *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(Cv) + off) = u;
+        else *reinterpret_cast<uint4*>(reinterpret_cast<float*>(Cv) + off) = u;
+      }
+    }
+  };
+
+  // Waves 0-3 issue the next K-step's DMA in the first half of the MFMAs and waves 4-7 (their
+  // SIMD partners) in the second, so one wave of each SIMD pair always has MFMAs to issue while
+  // the other stalls on DMA issue; the stash stores go in the other half.
+  const int hl = 0;
+  // MFMAs of the K-step in stage st. The next K-step's G DMA pieces (into the other stage, free
+  // since the barrier that opened this K-step) are issued two per M-fragment block in the first
+  // half: a piece costs its wave ~100 issue cycles, which the SIMD's partner wave fills with
+  // MFMAs instead of both waves stalling on a burst of issues at the top of the K-step.
+  auto compute = [&](int st, bool nxt, int nst, int nm0, int nn0, int nk0) {
+    const char* S0 = smem + st * STAGE;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = 4 * h + lq;
+      bf16x8 af[4], bfr[NF];
+#ifdef NT_NO_DSREAD  // tools/nt_trace: MFMAs on register operands, no LDS reads (wrong results)
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf) {
+        uint4 u = make_uint4(lane + mf, c, 3, 4);
+        asm volatile("" : "+v"(u.x), "+v"(u.y), "+v"(u.z), "+v"(u.w));
+        af[mf] = __builtin_bit_cast(bf16x8, u);
+      }
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf) {
+        uint4 u = make_uint4(lane + nf, c, 5, 6);
+        asm volatile("" : "+v"(u.x), "+v"(u.y), "+v"(u.z), "+v"(u.w));
+        bfr[nf] = __builtin_bit_cast(bf16x8, u);
+      }
+#else
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf)
+        af[mf] = *reinterpret_cast<const bf16x8*>(S0 + a_off[mf] + ((c ^ a_sw[mf]) << 4));
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf)
+        bfr[nf] = *reinterpret_cast<const bf16x8*>(S0 + b_off[nf] + ((c ^ b_sw[nf]) << 4));
+#endif
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf) {
+#ifndef NT_NO_MFMA
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf)
+          acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nf], af[mf], acc[mf][nf], 0, 0, 0);
+#endif
+        if (h == hl && nxt) {
+          if (2 * mf < G) piece(nm0, nn0, nk0, nst, 2 * mf);
+          if (2 * mf + 1 < G) piece(nm0, nn0, nk0, nst, 2 * mf + 1);
+        }
+        if (STASH && h != hl && sk < NSTEPS) {
+#pragma unroll
+          for (int j = 0; j < NSTEPS; ++j)
+            if (sk == j) stash_store(j * SPS + mf);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+  // lane (row l15 of fragment mf, group lq) holds columns lq*Q + 4*nf + r: one contiguous run
+  auto epilogue = [&](int tile) {
+    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    const int gc0 = tn * BN + wn * W + lq * Q;
+    if (STASH) {  // store what is left of the previous stash (K-loops shorter than NSTEPS)
+#pragma unroll
+      for (int j = 0; j < NSTEPS; ++j)
+        if (j >= sk)
+#pragma unroll
+          for (int b = 0; b < SPS; ++b) stash_store(j * SPS + b);
+      sk = 0;
+      srow = tm * 256 + wm * 64 + l15;
+      sgc = gc0;
+    }
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf) {
+      const int gr = tm * 256 + wm * 64 + mf * 16 + l15;
+      if (gr < M) {
+#pragma unroll
+        for (int c8 = 0; c8 < Q / 8; ++c8) {
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = acc[mf][(8 * c8 + e) >> 2][e & 3];
+          epilogue_w<8>(epi, key, N, gr, gc0 + 8 * c8, v);
+          if (STASH) {
+            if (OUT == 1 && epi.beta != 0.f) {
+              float o[8];
+              ldw<8>(reinterpret_cast<const float*>(Cv) + (int64_t)gr * ldc + gc0 + 8 * c8, o);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] += epi.beta * o[e];
+            }
+            if (OUT == 0) {
+              uint32_t* d = stash[mf * CPM + c8];
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                d[q] = (uint32_t)f2bf(v[2 * q]) | ((uint32_t)f2bf(v[2 * q + 1]) << 16);
+            } else {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) stash[mf * CPM + 2 * c8 + (q >> 2)][q & 3] = __float_as_uint(v[q]);
+            }
+            continue;
+          }
+#ifdef NT_NO_STORE  // tools/nt_trace: time the kernel without its output stores
+          if (v[0] == 12345.f)
+#endif
+          store_w<OUT, 8>(Cv, (int64_t)gr * ldc + gc0 + 8 * c8, epi.beta, v);
+        }
+      }
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf) acc[mf][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+
+  if (S == 0) return;
+#pragma unroll
+  for (int q = 0; q < NS - 1; ++q)
+    if (q < S) {
+      int m0, n0, k0;
+      position(q, m0, n0, k0);
+#pragma unroll
+      for (int p = 0; p < G; ++p) piece(m0, n0, k0, q, p);
+    }
+  // vmcnt(n) for the wave-uniform counts the loop can need
+  auto wait_vm = [](int n) {
+    if (n == SPS) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPS) : "memory");
+    else if (n == 2 * SPS) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * SPS) : "memory");
+    else if (n == G) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+    else if (n == G + SPS) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G + SPS) : "memory");
+    else if (n == G + 2 * SPS) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G + 2 * SPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  // One barrier per K-step: K-step s's DMA was issued during K-step s-1's MFMAs; the barrier
+  // after its vmcnt wait both publishes it and frees the other stage for K-step s+1's DMA.
+  // The epilogue of tile i runs at the top of the next tile's first iteration (its stores stay
+  // in flight across that K-step: vmcnt(E)).
+  bool pend = false, counted = false;  // counted: the last tile was full (exact store counts)
+  int sc1 = 0, sc2 = 0;  // exact stash stores (0 or SPS) issued by the last two K-steps
+  int ptile = 0;
+  for (int s = 0; s < S; ++s) {
+    const int st = NS == 2 ? (s & 1) : s % 3;
+    const int i = s / nk, kt = s - i * nk;
+    NT_STEP(s, 0);
+    if (pend) {
+      epilogue(ptile);
+      NT_TRACE(i - 1, 2);
+      pend = false;
+      counted = (ptile / tiles_n) * 256 + 256 <= M;
+      if (STASH) wait_vm(NS == 2 ? sc1 : (s + 1 < S ? G : 0) + sc1 + sc2);  // see below
+      else if (counted) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(E) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (STASH) {
+      // younger than K-step s's DMA (issued in K-step s-NS+1's first MFMA half): the stash
+      // stores of the later K-steps' second halves and, with 3 stages, K-step s+1's DMA
+      wait_vm(NS == 2 ? sc1 : (s + 1 < S ? G : 0) + sc1 + sc2);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    NT_STEP(s, 1);
+    asm volatile("s_barrier" ::: "memory");  // K-step s landed for every wave; stage st^1 free
+    NT_STEP(s, 2);
+    if (kt == 0) NT_TRACE(i, 0);
+    if (s == 0) NT_CLK(0);
+    int nm0 = 0, nn0 = 0, nk0 = 0;
+    const bool nxt = s + NS - 1 < S;
+    if (nxt) position(s + NS - 1, nm0, nn0, nk0);
+    compute(st, nxt, NS == 2 ? (st ^ 1) : (st + 2) % 3, nm0, nn0, nk0);
+    const bool stored = STASH && sk < NSTEPS;
+    if (stored) ++sk;
+    sc2 = sc1;
+    sc1 = stored && counted ? SPS : 0;  // counted: the stashed tile is full (no skipped rows)
+    NT_STEP(s, 3);
+    if (kt == nk - 1) {
+      NT_TRACE(i, 1);
+      pend = true;
+      ptile = first + i * stride;
+    }
+  }
+  epilogue(ptile);
+  if (STASH)
+#pragma unroll
+    for (int ci = 0; ci < E; ++ci) stash_store(ci);
+  NT_TRACE(n_mine - 1, 2);
+  NT_CLK(1);
+}
+
 // Split-K combine: v = sum_s slab[s][m][n] (fp32), then the GEMM epilogue, 8 columns per thread.
 template <int OUT>
 __global__ void splitk_epilogue_kernel(const float* __restrict__ ws, int split, int M, int N,
@@ -813,6 +1169,49 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
                       (uintptr_t)workspace % 16 == 0,
                   "mmt_gemm: split-K needs a 16-B aligned workspace of split_k*M*N floats");
     out_kind = 2;
+  }
+  // Persistent 256 x BN NT kernel (variant -1 auto, 5/6/7 force BN 256/192/128)
+  if (!transA && transB && batch == 1 && out_kind != 2 && K % 64 == 0 &&
+      (g_variant < 0 || g_variant >= 5)) {
+    static int n_cu = 0;
+    if (!n_cu) {
+      int dev = 0;
+      hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          n_cu <= 0)
+        n_cu = 256;
+    }
+    const int tm256 = (M + 255) / 256;
+    int bn = 0;
+    if (g_variant == 5) bn = N % 256 == 0 ? 256 : 0;
+    else if (g_variant == 6) bn = N % 192 == 0 ? 192 : 0;
+    else if (g_variant == 7) bn = N % 128 == 0 ? 128 : 0;
+    else if (final_kind == 0 && N >= 1152 && N % 192 == 0 && tm256 * (N / 192) >= n_cu)
+      // measured (tools/gemm_bench.py, graph-timed): wins on the wide bf16-output projections
+      // (MLP up 159 -> 147 us, QKV 113 -> 101 us at B = 256); the narrow (N = 384) and fp32
+      // residual-stream shapes stay on the 128 x 128 kernels, which are faster there
+      bn = 192;
+    if (bn) {
+      const int tn = N / bn, n_tiles = ((M + 255) / 256) * tn;
+      const int grid = std::min(n_tiles, n_cu);
+#define GN(BNV, OUT, ST, NSV)                                                                     \
+  hipLaunchKernelGGL((gemm_nt256_kernel<BNV, OUT, ST, NSV>), dim3(grid), dim3(NT3), 0, s, M, N, K, \
+                     (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, tn, n_tiles, epi)
+      // the register stash fits 2 waves/SIMD for bf16 at BN <= 192 and fp32 at BN 128;
+      // BN 128 has LDS for 3 stages (DMA two K-steps ahead)
+      if (final_kind == 0) {
+        if (bn == 256) GN(256, 0, false, 2);
+        else if (bn == 192) GN(192, 0, true, 2);
+        else GN(128, 0, true, 3);
+      } else {
+        if (bn == 256) GN(256, 1, false, 2);
+        else if (bn == 192) GN(192, 1, false, 2);
+        else GN(128, 1, true, 3);
+      }
+#undef GN
+      MMT_CHECK_LAUNCH("mmt_gemm(nt256)");
+      return MMT_OK;
+    }
   }
   const int k_chunk = ((K + split_k - 1) / split_k + 63) / 64 * 64;
   if (out_kind == 2) split_k = (K + k_chunk - 1) / k_chunk;  // no empty K-splits

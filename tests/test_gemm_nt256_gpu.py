@@ -1,0 +1,97 @@
+"""GPU numerics of the persistent 256 x BN NT GEMM (gemm_nt256_kernel) for each tile width, with
+partial last row tiles, several tiles per workgroup (persistent walk) and every epilogue, against
+a torch fp32 reference of the same bf16 operands (same bars as tests/test_gemm_gpu.py)."""
+import pytest
+import torch
+
+from oracle import rng as R
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = {256: 5, 192: 6, 128: 7}
+
+
+def _mk(shape, dev, g):
+    return torch.randn(shape, generator=g).to(torch.bfloat16).to(dev)
+
+
+def _close_bf16(out, ref):
+    err = (out.float() - ref).abs()
+    tol = (ref.abs() * 2 ** -7) + 1e-3 * ref.abs().max()
+    assert bool((err <= tol).all()), f"max err {err.max().item()}"
+    assert (out.float() == ref.to(torch.bfloat16).float()).float().mean().item() > 0.97
+
+
+@pytest.fixture
+def variant():
+    from multi_modal_transformers_tokenmerge_amd import _C
+    yield lambda bn: _C.call("mmt_gemm_set_variant", VARIANTS[bn])
+    _C.call("mmt_gemm_set_variant", -1)
+
+
+# (M, K): partial last tile, one tile, many tiles per workgroup (> 256 tiles), long K
+@pytest.mark.parametrize("bn", [256, 192, 128])
+@pytest.mark.parametrize("M,K", [(300, 64), (256, 384), (70000, 128), (1000, 1536)])
+def test_nt256_plain(dev, variant, bn, M, K):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    variant(bn)
+    N = 2 * bn if M < 5000 else bn * 3
+    g = torch.Generator().manual_seed(M + K + bn)
+    a, w = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    ref = a.float() @ w.float().t()
+    out = Kn.gemm(a, w, False, True, split_k=1)
+    _close_bf16(out, ref)
+    out32 = Kn.gemm(a, w, False, True, out_mode=Kn.OUT_F32, split_k=1)
+    torch.testing.assert_close(out32, ref, rtol=1e-5, atol=1e-5 * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("bn", [256, 192, 128])
+def test_nt256_epilogues(dev, variant, bn):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    variant(bn)
+    g = torch.Generator().manual_seed(bn)
+    M, N, K = 1300, 2 * bn * 3, 192
+    a, w = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    bias = torch.randn(N, generator=g).to(dev)
+    rng = torch.tensor([1234, 7], dtype=torch.int32, device=dev)
+    keep = torch.from_numpy(R.dropout_mask_2d(1234, 7, 3, 2, M, N, 5 * M, 0.9)).to(dev)
+    base = a.float() @ w.float().t()
+    # bias + relu + dropout + bf16 residual, bf16 out
+    res = _mk((M, N), dev, g)
+    out = Kn.gemm(a, w, False, True, bias=bias, act=Kn.ACT_RELU, rng=rng, drop_layer=3,
+                  drop_site=2, keep_prob=0.9, drop_row_offset=5 * M, residual=res, split_k=1)
+    ref = torch.where(keep, torch.relu(base + bias) / 0.9, torch.zeros_like(base)) + res.float()
+    _close_bf16(out, ref)
+    # dropout + fp32 residual, fp32 out (the residual-stream projections)
+    res32 = torch.randn((M, N), generator=g).to(dev)
+    out = Kn.gemm(a, w, False, True, bias=bias, rng=rng, drop_layer=3, drop_site=2,
+                  keep_prob=0.9, drop_row_offset=5 * M, residual=res32, out_mode=Kn.OUT_F32,
+                  split_k=1)
+    ref = torch.where(keep, (base + bias) / 0.9, torch.zeros_like(base)) + res32
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)
+    # gate (relu-backward mask) and fp32 accumulate (beta = 1)
+    gate = _mk((M, N), dev, g)
+    out = Kn.gemm(a, w, False, True, gate=gate, gate_scale=1 / 0.9, split_k=1)
+    _close_bf16(out, base * (gate.float() > 0).float() / 0.9)
+    c = torch.randn((M, N), generator=g).to(dev)
+    c0 = c.clone()
+    Kn.gemm(a, w, False, True, out=c, out_mode=Kn.OUT_F32, beta=1.0, split_k=1)
+    torch.testing.assert_close(c, c0 + base, rtol=1e-5, atol=1e-3)
+
+
+def test_nt256_auto_matches_reference_path(dev):
+    """Auto choice at a step shape (MLP up-projection, B = 64) vs the 128 x 128 glds kernel."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn, _C
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 64 * 276, 1536, 384
+    a, w = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    bias = torch.randn(N, generator=g).to(dev)
+    o_new = Kn.gemm(a, w, False, True, bias=bias, act=Kn.ACT_RELU, split_k=1)
+    _C.call("mmt_gemm_set_variant", 4)
+    try:
+        o_old = Kn.gemm(a, w, False, True, bias=bias, act=Kn.ACT_RELU, split_k=1)
+    finally:
+        _C.call("mmt_gemm_set_variant", -1)
+    # identical accumulation order is not guaranteed across kernels: compare within 1 bf16 ulp
+    _close_bf16(o_new, torch.relu(a.float() @ w.float().t() + bias))
+    assert ((o_new.float() - o_old.float()).abs() <= o_old.float().abs() * 2 ** -7 + 1e-6).all()
