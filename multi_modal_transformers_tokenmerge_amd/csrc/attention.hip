@@ -97,6 +97,9 @@ __device__ __forceinline__ uint64_t sets_bits(const AttnMask& m, uint32_t sel, i
 // Bit of accumulator register r of this lane inside a 32-row word pre-shifted by 4*(lane>>5):
 // acc row(r) = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
 __device__ __forceinline__ constexpr int rbit(int r) { return (r & 3) + 8 * (r >> 2); }
+// 2^x as the bare v_exp_f32 (exp2f adds a denormal-range fix-up of four more VALU ops per call;
+// arguments here are <= 0 after the max subtraction and results below 2^-126 are negligible)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 // all-ones if the bit is set, else 0
 __device__ __forceinline__ int bitmask_of(uint32_t w, int b) { return (int)(w << (31 - b)) >> 31; }
 
@@ -279,14 +282,14 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(Geo g, AttnMask mask,
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float mn = fmaxf(m, tmax);
       const float mnc = mn == -INFINITY ? 0.f : mn * c;
-      const float alpha = exp2f(m * c - mnc);  // m = -inf -> 0 (nothing accumulated yet)
+      const float alpha = fast_exp2(m * c - mnc);  // m = -inf -> 0 (nothing accumulated yet)
       float rs = 0.f;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const uint32_t w = dw[u] >> (4 * hh);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(fmaf(sacc[u][r], c, -mnc));
+          const float p = fast_exp2(fmaf(sacc[u][r], c, -mnc));
           rs += p;
           sacc[u][r] = __int_as_float(__float_as_int(p) & bitmask_of(w, rbit(r)));
         }
@@ -446,7 +449,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mask
         const uint32_t wd = dw[u] >> (4 * hh);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = __int_as_float(__float_as_int(exp2f(fmaf(sacc[r], sl2, -lse2))) &
+          const float p = __int_as_float(__float_as_int(fast_exp2(fmaf(sacc[r], sl2, -lse2))) &
                                          bitmask_of(wv, rbit(r)));
           const float t = __int_as_float(__float_as_int(pacc[r] * drop_scale) & bitmask_of(wd, rbit(r)));
           ds[u][r] = p * (t - dlt);
@@ -602,7 +605,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask ma
         floatx16 pd, dsv;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = __int_as_float(__float_as_int(exp2f(fmaf(sacc[r], sl2, -lr[r]))) &
+          const float p = __int_as_float(__float_as_int(fast_exp2(fmaf(sacc[r], sl2, -lr[r]))) &
                                          bitmask_of(wv, rbit(r)));
           const int keep = bitmask_of(wd, rbit(r));
           pd[r] = __int_as_float(__float_as_int(p) & keep);  // drop_scale applied to dV at the end
