@@ -84,6 +84,57 @@ __global__ void patch_im2col_rows_kernel(const T* __restrict__ img, int64_t s_im
   }
 }
 
+// Same im2col for uint8 images, PG patches per 256-thread workgroup through LDS: the patches'
+// P x P x C bytes are read as dwords (P*C % 4 == 0), normalised once into a bf16 LDS image, and
+// the PG*OH*OW rows of K values are written as consecutive 16-B chunks (fully coalesced); the
+// row-segment kernel's 8-B stores touched a new cache line every 72 B of a wave's store.
+template <int SEG, int PG>
+__global__ __launch_bounds__(256) void patch_im2col_lds_kernel(
+    const uint8_t* __restrict__ img, int64_t s_img, int Himg, int C, int P, int KH, int S, int OH,
+    int OW, int64_t npatch, int K, bf16_t* __restrict__ out, float in_scale) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  bf16_t* pix = reinterpret_cast<bf16_t*>(dsm);  // [PG][P][P*C]
+  const int PPD = Himg / P, NP = PPD * PPD, RB = P * C;  // bytes per patch row
+  const int64_t p0 = (int64_t)blockIdx.x * PG;
+  const int np = (int)min<int64_t>(PG, npatch - p0);
+  const int words = np * P * (RB / 4);
+  for (int w = threadIdx.x; w < words; w += 256) {
+    const int pl = w / (P * (RB / 4)), rem = w - pl * (P * (RB / 4));
+    const int y = rem / (RB / 4), xw = rem - y * (RB / 4);
+    const int64_t pimg = p0 + pl;
+    const int p = (int)(pimg % NP);
+    const int64_t bi = pimg / NP;
+    const int py = p / PPD, px = p % PPD;
+    const uint32_t u = *reinterpret_cast<const uint32_t*>(
+        img + bi * s_img + ((int64_t)(py * P + y) * Himg + px * P) * C + xw * 4);
+    bf16_t* d = pix + (pl * P + y) * RB + xw * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = f2bf(normalize_px((float)((u >> (8 * q)) & 0xffu), in_scale));
+  }
+  __syncthreads();
+  const int per = OH * OW, kc = K / 8;
+  const int chunks = np * per * kc;
+  bf16_t* obase = out + p0 * per * K;
+  for (int ch = threadIdx.x; ch < chunks; ch += 256) {
+    const int r = ch / kc, k0 = (ch - r * kc) * 8;
+    const int pl = r / per, o = r - pl * per;
+    const int oy = o / OW, ox = o - oy * OW;
+    const bf16_t* src = pix + (pl * P + oy * S) * RB + ox * S * C;
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t h2[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int k = k0 + 2 * q + e, ky = k / SEG;
+        h2[e] = src[ky * RB + (k - ky * SEG)];
+      }
+      w[q] = h2[0] | (h2[1] << 16);
+    }
+    *reinterpret_cast<uint4*>(obase + (int64_t)r * K + k0) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 // max over the `win` conv positions of each patch (3x3 window on a 3x3 map -> 1x1), per channel.
 __global__ void maxpool_patch_kernel(const float* __restrict__ conv, int64_t npatch, int win,
                                      int C, float* __restrict__ pooled, uint8_t* __restrict__ arg) {
@@ -297,7 +348,14 @@ extern "C" int mmt_patch_im2col(const void* img, int in_dtype, int B, int I, int
   const float sc = normalize ? 1.f : 0.f, bi = 0.f;  // sc: the normalize flag of normalize_px
   const int64_t s_img = (int64_t)Himg * Himg * C;
   MMT_CHECK_ARG(in_dtype == 2 || in_dtype == MMT_F32, "mmt_patch_im2col: dtype must be fp32 (0) or uint8 (2)");
-  if (KW * C == 36) {  // the 12x12 RGB stem conv (gato_resnet.yaml:45-60): row-segment kernel
+  if (KW * C == 36 && in_dtype == 2 && (P * C) % 4 == 0 && P * P * C * 2 * 8 <= 65536) {
+    // the 12x12 RGB stem conv (gato_resnet.yaml:45-60) on uint8 images: LDS-staged kernel
+    const int64_t npatch = (int64_t)B * I * NP;
+    constexpr int PG = 8;
+    hipLaunchKernelGGL((patch_im2col_lds_kernel<36, PG>), dim3((npatch + PG - 1) / PG), dim3(256),
+                       (size_t)PG * P * P * C * 2, as_stream(stream), (const uint8_t*)img, s_img,
+                       Himg, C, P, KH, S, OH, OW, npatch, K, (bf16_t*)out, sc);
+  } else if (KW * C == 36) {  // row-segment kernel (fp32 images)
     const int64_t nr = rows * KH;
     if (in_dtype == 2)
       hipLaunchKernelGGL((patch_im2col_rows_kernel<uint8_t, 36>), dim3((nr + 255) / 256), dim3(256),

@@ -26,6 +26,7 @@ def _im2col_ref(images, P, KH, KW, S, normalize):
 
 
 @pytest.mark.parametrize("dtype,H,P,KH,KW,S,C", [("u8", 64, 16, 12, 12, 2, 3),
+                                               ("u8", 48, 16, 12, 12, 2, 3),  # partial LDS group
                                                ("f32", 32, 16, 12, 12, 2, 3),
                                                ("u8", 32, 8, 4, 2, 2, 4)])
 def test_patch_im2col_matches_oracle(dev, dtype, H, P, KH, KW, S, C):
