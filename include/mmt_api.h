@@ -290,6 +290,20 @@ int mmt_fourier_bwd(const void* dfeats, int B, int F, const int32_t* t, const fl
 /* optax.l2_loss summed over actions, mean over batch; dpred = (pred-eps)*grad_scale/B (bf16). */
 int mmt_diffusion_loss(const float* pred, int64_t ld_pred, const float* eps, int B, int A,
                        float grad_scale, float* loss, void* dpred, mmt_stream_t stream);
+/* DiffusionActionHead.predict_action (diffusion.py:146-209), SURVEY §8f row 2: all `steps`
+ * DDPM steps (t = steps-1 .. 0) in one launch, one wave per sample. The first denoiser Dense is
+ * pre-split by the caller: P (B, H) fp32 = readout_mean . W1[:, A+T:]^T, Q (steps, H) fp32 =
+ * time_emb(t) . W1[:, A:A+T]^T + b1; w1 is the bf16 W1 (row stride ld_w1, its first A columns
+ * are read), w2 the bf16 (A, H) output kernel, b2 (A,), coef (steps, 3) = [1/sqrt(a_t),
+ * (1-a_t)/sqrt(1-abar_t), sqrt(b_t)]. z_in (B, A) injects the initial sample (else drawn from the
+ * counter stream keyed by rng and the global sample index); the same z is the noise of every step
+ * (the reference never splits its keys, :178). A must be 8 (:200). Writes actions (B, A) fp32
+ * and, if z_out is non-NULL, z (B, A). */
+int mmt_diffusion_sample(const uint32_t* rng, int B, int A, int steps, int64_t sample_offset,
+                         const float* P, int64_t ld_p, const float* Q, int64_t ld_q,
+                         const void* w1, int64_t ld_w1, const void* w2, const float* b2,
+                         const float* coef, const float* z_in, int H, float* actions,
+                         float* z_out, mmt_stream_t stream);
 
 /* ------------------------------------------------------------------ T5 encoder pieces
  * (tokenizers/text/t5_base.py:8-15, frozen FlaxT5 encoder): T5LayerNorm and the shared

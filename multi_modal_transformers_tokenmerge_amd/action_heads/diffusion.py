@@ -110,5 +110,64 @@ class DiffusionActionHead:
                 _C.ptr(self.fourier.data), _C.ptr(self.fourier.grad), _C.stream_ptr())
         return dcat[:, self.A + self.time_dim:]
 
-    def predict_action(self, *a, **k):  # SURVEY §8(f) row 2 (inference sampler): next
-        raise NotImplementedError("the 32-step DDPM sampler (diffusion.py:146-209) is §8(f) 'next'")
+    # ------------------------------------------------------------------------- predict_action
+    def sampler_coef(self, device) -> torch.Tensor:
+        """(steps, 3) fp32 [1/sqrt(a_t), (1-a_t)/sqrt(1-abar_t), sqrt(b_t)] (:182-184)."""
+        key = ("coef", device)
+        if key not in self._dev_consts:
+            b = self.betas_np.astype(np.float32)
+            a = (np.float32(1) - b).astype(np.float32)
+            c = np.stack([np.float32(1) / np.sqrt(a),
+                          (np.float32(1) - a) / np.sqrt(np.float32(1) - self.alpha_hats_np),
+                          np.sqrt(b)], axis=1).astype(np.float32)
+            self._dev_consts[key] = torch.from_numpy(np.ascontiguousarray(c)).to(device)
+        return self._dev_consts[key]
+
+    def time_embeddings(self, device) -> torch.Tensor:
+        """FourierFeatures (:41-51) + its MLPBlock for every t = 0..steps-1 -> (steps, T) bf16,
+        through the training path's kernels (prep kernel with injected t, two GEMMs)."""
+        S, A = self.steps, self.A
+        t_in = torch.arange(S, dtype=torch.int32, device=device)
+        zeros = torch.zeros((S, A), dtype=torch.float32, device=device)
+        scratch = self.new_cat(S, device)
+        feats = torch.empty((S, self.time_dim), dtype=torch.bfloat16, device=device)
+        t_out = torch.empty(S, dtype=torch.int32, device=device)
+        eps_out = torch.empty((S, A), dtype=torch.float32, device=device)
+        _C.call("mmt_diffusion_prep", None, S, A, S, 0, _C.ptr(zeros), _C.ptr(self.consts(device)),
+                _C.ptr(self.fourier.data), self.F, _C.ptr(t_in), _C.ptr(zeros), _C.ptr(t_out),
+                _C.ptr(eps_out), _C.ptr(scratch), scratch.stride(0), _C.ptr(feats),
+                _C.stream_ptr())
+        ht = self.t1.fwd(feats, act=K.ACT_RELU)
+        return self.t2.fwd(ht)
+
+    def predict_action(self, readout_mean: torch.Tensor, rng=None, sample_offset: int = 0,
+                       z: torch.Tensor | None = None, return_noise: bool = False):
+        """Reference :146-209 (the 32-step DDPM loop of jax.lax.scan) on the device.
+        readout_mean: (B, D) bf16 = mean of the readout tokens (:102). The initial sample z is
+        drawn from the counter stream (rng = the (seed, step) device tensor, keyed by the global
+        sample index sample_offset + b) unless injected. Returns actions (B, A) fp32 (and z)."""
+        if readout_mean.dim() != 2 or readout_mean.shape[1] != self.D \
+                or readout_mean.dtype != torch.bfloat16 or readout_mean.stride(1) != 1:
+            raise ValueError(f"readout_mean must be bf16 (B, {self.D}) with unit inner stride")
+        if self.A != 8:
+            raise ValueError("the reference sampler hard-codes an 8-dim action (diffusion.py:200)")
+        B = readout_mean.shape[0]
+        dev = readout_mean.device
+        if z is not None and (tuple(z.shape) != (B, self.A) or z.dtype != torch.float32
+                              or not z.is_contiguous()):
+            raise ValueError(f"z must be contiguous fp32 ({B}, {self.A})")
+        if z is None and rng is None:
+            raise ValueError("need rng (or an injected initial sample z)")
+        A, T = self.A, self.time_dim
+        temb = self.time_embeddings(dev)
+        w1 = self.d1.w.bf16
+        # concatenate([noisy, time_emb, readout]) . W1^T (OctoDenoise :61) split along the input
+        Q = K.gemm(temb, w1[:, A:A + T], trans_b=True, bias=self.d1.b.data, out_mode=K.OUT_F32)
+        P = K.gemm(readout_mean, w1[:, A + T:], trans_b=True, out_mode=K.OUT_F32)
+        actions = torch.empty((B, A), dtype=torch.float32, device=dev)
+        z_out = torch.empty((B, A), dtype=torch.float32, device=dev) if return_noise else None
+        _C.call("mmt_diffusion_sample", _C.ptr(rng), B, A, self.steps, sample_offset, _C.ptr(P),
+                P.stride(0), _C.ptr(Q), Q.stride(0), _C.ptr(w1), w1.stride(0),
+                _C.ptr(self.d2.w.bf16), _C.ptr(self.d2.b.data), _C.ptr(self.sampler_coef(dev)),
+                _C.ptr(z), self.hidden, _C.ptr(actions), _C.ptr(z_out), _C.stream_ptr())
+        return (actions, z_out) if return_noise else actions

@@ -155,7 +155,8 @@ class Encoder1DBlock:
         # dh gated by (h > 0): relu + hidden-dropout backward fused into the dX GEMM epilogue
         dz1 = self.mlp.dense_out.bwd(dz2, sv["h"], bias_grad_done=True, gate=sv["h"],
                                      gate_scale=(1.0 / kp) if dropping else 1.0)
-        dy1 = self.mlp.dense.bwd(dz1, sv["y1"].view(B * L2, D), out_mode=K.OUT_F32)
+        # dX of the LN-fed Dense in bf16 (the LN backward accumulates in fp32): halves its traffic
+        dy1 = self.mlp.dense.bwd(dz1, sv["y1"].view(B * L2, D))
         dx1 = self.ln1.bwd(dy1.view(B, L2, D), sv["x1"], sv["mu1"], sv["rs1"], addend=dx2)
         if sv["tome"] is not None:
             s0, t, r, pos, size_in, size_out = sv["tome"][:6]
@@ -166,7 +167,7 @@ class Encoder1DBlock:
         do = self.out.bwd(dzo, sv["o"].view(B * L, D), bias_grad_done=True)
         dqkv = K.attn_bwd(sv["qkv"], sv["o"], do.view(B, L, D), sv["lse"], self.H, self.scale,
                           ctx.table, sv["bits"], kpa)
-        dy0 = self.qkv.bwd(dqkv.view(B * L, 3 * D), sv["y0"].view(B * L, D), out_mode=K.OUT_F32)
+        dy0 = self.qkv.bwd(dqkv.view(B * L, 3 * D), sv["y0"].view(B * L, D))
         return self.ln0.bwd(dy0.view(B, L, D), sv["x"], sv["mu0"], sv["rs0"], addend=dx1)
 
 

@@ -130,10 +130,29 @@ __device__ __forceinline__ bf16x8 row_frag(const bf16_t* tile, int rbase, int s,
                                           8 * (lane >> 5));
 }
 
-// Same fragment straight from global memory (rows beyond L read as zero).
+// Same fragment straight from global memory (rows beyond L read as zero). The load itself is
+// unconditional (callers clamp rowp to a valid row): a load under a per-lane branch makes the
+// compiler drain every outstanding load (vmcnt(0)) at the join, which inside the tile loop would
+// also drain the next tile's prefetch.
 __device__ __forceinline__ bf16x8 row_frag_global(const bf16_t* rowp, bool valid, int s, int lane) {
-  if (!valid) return (bf16x8){};
-  return *reinterpret_cast<const bf16x8*>(rowp + 16 * s + 8 * (lane >> 5));
+  const uint4 v = *reinterpret_cast<const uint4*>(rowp + 16 * s + 8 * (lane >> 5));
+  const uint32_t m = valid ? 0xffffffffu : 0u;
+  return __builtin_bit_cast(bf16x8, make_uint4(v.x & m, v.y & m, v.z & m, v.w & m));
+}
+
+// Dropout keep words t0/32 and t0/32 + 1 of one row (all ones past the last word, for an invalid
+// row, or without dropout). Branch-free loads from clamped addresses, for the reason above;
+// `row` must be a valid row index.
+__device__ __forceinline__ void load_drop_words(const uint32_t* bits, int words, int row,
+                                                bool valid, int t0, uint32_t dw[2]) {
+  dw[0] = dw[1] = 0xffffffffu;
+  if (bits) {  // kernel-uniform
+    const int w0 = t0 >> 5, w1 = min(w0 + 1, words - 1);
+    const uint32_t* p = bits + (int64_t)row * words;
+    const uint32_t a = p[w0], c = p[w1];
+    dw[0] = valid ? a : 0xffffffffu;
+    dw[1] = (valid && w0 + 1 < words) ? c : 0xffffffffu;
+  }
 }
 
 // Pack accumulator registers 8s..8s+7 to a bf16 operand fragment.
@@ -238,11 +257,8 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(Geo g, AttnMask mask,
     const bf16_t* Ks = smem + buf * 2 * TILE;
     const bf16_t* Vs = Ks + TILE;
     if (wave_live) {
-      uint32_t dw[2] = {0xffffffffu, 0xffffffffu};
-      if (drop_bits && qv) {
-        dw[0] = drop_bits[(int64_t)q * drop_words + (kt >> 5)];
-        if ((kt >> 5) + 1 < drop_words) dw[1] = drop_bits[(int64_t)q * drop_words + (kt >> 5) + 1];
-      }
+      uint32_t dw[2];
+      load_drop_words(drop_bits, drop_words, qv ? q : 0, qv, kt, dw);
       floatx16 sacc[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -254,13 +270,18 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(Geo g, AttnMask mask,
                                                             qf[s], sacc[u], 0, 0, 0);
       }
       const uint64_t vm = sets_bits(mask, visq, kt);
-      if (brow) {
+      if (brow) {  // registers 4 r4 .. 4 r4 + 3 hold 4 consecutive keys: one float4 (L % 4 == 0)
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int kk = kt + 32 * u + rbit(r) + 4 * hh;
-            sacc[u][r] = sacc[u][r] * (g.scale * LOG2E) + (kk < L ? brow[kk] * LOG2E : 0.f);
+          for (int r4 = 0; r4 < 4; ++r4) {
+            const int k4 = kt + 32 * u + 8 * r4 + 4 * hh;
+            const float4 bv = *reinterpret_cast<const float4*>(brow + min(k4, L - 4));
+            const float kb = k4 < L ? LOG2E : 0.f;
+            const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              sacc[u][4 * r4 + e] = sacc[u][4 * r4 + e] * (g.scale * LOG2E) + bb[e] * kb;
           }
       }
       if (!__all(vm == ~0ull)) {  // partially visible tile: masked scores -> -inf
@@ -337,33 +358,6 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(Geo g, AttnMask mask,
   }
 }
 
-// =============================================================================== bwd: delta
-// delta[b, h, q] = sum_d dO * O  (fp32)
-template <int DH>
-__global__ void attn_bwd_delta_kernel(const bf16_t* __restrict__ o, int64_t o_s_b, int64_t o_s_t,
-                                      const bf16_t* __restrict__ dout, int64_t d_s_b,
-                                      int64_t d_s_t, int B, int L, int H,
-                                      float* __restrict__ delta) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)B * H * L) return;
-  const int q = idx % L, h = (idx / L) % H, b = idx / ((int64_t)L * H);
-  const bf16_t* op = o + b * o_s_b + (int64_t)q * o_s_t + h * DH;
-  const bf16_t* dp = dout + b * d_s_b + (int64_t)q * d_s_t + h * DH;
-  float acc = 0.f;
-#pragma unroll
-  for (int c = 0; c < DH; c += 8) {
-    const uint4 a = *reinterpret_cast<const uint4*>(op + c);
-    const uint4 d = *reinterpret_cast<const uint4*>(dp + c);
-    const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, dw[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      acc += __uint_as_float(aw[j] << 16) * __uint_as_float(dw[j] << 16);
-      acc += __uint_as_float(aw[j] & 0xffff0000u) * __uint_as_float(dw[j] & 0xffff0000u);
-    }
-  }
-  delta[idx] = acc;
-}
-
 // =============================================================================== bwd: dQ
 template <int DH>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mask,
@@ -372,7 +366,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mask
                                                          const bf16_t* __restrict__ dout,
                                                          int64_t d_s_b, int64_t d_s_t,
                                                          const float* __restrict__ lse,
-                                                         const float* __restrict__ delta,
+                                                         const bf16_t* __restrict__ o,
+                                                         int64_t o_s_b, int64_t o_s_t,
+                                                         float* __restrict__ delta,
                                                          bf16_t* __restrict__ dqkv,
                                                          int64_t dq_s_b, int64_t dq_s_t) {
   constexpr int STR = DH + 8;
@@ -401,7 +397,21 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mask
   const uint32_t visq = qv ? mask.vis[set_of(mask, q)] : 0u;
   const int64_t row_bh = ((int64_t)b * g.H + h) * L;
   const float lse2 = qv ? lse[row_bh + q] * LOG2E : INFINITY;
-  const float dlt = qv ? delta[row_bh + q] : 0.f;
+  // delta = rowsum(dO * O) of this query (fp32), fused here: the lane pair (q, hh = 0/1) holds
+  // dO[d = 16 s + 8 h + j]; the dK/dV kernel, launched next on the stream, reads it back.
+  float dlt;
+  {
+    const bf16_t* orow = o + (int64_t)b * o_s_b + (int64_t)(qv ? q : 0) * o_s_t + h * DH;
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const bf16x8 of = row_frag_global(orow, qv, s, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part = fmaf((float)of[j], (float)df[s][j], part);
+    }
+    dlt = part + __shfl_xor(part, 32, 64);
+    if (qv && lane < 32) delta[row_bh + q] = dlt;
+  }
   const float sl2 = g.scale * LOG2E;
   floatx16 dqacc[ND];
 #pragma unroll
@@ -423,11 +433,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mask
     const bf16_t* Ks = smem + buf * 2 * TILE;
     const bf16_t* Vs = Ks + TILE;
     if (wave_live) {
-      uint32_t dw[2] = {0xffffffffu, 0xffffffffu};
-      if (drop_bits && qv) {
-        dw[0] = drop_bits[(int64_t)q * drop_words + (kt >> 5)];
-        if ((kt >> 5) + 1 < drop_words) dw[1] = drop_bits[(int64_t)q * drop_words + (kt >> 5) + 1];
-      }
+      uint32_t dw[2];
+      load_drop_words(drop_bits, drop_words, qv ? q : 0, qv, kt, dw);
       const uint64_t vm = sets_bits(mask, visq, kt);
       floatx16 ds[2];
 #pragma unroll
@@ -542,11 +549,11 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask ma
 
   TilePair<DH> pf;
   float rowv = 0.f;  // thread t < 128 stages lse (t < 64) or delta (64 <= t < 128) of one row
-  auto load_rows = [&](int q0) {
+  auto load_rows = [&](int q0) {  // waves 0 (lse) and 1 (delta); clamped, branch-free load
     if (threadIdx.x < 2 * KT) {
       const int qq = q0 + (threadIdx.x & (KT - 1));
-      rowv = threadIdx.x < KT ? (qq < L ? lse[row_bh + qq] * LOG2E : INFINITY)
-                              : (qq < L ? delta[row_bh + qq] : 0.f);
+      const float v = (threadIdx.x < KT ? lse : delta)[row_bh + min(qq, L - 1)];
+      rowv = threadIdx.x < KT ? (qq < L ? v * LOG2E : INFINITY) : (qq < L ? v : 0.f);
     }
   };
   auto store_rows = [&](int bi) {
@@ -570,11 +577,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask ma
     const bf16_t* Qs = smem + buf * 2 * TILE;
     const bf16_t* Ds = Qs + TILE;
     if (wave_live) {
-      uint32_t dw[2] = {0xffffffffu, 0xffffffffu};
-      if (drop_bits_t && kv) {
-        dw[0] = drop_bits_t[(int64_t)key * drop_words + (qt >> 5)];
-        if ((qt >> 5) + 1 < drop_words) dw[1] = drop_bits_t[(int64_t)key * drop_words + (qt >> 5) + 1];
-      }
+      uint32_t dw[2];
+      load_drop_words(drop_bits_t, drop_words, kv ? key : 0, kv, qt, dw);
       const uint64_t qm = sets_bits(mask, selq, qt);
 #pragma unroll 1
       for (int u = 0; u < 2; ++u) {  // 32-query sub-tiles (not unrolled: keeps 2 waves/SIMD)
@@ -751,6 +755,7 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   MMT_CHECK_ARG(s_t % 8 == 0 && s_b % 8 == 0 && o_s_t % 4 == 0 && o_s_b % 4 == 0,
                 "mmt_attn_fwd: strides must keep 16-B rows");
   MMT_CHECK_ARG(keep_prob > 0.f && keep_prob <= 1.f, "mmt_attn_fwd: keep_prob");
+  MMT_CHECK_ARG(!bias || L % 4 == 0, "mmt_attn_fwd: the additive bias needs L %% 4 == 0 (float4 rows)");
   AttnMask m;
   int rc = fill_mask(m, n_sets, set_start, set_len, set_vis, L);
   if (rc) return rc;
@@ -787,14 +792,11 @@ extern "C" int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   const int words = (L + 31) / 32;
   const float dscale = drop_bits ? 1.f / keep_prob : 1.f;
   hipStream_t s = as_stream(stream);
-  const int64_t nd = (int64_t)B * H * L;
-  ATTN_DISPATCH(DH, hipLaunchKernelGGL(attn_bwd_delta_kernel<DH>, dim3((nd + 255) / 256), dim3(256),
-                                       0, s, (const bf16_t*)o, o_s_b, o_s_t, (const bf16_t*)dout,
-                                       d_s_b, d_s_t, B, L, H, delta));
   dim3 grid((L + 127) / 128, H, B);
   ATTN_DISPATCH(DH, hipLaunchKernelGGL(attn_bwd_dq_kernel<DH>, grid, dim3(NT), 0, s, g, m, drop_bits,
                                        words, dscale, (const bf16_t*)dout, d_s_b, d_s_t,
-                                       lse, delta, (bf16_t*)dqkv, dq_s_b, dq_s_t));
+                                       lse, (const bf16_t*)o, o_s_b, o_s_t, delta, (bf16_t*)dqkv,
+                                       dq_s_b, dq_s_t));
   ATTN_DISPATCH(DH, hipLaunchKernelGGL(attn_bwd_dkdv_kernel<DH>, grid, dim3(NT), 0, s, g, m,
                                        drop_bits_t, words, dscale, (const bf16_t*)dout,
                                        d_s_b, d_s_t, lse, delta, (bf16_t*)dqkv, dq_s_b, dq_s_t));

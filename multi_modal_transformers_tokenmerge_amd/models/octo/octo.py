@@ -184,6 +184,20 @@ class Octo:
         st.update(head_sv=hsv, xL_shape=tuple(xL.shape))
         return loss, st
 
+    def predict_diffusion_action(self, text_tokens, images, rng, sample_offset=0, train=True,
+                                 z: Optional[torch.Tensor] = None, return_noise=False,
+                                 positions=None):
+        """Reference :147-154: readouts (the reference's backbone always runs with
+        train=True, :120, and its image encoder samples positions by default) -> readout mean ->
+        the 32-step DDPM sampler (action_heads/diffusion.py:146-209). Returns (B, 8) fp32."""
+        xL, _ = self.generate_readouts(text_tokens, images, train, rng, sample_offset, positions)
+        B = xL.shape[0]
+        e = torch.empty((B, self.D), dtype=torch.bfloat16, device=xL.device)
+        _C.call("mmt_rows_mean_fwd", _C.ptr(xL), xL.stride(0), xL.stride(1), B, self.D,
+                _C.ptr(self.readout_rows), self.readout_rows.numel(), _C.ptr(e), e.stride(0),
+                _C.stream_ptr())
+        return self.head.predict_action(e, rng, sample_offset, z, return_noise)
+
     def backward(self, st: Dict):
         """Reverse schedule of compute_diffusion_denoise_loss; writes every parameter gradient
         into the flat gradient buffer (which must be zeroed before the forward)."""

@@ -1,12 +1,10 @@
 #!/bin/bash
-# smoke + bench with the CPU baseline + kernel-trace profile + two PMC passes on the probe GEMM.
+# attention/sampler/octo parity on the GPU, attention micro-bench, bench line
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
-timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_full.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --probe-only > gpurun_out/pmc_fetch.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --probe-only > gpurun_out/pmc_write.log 2>&1
-rc=$?
-echo "exit $rc" >> gpurun_out/smoke.log
-exit $rc
+timeout -k 10 500 python -u -m pytest -x -v --timeout 180 --timeout-method thread \
+  tests/test_sampler_gpu.py tests/test_attn_norm_gpu.py tests/test_t5_stem_gpu.py \
+  tests/test_octo_gpu.py tests/test_gemm_nt256_gpu.py > gpurun_out/r1b_tests.log 2>&1 &&
+timeout -k 10 200 python tools/attn_bench.py > gpurun_out/r1b_attn.log 2>&1 &&
+timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/r1b_bench.log 2>&1
