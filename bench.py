@@ -78,10 +78,14 @@ def algorithmic_flops_per_sample(model) -> float:
     return 3 * (tr + stem) + t5
 
 
+PROBE_KERNEL = "gemm_nt256_kernel<192, 0, true, 2>"
+
+
 def probe_dominant_gemm(model, B, reps=20):
     """Average duration (HIP events on the launching stream) of the MLP up-projection GEMM of
     block 0 at the step's exact shape: M = B*L1, N = mlp_dim, K = D (bias+relu+dropout fused);
-    the library's automatic choice for this NT shape is the direct-to-LDS kernel."""
+    the library's automatic choice for this NT shape (N >= 1152, N % 192 == 0, K <= 512) is the
+    persistent 256 x 192 kernel gemm_nt256_kernel<192, 0, true, 2> (csrc/gemm.hip)."""
     cfg = model.cfg
     blk = model.stack.blocks[0]
     sets, _, ts, r = model.layer_sets[0]
@@ -117,7 +121,7 @@ def probe_dominant_gemm(model, B, reps=20):
     e1.synchronize()
     avg_ms = e0.elapsed_time(e1) / reps
     flops = 2.0 * M * cfg.mlp_dim * D
-    return dict(kernel="gemm_glds_nt_kernel<0> (MLP Dense_0 fwd, bias+relu+dropout epilogue)",
+    return dict(kernel=PROBE_KERNEL + " (MLP Dense_0 fwd, bias+relu+dropout epilogue)",
                 shape=[M, cfg.mlp_dim, D], avg_us=avg_ms * 1e3, flops=flops,
                 tflops=flops / (avg_ms * 1e-3) / 1e12)
 
@@ -130,7 +134,7 @@ def gemm_traffic(shape):
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_gemm_pmc.json")), reverse=True):
         with open(f) as fh:
             d = json.load(fh)
-        if list(d.get("shape_MNK", [])) == list(shape):
+        if list(d.get("shape_MNK", [])) == list(shape) and d.get("kernel") == PROBE_KERNEL:
             return d["hbm_bytes_per_launch"]
     return None
 
