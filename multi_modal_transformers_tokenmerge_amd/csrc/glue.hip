@@ -100,7 +100,8 @@ __global__ void seq_assemble_bwd_kernel(int B, int L, int D, const int32_t* __re
 
 // d(row_emb)[tok] += dx0[b, l(j)] over every image token (b, j) with rtok == tok (same for col).
 // One workgroup = 64 columns x a slice of the image tokens; the two (Q x 64) partial tables are
-// accumulated with LDS atomics and flushed with one global atomic per table entry.
+// accumulated with LDS atomics and flushed with one global atomic per table entry. Measured:
+// bound by the LDS float atomics (~50 M per step at B = 256); fewer, longer workgroups were slower.
 constexpr int EMB_COLS = 64, EMB_SPLIT = 128;
 __global__ __launch_bounds__(256) void embed_grad_kernel(int B, int L, int D, int NI, int Q,
                                                          const int32_t* __restrict__ img_rows,
@@ -216,20 +217,28 @@ __global__ void diffusion_prep_kernel(const uint32_t* __restrict__ rng, int B, i
   }
 }
 
-// dW[k] += sum_b 2 pi t_b (cos(h) dsin - sin(h) dcos)
+// dW[k] += sum_b 2 pi t_b (cos(h) dsin - sin(h) dcos); the batch is split over grid.y
+// (FB_B samples per workgroup, fp32 atomics into dw) so the launch is not one serial loop over B.
+constexpr int FB_B = 8;
 __global__ void fourier_bwd_kernel(const bf16_t* __restrict__ dfeats, int B, int F,
                                    const int32_t* __restrict__ t, const float* __restrict__ fw,
                                    float* __restrict__ dw) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= F) return;
+  const int b0 = blockIdx.y * FB_B;
+  const float w = fw[k];
   float acc = 0.f;
-  for (int b = 0; b < B; ++b) {
-    const float tt = 2.f * 3.141592653589793f * (float)t[b];
-    const float h = tt * fw[k];
-    const float dc = bf2f(dfeats[(int64_t)b * 2 * F + k]), ds = bf2f(dfeats[(int64_t)b * 2 * F + F + k]);
-    acc += tt * (cosf(h) * ds - sinf(h) * dc);
+#pragma unroll
+  for (int i = 0; i < FB_B; ++i) {
+    const int b = b0 + i;
+    if (b < B) {
+      const float tt = 2.f * 3.141592653589793f * (float)t[b];
+      const float h = tt * w;
+      const float dc = bf2f(dfeats[(int64_t)b * 2 * F + k]), ds = bf2f(dfeats[(int64_t)b * 2 * F + F + k]);
+      acc += tt * (cosf(h) * ds - sinf(h) * dc);
+    }
   }
-  dw[k] += acc;
+  atomicAdd(dw + k, acc);
 }
 
 // loss = mean_b sum_j 0.5 (pred - eps)^2 (optax.l2_loss, diffusion.py:141-142);
@@ -410,7 +419,8 @@ extern "C" int mmt_diffusion_prep(const uint32_t* rng, int B, int A, int steps,
 extern "C" int mmt_fourier_bwd(const void* dfeats, int B, int F, const int32_t* t,
                                const float* fourier_w, float* dw, mmt_stream_t stream) {
   MMT_CHECK_ARG(dfeats && t && fourier_w && dw && B > 0 && F > 0, "mmt_fourier_bwd: args");
-  hipLaunchKernelGGL(fourier_bwd_kernel, dim3((F + 255) / 256), dim3(256), 0, as_stream(stream),
+  hipLaunchKernelGGL(fourier_bwd_kernel, dim3((F + 63) / 64, (B + FB_B - 1) / FB_B), dim3(64), 0,
+                     as_stream(stream),
                      (const bf16_t*)dfeats, B, F, t, fourier_w, dw);
   MMT_CHECK_LAUNCH("mmt_fourier_bwd");
   return MMT_OK;

@@ -160,12 +160,27 @@ __global__ void maxpool_patch_kernel(const float* __restrict__ conv, int64_t npa
 __global__ void maxpool_patch_bwd_kernel(const float* __restrict__ dpooled,
                                          const uint8_t* __restrict__ arg, int64_t npatch, int win,
                                          int C, bf16_t* __restrict__ G) {
+  // one thread per (patch, window slot, 8 channels): one 16-B store of G
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= npatch * win * C) return;
-  const int c = idx % C;
-  const int s = (idx / C) % win;
-  const int64_t p = idx / ((int64_t)C * win);
-  G[idx] = (arg[p * C + c] == s) ? f2bf(dpooled[p * C + c]) : (bf16_t)0;
+  const int c8 = C / 8;
+  if (idx >= npatch * win * c8) return;
+  const int c = (int)(idx % c8) * 8;
+  const int s = (int)((idx / c8) % win);
+  const int64_t p = idx / ((int64_t)c8 * win);
+  const uint2 a = *reinterpret_cast<const uint2*>(arg + p * C + c);
+  const float4 d0 = *reinterpret_cast<const float4*>(dpooled + p * C + c);
+  const float4 d1 = *reinterpret_cast<const float4*>(dpooled + p * C + c + 4);
+  const float d[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+  uint32_t w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t lo = ((q < 2 ? a.x : a.y) >> (16 * (q & 1))) & 0xffu;
+    const uint32_t hi = ((q < 2 ? a.x : a.y) >> (16 * (q & 1) + 8)) & 0xffu;
+    const uint32_t vlo = lo == (uint32_t)s ? (uint32_t)f2bf(d[2 * q]) : 0u;
+    const uint32_t vhi = hi == (uint32_t)s ? (uint32_t)f2bf(d[2 * q + 1]) : 0u;
+    w[q] = vlo | (vhi << 16);
+  }
+  *reinterpret_cast<uint4*>(G + (p * win + s) * C + c) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 __device__ __forceinline__ float gelu_tanh(float z) {
@@ -298,6 +313,190 @@ __global__ __launch_bounds__(GN_NT) void groupnorm_gelu_bwd_kernel(
   }
 }
 
+// Register-resident variants (R*C == NV * GN_NT * 4, C a power of two <= 256): every thread
+// keeps its NV float4 of the sample in registers, so x (and dy) are read once with all loads in
+// flight, and each thread owns one fixed channel quad c0..c0+3 ((4 t) % C): the per-channel sums
+// reduce across the lanes sharing it with xor shuffles, then across the 4 waves in LDS.
+template <int NV>
+__global__ __launch_bounds__(GN_NT) void groupnorm_gelu_fwd_reg_kernel(
+    const float* __restrict__ x, int R, int C, int G, float eps, const float* __restrict__ gamma,
+    const float* __restrict__ beta, bf16_t* __restrict__ y, float* __restrict__ mean,
+    float* __restrict__ rstd) {
+  __shared__ float red[2][GN_NT / 64][256];
+  __shared__ float gst[2][256];
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const float4* xb = reinterpret_cast<const float4*>(x + (int64_t)b * R * C);
+  float4 v[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = xb[t + k * GN_NT];
+  const int c0 = (4 * t) % C, cpg = C / G;
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const float e4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s1[e] += e4[e];
+      s2[e] = fmaf(e4[e], e4[e], s2[e]);
+    }
+  }
+  for (int o = C / 4; o < 64; o <<= 1)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s1[e] += __shfl_xor(s1[e], o, 64);
+      s2[e] += __shfl_xor(s2[e], o, 64);
+    }
+  if (lane < C / 4)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[0][wave][c0 + e] = s1[e];
+      red[1][wave][c0 + e] = s2[e];
+    }
+  __syncthreads();
+  if (t < G) {
+    float a = 0.f, q = 0.f;
+    for (int w = 0; w < GN_NT / 64; ++w)
+      for (int j = 0; j < cpg; ++j) {
+        a += red[0][w][t * cpg + j];
+        q += red[1][w][t * cpg + j];
+      }
+    const float n = (float)R * cpg;
+    const float mu = a / n;
+    const float rs = rsqrtf(fmaxf(0.f, q / n - mu * mu) + eps);
+    gst[0][t] = mu;
+    gst[1][t] = rs;
+    mean[b * G + t] = mu;
+    rstd[b * G + t] = rs;
+  }
+  __syncthreads();
+  float mu[4], rs[4], ga[4], be[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int g = (c0 + e) / cpg;
+    mu[e] = gst[0][g];
+    rs[e] = gst[1][g];
+    ga[e] = gamma[c0 + e];
+    be[e] = beta[c0 + e];
+  }
+  uint2* yb = reinterpret_cast<uint2*>(y + (int64_t)b * R * C);
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const float e4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = gelu_tanh((e4[e] - mu[e]) * rs[e] * ga[e] + be[e]);
+    yb[t + k * GN_NT] = make_uint2((uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16),
+                                   (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16));
+  }
+}
+
+template <int NV>
+__global__ __launch_bounds__(GN_NT) void groupnorm_gelu_bwd_reg_kernel(
+    const float* __restrict__ dy, const float* __restrict__ x, int R, int C, int G,
+    const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ mean, const float* __restrict__ rstd, float* dx, int accumulate,
+    float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float red[4][GN_NT / 64][256];
+  __shared__ float gm[2][256];
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const float4* xb = reinterpret_cast<const float4*>(x + (int64_t)b * R * C);
+  const float4* db = reinterpret_cast<const float4*>(dy + (int64_t)b * R * C);
+  float4 xv[NV], dv[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    xv[k] = xb[t + k * GN_NT];
+    dv[k] = db[t + k * GN_NT];
+  }
+  const int c0 = (4 * t) % C, cpg = C / G;
+  float mu[4], rs[4], ga[4], be[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int g = (c0 + e) / cpg;
+    mu[e] = mean[b * G + g];
+    rs[e] = rstd[b * G + g];
+    ga[e] = gamma[c0 + e];
+    be[e] = beta[c0 + e];
+  }
+  float a[4][4] = {};  // [sum dxhat, sum dxhat*xhat, sum dz*xhat, sum dz][channel]
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    float* xe = reinterpret_cast<float*>(&xv[k]);
+    float* de = reinterpret_cast<float*>(&dv[k]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float xh = (xe[e] - mu[e]) * rs[e];
+      const float dz = de[e] * gelu_tanh_grad(xh * ga[e] + be[e]);
+      xe[e] = xh;  // keep xhat and dz for the final pass
+      de[e] = dz;
+      a[0][e] += dz * ga[e];
+      a[1][e] = fmaf(dz * ga[e], xh, a[1][e]);
+      a[2][e] = fmaf(dz, xh, a[2][e]);
+      a[3][e] += dz;
+    }
+  }
+  for (int o = C / 4; o < 64; o <<= 1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[i][e] += __shfl_xor(a[i][e], o, 64);
+  if (lane < C / 4)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[i][wave][c0 + e] = a[i][e];
+  __syncthreads();
+  if (t < G) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int w = 0; w < GN_NT / 64; ++w)
+      for (int j = 0; j < cpg; ++j) {
+        s1 += red[0][w][t * cpg + j];
+        s2 += red[1][w][t * cpg + j];
+      }
+    const float n = (float)R * cpg;
+    gm[0][t] = s1 / n;
+    gm[1][t] = s2 / n;
+  }
+  if (t < C) {
+    float s3 = 0.f, s4 = 0.f;
+    for (int w = 0; w < GN_NT / 64; ++w) {
+      s3 += red[2][w][t];
+      s4 += red[3][w][t];
+    }
+    atomicAdd(dgamma + t, s3);
+    atomicAdd(dbeta + t, s4);
+  }
+  __syncthreads();
+  float m1[4], m2[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int g = (c0 + e) / cpg;
+    m1[e] = gm[0][g];
+    m2[e] = gm[1][g];
+  }
+  float4* dxb = reinterpret_cast<float4*>(dx + (int64_t)b * R * C);
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const float* xe = reinterpret_cast<const float*>(&xv[k]);
+    const float* de = reinterpret_cast<const float*>(&dv[k]);
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = rs[e] * (de[e] * ga[e] - m1[e] - xe[e] * m2[e]);
+    float4 r = make_float4(o[0], o[1], o[2], o[3]);
+    if (accumulate) {
+      const float4 p = dxb[t + k * GN_NT];
+      r.x += p.x; r.y += p.y; r.z += p.z; r.w += p.w;
+    }
+    dxb[t + k * GN_NT] = r;
+  }
+}
+
+// NV of the register-resident kernels for this (R, C), or 0 (general kernel).
+inline int gn_reg_nv(int R, int C) {
+  if (C < 4 || C > 256 || (C & (C - 1)) || (int64_t)R * C % (GN_NT * 4)) return 0;
+  const int64_t nv = (int64_t)R * C / (GN_NT * 4);
+  return (nv == 4 || nv == 8 || nv == 16 || nv == 32) ? (int)nv : 0;
+}
+
 // encode_patch_position (image_tokenizer.py:74-132) for every (b, i, p):
 // interval [k*P, (k+1)*P) -> floor(idx / Himg * (Q - 1)) in fp32; "row" token from interval
 // p % PPD, "col" from p // PPD (the reference's transposed convention, :91-92, pinned by
@@ -392,8 +591,9 @@ extern "C" int mmt_maxpool_patch(const void* conv, int64_t npatch, int win, int 
 
 extern "C" int mmt_maxpool_patch_bwd(const void* dpooled, const uint8_t* argmax, int64_t npatch,
                                      int win, int C, void* G, mmt_stream_t stream) {
-  MMT_CHECK_ARG(dpooled && argmax && G && npatch > 0 && win > 0 && C > 0, "mmt_maxpool_patch_bwd: args");
-  const int64_t n = npatch * win * C;
+  MMT_CHECK_ARG(dpooled && argmax && G && npatch > 0 && win > 0 && C > 0 && C % 8 == 0,
+                "mmt_maxpool_patch_bwd: args (C %% 8 == 0)");
+  const int64_t n = npatch * win * (C / 8);
   hipLaunchKernelGGL(maxpool_patch_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0,
                      as_stream(stream), (const float*)dpooled, argmax, npatch, win, C, (bf16_t*)G);
   MMT_CHECK_LAUNCH("mmt_maxpool_patch_bwd");
@@ -406,9 +606,20 @@ extern "C" int mmt_groupnorm_gelu_fwd(const void* x, int B, int R, int C, int G,
   MMT_CHECK_ARG(x && y && gamma && beta && mean && rstd && B > 0 && R > 0,
                 "mmt_groupnorm_gelu_fwd: args");
   MMT_CHECK_ARG(C > 0 && GN_NT % C == 0 && G > 0 && C % G == 0, "mmt_groupnorm_gelu_fwd: C=%d G=%d", C, G);
-  const size_t sh = sizeof(float) * (2 * GN_NT + 2 * G);
-  hipLaunchKernelGGL(groupnorm_gelu_fwd_kernel, dim3(B), dim3(GN_NT), sh, as_stream(stream),
-                     (const float*)x, R, C, G, eps, gamma, beta, (bf16_t*)y, mean, rstd);
+  const int nv = gn_reg_nv(R, C);
+#define GN_FWD_REG(NV_)                                                                          \
+  hipLaunchKernelGGL(groupnorm_gelu_fwd_reg_kernel<NV_>, dim3(B), dim3(GN_NT), 0, as_stream(stream), \
+                     (const float*)x, R, C, G, eps, gamma, beta, (bf16_t*)y, mean, rstd)
+  if (nv == 4) GN_FWD_REG(4);
+  else if (nv == 8) GN_FWD_REG(8);
+  else if (nv == 16) GN_FWD_REG(16);
+  else if (nv == 32) GN_FWD_REG(32);
+  else {
+    const size_t sh = sizeof(float) * (2 * GN_NT + 2 * G);
+    hipLaunchKernelGGL(groupnorm_gelu_fwd_kernel, dim3(B), dim3(GN_NT), sh, as_stream(stream),
+                       (const float*)x, R, C, G, eps, gamma, beta, (bf16_t*)y, mean, rstd);
+  }
+#undef GN_FWD_REG
   MMT_CHECK_LAUNCH("mmt_groupnorm_gelu_fwd");
   return MMT_OK;
 }
@@ -420,10 +631,22 @@ extern "C" int mmt_groupnorm_gelu_bwd(const void* dy, const void* x, int B, int 
   MMT_CHECK_ARG(dy && x && dx && gamma && beta && mean && rstd && dgamma && dbeta && B > 0,
                 "mmt_groupnorm_gelu_bwd: args");
   MMT_CHECK_ARG(C > 0 && GN_NT % C == 0 && G > 0 && C % G == 0, "mmt_groupnorm_gelu_bwd: C/G");
-  const size_t sh = sizeof(float) * (4 * GN_NT + 2 * G);
-  hipLaunchKernelGGL(groupnorm_gelu_bwd_kernel, dim3(B), dim3(GN_NT), sh, as_stream(stream),
-                     (const float*)dy, (const float*)x, R, C, G, gamma, beta, mean, rstd,
-                     (float*)dx, accumulate, dgamma, dbeta);
+  const int nv = gn_reg_nv(R, C);
+#define GN_BWD_REG(NV_)                                                                          \
+  hipLaunchKernelGGL(groupnorm_gelu_bwd_reg_kernel<NV_>, dim3(B), dim3(GN_NT), 0, as_stream(stream), \
+                     (const float*)dy, (const float*)x, R, C, G, gamma, beta, mean, rstd,          \
+                     (float*)dx, accumulate, dgamma, dbeta)
+  if (nv == 4) GN_BWD_REG(4);
+  else if (nv == 8) GN_BWD_REG(8);
+  else if (nv == 16) GN_BWD_REG(16);
+  else if (nv == 32) GN_BWD_REG(32);
+  else {
+    const size_t sh = sizeof(float) * (4 * GN_NT + 2 * G);
+    hipLaunchKernelGGL(groupnorm_gelu_bwd_kernel, dim3(B), dim3(GN_NT), sh, as_stream(stream),
+                       (const float*)dy, (const float*)x, R, C, G, gamma, beta, mean, rstd,
+                       (float*)dx, accumulate, dgamma, dbeta);
+  }
+#undef GN_BWD_REG
   MMT_CHECK_LAUNCH("mmt_groupnorm_gelu_bwd");
   return MMT_OK;
 }

@@ -4,9 +4,9 @@ End-to-end parity harness: run one HIP training step (forward loss + every param
 and the fp32 CPU restatement (oracle/octo_ref.py) on identical inputs, identical dropout streams
 and the HIP run's own position tokens, diffusion (t, eps) and ToMe indices.
 
-Tolerance (see tests/test_octo_gpu.py for the derivation):
-  loss: relative difference <= 2e-2
-  gradients: cosine similarity >= 0.98 per parameter tensor, >= 0.99 on the concatenation
+Tolerance (see tests/test_octo_gpu.py for the derivation from the measured noise floor):
+  loss: relative difference <= 4e-2
+  gradients: cosine similarity >= 0.96 per parameter tensor, >= 0.985 on the concatenation
 """
 import dataclasses
 
@@ -69,8 +69,9 @@ def run_parity(cfg, B, seed=0):
     return out
 
 
-def check(res, cos_min=0.98):
-    assert abs(res["loss"] - res["ref_loss"]) <= 2e-2 * abs(res["ref_loss"]), res["loss"]
+def check(res, cos_min=0.96, cos_all_min=0.985, loss_rel=4e-2):
+    assert abs(res["loss"] - res["ref_loss"]) <= loss_rel * abs(res["ref_loss"]), \
+        (res["loss"], res["ref_loss"])
     bad = {k: v for k, v in res["cos"].items() if v < cos_min}
     assert not bad, f"low gradient cosine: {dict(list(bad.items())[:8])}"
-    assert res["cos_all"] >= 0.99
+    assert res["cos_all"] >= cos_all_min, res["cos_all"]

@@ -4,10 +4,15 @@ run's own position tokens, diffusion (t, eps) and ToMe indices injected into the
 
 The oracle computes with the bf16-rounded Dense/attention kernels the HIP path actually multiplies
 (its bf16 shadow), fp32 everywhere else. Remaining differences come from bf16 activations
-(LayerNorm outputs, q/k/v, attention probabilities, MLP hidden) and from relu gates that flip under
-the resulting forward perturbation, so the end-to-end tolerance is (per-op tests are far tighter):
-  loss: relative difference <= 2e-2
-  gradients: cosine similarity >= 0.98 per parameter tensor, >= 0.99 on the concatenation
+(LayerNorm outputs, q/k/v, attention probabilities, MLP hidden, stem GroupNorm output, im2col
+pixels) and from relu gates that flip under the resulting forward perturbation. The end-to-end bar
+is set from the measured noise floor of that comparison (tools/parity_sweep.py, 12 runs over
+seeds x ToMe on/off x dropout on/off, profiles/r01_parity_sweep.txt: loss within 2.7 %, global
+gradient cosine >= 0.988, per-tensor >= 0.970 — the same with fp32 or bf16 LayerNorm input
+gradients), with margin, and is checked on two seeds:
+  loss: relative difference <= 4e-2
+  gradients: cosine similarity >= 0.96 per parameter tensor, >= 0.985 on the concatenation
+The per-op GPU tests (GEMM, attention, LayerNorm, ToMe, stem, sampler) carry the tight bars.
 """
 import pytest
 
@@ -19,11 +24,13 @@ pytestmark = pytest.mark.gpu
 def test_octo_tiny_parity(dev):
     from multi_modal_transformers_tokenmerge_amd.models.octo.config import get_config
     cfg = get_config("octo-tiny", num_blocks=2)
-    _check(run_parity(cfg, 3))
+    for seed in (0, 1):
+        _check(run_parity(cfg, 3, seed=seed))
 
 
 def test_octo_small_tome_parity(dev):
     from multi_modal_transformers_tokenmerge_amd.models.octo.config import get_config
     from multi_modal_transformers_tokenmerge_amd.tokenizers.text.t5_base import T5Config
     cfg = get_config("octo-small-tome16", num_blocks=3, t5=T5Config(num_layers=2))
-    _check(run_parity(cfg, 2))
+    for seed in (0, 1):
+        _check(run_parity(cfg, 2, seed=seed))

@@ -1,0 +1,95 @@
+"""Stem and head side kernels vs torch fp32/fp64 references of the same op (same inputs):
+GroupNorm+gelu forward/backward (image_tokenizer.py:165-167, gato_resnet.yaml:68-77; both the
+register-resident kernels, R*C = NV*1024, and the general one), per-patch max-pool forward/backward
+(:159, window 3x3 stride 1 VALID on the conv map) and the FourierFeatures kernel gradient
+(diffusion.py:41-48)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from multi_modal_transformers_tokenmerge_amd import _C, _kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+def _gelu_tanh(z):
+    return 0.5 * z * (1.0 + torch.tanh(math.sqrt(2.0 / math.pi) * (z + 0.044715 * z ** 3)))
+
+
+def _gn_gelu_ref(x, G, gamma, beta, eps):
+    B, R, C = x.shape
+    xg = x.view(B, R, G, C // G)
+    mu = xg.mean(dim=(1, 3), keepdim=True)
+    var = xg.var(dim=(1, 3), unbiased=False, keepdim=True)
+    xh = ((xg - mu) / torch.sqrt(var + eps)).view(B, R, C)
+    return _gelu_tanh(xh * gamma + beta)
+
+
+@pytest.mark.parametrize("B,R,C,G", [(5, 256, 64, 32), (3, 64, 64, 32), (2, 100, 64, 32),
+                                     (4, 512, 64, 16)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_groupnorm_gelu(dev, B, R, C, G, accumulate):
+    g = torch.Generator().manual_seed(R + C)
+    x = torch.randn((B, R, C), generator=g) * 2 + 0.5
+    gamma = 1 + 0.1 * torch.randn(C, generator=g)
+    beta = 0.1 * torch.randn(C, generator=g)
+    dy = torch.randn((B, R, C), generator=g)
+    prior = torch.randn((B, R, C), generator=g)
+    eps = 1e-6
+    xd, gd, bd, dyd = x.to(dev), gamma.to(dev), beta.to(dev), dy.to(dev)
+    y, mu, rs = K.groupnorm_gelu_fwd(xd.contiguous(), G, gd, bd, eps)
+    dgam = torch.zeros(C, device=dev)
+    dbet = torch.zeros(C, device=dev)
+    dx = prior.to(dev).clone() if accumulate else None
+    dx = K.groupnorm_gelu_bwd(dyd, xd, G, gd, bd, mu, rs, dgam, dbet, dx=dx, accumulate=accumulate)
+    torch.cuda.synchronize()
+
+    x64 = x.double().requires_grad_()
+    g64 = gamma.double().requires_grad_()
+    b64 = beta.double().requires_grad_()
+    ref = _gn_gelu_ref(x64, G, g64, b64, eps)
+    ref.backward(dy.double())
+    np.testing.assert_allclose(y.float().cpu().numpy(), ref.detach().numpy(), atol=2e-2, rtol=1e-2)
+    want_dx = x64.grad + (prior.double() if accumulate else 0)
+    np.testing.assert_allclose(dx.cpu().double().numpy(), want_dx.numpy(), atol=2e-3, rtol=2e-3)
+    np.testing.assert_allclose(dgam.cpu().double().numpy(), g64.grad.numpy(), rtol=2e-3, atol=1e-2)
+    np.testing.assert_allclose(dbet.cpu().double().numpy(), b64.grad.numpy(), rtol=2e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("npatch,win,C", [(37, 9, 64), (8, 4, 16)])
+def test_maxpool_patch_fwd_bwd(dev, npatch, win, C):
+    g = torch.Generator().manual_seed(npatch)
+    conv = torch.randn((npatch * win, C), generator=g)
+    conv[:win, :3] = 1.0  # ties: the first maximum wins
+    pooled, arg = K.maxpool_patch(conv.to(dev), win)
+    dpooled = torch.randn((npatch, C), generator=g)
+    G = K.maxpool_patch_bwd(dpooled.to(dev), arg, win)
+    torch.cuda.synchronize()
+    v = conv.view(npatch, win, C)
+    want_arg = torch.argmax((v == v.max(dim=1, keepdim=True).values).int(), dim=1)  # first max
+    assert torch.equal(pooled.cpu(), v.max(dim=1).values)
+    assert torch.equal(arg.cpu().long(), want_arg)
+    want_G = torch.zeros((npatch, win, C))
+    want_G.scatter_(1, want_arg.unsqueeze(1), dpooled.unsqueeze(1))
+    assert torch.equal(G.cpu().float().view(npatch, win, C), want_G.to(torch.bfloat16).float())
+
+
+@pytest.mark.parametrize("B,F", [(256, 192), (7, 96)])
+def test_fourier_bwd(dev, B, F):
+    g = torch.Generator().manual_seed(B)
+    dfeats = torch.randn((B, 2 * F), generator=g).to(torch.bfloat16)
+    t = torch.randint(0, 32, (B,), generator=g, dtype=torch.int32)
+    w = torch.randn(F, generator=g)
+    dw = torch.full((F,), 0.25)
+    dwd = dw.to(dev)
+    dfd, td, wd = dfeats.to(dev), t.to(dev), w.to(dev)  # keep the device copies alive
+    _C.call("mmt_fourier_bwd", _C.ptr(dfd), B, F, _C.ptr(td), _C.ptr(wd), _C.ptr(dwd),
+            _C.stream_ptr())
+    torch.cuda.synchronize()
+    tt = 2 * np.pi * t.double().numpy()[:, None]
+    h = tt * w.double().numpy()[None, :]
+    d = dfeats.double().numpy()
+    want = 0.25 + (tt * (np.cos(h) * d[:, F:] - np.sin(h) * d[:, :F])).sum(0)
+    np.testing.assert_allclose(dwd.cpu().double().numpy(), want, rtol=1e-3, atol=1e-2)
