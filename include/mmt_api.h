@@ -305,6 +305,23 @@ int mmt_diffusion_sample(const uint32_t* rng, int B, int A, int steps, int64_t s
                          const float* coef, const float* z_in, int H, float* actions,
                          float* z_out, mmt_stream_t stream);
 
+/* ------------------------------------------------------------------ continuous / categorical heads
+ * (SURVEY §8f row 4). Grouped readout means (categorical.py:32-37): out (B, G, D) bf16 = mean of
+ * the rows with row_group[l] == g (counts[g] rows); backward writes the whole fp32 dx (B, L, D). */
+int mmt_rows_group_mean_fwd(const void* x, int64_t xs_b, int64_t xs_t, int B, int L, int D,
+                            const int32_t* row_group, int G, const int32_t* counts, void* out,
+                            mmt_stream_t stream);
+int mmt_rows_group_mean_bwd(const void* de, int B, int L, int D, const int32_t* row_group, int G,
+                            const int32_t* counts, void* dx, mmt_stream_t stream);
+/* kind 0: ContinuousActionHead tanh squash (continuous.py:26) + compute_l2_loss (octo.py:167-174);
+ * kind 1: CategoricalActionHead logits + compute_ce_loss with assign_bins (octo.py:187-198,
+ * categorical.py:12-22: digitize over `edges`, one_hot(bin, N) zero past the last class).
+ * loss (+=, zero it first) = inv_count x sum of the per-row losses; dz bf16 (R, N). y NULL:
+ * forward only (kind 0 writes pred). */
+int mmt_action_head(int kind, const float* z, int64_t ldz, int R, int N, const float* y,
+                    const float* edges, int n_edges, float max_action, float inv_count, float* pred,
+                    float* loss, void* dz, mmt_stream_t stream);
+
 /* ------------------------------------------------------------------ T5 encoder pieces
  * (tokenizers/text/t5_base.py:8-15, frozen FlaxT5 encoder): T5LayerNorm and the shared
  * embedding lookup. */

@@ -55,6 +55,9 @@ SIGNATURES: dict[str, list] = {
     "mmt_fourier_bwd": [P, I, I, P, P, P, P],
     "mmt_diffusion_loss": [P, L, P, I, I, F, P, P, P],
     "mmt_diffusion_sample": [P, I, I, I, L, P, L, P, L, P, L, P, P, P, P, I, P, P, P],
+    "mmt_rows_group_mean_fwd": [P, L, L, I, I, I, P, I, P, P, P],
+    "mmt_rows_group_mean_bwd": [P, I, I, I, P, I, P, P, P],
+    "mmt_action_head": [I, P, L, I, I, P, P, I, F, F, P, P, P, P],
     "mmt_rmsnorm_fwd": [P, L, I, P, F, P, P],
     "mmt_embedding_gather": [P, L, I, P, I, P, P],
     "mmt_adamw": [P, P, P, P, P, L, P, F, F, F, F, F, F, P],

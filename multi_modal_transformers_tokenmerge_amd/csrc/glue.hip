@@ -166,6 +166,90 @@ __global__ void rows_mean_bwd_kernel(const bf16_t* __restrict__ de, int64_t ld_d
   dx[idx] = row_flag[l] >= 0 ? bf2f(de[b * ld_de + d]) / nrows : 0.f;
 }
 
+// Grouped readout means (categorical.py:32-37: "batch (action timestep) embeddings -> batch action
+// timestep embeddings", mean over timestep): out[b, g, :] = mean of the rows l with
+// row_group[l] == g (counts[g] of them); bf16 (B, G, D). Backward: dx[b, l, :] = de[b, g(l), :] /
+// counts[g], 0 for rows in no group (whole fp32 buffer).
+__global__ void rows_group_mean_fwd_kernel(const float* __restrict__ x, int64_t xs_b, int64_t xs_t,
+                                           int L, int D, const int32_t* __restrict__ row_group,
+                                           int G, const int32_t* __restrict__ counts,
+                                           bf16_t* __restrict__ out) {
+  const int b = blockIdx.x, g = blockIdx.y;
+  const float inv = 1.f / (float)counts[g];
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = 0.f;
+    for (int l = 0; l < L; ++l)
+      if (row_group[l] == g) s += x[b * xs_b + (int64_t)l * xs_t + d];
+    out[((int64_t)b * G + g) * D + d] = f2bf(s * inv);
+  }
+}
+
+__global__ void rows_group_mean_bwd_kernel(const bf16_t* __restrict__ de, int B, int L, int D,
+                                           const int32_t* __restrict__ row_group, int G,
+                                           const int32_t* __restrict__ counts,
+                                           float* __restrict__ dx) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)B * L * D) return;
+  const int d = idx % D;
+  const int l = (idx / D) % L;
+  const int b = idx / ((int64_t)D * L);
+  const int g = row_group[l];
+  dx[idx] = g >= 0 ? bf2f(de[((int64_t)b * G + g) * D + d]) / (float)counts[g] : 0.f;
+}
+
+// Continuous and categorical action-head losses, one wave per row of z (fp32, row stride ldz):
+// kind 0 — ContinuousActionHead (continuous.py:19-26) + compute_l2_loss (octo.py:167-174), rows = B,
+//   N = A: p = tanh(z / m) m (written to pred if non-NULL); loss += inv_count sum_a (p - y)^2;
+//   dz = 2 (p - y)(1 - tanh^2) inv_count.
+// kind 1 — CategoricalActionHead + compute_ce_loss (octo.py:187-198), rows = B*A, N = num_bins:
+//   bin = jnp.digitize(y, edges) = #edges <= y (edges = linspace(-m, m, N+1)), label =
+//   one_hot(bin, N) — all zero when bin >= N, the reference's off-by-one kept; loss += inv_count
+//   (sum(label) logsumexp(z) - label . z); dz = (sum(label) softmax(z) - label) inv_count.
+// y NULL: forward only (kind 0 writes pred). loss is accumulated atomically (zero it first).
+__global__ __launch_bounds__(256) void action_head_kernel(
+    int kind, const float* __restrict__ z, int64_t ldz, int R, int N, const float* __restrict__ y,
+    const float* __restrict__ edges, int n_edges, float max_action, float inv_count,
+    float* __restrict__ pred, float* __restrict__ loss, bf16_t* __restrict__ dz) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const float* zr = z + (int64_t)r * ldz;
+  float row_loss = 0.f;
+  if (kind == 0) {
+    for (int a = lane; a < N; a += 64) {
+      const float th = tanhf(zr[a] / max_action);
+      const float p = th * max_action;
+      if (pred) pred[(int64_t)r * N + a] = p;
+      if (y) {
+        const float d = p - y[(int64_t)r * N + a];
+        row_loss += d * d;
+        dz[(int64_t)r * N + a] = f2bf(2.f * d * (1.f - th * th) * inv_count);
+      }
+    }
+  } else {
+    const float yv = y[r];
+    int bin = 0;
+    for (int i = 0; i < n_edges; ++i) bin += edges[i] <= yv ? 1 : 0;
+    const float has = bin < N ? 1.f : 0.f;
+    float mx = -INFINITY;
+    for (int c = lane; c < N; c += 64) mx = fmaxf(mx, zr[c]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    float se = 0.f;
+    for (int c = lane; c < N; c += 64) se += expf(zr[c] - mx);
+    se = wave_sum(se);
+    const float lse = mx + logf(se);
+    for (int c = lane; c < N; c += 64) {
+      const float lab = (c == bin) ? 1.f : 0.f;
+      dz[(int64_t)r * N + c] = f2bf((has * expf(zr[c] - lse) - lab) * inv_count);
+    }
+    if (lane == 0 && bin < N) row_loss = lse - zr[bin];
+  }
+  if (!y) return;
+  row_loss = wave_sum(row_loss);
+  if (lane == 0) atomicAdd(loss, row_loss * inv_count);
+}
+
 // Diffusion noising + Fourier features (diffusion.py:41-51, 110-131):
 //   t ~ U{0..steps-1}, eps ~ N(0, 1) (Box-Muller on the counter stream) unless injected;
 //   noisy = sqrt(abar_t) a + sqrt(1 - abar_t) eps  -> cat[:, 0:A]  (bf16)
@@ -397,6 +481,44 @@ extern "C" int mmt_rows_mean_bwd(const void* de, int64_t ld_de, int B, int L, in
   hipLaunchKernelGGL(rows_mean_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream),
                      (const bf16_t*)de, ld_de, B, L, D, row_flag, nrows, (float*)dx);
   MMT_CHECK_LAUNCH("mmt_rows_mean_bwd");
+  return MMT_OK;
+}
+
+extern "C" int mmt_rows_group_mean_fwd(const void* x, int64_t xs_b, int64_t xs_t, int B, int L,
+                                       int D, const int32_t* row_group, int G,
+                                       const int32_t* counts, void* out, mmt_stream_t stream) {
+  MMT_CHECK_ARG(x && row_group && counts && out && B > 0 && L > 0 && D > 0 && G > 0,
+                "mmt_rows_group_mean_fwd: args");
+  hipLaunchKernelGGL(rows_group_mean_fwd_kernel, dim3(B, G), dim3(256), 0, as_stream(stream),
+                     (const float*)x, xs_b, xs_t, L, D, row_group, G, counts, (bf16_t*)out);
+  MMT_CHECK_LAUNCH("mmt_rows_group_mean_fwd");
+  return MMT_OK;
+}
+
+extern "C" int mmt_rows_group_mean_bwd(const void* de, int B, int L, int D, const int32_t* row_group,
+                                       int G, const int32_t* counts, void* dx, mmt_stream_t stream) {
+  MMT_CHECK_ARG(de && row_group && counts && dx && B > 0 && L > 0 && D > 0 && G > 0,
+                "mmt_rows_group_mean_bwd: args");
+  const int64_t n = (int64_t)B * L * D;
+  hipLaunchKernelGGL(rows_group_mean_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0,
+                     as_stream(stream), (const bf16_t*)de, B, L, D, row_group, G, counts,
+                     (float*)dx);
+  MMT_CHECK_LAUNCH("mmt_rows_group_mean_bwd");
+  return MMT_OK;
+}
+
+extern "C" int mmt_action_head(int kind, const float* z, int64_t ldz, int R, int N, const float* y,
+                               const float* edges, int n_edges, float max_action, float inv_count,
+                               float* pred, float* loss, void* dz, mmt_stream_t stream) {
+  MMT_CHECK_ARG(z && R > 0 && N > 0 && ldz >= N && (kind == 0 || kind == 1),
+                "mmt_action_head: args");
+  MMT_CHECK_ARG(!y || (loss && dz), "mmt_action_head: a loss needs loss and dz outputs");
+  MMT_CHECK_ARG(kind == 0 ? (max_action > 0.f && (y || pred)) : (y && edges && n_edges > 1),
+                "mmt_action_head: kind %d arguments", kind);
+  hipLaunchKernelGGL(action_head_kernel, dim3((R + 3) / 4), dim3(256), 0, as_stream(stream), kind,
+                     z, ldz, R, N, y, edges, n_edges, max_action, inv_count, pred, loss,
+                     (bf16_t*)dz);
+  MMT_CHECK_LAUNCH("mmt_action_head");
   return MMT_OK;
 }
 

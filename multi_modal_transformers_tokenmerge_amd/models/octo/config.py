@@ -29,6 +29,10 @@ class OctoConfig:
     num_observation_blocks: int = 1
     action_space_dim: int = 8
     diffusion_steps: int = 32
+    # action heads built (octo.py:83-87 config.action_heads.heads); the bench path is diffusion only
+    action_heads: tuple = ("diffusion",)
+    num_bins: int = 256
+    max_action: float = 5.0
     dropout_rate: float = 0.1
     attention_dropout_rate: float = 0.1
     layer_norm_eps: float = 1e-6

@@ -24,6 +24,8 @@ import numpy as np
 import torch
 
 from ... import _C, _kernels as K
+from ...action_heads.categorical import CategoricalActionHead
+from ...action_heads.continuous import ContinuousActionHead
 from ...action_heads.diffusion import DiffusionActionHead
 from ...attention_blocks.attention import LayerCtx, StackedEncoder1DBlock
 from ...layers import Dense
@@ -76,6 +78,14 @@ class Octo:
         # ---- head
         self.head = DiffusionActionHead(store, "diffusion_action_head", D, cfg.action_space_dim,
                                         cfg.diffusion_steps)
+        self.continuous_head = self.categorical_head = None
+        if "continuous" in cfg.action_heads:
+            self.continuous_head = ContinuousActionHead(store, "continuous_action_head", D,
+                                                        cfg.action_space_dim, cfg.max_action)
+        if "categorical" in cfg.action_heads:
+            self.categorical_head = CategoricalActionHead(store, "categorical_action_head", D,
+                                                          cfg.action_space_dim, cfg.num_bins,
+                                                          cfg.max_action)
         store.materialize(self.device, seed)
         self.t5 = T5Tokenizer(cfg.t5).materialize(self.device, seed + 1) if self.has_text else None
         self._build_tables()
@@ -133,6 +143,16 @@ class Octo:
         flag = np.full(self.L_final, -1, np.int32)
         flag[rows] = np.arange(len(rows))
         self.readout_flag = torch.from_numpy(flag).to(self.device)
+        # categorical head: readout i belongs to action i // (n / A) ("batch (action timestep)
+        # embeddings", categorical.py:32-36)
+        A = cfg.action_space_dim
+        self.readout_group = self.readout_group_counts = None
+        if len(rows) % A == 0:
+            per = len(rows) // A
+            grp = np.full(self.L_final, -1, np.int32)
+            grp[rows] = np.arange(len(rows)) // per
+            self.readout_group = torch.from_numpy(grp).to(self.device)
+            self.readout_group_counts = torch.full((A,), per, dtype=torch.int32, device=self.device)
 
     def layer_ctxs(self, train: bool, rng, sample_offset: int) -> List[LayerCtx]:
         return [LayerCtx(layer=i, sets=s, table=t, tome_set=ts, r=r, train=train, rng=rng,
@@ -198,19 +218,83 @@ class Octo:
                 _C.stream_ptr())
         return self.head.predict_action(e, rng, sample_offset, z, return_noise)
 
+    # ------------------------------------------------------------------ other action heads
+    def _readout_mean(self, xL):
+        B = xL.shape[0]
+        e = torch.empty((B, self.D), dtype=torch.bfloat16, device=xL.device)
+        _C.call("mmt_rows_mean_fwd", _C.ptr(xL), xL.stride(0), xL.stride(1), B, self.D,
+                _C.ptr(self.readout_rows), self.readout_rows.numel(), _C.ptr(e), e.stride(0),
+                _C.stream_ptr())
+        return e
+
+    def _readout_group_means(self, xL):
+        if self.readout_group is None:
+            raise ValueError("the readout count must be a multiple of action_space_dim "
+                             "(categorical.py:32-36)")
+        B, A = xL.shape[0], self.cfg.action_space_dim
+        g = torch.empty((B, A, self.D), dtype=torch.bfloat16, device=xL.device)
+        _C.call("mmt_rows_group_mean_fwd", _C.ptr(xL), xL.stride(0), xL.stride(1), B, self.L_final,
+                self.D, _C.ptr(self.readout_group), A, _C.ptr(self.readout_group_counts), _C.ptr(g),
+                _C.stream_ptr())
+        return g
+
+    def _need(self, head, name):
+        if head is None:
+            raise ValueError(f"{name} head not built: add it to OctoConfig.action_heads")
+        return head
+
+    def predict_continuous_action(self, text_tokens, images, rng=None, sample_offset=0, train=True):
+        """Reference :158-165 -> (B, 1, A) fp32."""
+        h = self._need(self.continuous_head, "continuous")
+        xL, _ = self.generate_readouts(text_tokens, images, train, rng, sample_offset)
+        return h.forward(self._readout_mean(xL))
+
+    def compute_l2_loss(self, text_tokens, images, actions, train=True, rng=None, sample_offset=0):
+        """Reference :167-174, batch-averaged as continuous_train_step (:262). (loss, saved)."""
+        h = self._need(self.continuous_head, "continuous")
+        xL, st = self.generate_readouts(text_tokens, images, train, rng, sample_offset)
+        loss, hsv = h.loss_forward(self._readout_mean(xL), actions)
+        st.update(head_kind="continuous", head_sv=hsv, xL_shape=tuple(xL.shape))
+        return loss, st
+
+    def predict_action_logits(self, text_tokens, images, rng=None, sample_offset=0, train=True):
+        """Reference :178-185 -> (B, A, num_bins) fp32."""
+        h = self._need(self.categorical_head, "categorical")
+        xL, _ = self.generate_readouts(text_tokens, images, train, rng, sample_offset)
+        return h.forward(self._readout_group_means(xL))
+
+    def compute_ce_loss(self, text_tokens, images, actions, train=True, rng=None, sample_offset=0):
+        """Reference :187-198, averaged as categorical_train_step (:302). (loss, saved)."""
+        h = self._need(self.categorical_head, "categorical")
+        xL, st = self.generate_readouts(text_tokens, images, train, rng, sample_offset)
+        loss, hsv = h.loss_forward(self._readout_group_means(xL), actions)
+        st.update(head_kind="categorical", head_sv=hsv, xL_shape=tuple(xL.shape))
+        return loss, st
+
     def backward(self, st: Dict):
-        """Reverse schedule of compute_diffusion_denoise_loss; writes every parameter gradient
-        into the flat gradient buffer (which must be zeroed before the forward)."""
+        """Reverse schedule of compute_diffusion_denoise_loss / compute_l2_loss / compute_ce_loss;
+        writes every parameter gradient into the flat gradient buffer (which must be zeroed
+        before the forward)."""
         B = st["B"]
         D = self.D
-        de = self.head.loss_backward(st["head_sv"])
-        dxL = torch.empty(st["xL_shape"], dtype=torch.float32, device=de.device)
-        _C.call("mmt_rows_mean_bwd", _C.ptr(de), de.stride(0), B, self.L_final, D,
-                _C.ptr(self.readout_flag), self.readout_rows.numel(), _C.ptr(dxL), _C.stream_ptr())
+        kind = st.get("head_kind", "diffusion")
+        if kind == "categorical":
+            dg = self.categorical_head.loss_backward(st["head_sv"])
+            dxL = torch.empty(st["xL_shape"], dtype=torch.float32, device=dg.device)
+            _C.call("mmt_rows_group_mean_bwd", _C.ptr(dg), B, self.L_final, D,
+                    _C.ptr(self.readout_group), self.cfg.action_space_dim,
+                    _C.ptr(self.readout_group_counts), _C.ptr(dxL), _C.stream_ptr())
+        else:
+            head = self.continuous_head if kind == "continuous" else self.head
+            de = head.loss_backward(st["head_sv"])
+            dxL = torch.empty(st["xL_shape"], dtype=torch.float32, device=de.device)
+            _C.call("mmt_rows_mean_bwd", _C.ptr(de), de.stride(0), B, self.L_final, D,
+                    _C.ptr(self.readout_flag), self.readout_rows.numel(), _C.ptr(dxL),
+                    _C.stream_ptr())
         dx0 = self.stack.backward(dxL, st["stack_sv"], st["ctxs"])
         NI, T = st["NI"], st["T"]
-        dimg = torch.empty((B, NI, D), dtype=torch.bfloat16, device=de.device)
-        dtxt = torch.empty((B, T, D), dtype=torch.bfloat16, device=de.device) if self.text_proj else None
+        dimg = torch.empty((B, NI, D), dtype=torch.bfloat16, device=dxL.device)
+        dtxt = torch.empty((B, T, D), dtype=torch.bfloat16, device=dxL.device) if self.text_proj else None
         it = self.image_tokenizer
         _C.call("mmt_seq_assemble_bwd", B, self.L0, D, _C.ptr(self.row_src), _C.ptr(dx0),
                 _C.ptr(dtxt), T, _C.ptr(dimg), NI, _C.ptr(st["rt"]), _C.ptr(st["ct"]),
@@ -272,6 +356,28 @@ def create_octo_train_state(model: Octo, tx: AdamW | None = None, seed: int = 12
     """Reference octo.py:334-386 (parameters were initialised by Octo(...))."""
     rng = torch.tensor([seed, 0], dtype=torch.int32, device=model.device)
     return OCTOTrainState(model, tx or AdamW(), rng, allreduce, sample_offset)
+
+
+def _head_train_step(loss_fn, model: Octo, train_state: OCTOTrainState, text_tokens, images,
+                     actions):
+    model.store.zero_grad()
+    loss, st = loss_fn(text_tokens, images, actions, True, train_state.rng,
+                       train_state.sample_offset)
+    model.backward(st)
+    if train_state.allreduce is not None:
+        train_state.allreduce(model.store.flat_grad)
+    train_state.apply_gradients()
+    return train_state, loss
+
+
+def continuous_train_step(model: Octo, train_state: OCTOTrainState, text_tokens, images, actions):
+    """Reference octo.py:242-280: value_and_grad of mean(compute_l2_loss), apply_gradients."""
+    return _head_train_step(model.compute_l2_loss, model, train_state, text_tokens, images, actions)
+
+
+def categorical_train_step(model: Octo, train_state: OCTOTrainState, text_tokens, images, actions):
+    """Reference octo.py:282-320: value_and_grad of mean(compute_ce_loss), apply_gradients."""
+    return _head_train_step(model.compute_ce_loss, model, train_state, text_tokens, images, actions)
 
 
 def diffusion_train_step(model: Octo, train_state: OCTOTrainState, text_tokens, images, actions,
