@@ -895,6 +895,7 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
       if (u.x == 0x12345u)
 #endif
       {
+        // plain stores: non-temporal ones (MMT_NT_STORE experiment) doubled this kernel's time
         if (OUT == 0) *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(Cv) + off) = u;
         else *reinterpret_cast<uint4*>(reinterpret_cast<float*>(Cv) + off) = u;
       }
