@@ -305,6 +305,12 @@ int mmt_diffusion_sample(const uint32_t* rng, int B, int A, int steps, int64_t s
                          const float* coef, const float* z_in, int H, float* actions,
                          float* z_out, mmt_stream_t stream);
 
+/* Transposed bf16 weight shadows (this build's layout, no reference twin): for each of n
+ * matrices, desc[5i..5i+4] = {src_off, dst_off, rows, cols, first_tile} (elements / 64x64 tiles,
+ * first_tile = running tile count), dst[dst_off + c*rows + r] = src[src_off + r*cols + c]. */
+int mmt_transpose_bf16_batched(const void* src, void* dst, const int64_t* desc, int n,
+                               int64_t total_tiles, mmt_stream_t stream);
+
 /* ------------------------------------------------------------------ continuous / categorical heads
  * (SURVEY §8f row 4). Grouped readout means (categorical.py:32-37): out (B, G, D) bf16 = mean of
  * the rows with row_group[l] == g (counts[g] rows); backward writes the whole fp32 dx (B, L, D). */

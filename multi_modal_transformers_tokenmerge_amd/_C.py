@@ -62,6 +62,7 @@ SIGNATURES: dict[str, list] = {
     "mmt_embedding_gather": [P, L, I, P, I, P, P],
     "mmt_adamw": [P, P, P, P, P, L, P, F, F, F, F, F, F, P],
     "mmt_cast_f32_bf16": [P, P, L, P],
+    "mmt_transpose_bf16_batched": [P, P, P, I, L, P],
     "mmt_step_advance": [P, P],
 }
 _VOID = {"mmt_tome_set_match_path", "mmt_gemm_set_variant"}

@@ -5,6 +5,8 @@
 // parameter buffer, and the device-side step counter that keys every random stream.
 #include <math.h>
 
+#include <algorithm>
+
 #include "common.h"
 
 using namespace mmt;
@@ -410,6 +412,34 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
   }
 }
 
+// Transposed bf16 weight shadows: dst (cols, rows) = src (rows, cols)^T for a batch of matrices
+// (desc: n x {src_off, dst_off, rows, cols, first_tile} elements / tiles), 64 x 64 tiles through a
+// padded LDS tile; grid-stride over all tiles. Lets every dX product run as an NT GEMM.
+__global__ __launch_bounds__(256) void transpose_bf16_batched_kernel(
+    const bf16_t* __restrict__ src, bf16_t* __restrict__ dst, const int64_t* __restrict__ desc,
+    int n, int64_t total_tiles) {
+  __shared__ bf16_t tile[64][66];
+  for (int64_t t = blockIdx.x; t < total_tiles; t += gridDim.x) {
+    int m = 0;
+    while (m + 1 < n && desc[5 * (m + 1) + 4] <= t) ++m;
+    const int64_t so = desc[5 * m], dso = desc[5 * m + 1];
+    const int rows = (int)desc[5 * m + 2], cols = (int)desc[5 * m + 3];
+    const int64_t lt = t - desc[5 * m + 4];
+    const int tcols = (cols + 63) / 64;
+    const int r0 = (int)(lt / tcols) * 64, c0 = (int)(lt % tcols) * 64;
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+      const int rr = i >> 6, cc = i & 63;
+      if (r0 + rr < rows && c0 + cc < cols) tile[rr][cc] = src[so + (int64_t)(r0 + rr) * cols + c0 + cc];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+      const int cc = i >> 6, rr = i & 63;  // dst row = source column
+      if (r0 + rr < rows && c0 + cc < cols) dst[dso + (int64_t)(c0 + cc) * rows + r0 + rr] = tile[rr][cc];
+    }
+  }
+}
+
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ a, bf16_t* __restrict__ b, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -519,6 +549,16 @@ extern "C" int mmt_action_head(int kind, const float* z, int64_t ldz, int R, int
                      z, ldz, R, N, y, edges, n_edges, max_action, inv_count, pred, loss,
                      (bf16_t*)dz);
   MMT_CHECK_LAUNCH("mmt_action_head");
+  return MMT_OK;
+}
+
+extern "C" int mmt_transpose_bf16_batched(const void* src, void* dst, const int64_t* desc, int n,
+                                          int64_t total_tiles, mmt_stream_t stream) {
+  MMT_CHECK_ARG(src && dst && desc && n > 0 && total_tiles > 0, "mmt_transpose_bf16_batched: args");
+  const int grid = (int)std::min<int64_t>(total_tiles, 4096);
+  hipLaunchKernelGGL(transpose_bf16_batched_kernel, dim3(grid), dim3(256), 0, as_stream(stream),
+                     (const bf16_t*)src, (bf16_t*)dst, desc, n, total_tiles);
+  MMT_CHECK_LAUNCH("mmt_transpose_bf16_batched");
   return MMT_OK;
 }
 

@@ -32,7 +32,8 @@ class Dense:
     def __init__(self, store: ParamStore, name: str, in_f: int, out_f: int, use_bias: bool = True,
                  kernel_init=None, bias_init=None):
         self.in_f, self.out_f = in_f, out_f
-        self.w = store.add(f"{name}/kernel", (out_f, in_f), kernel_init or he_normal((in_f, out_f)))
+        self.w = store.add(f"{name}/kernel", (out_f, in_f), kernel_init or he_normal((in_f, out_f)),
+                           transposed=True)
         self.b = store.add(f"{name}/bias", (out_f,), bias_init or normal(0.01)) if use_bias else None
 
     def fwd(self, x2d: torch.Tensor, out=None, out_mode=K.OUT_BF16, **epi) -> torch.Tensor:
@@ -47,7 +48,8 @@ class Dense:
         if self.b is not None and not bias_grad_done:
             K.colsum(dy2d, self.b.grad)
         if need_dx:
-            return K.gemm(dy2d, self.w.bf16, trans_b=False, out=dx_out, **dx_epi)
+            # dX = dY . W as an NT product on the transposed shadow W^T (in, out)
+            return K.gemm(dy2d, self.w.bf16_t, trans_b=True, out=dx_out, **dx_epi)
         return None
 
 

@@ -348,6 +348,7 @@ class OCTOTrainState:
                 _C.ptr(s.flat_bf16), s.flat.numel(), _C.ptr(self.rng), tx.learning_rate, tx.b1,
                 tx.b2, tx.eps, tx.weight_decay, getattr(self.allreduce, "grad_scale", 1.0),
                 _C.stream_ptr())
+        s.refresh_transposed()
         _C.call("mmt_step_advance", _C.ptr(self.rng), _C.stream_ptr())
 
 

@@ -78,6 +78,8 @@ class Param:
     offset: int = -1
     data: torch.Tensor | None = None      # fp32 master view
     bf16: torch.Tensor | None = None      # bf16 shadow view
+    transposed: bool = False              # also keep a transposed bf16 shadow (2-D weights)
+    bf16_t: torch.Tensor | None = None    # its (cols, rows) view
     grad: torch.Tensor | None = None      # fp32 grad view
 
     @property
@@ -92,10 +94,12 @@ class ParamStore:
         self.n = 0
         self.flat = self.flat_bf16 = self.flat_grad = self.m = self.v = None
 
-    def add(self, name: str, shape, init) -> Param:
+    def add(self, name: str, shape, init, transposed: bool = False) -> Param:
         if name in self.by_name:
             raise KeyError(f"duplicate parameter {name}")
-        p = Param(name, tuple(int(s) for s in shape), init)
+        if transposed and len(shape) != 2:
+            raise ValueError("only 2-D parameters keep a transposed shadow")
+        p = Param(name, tuple(int(s) for s in shape), init, transposed=transposed)
         p.offset = self.n
         self.n += (p.numel + ALIGN - 1) // ALIGN * ALIGN
         self.params.append(p)
@@ -115,8 +119,37 @@ class ParamStore:
         self.flat_grad = torch.zeros_like(self.flat)
         self.m = torch.zeros_like(self.flat)
         self.v = torch.zeros_like(self.flat)
+        # transposed bf16 shadows of the 2-D weights (same offsets, (cols, rows) views): every
+        # dX = dY . W then runs as an NT GEMM; refreshed after each optimizer step
+        tps = [p for p in self.params if p.transposed]
+        self.flat_bf16_t = torch.zeros_like(self.flat_bf16) if tps else None
+        self._t_desc, self._t_tiles = None, 0
+        if tps:
+            rows = []
+            tiles = 0
+            for p in tps:
+                r, c = p.shape
+                rows += [p.offset, p.offset, r, c, tiles]
+                tiles += -(-r // 64) * -(-c // 64)
+            self._t_desc = torch.tensor(rows, dtype=torch.int64, device=device)
+            self._t_tiles = tiles
         self._bind()
+        self.refresh_transposed()
         return self
+
+    def refresh_transposed(self):
+        """Re-derive the transposed bf16 shadows from the bf16 shadow (one batched launch; on a
+        host-resident store, used by the checkpoint tools, a host transpose)."""
+        if self.flat_bf16_t is None:
+            return
+        if self.flat_bf16.is_cuda:
+            from . import _C
+            _C.call("mmt_transpose_bf16_batched", _C.ptr(self.flat_bf16), _C.ptr(self.flat_bf16_t),
+                    _C.ptr(self._t_desc), self._t_desc.numel() // 5, self._t_tiles, _C.stream_ptr())
+        else:
+            for p in self.params:
+                if p.transposed:
+                    p.bf16_t.copy_(p.bf16.t())
 
     def _bind(self):
         for p in self.params:
@@ -124,6 +157,8 @@ class ParamStore:
             p.data = self.flat[sl].view(p.shape)
             p.bf16 = self.flat_bf16[sl].view(p.shape)
             p.grad = self.flat_grad[sl].view(p.shape)
+            if p.transposed:
+                p.bf16_t = self.flat_bf16_t[sl].view(p.shape[1], p.shape[0])
 
     def zero_grad(self):
         self.flat_grad.zero_()
@@ -131,6 +166,7 @@ class ParamStore:
     def sync_shadow(self):
         """Re-derive the bf16 shadow after the master was modified outside AdamW."""
         self.flat_bf16.copy_(self.flat.to(torch.bfloat16))
+        self.refresh_transposed()
 
     def num_params(self) -> int:
         return sum(p.numel for p in self.params)
