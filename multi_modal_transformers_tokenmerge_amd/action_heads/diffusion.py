@@ -110,6 +110,34 @@ class DiffusionActionHead:
                 _C.ptr(self.fourier.data), _C.ptr(self.fourier.grad), _C.stream_ptr())
         return dcat[:, self.A + self.time_dim:]
 
+    # ------------------------------------------------------------------ predict_denoise_term
+    def predict_denoise_term(self, readout_mean: torch.Tensor, time: torch.Tensor,
+                             noisy_actions: torch.Tensor) -> torch.Tensor:
+        """Reference :88-107 (``OctoDenoise(noisy, time, mean(readouts))``) for given integer
+        times (B,) or (B, 1) and noisy actions (B, A) fp32. Returns eps_hat (B, A) fp32."""
+        B = readout_mean.shape[0]
+        dev = readout_mean.device
+        t = time.reshape(-1).to(torch.int32).contiguous()
+        if t.numel() != B or tuple(noisy_actions.shape) != (B, self.A):
+            raise ValueError("time must hold one step per sample and noisy_actions be (B, A)")
+        if readout_mean.shape[1] != self.D or readout_mean.dtype != torch.bfloat16:
+            raise ValueError(f"readout_mean must be bf16 (B, {self.D})")
+        cat = self.new_cat(B, dev)
+        zeros = torch.zeros((B, self.A), dtype=torch.float32, device=dev)
+        feats = torch.empty((B, self.time_dim), dtype=torch.bfloat16, device=dev)
+        t_out = torch.empty(B, dtype=torch.int32, device=dev)
+        eps_out = torch.empty((B, self.A), dtype=torch.float32, device=dev)
+        _C.call("mmt_diffusion_prep", None, B, self.A, self.steps, 0, _C.ptr(zeros),
+                _C.ptr(self.consts(dev)), _C.ptr(self.fourier.data), self.F, _C.ptr(t),
+                _C.ptr(zeros), _C.ptr(t_out), _C.ptr(eps_out), _C.ptr(cat), cat.stride(0),
+                _C.ptr(feats), _C.stream_ptr())
+        cat[:, :self.A].copy_(noisy_actions)           # the given noisy sample (bf16 operand)
+        self.readout_slot(cat).copy_(readout_mean)
+        ht = self.t1.fwd(feats, act=K.ACT_RELU)
+        self.t2.fwd(ht, out=cat[:, self.A:self.A + self.time_dim])
+        hd = self.d1.fwd(cat, act=K.ACT_RELU)
+        return self.d2.fwd(hd, out_mode=K.OUT_F32)
+
     # ------------------------------------------------------------------------- predict_action
     def sampler_coef(self, device) -> torch.Tensor:
         """(steps, 3) fp32 [1/sqrt(a_t), (1-a_t)/sqrt(1-abar_t), sqrt(b_t)] (:182-184)."""

@@ -204,6 +204,12 @@ class Octo:
         st.update(head_sv=hsv, xL_shape=tuple(xL.shape))
         return loss, st
 
+    def predict_diffusion_denoise_term(self, text_tokens, images, time, noisy_actions, rng=None,
+                                       sample_offset=0, train=True):
+        """Reference :130-137: readouts -> readout mean -> OctoDenoise (diffusion.py:88-107)."""
+        xL, _ = self.generate_readouts(text_tokens, images, train, rng, sample_offset)
+        return self.head.predict_denoise_term(self._readout_mean(xL), time, noisy_actions)
+
     def predict_diffusion_action(self, text_tokens, images, rng, sample_offset=0, train=True,
                                  z: Optional[torch.Tensor] = None, return_noise=False,
                                  positions=None):

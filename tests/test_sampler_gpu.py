@@ -89,3 +89,21 @@ def test_octo_predict_diffusion_action(dev):
     a = model.predict_diffusion_action(text, images, rng)
     torch.cuda.synchronize()
     assert a.shape == (B, 8) and torch.isfinite(a).all() and a.abs().max() <= 5.0
+
+
+def test_predict_denoise_term_matches_oracle(dev):
+    """diffusion.py:88-107: eps_hat = Dense_1(relu(Dense_0([noisy | temb(t) | readout_mean])))."""
+    head = _head(dev, 384, seed=9)
+    B = 7
+    g = torch.Generator().manual_seed(1)
+    readout = (torch.randn((B, 384), generator=g) * 0.5).to(torch.bfloat16).to(dev)
+    t = torch.randint(0, 32, (B,), generator=g, dtype=torch.int32)
+    noisy = torch.randn((B, 8), generator=g)
+    eps = head.predict_denoise_term(readout, t.to(dev), noisy.to(dev))
+    temb = _np(head.time_embeddings(dev))
+    torch.cuda.synchronize()
+    w1, b1 = _np(head.d1.w.bf16), _np(head.d1.b.data)
+    x = np.concatenate([ref.bf16(noisy.numpy()), temb[t.numpy()], ref.bf16(_np(readout))], axis=1)
+    h = ref.bf16(np.maximum(x @ w1.T + b1, 0.0))
+    want = h @ _np(head.d2.w.bf16).T + _np(head.d2.b.data)
+    np.testing.assert_allclose(_np(eps), want, atol=2e-3, rtol=2e-3)
