@@ -38,7 +38,10 @@ namespace {
 
 constexpr int MAX_SETS = 16;
 constexpr int KT = 64;      // keys (or queries) per LDS tile
-constexpr int NT = 256;     // threads per workgroup (4 waves x 32 rows)
+constexpr int NT = 256;      // forward threads per workgroup (4 waves x 32 query rows)
+constexpr int QB = NT / 2;   // forward query rows per workgroup
+// The backward kernels take their workgroup size as a template parameter: 4 waves (128 rows) or
+// 2 waves (64 rows), chosen per launch by how well L fills the row blocks (bwd_threads()).
 constexpr int MAXL = 4096;
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
@@ -166,10 +169,10 @@ __device__ __forceinline__ bf16x8 pack_frag(const floatx16& x, int s) {
 // Register-staged copy of two KT x DH bf16 tiles (rows r0.., zero past L) -> LDS [KT][DH+8].
 // Loads are branch-free (rows clamped to L-1, zeroed at the LDS store), so the compiler keeps
 // counted vmcnt waits and the prefetch stays in flight through the MFMAs.
-template <int DH>
+template <int DH, int NTT = NT>
 struct TilePair {
   static constexpr int CPR = DH / 8;            // 16-B chunks per row
-  static constexpr int PER = KT * CPR / NT;     // chunks per thread per tile
+  static constexpr int PER = KT * CPR / NTT;    // chunks per thread per tile
   uint4 a[PER], b[PER];
   uint32_t ok;
   __device__ __forceinline__ void load(const bf16_t* pa, int64_t sa, const bf16_t* pb, int64_t sb,
@@ -177,7 +180,7 @@ struct TilePair {
     ok = 0;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int c = threadIdx.x + i * NT, row = c / CPR, ch = c % CPR;
+      const int c = threadIdx.x + i * NTT, row = c / CPR, ch = c % CPR;
       const int rr = min(r0 + row, L - 1);
       ok |= (r0 + row < L ? 1u : 0u) << i;
       a[i] = *reinterpret_cast<const uint4*>(pa + (int64_t)rr * sa + ch * 8);
@@ -187,7 +190,7 @@ struct TilePair {
   __device__ __forceinline__ void store(bf16_t* la, bf16_t* lb) const {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int c = threadIdx.x + i * NT, row = c / CPR, ch = c % CPR;
+      const int c = threadIdx.x + i * NTT, row = c / CPR, ch = c % CPR;
       const uint32_t m = ((ok >> i) & 1u) ? 0xffffffffu : 0u;
       *reinterpret_cast<uint4*>(la + row * (DH + 8) + ch * 8) =
           make_uint4(a[i].x & m, a[i].y & m, a[i].z & m, a[i].w & m);
@@ -220,7 +223,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(Geo g, AttnMask mask,
   const int b = blockIdx.z, h = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
   const int L = g.L, D = g.H * DH;
-  const int q0 = blockIdx.x * 128, q1 = min(L, q0 + 128);
+  const int q0 = blockIdx.x * QB, q1 = min(L, q0 + QB);
   const int q = q0 + wave * 32 + (lane & 31);
   const bool qv = q < L;
   const bool wave_live = q0 + wave * 32 < L;
@@ -359,8 +362,8 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(Geo g, AttnMask mask,
 }
 
 // =============================================================================== bwd: dQ
-template <int DH>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mask,
+template <int DH, int NTT>
+__global__ __launch_bounds__(NTT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mask,
                                                          const uint32_t* __restrict__ drop_bits,
                                                          int drop_words, float drop_scale,
                                                          const bf16_t* __restrict__ dout,
@@ -379,7 +382,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mask
   const int b = blockIdx.z, h = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
   const int L = g.L, D = g.H * DH;
-  const int q0 = blockIdx.x * 128, q1 = min(L, q0 + 128);
+  const int q0 = blockIdx.x * (NTT / 2), q1 = min(L, q0 + NTT / 2);
   const int q = q0 + wave * 32 + (lane & 31);
   const bool qv = q < L;
   const bool wave_live = q0 + wave * 32 < L;
@@ -419,7 +422,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mask
 #pragma unroll
     for (int r = 0; r < 16; ++r) dqacc[d][r] = 0.f;
 
-  TilePair<DH> pf;
+  TilePair<DH, NTT> pf;
   int kt = next_key_tile(mask, q0, q1, 0, L);
   if (kt < L) {
     pf.load(kbase, g.s_t, vbase, g.s_t, kt, L);
@@ -497,8 +500,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mask
 }
 
 // =============================================================================== bwd: dK, dV
-template <int DH>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask mask,
+template <int DH, int NTT>
+__global__ __launch_bounds__(NTT, 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask mask,
                                                            const uint32_t* __restrict__ drop_bits_t,
                                                            int drop_words, float drop_scale,
                                                            const bf16_t* __restrict__ dout,
@@ -516,7 +519,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask ma
   const int b = blockIdx.z, h = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
   const int L = g.L, D = g.H * DH;
-  const int kb0 = blockIdx.x * 128, kb1 = min(L, kb0 + 128);
+  const int kb0 = blockIdx.x * (NTT / 2), kb1 = min(L, kb0 + NTT / 2);
   const int key = kb0 + wave * 32 + (lane & 31);
   const bool kv = key < L;
   const bool wave_live = kb0 + wave * 32 < L;
@@ -547,7 +550,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask ma
       dv[d][r] = 0.f;
     }
 
-  TilePair<DH> pf;
+  TilePair<DH, NTT> pf;
   float rowv = 0.f;  // thread t < 128 stages lse (t < 64) or delta (64 <= t < 128) of one row
   auto load_rows = [&](int q0) {  // waves 0 (lse) and 1 (delta); clamped, branch-free load
     if (threadIdx.x < 2 * KT) {
@@ -730,6 +733,25 @@ int fill_mask(AttnMask& m, int n_sets, const int32_t* starts, const int32_t* len
     else { MMT_CHECK_ARG(false, "attention: head dim %d unsupported (64, 128)", Dh); } \
   } while (0)
 
+// Backward workgroup size: 2 waves (64 rows) when that fills the row blocks clearly better than
+// 4 waves (128 rows) — measured at B = 256, Dh = 64: L = 292 398 -> 380 us, L = 132 177 -> 138 us,
+// L = 212 (equal fill) 234 -> 257 us, so the smaller blocks must gain > 10 % fill.
+inline int bwd_threads(int L) {
+  const double f128 = (double)L / (((L + 127) / 128) * 128);
+  const double f64 = (double)L / (((L + 63) / 64) * 64);
+  return f64 > f128 + 0.10 ? 128 : 256;
+}
+
+#define ATTN_BWD_LAUNCH(DH_, NTT_)                                                                \
+  do {                                                                                            \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DH_, NTT_>), grid, dim3(NTT_), 0, s, g, m, drop_bits,  \
+                       words, dscale, (const bf16_t*)dout, d_s_b, d_s_t, lse, (const bf16_t*)o,   \
+                       o_s_b, o_s_t, delta, (bf16_t*)dqkv, dq_s_b, dq_s_t);                       \
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DH_, NTT_>), grid, dim3(NTT_), 0, s, g, m,           \
+                       drop_bits_t, words, dscale, (const bf16_t*)dout, d_s_b, d_s_t, lse, delta,  \
+                       (bf16_t*)dqkv, dq_s_b, dq_s_t);                                             \
+  } while (0)
+
 extern "C" int mmt_dropout_bits(const uint32_t* rng, uint32_t layer, uint32_t site, int rows,
                                 int cols, float keep_prob, uint32_t* out, uint32_t* out_t,
                                 mmt_stream_t stream) {
@@ -761,7 +783,7 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   if (rc) return rc;
   Geo g{(const bf16_t*)qkv, s_b, s_t, L, H, scale};
   const int words = (L + 31) / 32;
-  dim3 grid((L + 127) / 128, H, B);
+  dim3 grid((L + QB - 1) / QB, H, B);
   const float dscale = drop_bits ? 1.f / keep_prob : 1.f;
   ATTN_DISPATCH(DH, hipLaunchKernelGGL(attn_fwd_kernel<DH>, grid, dim3(NT), 0, as_stream(stream),
                                        g, m, drop_bits, words, dscale, bias, (bf16_t*)o,
@@ -792,14 +814,13 @@ extern "C" int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   const int words = (L + 31) / 32;
   const float dscale = drop_bits ? 1.f / keep_prob : 1.f;
   hipStream_t s = as_stream(stream);
-  dim3 grid((L + 127) / 128, H, B);
-  ATTN_DISPATCH(DH, hipLaunchKernelGGL(attn_bwd_dq_kernel<DH>, grid, dim3(NT), 0, s, g, m, drop_bits,
-                                       words, dscale, (const bf16_t*)dout, d_s_b, d_s_t,
-                                       lse, (const bf16_t*)o, o_s_b, o_s_t, delta, (bf16_t*)dqkv,
-                                       dq_s_b, dq_s_t));
-  ATTN_DISPATCH(DH, hipLaunchKernelGGL(attn_bwd_dkdv_kernel<DH>, grid, dim3(NT), 0, s, g, m,
-                                       drop_bits_t, words, dscale, (const bf16_t*)dout,
-                                       d_s_b, d_s_t, lse, delta, (bf16_t*)dqkv, dq_s_b, dq_s_t));
+  if (bwd_threads(L) == 128) {
+    dim3 grid((L + 63) / 64, H, B);
+    ATTN_DISPATCH(DH, ATTN_BWD_LAUNCH(DH, 128));
+  } else {
+    dim3 grid((L + 127) / 128, H, B);
+    ATTN_DISPATCH(DH, ATTN_BWD_LAUNCH(DH, 256));
+  }
   MMT_CHECK_LAUNCH("mmt_attn_bwd");
   return MMT_OK;
 }
