@@ -19,9 +19,12 @@ DROP_ATTN, DROP_ATTN_OUT, DROP_MLP_HIDDEN, DROP_MLP_OUT = 0, 1, 2, 3  # dropout 
 
 
 def split_k_for(n_out: int, k_out: int, m_red: int) -> int:
-    """Split of the M-reduction of a weight-gradient GEMM so the launch fills the 256 CUs."""
-    tiles = math.ceil(n_out / 128) * math.ceil(k_out / 128)
-    want = max(1, math.ceil(512 / tiles))
+    """Split of the M-reduction of a weight-gradient GEMM so the launch fills the 256 CUs once:
+    the TN products run on the 256 x 192-tile kernel at one workgroup per CU (csrc/gemm.hip
+    gemm_big_kernel), so the split is sized for ~256 of ITS tiles (sizing it for 128 x 128 tiles
+    left 1536 x 384 at 180 workgroups)."""
+    tiles = math.ceil(n_out / 256) * math.ceil(k_out / 192)
+    want = max(1, 256 // tiles)
     return int(max(1, min(want, m_red // 256, 64)))
 
 
