@@ -12,7 +12,6 @@ separately. MLPBlocks here run with dropout disabled, as in the reference (they 
 """
 from __future__ import annotations
 
-import math
 
 import numpy as np
 import torch

@@ -15,7 +15,7 @@ Every op is a libmmt_hip kernel (see layers.py); backward is explicit.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import List, Optional
 
 import torch

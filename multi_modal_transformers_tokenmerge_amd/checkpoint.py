@@ -161,7 +161,6 @@ def _drop1(a):
 
 
 def _rules(model) -> Dict[str, Rule]:
-    cfg = model.cfg
     rules: Dict[str, Rule] = {}
     it = model.image_tokenizer
     rn = it.resnet
@@ -207,7 +206,6 @@ def _rules(model) -> Dict[str, Rule]:
         for d in ("Dense_0", "Dense_1"):
             rules[f"{ours}/{blk}/{d}/kernel"] = ([f"{hd}/{blk}/{d}/kernel"], _dense_T, _dense_T)
             rules[f"{ours}/{blk}/{d}/bias"] = ([f"{hd}/{blk}/{d}/bias"], _ident, _ident)
-    del cfg
     return rules
 
 

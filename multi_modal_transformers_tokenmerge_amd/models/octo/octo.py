@@ -17,7 +17,7 @@ step is captured into a HIP graph and replayed (see OCTOTrainState.graphed_step)
 """
 from __future__ import annotations
 
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional
 
 import numpy as np

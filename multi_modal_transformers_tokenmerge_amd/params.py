@@ -18,7 +18,7 @@ fan_in, truncated_normal), normal(0.01) biases, LayerNorm ones/zeros, ...).
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Callable, Dict, List, Tuple
 
 import torch

@@ -8,7 +8,6 @@ Tolerance (see tests/test_octo_gpu.py for the derivation from the measured noise
   loss: relative difference <= 4e-2
   gradients: cosine similarity >= 0.96 per parameter tensor, >= 0.985 on the concatenation
 """
-import dataclasses
 
 import numpy as np
 import torch
