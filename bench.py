@@ -78,14 +78,14 @@ def algorithmic_flops_per_sample(model) -> float:
     return 3 * (tr + stem) + t5
 
 
-PROBE_KERNEL = "gemm_nt256_kernel<192, 0, true, 2>"
+PROBE_KERNEL = "gemm_nt256_kernel<256, 0, false, 2>"
 
 
 def probe_dominant_gemm(model, B, reps=20):
     """Average duration (HIP events on the launching stream) of the MLP up-projection GEMM of
     block 0 at the step's exact shape: M = B*L1, N = mlp_dim, K = D (bias+relu+dropout fused);
-    the library's automatic choice for this NT shape (N >= 1152, N % 192 == 0, K <= 512) is the
-    persistent 256 x 192 kernel gemm_nt256_kernel<192, 0, true, 2> (csrc/gemm.hip)."""
+    the library's automatic choice for this NT shape (N >= 1152, N % 256 == 0, K <= 512) is the
+    persistent 256 x 256 kernel gemm_nt256_kernel<256, 0, false, 2> (csrc/gemm.hip)."""
     cfg = model.cfg
     blk = model.stack.blocks[0]
     sets, _, ts, r = model.layer_sets[0]

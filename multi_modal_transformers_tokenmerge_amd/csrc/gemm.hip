@@ -1187,12 +1187,14 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     if (g_variant == 5) bn = N % 256 == 0 ? 256 : 0;
     else if (g_variant == 6) bn = N % 192 == 0 ? 192 : 0;
     else if (g_variant == 7) bn = N % 128 == 0 ? 128 : 0;
-    else if (final_kind == 0 && N >= 1152 && N % 192 == 0 && K <= 512 && tm256 * (N / 192) >= n_cu)
-      // measured (tools/gemm_bench.py, graph-timed): wins on the wide bf16-output projections
-      // (MLP up 159 -> 147 us, QKV 113 -> 101 us at B = 256); the narrow (N = 384) and fp32
-      // residual-stream shapes stay on the 128 x 128 kernels, which are faster there, and so do
-      // the deep-K T5 projections (K = 768: 2304 x 768 measured slower on the 256-row tiles)
-      bn = 192;
+    else if (final_kind == 0 && N >= 1152 && K <= 512 && (N % 256 == 0 || N % 192 == 0) &&
+             tm256 * (N / (N % 256 == 0 ? 256 : 192)) >= n_cu)
+      // measured (tools/gemm_bench.py --variant=5/6/7, graph-timed, B = 256): 256-wide tiles
+      // where N allows (MLP up with bias+relu+dropout 153 -> 135 us, plain 145 -> 143 us), else
+      // 192 (QKV N = 1152: 111 -> 100 us); the narrow (N = 384) and fp32 residual-stream shapes
+      // stay on the 128 x 128 kernels, which are faster there, and so do the deep-K T5
+      // projections (K = 768: 2304 x 768 measured slower on the 256-row tiles)
+      bn = N % 256 == 0 ? 256 : 192;
     if (bn) {
       const int tn = N / bn, n_tiles = ((M + 255) / 256) * tn;
       const int grid = std::min(n_tiles, n_cu);

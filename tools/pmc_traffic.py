@@ -42,7 +42,7 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("--shape", type=int, nargs=3, required=True)
     ap.add_argument("--out", required=True)
-    ap.add_argument("--kernel", default="gemm_nt256_kernel<192, 0, true, 2>",
+    ap.add_argument("--kernel", default="gemm_nt256_kernel<256, 0, false, 2>",
                     help="substring of the demangled kernel name (bench.py PROBE_KERNEL)")
     a = ap.parse_args()
     fetch = per_dispatch(a.fetch_dir, "FETCH_SIZE", a.kernel)
