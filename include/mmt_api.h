@@ -173,13 +173,14 @@ int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, int L, int H,
                  mmt_stream_t stream);
 /* Backward: writes dq, dk, dv into dqkv (same row layout as qkv). delta: fp32 (B, H, L)
  * workspace (rowsum(dO * O)). drop_bits_t: the transposed keep mask (mmt_dropout_bits out_t);
- * both or neither of drop_bits / drop_bits_t. */
+ * both or neither of drop_bits / drop_bits_t. bias_grad (fp32 [3 H Dh], may be NULL) += the
+ * column sums of dq | dk | dv over (B, L): the bias gradient of the fused QKV projection. */
 int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, int L, int H, int Dh,
                  float scale, int n_sets, const int32_t* set_start, const int32_t* set_len,
                  const uint32_t* set_vis, const uint32_t* drop_bits, const uint32_t* drop_bits_t,
                  float keep_prob, const void* o, int64_t o_s_b, int64_t o_s_t, const void* dout,
                  int64_t d_s_b, int64_t d_s_t, const float* lse, float* delta, void* dqkv,
-                 int64_t dq_s_b, int64_t dq_s_t, mmt_stream_t stream);
+                 int64_t dq_s_b, int64_t dq_s_t, float* bias_grad, mmt_stream_t stream);
 /* Keep bitmask (rows, ceil(cols/32)) of a dropout stream (flax Dropout keep-mask, broadcast over
  * batch and heads for attention): bit c of word (r, c/32) set iff keep_elem(key(rng, layer,
  * site), r*cols + c), i.e. the 16-bit half (idx & 1) of mix32(key ^ (idx >> 1)) is below

@@ -35,7 +35,7 @@ SIGNATURES: dict[str, list] = {
     "mmt_gemm_set_variant": [I],
     "mmt_gemm": [I, I, I, P, I, L, P, I, L, P, I, L, I, L, L, L, I, P, P, L, P],
     "mmt_attn_fwd": [P, L, L, I, I, I, I, F, I, P, P, P, P, F, P, P, L, L, P, P],
-    "mmt_attn_bwd": [P, L, L, I, I, I, I, F, I, P, P, P, P, P, F, P, L, L, P, L, L, P, P, P, L, L, P],
+    "mmt_attn_bwd": [P, L, L, I, I, I, I, F, I, P, P, P, P, P, F, P, L, L, P, L, L, P, P, P, L, L, P, P],
     "mmt_dropout_bits": [P, U32, U32, I, I, F, P, P, P],
     "mmt_seqnorm_fwd": [P, I, L, L, I, I, I, P, P, F, P, L, L, P, P, P],
     "mmt_seqnorm_bwd": [P, I, L, L, P, I, L, L, I, I, I, P, P, P, P, L, L, P, L, L, P, P, P],

@@ -274,8 +274,10 @@ def attn_fwd(qkv: torch.Tensor, H: int, scale: float, table: SetTable | None = N
 
 
 def attn_bwd(qkv, o, dout, lse, H: int, scale: float, table: SetTable | None = None,
-             drop_bits=None, keep_prob: float = 1.0, dqkv: torch.Tensor | None = None):
-    _dev(qkv, o, dout, lse, drop_bits, dqkv)
+             drop_bits=None, keep_prob: float = 1.0, dqkv: torch.Tensor | None = None,
+             bias_grad: torch.Tensor | None = None):
+    """bias_grad (fp32 [3*H*Dh], optional) += column sums of dqkv (the QKV bias gradient)."""
+    _dev(qkv, o, dout, lse, drop_bits, dqkv, bias_grad)
     B, L, Dh = _qkv_geo(qkv, H)
     t = table or SetTable.none(L)
     if dout.stride(-1) != 1 or o.stride(-1) != 1:
@@ -286,10 +288,13 @@ def attn_bwd(qkv, o, dout, lse, H: int, scale: float, table: SetTable | None = N
     if drop_bits is not None and (drop_bits.dim() != 3 or drop_bits.shape[0] != 2):
         raise ValueError("attn_bwd needs the (2, L, W) mask of dropout_bits (row-major + transposed)")
     bits, bits_t = (None, None) if drop_bits is None else (drop_bits[0], drop_bits[1])
+    if bias_grad is not None and (bias_grad.dtype != torch.float32 or bias_grad.numel() != 3 * H * Dh
+                                  or not bias_grad.is_contiguous()):
+        raise ValueError("bias_grad must be contiguous fp32 [3*H*Dh]")
     _C.call("mmt_attn_bwd", ptr(qkv), qkv.stride(0), qkv.stride(1), B, L, H, Dh, scale, t.n,
             t.starts, t.lens, t.vis, ptr(bits), ptr(bits_t), keep_prob, ptr(o), o.stride(0), o.stride(1),
             ptr(dout), dout.stride(0), dout.stride(1), ptr(lse), ptr(delta), ptr(dqkv),
-            dqkv.stride(0), dqkv.stride(1), _C.stream_ptr())
+            dqkv.stride(0), dqkv.stride(1), ptr(bias_grad), _C.stream_ptr())
     return dqkv
 
 

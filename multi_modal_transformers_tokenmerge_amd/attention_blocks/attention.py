@@ -165,9 +165,10 @@ class Encoder1DBlock:
         dzo = K.dropout_bwd(dx1f, rng, ctx.layer, DROP_ATTN_OUT, kp, row_offset=ctx.sample_offset * L,
                             colsum_out=self.out.b.grad)
         do = self.out.bwd(dzo, sv["o"].view(B * L, D), bias_grad_done=True)
+        # the QKV bias gradient (column sums of dqkv) is accumulated inside the attention backward
         dqkv = K.attn_bwd(sv["qkv"], sv["o"], do.view(B, L, D), sv["lse"], self.H, self.scale,
-                          ctx.table, sv["bits"], kpa)
-        dy0 = self.qkv.bwd(dqkv.view(B * L, 3 * D), sv["y0"].view(B * L, D))
+                          ctx.table, sv["bits"], kpa, bias_grad=self.qkv.b.grad)
+        dy0 = self.qkv.bwd(dqkv.view(B * L, 3 * D), sv["y0"].view(B * L, D), bias_grad_done=True)
         return self.ln0.bwd(dy0.view(B, L, D), sv["x"], sv["mu0"], sv["rs0"], addend=dx1)
 
 

@@ -166,6 +166,40 @@ __device__ __forceinline__ bf16x8 pack_frag(const floatx16& x, int s) {
   return r;
 }
 
+// Column sums of output accumulators (rows = head dims d = 32 dsub + rbit(r) + 4 hh, columns =
+// the 32 row-lanes of each half-wave), times `scale`, atomically added to gbias[0 .. 32 ND): the
+// bias gradient of the fused QKV projection (colsum of dq / dk / dv) without re-reading dqkv.
+// Transposed through LDS (`red`: the idle K/V staging buffers, >= waves x 32 ND x 33 floats; rows
+// padded to 33 so both phases are bank-conflict free), per-wave sums in `wsum` [waves][32 ND],
+// one global atomic per d per workgroup. Every thread of the workgroup must call it.
+static_assert(4 * KT * (64 + 8) * 2 >= 4 * 64 * 33 * 4, "colsum staging must fit the K/V buffers");
+template <int ND, int NTT>
+__device__ __forceinline__ void colsum_atomic(const floatx16 (&acc)[ND], float scale, float* red,
+                                              float* wsum, float* gbias, int lane, int wave) {
+  constexpr int ROWS = 32 * ND;
+  float* rw = red + wave * (ROWS * 33);
+  const int hh = lane >> 5, c = lane & 31;
+#pragma unroll
+  for (int d = 0; d < ND; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rw[(32 * d + rbit(r) + 4 * hh) * 33 + c] = acc[d][r] * scale;
+  __syncthreads();
+  for (int row = lane; row < ROWS; row += 64) {
+    float sum = 0.f;
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) sum += rw[row * 33 + i];
+    wsum[wave * ROWS + row] = sum;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < ROWS; i += NTT) {
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < NTT / 64; ++w) sum += wsum[w * ROWS + i];
+    atomicAdd(gbias + i, sum);
+  }
+  __syncthreads();  // red / wsum may be reused by the next call
+}
+
 // Register-staged copy of two KT x DH bf16 tiles (rows r0.., zero past L) -> LDS [KT][DH+8].
 // Loads are branch-free (rows clamped to L-1, zeroed at the LDS store), so the compiler keeps
 // counted vmcnt waits and the prefetch stays in flight through the MFMAs.
@@ -373,12 +407,14 @@ __global__ __launch_bounds__(NTT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mas
                                                          int64_t o_s_b, int64_t o_s_t,
                                                          float* __restrict__ delta,
                                                          bf16_t* __restrict__ dqkv,
-                                                         int64_t dq_s_b, int64_t dq_s_t) {
+                                                         int64_t dq_s_b, int64_t dq_s_t,
+                                                         float* __restrict__ bgrad) {
   constexpr int STR = DH + 8;
   constexpr int NS = DH / 16;
   constexpr int ND = DH / 32;
   constexpr int TILE = KT * STR;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE];  // [buf][K | V]
+  __shared__ float s_wsum[NTT / 64 * DH];
   const int b = blockIdx.z, h = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
   const int L = g.L, D = g.H * DH;
@@ -482,6 +518,9 @@ __global__ __launch_bounds__(NTT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mas
     buf ^= 1;
     kt = kn;
   }
+  if (bgrad)  // kernel-uniform; the loop's last barrier freed the staging buffers
+    colsum_atomic<ND, NTT>(dqacc, g.scale, reinterpret_cast<float*>(smem), s_wsum,
+                           bgrad + h * DH, lane, wave);
   if (qv) {
     bf16_t* orow = dqkv + (int64_t)b * dq_s_b + (int64_t)q * dq_s_t + h * DH;
 #pragma unroll
@@ -509,13 +548,15 @@ __global__ __launch_bounds__(NTT, 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask m
                                                            const float* __restrict__ lse,
                                                            const float* __restrict__ delta,
                                                            bf16_t* __restrict__ dqkv,
-                                                           int64_t dq_s_b, int64_t dq_s_t) {
+                                                           int64_t dq_s_b, int64_t dq_s_t,
+                                                           float* __restrict__ bgrad) {
   constexpr int STR = DH + 8;
   constexpr int NS = DH / 16;
   constexpr int ND = DH / 32;
   constexpr int TILE = KT * STR;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE];  // [buf][Q | dO]
   __shared__ __attribute__((aligned(16))) float s_rows[2][2][KT];  // [buf][lse*log2e | delta]
+  __shared__ float s_wsum[NTT / 64 * DH];
   const int b = blockIdx.z, h = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
   const int L = g.L, D = g.H * DH;
@@ -642,6 +683,12 @@ __global__ __launch_bounds__(NTT, 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask m
     buf ^= 1;
     qt = qn;
   }
+  if (bgrad) {  // kernel-uniform: bias gradients of the K and V projections
+    colsum_atomic<ND, NTT>(dk, g.scale, reinterpret_cast<float*>(smem), s_wsum,
+                           bgrad + D + h * DH, lane, wave);
+    colsum_atomic<ND, NTT>(dv, drop_scale, reinterpret_cast<float*>(smem), s_wsum,
+                           bgrad + 2 * D + h * DH, lane, wave);
+  }
   if (kv) {
     bf16_t* krow_o = dqkv + (int64_t)b * dq_s_b + (int64_t)key * dq_s_t + D + h * DH;
 #pragma unroll
@@ -746,10 +793,10 @@ inline int bwd_threads(int L) {
   do {                                                                                            \
     hipLaunchKernelGGL((attn_bwd_dq_kernel<DH_, NTT_>), grid, dim3(NTT_), 0, s, g, m, drop_bits,  \
                        words, dscale, (const bf16_t*)dout, d_s_b, d_s_t, lse, (const bf16_t*)o,   \
-                       o_s_b, o_s_t, delta, (bf16_t*)dqkv, dq_s_b, dq_s_t);                       \
+                       o_s_b, o_s_t, delta, (bf16_t*)dqkv, dq_s_b, dq_s_t, bias_grad);            \
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DH_, NTT_>), grid, dim3(NTT_), 0, s, g, m,           \
                        drop_bits_t, words, dscale, (const bf16_t*)dout, d_s_b, d_s_t, lse, delta,  \
-                       (bf16_t*)dqkv, dq_s_b, dq_s_t);                                             \
+                       (bf16_t*)dqkv, dq_s_b, dq_s_t, bias_grad);                                  \
   } while (0)
 
 extern "C" int mmt_dropout_bits(const uint32_t* rng, uint32_t layer, uint32_t site, int rows,
@@ -799,7 +846,7 @@ extern "C" int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
                             float keep_prob, const void* o, int64_t o_s_b, int64_t o_s_t,
                             const void* dout, int64_t d_s_b, int64_t d_s_t, const float* lse,
                             float* delta, void* dqkv, int64_t dq_s_b, int64_t dq_s_t,
-                            mmt_stream_t stream) {
+                            float* bias_grad, mmt_stream_t stream) {
   MMT_CHECK_ARG(qkv && o && dout && lse && delta && dqkv, "mmt_attn_bwd: null pointer");
   MMT_CHECK_ARG(B > 0 && L > 0 && H > 0 && L <= MAXL, "mmt_attn_bwd: bad shape");
   MMT_CHECK_ARG(s_t % 8 == 0 && d_s_t % 8 == 0 && dq_s_t % 4 == 0 && o_s_t % 8 == 0,

@@ -84,10 +84,14 @@ def test_attention_fwd_bwd(dev, B, L, H, Dh, masked, drop):
     ref = ref_attention(qf, H, scale, mask, keep, keep_prob)
     assert rel(o, ref) < 1e-2
     dout = torch.randn((B, L, H * Dh), generator=g).bfloat16().to(dev)
-    dqkv = K.attn_bwd(qkv, o, dout, lse, H, scale, table, bits, keep_prob)
+    bgrad = torch.full((3 * H * Dh,), 0.5, device=dev)
+    dqkv = K.attn_bwd(qkv, o, dout, lse, H, scale, table, bits, keep_prob, bias_grad=bgrad)
     ref.backward(dout.float())
     gr = qf.grad.view(B, L, 3, H * Dh)
     gk = dqkv.float().view(B, L, 3, H * Dh)
+    # fused QKV bias gradient = column sums of dqkv (summed before the bf16 rounding of dqkv)
+    torch.testing.assert_close(bgrad - 0.5, dqkv.float().sum((0, 1)), rtol=2e-2,
+                               atol=2e-2 * float(dqkv.float().sum((0, 1)).abs().max()) + 1e-3)
     for i in range(3):
         assert rel(gk[:, :, i], gr[:, :, i]) < 2e-2, ("qkv"[i], rel(gk[:, :, i], gr[:, :, i]))
 
