@@ -190,6 +190,9 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--overlap-stages", type=int, default=3,
+                    help="N > 1: backward split into this many block ranges, each range's gradient "
+                         "all-reduce overlapped with the rest of the backward (1 = no overlap)")
     ap.add_argument("--probe-only", action="store_true",
                     help="only launch the dominant GEMM (for rocprofv3 --pmc traffic passes)")
     args = ap.parse_args()
@@ -198,7 +201,8 @@ def main():
     N = di.world_size
     if args.gpus != N and N > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {N}", file=sys.stderr)
-    dev = torch.device("cuda", di.local_rank)
+    # (local_rank modulo the visible devices: lets a 2-rank gloo rehearsal share one GPU)
+    dev = torch.device("cuda", di.local_rank % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     cfg = get_config(args.config)
     B = args.batch
@@ -222,6 +226,22 @@ def main():
         model.backward(st)
         loss_buf.copy_(loss)
 
+    # N > 1: the backward runs as S block-range stages; after each stage the gradient region it
+    # finalised is all-reduced asynchronously (RCCL stream) while the next stages compute, and
+    # AdamW waits for all of them
+    S = max(1, min(args.overlap_stages, cfg.num_blocks)) if reducer else 1
+    regions = model.grad_regions(S) if S > 1 else None
+    stage_state = {}
+
+    def fwd_stage(k):
+        if k == 0:
+            model.store.zero_grad()
+            loss, st = model.compute_diffusion_denoise_loss(txt, img, act, True, state.rng,
+                                                            state.sample_offset)
+            loss_buf.copy_(loss)
+            stage_state["st"] = st
+        model.backward_stage(stage_state["st"], k, S)
+
     def opt():
         state.apply_gradients()
 
@@ -239,20 +259,41 @@ def main():
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
-        g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1, pool=pool):
-            fwd_bwd()
-            if not reducer:
+        if S > 1:
+            for k in range(S):   # one graph per backward stage (the first also holds the forward)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    fwd_stage(k)
+                graphs.append(g)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
                 opt()
-        graphs.append(g1)
-        if reducer:
-            g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2, pool=pool):
-                opt()
-            graphs.append(g2)
+            graphs.append(g)
+        else:
+            g1 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1, pool=pool):
+                fwd_bwd()
+                if not reducer:
+                    opt()
+            graphs.append(g1)
+            if reducer:
+                g2 = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g2, pool=pool):
+                    opt()
+                graphs.append(g2)
 
     def step():
-        if use_graph:
+        if use_graph and S > 1:
+            works = []
+            flat = model.store.flat_grad
+            for k in range(S):
+                graphs[k].replay()
+                lo, hi = regions[k]
+                works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+            for w in works:
+                w.wait()
+            graphs[S].replay()
+        elif use_graph:
             graphs[0].replay()
             if reducer:
                 reducer(model.store.flat_grad)

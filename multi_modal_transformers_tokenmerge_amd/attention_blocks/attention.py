@@ -190,7 +190,10 @@ class StackedEncoder1DBlock:
             saved.append(sv)
         return x, saved
 
-    def backward(self, dx, saved, ctxs):
-        for blk, sv, ctx in zip(reversed(self.blocks), reversed(saved), reversed(ctxs)):
-            dx = blk.backward(dx, sv, ctx)
+    def backward(self, dx, saved, ctxs, lo: int = 0, hi: int | None = None):
+        """Backward through blocks hi-1 .. lo (all by default); a staged backward (gradient
+        all-reduce overlapped with the remaining blocks) calls it in several ranges."""
+        hi = len(self.blocks) if hi is None else hi
+        for i in range(hi - 1, lo - 1, -1):
+            dx = self.blocks[i].backward(dx, saved[i], ctxs[i])
         return dx

@@ -39,8 +39,8 @@ def init_from_env(backend: str | None = None) -> DistInfo:
         return DistInfo()
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend is None:  # MMT_DIST_BACKEND=gloo: CPU-transport rehearsal of the multi-rank path
+        backend = os.environ.get("MMT_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         torch.cuda.set_device(local)
         dist.init_process_group(backend, device_id=torch.device("cuda", local))

@@ -277,10 +277,45 @@ class Octo:
         st.update(head_kind="categorical", head_sv=hsv, xL_shape=tuple(xL.shape))
         return loss, st
 
+    # ------------------------------------------------------------------ staged backward
+    def _stage_bounds(self, n_stages: int) -> List[int]:
+        nb = self.cfg.num_blocks
+        return [nb * (n_stages - i) // n_stages for i in range(n_stages + 1)]  # nb .. 0
+
+    def grad_regions(self, n_stages: int) -> List[tuple]:
+        """Flat-gradient index ranges that are final after each backward stage (stage 0: the
+        heads and the last blocks, declared last in the store; the last stage: the first blocks
+        and everything declared before them)."""
+        b = self._stage_bounds(n_stages)
+        off = [self.store.by_name[f"StackedEncoder1DBlock_0/Block_{j}/LayerNorm_0/scale"].offset
+               if j < self.cfg.num_blocks else self.store.n for j in b]
+        regions = []
+        for i in range(n_stages):
+            hi = self.store.n if i == 0 else off[i]
+            lo = 0 if i == n_stages - 1 else off[i + 1]
+            regions.append((lo, hi))
+        return regions
+
+    def backward_stage(self, st: Dict, stage: int, n_stages: int):
+        """Stage `stage` of a backward split into n_stages block ranges (the heads run in stage
+        0, the stem / embeddings in the last): backward(st) == all stages in order."""
+        b = self._stage_bounds(n_stages)
+        if stage == 0:
+            st["_dx"] = self._backward_head(st)
+        dx = self.stack.backward(st["_dx"], st["stack_sv"], st["ctxs"], lo=b[stage + 1], hi=b[stage])
+        if stage == n_stages - 1:
+            self._backward_tokens(st, dx)
+            st.pop("_dx", None)
+        else:
+            st["_dx"] = dx
+
     def backward(self, st: Dict):
         """Reverse schedule of compute_diffusion_denoise_loss / compute_l2_loss / compute_ce_loss;
         writes every parameter gradient into the flat gradient buffer (which must be zeroed
         before the forward)."""
+        self.backward_stage(st, 0, 1)
+
+    def _backward_head(self, st: Dict):
         B = st["B"]
         D = self.D
         kind = st.get("head_kind", "diffusion")
@@ -297,10 +332,14 @@ class Octo:
             _C.call("mmt_rows_mean_bwd", _C.ptr(de), de.stride(0), B, self.L_final, D,
                     _C.ptr(self.readout_flag), self.readout_rows.numel(), _C.ptr(dxL),
                     _C.stream_ptr())
-        dx0 = self.stack.backward(dxL, st["stack_sv"], st["ctxs"])
+        return dxL
+
+    def _backward_tokens(self, st: Dict, dx0):
+        B = st["B"]
+        D = self.D
         NI, T = st["NI"], st["T"]
-        dimg = torch.empty((B, NI, D), dtype=torch.bfloat16, device=dxL.device)
-        dtxt = torch.empty((B, T, D), dtype=torch.bfloat16, device=dxL.device) if self.text_proj else None
+        dimg = torch.empty((B, NI, D), dtype=torch.bfloat16, device=dx0.device)
+        dtxt = torch.empty((B, T, D), dtype=torch.bfloat16, device=dx0.device) if self.text_proj else None
         it = self.image_tokenizer
         _C.call("mmt_seq_assemble_bwd", B, self.L0, D, _C.ptr(self.row_src), _C.ptr(dx0),
                 _C.ptr(dtxt), T, _C.ptr(dimg), NI, _C.ptr(st["rt"]), _C.ptr(st["ct"]),

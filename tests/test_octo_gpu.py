@@ -34,3 +34,34 @@ def test_octo_small_tome_parity(dev):
     cfg = get_config("octo-small-tome16", num_blocks=3, t5=T5Config(num_layers=2))
     for seed in (0, 1):
         _check(run_parity(cfg, 2, seed=seed))
+
+
+def test_staged_backward_matches_backward(dev):
+    """The block-range stages used to overlap the gradient all-reduce (bench.py, N > 1) write
+    the gradients of the one-piece backward (up to the order of the fp32 atomics some bias and
+    embedding gradients use), and each stage's region is final after it."""
+    import torch
+    from multi_modal_transformers_tokenmerge_amd.models.octo.config import get_config
+    from multi_modal_transformers_tokenmerge_amd.models.octo.octo import Octo, create_octo_train_state
+    from oracle.parity import _inputs
+    model = Octo(get_config("octo-tiny", num_blocks=4), dev, seed=0)
+    state = create_octo_train_state(model, seed=5)
+    images, text, actions = _inputs(model, 3)
+    img, act = torch.from_numpy(images).to(dev), torch.from_numpy(actions).to(dev)
+    model.store.zero_grad()
+    _, st = model.compute_diffusion_denoise_loss(None, img, act, True, state.rng, 0)
+    model.backward(st)
+    ref = model.store.flat_grad.clone()
+    S = 3
+    regions = model.grad_regions(S)
+    assert regions[0][1] == model.store.n and regions[-1][0] == 0
+    assert all(regions[i][0] == regions[i + 1][1] for i in range(S - 1))
+    model.store.zero_grad()
+    _, st = model.compute_diffusion_denoise_loss(None, img, act, True, state.rng, 0)
+    for k in range(S):
+        model.backward_stage(st, k, S)
+        lo, hi = regions[k]
+        torch.cuda.synchronize()
+        torch.testing.assert_close(model.store.flat_grad[lo:hi], ref[lo:hi], rtol=1e-4, atol=1e-6,
+                                   msg=f"stage {k} region")
+    torch.testing.assert_close(model.store.flat_grad, ref, rtol=1e-4, atol=1e-6)
