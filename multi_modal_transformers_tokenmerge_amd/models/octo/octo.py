@@ -176,7 +176,7 @@ class Octo:
                 txt = t5_out
         img_tok, (rt, ct), isv = self.image_tokenizer.forward(images, train, rng, sample_offset,
                                                               positions)
-        st.update(img_sv=isv, rt=rt, ct=ct)
+        st.update(img_sv=isv, rt=rt, ct=ct, img_tok=img_tok, txt=txt)
         x0 = torch.empty((B, self.L0, D), dtype=torch.float32, device=images.device)  # fp32 residual
         NI = img_tok.shape[1]
         _C.call("mmt_seq_assemble_fwd", B, self.L0, D, _C.ptr(self.row_src), _C.ptr(txt), T,
@@ -201,7 +201,7 @@ class Octo:
                 _C.ptr(self.head.readout_slot(cat)), cat.stride(0), _C.stream_ptr())
         loss, hsv = self.head.loss_forward(cat, actions, rng, sample_offset, inject.get("t"),
                                            inject.get("eps"))
-        st.update(head_sv=hsv, xL_shape=tuple(xL.shape))
+        st.update(head_sv=hsv, xL_shape=tuple(xL.shape), xL=xL)
         return loss, st
 
     def predict_diffusion_denoise_term(self, text_tokens, images, time, noisy_actions, rng=None,

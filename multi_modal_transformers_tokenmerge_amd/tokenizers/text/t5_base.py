@@ -98,7 +98,8 @@ class T5Tokenizer:
             self._bias_cache[T] = bias
         return self._bias_cache[T]
 
-    def __call__(self, input_ids: torch.Tensor) -> torch.Tensor:
+    def __call__(self, input_ids: torch.Tensor, layer_outputs: list | None = None) -> torch.Tensor:
+        """layer_outputs: if a list, receives the residual stream after each layer (parity tests)."""
         c = self.cfg
         B, T = input_ids.shape
         ids = input_ids.to(torch.int32).contiguous()
@@ -112,6 +113,8 @@ class T5Tokenizer:
             n = K.rmsnorm(x, ln1.bf16, c.layer_norm_epsilon)
             h = K.gemm(n, wi.bf16, trans_b=True, act=K.ACT_RELU)
             x = K.gemm(h, wo.bf16, trans_b=True, residual=x)
+            if layer_outputs is not None:
+                layer_outputs.append(x.view(B, T, c.d_model))
         x = K.rmsnorm(x, self.final_ln.bf16, c.layer_norm_epsilon)
         return x.view(B, T, c.d_model)
 

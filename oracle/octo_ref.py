@@ -121,6 +121,83 @@ def dense(p, name, x):
     return y + b if b is not None else y
 
 
+# ------------------------------------------------------------------ bf16 storage emulation
+class _RoundFwd(torch.autograd.Function):
+    """bf16 rounding of a stored activation; the gradient passes through unchanged."""
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+class _RoundGrad(torch.autograd.Function):
+    """Identity forward; the gradient is rounded to bf16 (a bf16-stored gradient tensor)."""
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+class _RoundBoth(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).to(x.dtype)
+
+
+class FlashAttnBF16(torch.autograd.Function):
+    """Softmax attention with the storage points of csrc/attention.hip: probabilities enter the
+    P.V product as bf16 (after the dropout keep mask), dS = P*(dP*keep/kp - delta) enters the dQ
+    and dK products as bf16, dV = bf16(P*keep)^T dO / kp, delta = rowsum(dO * bf16(O)).
+    q, k, v (B, L, H, Dh) bf16-valued fp32; allowed (L, L) bool; keep (L, L) bool or None;
+    bias (H, L, L) or None (T5 mode, added after the scale)."""
+    @staticmethod
+    def forward(ctx, q, k, v, allowed, keep, kp, scale, bias):
+        s = torch.einsum("bqhd,bkhd->bhqk", q, k) * scale
+        if bias is not None:
+            s = s + bias[None]
+        s = s.masked_fill(~allowed[None, None], float("-inf"))
+        m = s.amax(-1, keepdim=True)
+        p = torch.exp(s - m)
+        l = p.sum(-1, keepdim=True)
+        pk = p if keep is None else p * keep[None, None]
+        o = torch.einsum("bhqk,bkhd->bqhd", _bf(pk), v) / l.permute(0, 2, 1, 3) / kp
+        lse = m + torch.log(l)
+        ctx.save_for_backward(q, k, v, s, lse, _bf(o))
+        ctx.keep, ctx.kp, ctx.scale = keep, kp, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, s, lse, o16 = ctx.saved_tensors
+        keep, kp, scale = ctx.keep, ctx.kp, ctx.scale
+        P = torch.exp(s - lse)
+        dp = torch.einsum("bqhd,bkhd->bhqk", do, v) / kp
+        pk = P
+        if keep is not None:
+            dp = dp * keep[None, None]
+            pk = P * keep[None, None]
+        delta = (do * o16).sum(-1).permute(0, 2, 1)[..., None]          # (B, H, L, 1)
+        ds = _bf(P * (dp - delta))
+        dq = torch.einsum("bhqk,bkhd->bqhd", ds, k) * scale
+        dk = torch.einsum("bhqk,bqhd->bkhd", ds, q) * scale
+        dv = torch.einsum("bhqk,bqhd->bkhd", _bf(pk), do) / kp
+        return dq, dk, dv, None, None, None, None, None
+
+
 # ----------------------------------------------------------------------------------- T5
 def t5_bucket(rel, num_buckets=32, max_distance=128):
     ret = (rel > 0).long() * (num_buckets // 2)
@@ -133,31 +210,52 @@ def t5_bucket(rel, num_buckets=32, max_distance=128):
     return ret + torch.where(n < max_exact, n, large)
 
 
-def t5_encoder(tp: Dict[str, torch.Tensor], ids: torch.Tensor, num_layers: int, H: int, d_kv: int,
-               eps: float = 1e-6, prefix="T5Tokenizer_0", num_buckets=32, max_distance=128):
-    """FlaxT5 encoder forward (t5_base.py:11-15): RMS layer norm, relative-position-biased
-    attention without 1/sqrt(d) scaling, ReLU FF, pre-norm residuals, final norm."""
-    def rms(x, w):
-        return x * torch.rsqrt((x * x).mean(-1, keepdim=True) + eps) * w
-    B, T = ids.shape
-    x = tp[f"{prefix}/shared/embedding"][ids.long()]
+def t5_position_bias(tp, T, prefix="T5Tokenizer_0", num_buckets=32, max_distance=128):
     pos = torch.arange(T)
     bucket = t5_bucket(pos[None, :] - pos[:, None], num_buckets, max_distance)
-    bias = tp[f"{prefix}/relative_attention_bias"][bucket].permute(2, 0, 1)  # (H, T, T)
+    return tp[f"{prefix}/relative_attention_bias"][bucket].permute(2, 0, 1)  # (H, T, T)
+
+
+def t5_rms(x, w, eps, emulate_bf16=False):
+    y = x * torch.rsqrt((x * x).mean(-1, keepdim=True) + eps) * w
+    return _bf(y) if emulate_bf16 else y
+
+
+def t5_layer(tp, x, i, bias, H, d_kv, eps=1e-6, prefix="T5Tokenizer_0", emulate_bf16=False):
+    """One FlaxT5 encoder layer: pre-RMS-norm self-attention (relative bias, no 1/sqrt(d)) and
+    ReLU feed-forward, each added to the residual stream."""
+    q16 = _bf if emulate_bf16 else (lambda a: a)
+    B, T, _ = x.shape
     inner = H * d_kv
-    for i in range(num_layers):
-        p = f"{prefix}/block/{i}"
-        n = rms(x, tp[f"{p}/layer_0/layer_norm"])
-        qkv = n @ tp[f"{p}/SelfAttention/qkv"].t()
-        q, k, v = qkv.split(inner, dim=-1)
-        q, k, v = (a.view(B, T, H, d_kv) for a in (q, k, v))
+    p = f"{prefix}/block/{i}"
+    n = t5_rms(x, tp[f"{p}/layer_0/layer_norm"], eps, emulate_bf16)
+    qkv = q16(n @ tp[f"{p}/SelfAttention/qkv"].t())
+    q, k, v = qkv.split(inner, dim=-1)
+    q, k, v = (a.reshape(B, T, H, d_kv) for a in (q, k, v))
+    if emulate_bf16:
+        o = FlashAttnBF16.apply(q, k, v, torch.ones((T, T), dtype=torch.bool), None, 1.0, 1.0, bias)
+    else:
         s = torch.einsum("bqhd,bkhd->bhqk", q, k) + bias[None]
-        a = torch.softmax(s, -1)
-        o = torch.einsum("bhqk,bkhd->bqhd", a, v).reshape(B, T, inner)
-        x = x + o @ tp[f"{p}/SelfAttention/o"].t()
-        n = rms(x, tp[f"{p}/layer_1/layer_norm"])
-        x = x + torch.relu(n @ tp[f"{p}/DenseReluDense/wi"].t()) @ tp[f"{p}/DenseReluDense/wo"].t()
-    return rms(x, tp[f"{prefix}/final_layer_norm"])
+        o = torch.einsum("bhqk,bkhd->bqhd", torch.softmax(s, -1), v)
+    o = q16(o).reshape(B, T, inner)
+    x = q16(x + o @ tp[f"{p}/SelfAttention/o"].t())
+    n = t5_rms(x, tp[f"{p}/layer_1/layer_norm"], eps, emulate_bf16)
+    return q16(x + q16(torch.relu(n @ tp[f"{p}/DenseReluDense/wi"].t())) @ tp[f"{p}/DenseReluDense/wo"].t())
+
+
+def t5_encoder(tp: Dict[str, torch.Tensor], ids: torch.Tensor, num_layers: int, H: int, d_kv: int,
+               eps: float = 1e-6, prefix="T5Tokenizer_0", num_buckets=32, max_distance=128,
+               emulate_bf16: bool = False):
+    """FlaxT5 encoder forward (t5_base.py:11-15): RMS layer norm, relative-position-biased
+    attention without 1/sqrt(d) scaling, ReLU FF, pre-norm residuals, final norm.
+    emulate_bf16: round at the build's storage points (bf16 residual stream, norm outputs,
+    projections, attention probabilities; tokenizers/text/t5_base.py)."""
+    B, T = ids.shape
+    x = tp[f"{prefix}/shared/embedding"][ids.long()]
+    bias = t5_position_bias(tp, T, prefix, num_buckets, max_distance)
+    for i in range(num_layers):
+        x = t5_layer(tp, x, i, bias, H, d_kv, eps, prefix, emulate_bf16)
+    return t5_rms(x, tp[f"{prefix}/final_layer_norm"], eps, emulate_bf16)
 
 
 # ------------------------------------------------------------------------------ ToMe (torch)
@@ -185,15 +283,34 @@ def tome_merge_wavg(x_set, size, unm, src, dst, r):
 # ---------------------------------------------------------------------------- the model
 class OctoRef:
     """cfg: the build's OctoConfig; params: {name: fp32 CPU tensor requiring grad};
-    t5_params: {name: fp32 CPU tensor} (frozen)."""
+    t5_params: {name: fp32 CPU tensor} (frozen).
+
+    emulate_bf16=True rounds to bf16 at every point where the build STORES a bf16 tensor, in the
+    forward (LayerNorm / GroupNorm outputs, q/k/v, attention probabilities, attention output, MLP
+    hidden, stem im2col pixels, token embeddings, head inputs, the whole T5) and in the backward
+    (every gradient the build writes as bf16: dz of each dropout/Dense output, dq/dk/dv, dS,
+    dy of each LayerNorm-fed Dense, the head's dpred/dcat). What then remains between the two
+    is fp32 summation order, which is what the tight end-to-end bar measures. Without it the
+    restatement is plain fp32 (the CPU baseline)."""
 
     def __init__(self, cfg, params: Dict[str, torch.Tensor], t5_params: Optional[Dict] = None,
-                 dtype=torch.float32):
+                 dtype=torch.float32, emulate_bf16: bool = False):
         self.cfg = cfg
         self.dtype = dtype
         self.residual_round = None
         self.p = params
         self.t5p = t5_params
+        self.emulate = emulate_bf16
+
+    # storage-point rounding (identity without emulation)
+    def rb(self, x):
+        return _RoundFwd.apply(x) if self.emulate else x
+
+    def gb(self, x):
+        return _RoundGrad.apply(x) if self.emulate else x
+
+    def rbg(self, x):
+        return _RoundBoth.apply(x) if self.emulate else x
 
     def _q(self, x):
         """Optional emulation of a storage rounding of the residual stream (diagnostics only)."""
@@ -201,46 +318,60 @@ class OctoRef:
             return x
         return x + (x.detach().to(self.residual_round).to(x.dtype) - x.detach())
 
-    def forward_loss(self, text_ids, images, actions, *, seed: int, step: int, positions,
-                     t, eps, tome_indices: Optional[List] = None, sequence=None,
-                     sample_offset: int = 0, train: bool = True, record: Optional[list] = None):
-        """Returns (loss, extras). sequence: list of (kind, n, timestep, compressed_per_layer)."""
-        cfg, p = self.cfg, self.p
-        D, H = cfg.token_embedding_dim, cfg.num_heads
-        Dh = D // H
-        dt = self.dtype
+    # -------------------------------------------------------------------------- pieces
+    def stem(self, images, positions, trace=None):
+        """image_tokenizer.py:235-309: patches -> ResNetV2 stem -> Dense (+ row/col embeddings).
+        images (B, I, H, W, 3) in [0, 255]; returns (B, I*NP, D)."""
+        cfg, p, dt = self.cfg, self.p, self.dtype
+        rb, gb, rbg = self.rb, self.gb, self.rbg
         images = torch.as_tensor(images).to(dt)
         B, I = images.shape[:2]
-        # ---- image tokenizer (image_tokenizer.py:235-309)
         P = cfg.patch_size
         NP = (cfg.image_size[0] // P) ** 2
         patches = torch.stack([torch.stack([torch.from_numpy(image_to_patches(
             images[b, i].numpy(), P, True)) for i in range(I)]) for b in range(B)]).to(dt)
-        x = patches.reshape(B * I * NP, P, P, 3).permute(0, 3, 1, 2)           # NCHW
+        x = rb(patches.reshape(B * I * NP, P, P, 3).permute(0, 3, 1, 2))       # NCHW
         name = "ImageTokenizer_0/ResNetV2Block_0"
         wc = p[f"{name}/Conv_0/kernel"].view(64, 12, 12, 3).permute(0, 3, 1, 2)
-        x = F.conv2d(x, wc, p[f"{name}/Conv_0/bias"], stride=2)
+        x = gb(F.conv2d(x, wc, None, stride=2)) + p[f"{name}/Conv_0/bias"].view(1, -1, 1, 1)
         x = F.max_pool2d(x, 3, stride=1)                                       # (N, 64, 1, 1)
         x = x.reshape(B, I * NP, 64)
         residual = x
         for k in range(2):
             x = groupnorm(x, 32, p[f"{name}/GroupNorm_{k}/scale"], p[f"{name}/GroupNorm_{k}/bias"], 1e-6)
-            x = gelu_tanh(x)
-            x = dense(p, f"{name}/Conv_{k + 1}", x)   # 3x3 SAME conv on a 1x1 map = centre tap
+            x = rb(gelu_tanh(x))
+            x = gb(dense(p, f"{name}/Conv_{k + 1}", x))   # 3x3 SAME conv on a 1x1 map = centre tap
         x = x + residual
-        img = dense(p, f"{name}/Dense_0", x)                                    # (B, I*NP, D)
+        img = self.rbg(dense(p, f"{name}/Dense_0", rb(x)))                      # (B, I*NP, D)
+        if trace is not None:
+            trace["img"] = img.detach().clone()
         rt, ct = (torch.as_tensor(a).long() for a in positions)
-        img = img + p["ImageTokenizer_0/image_row_position_embedding/embedding"][rt] + \
+        return img + p["ImageTokenizer_0/image_row_position_embedding/embedding"][rt] + \
             p["ImageTokenizer_0/image_col_position_embedding/embedding"][ct]
-        # ---- text
-        txt = None
-        if self.t5p is not None and text_ids is not None:
-            t5o = t5_encoder(self.t5p, torch.as_tensor(text_ids), cfg.t5.num_layers,
-                             cfg.t5.num_heads, cfg.t5.d_kv, cfg.t5.layer_norm_epsilon).detach()
-            txt = dense(p, "TextProjection_0", t5o) if "TextProjection_0/kernel" in p else t5o
-        # ---- readouts (readout.py:18-33 on zeros)
+
+    def text(self, text_ids, trace=None):
+        """t5_base.py:8-15 (frozen) + the build's Dense(768 -> D) when D != 768."""
+        cfg, p = self.cfg, self.p
+        if self.t5p is None or text_ids is None:
+            return None
+        t5o = t5_encoder(self.t5p, torch.as_tensor(text_ids), cfg.t5.num_layers,
+                         cfg.t5.num_heads, cfg.t5.d_kv, cfg.t5.layer_norm_epsilon,
+                         emulate_bf16=self.emulate).detach()
+        txt = self.text_proj(t5o)
+        if trace is not None:
+            trace["t5"], trace["txt"] = t5o.detach().clone(), txt.detach().clone()
+        return txt
+
+    def text_proj(self, t5o):
+        p = self.p
+        return self.rbg(dense(p, "TextProjection_0", t5o)) if "TextProjection_0/kernel" in p else t5o
+
+    def assemble(self, img, txt, sequence, B):
+        """token_sequencer.py:255-269 + readout.py:18-33 (zeros + embedding) + the stack's
+        learned position embedding (attention.py:97-100)."""
+        p = self.p
+        NP = (self.cfg.image_size[0] // self.cfg.patch_size) ** 2
         ro = p["AddPositionEmbedding_0/pos_embedding"][None].expand(B, -1, -1)
-        # ---- assemble (token_sequencer.py:255-269)
         parts, ti, ii, ri = [], 0, 0, 0
         for kind, n, ts, _ in sequence:
             if kind in ("prefix", "text"):
@@ -250,76 +381,103 @@ class OctoRef:
             else:
                 parts.append(ro[:, ri:ri + n]); ri += n
         x = torch.cat(parts, dim=1)
-        L0 = x.shape[1]
-        x = self._q(x + p["StackedEncoder1DBlock_0/posembed_input/pos_embedding"][None])
-        # ---- stack
+        return self._q(x + p["StackedEncoder1DBlock_0/posembed_input/pos_embedding"][None])
+
+    def block(self, x, layer, sequence, size, *, seed, step, sample_offset=0, train=True,
+              tome_indices=None, trace=None):
+        """Encoder1DBlock (attention.py:41-69) with ToMe after the attention residual
+        (tome_attention.py:249-256 placement). Returns (x_out, size_out, (unm, src, dst) | None)."""
+        def tr(name, v):
+            if trace is not None:
+                trace[f"b{layer}/{name}"] = v.detach().clone()
+            return v
+        cfg, p = self.cfg, self.p
+        rb, gb, rbg = self.rb, self.gb, self.rbg
+        D, H = cfg.token_embedding_dim, cfg.num_heads
+        Dh = D // H
+        B, L = x.shape[:2]
         kp = 1.0 - cfg.dropout_rate
         kpa = 1.0 - cfg.attention_dropout_rate
+        blk = f"StackedEncoder1DBlock_0/Block_{layer}"
         lens = [s[1] for s in sequence]
-        size = None
-        for layer in range(cfg.num_blocks):
-            blk = f"StackedEncoder1DBlock_0/Block_{layer}"
-            L = x.shape[1]
-            if record is not None:
-                x.retain_grad()
-                record.append(x)
-            cur = [(k, lens[i] - layer * c, ts) for i, (k, _, ts, c) in enumerate(sequence)]
-            mask = torch.from_numpy(literal_mask(cur))
-            y = seq_layernorm(x, p[f"{blk}/LayerNorm_0/scale"], p[f"{blk}/LayerNorm_0/bias"], cfg.layer_norm_eps)
-            qkv = dense(p, f"{blk}/SelfAttention_0/qkv", y)
-            q, k, v = qkv.split(D, dim=-1)
-            q = q.view(B, L, H, Dh) / math.sqrt(Dh)
-            k, v = k.view(B, L, H, Dh), v.view(B, L, H, Dh)
-            s = torch.einsum("bqhd,bkhd->bhqk", q, k)
+        tr("x", x)
+        cur = [(k, lens[i] - layer * c, ts) for i, (k, _, ts, c) in enumerate(sequence)]
+        mask = torch.from_numpy(literal_mask(cur))
+        y = tr("y0", rbg(seq_layernorm(x, p[f"{blk}/LayerNorm_0/scale"], p[f"{blk}/LayerNorm_0/bias"],
+                                       cfg.layer_norm_eps)))
+        qkv = tr("qkv", rbg(dense(p, f"{blk}/SelfAttention_0/qkv", y)))
+        q, k, v = qkv.split(D, dim=-1)
+        k, v = k.reshape(B, L, H, Dh), v.reshape(B, L, H, Dh)
+        keep = (torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 0, L, L, 0, kpa))
+                if train else None)
+        if self.emulate:
+            o = FlashAttnBF16.apply(q.reshape(B, L, H, Dh), k, v, mask, keep,
+                                    kpa if train else 1.0, 1.0 / math.sqrt(Dh), None)
+            o = tr("o", rbg(o.reshape(B, L, D)))
+        else:
+            s = torch.einsum("bqhd,bkhd->bhqk", q.reshape(B, L, H, Dh) / math.sqrt(Dh), k)
             s = torch.where(mask[None, None], s, torch.finfo(torch.float32).min)
             a = torch.softmax(s, -1)
             if train:
-                keep = torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 0, L, L, 0, kpa))
                 a = torch.where(keep[None, None], a / kpa, torch.zeros_like(a))
-            o = torch.einsum("bhqk,bkhd->bqhd", a, v).reshape(B, L, D)
-            o = dense(p, f"{blk}/SelfAttention_0/out", o)
-            if train:
-                keep = torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 1, B * L, D,
-                                                          sample_offset * L, kp)).view(B, L, D)
-                o = torch.where(keep, o / kp, torch.zeros_like(o))
-            x = self._q(x + o)
-            # ToMe after the attention residual (tome_attention.py:249-256 placement)
-            merged = [i for i, c in enumerate(sequence) if c[3] > 0]
-            if merged:
-                si = merged[0]
-                r = sequence[si][3]
-                s0 = sum(ln for _, ln, _ in cur[:si])
-                tcur = cur[si][1]
-                if tome_indices is not None:
-                    unm, src, dst = tome_indices[layer]
-                else:  # standalone: canonical C matching on this restatement's own key metric
-                    from . import tome as T
-                    km = k.detach().float()[:, s0:s0 + tcur].contiguous().numpy()
-                    unm, src, dst, _ = T.canon_match(km, r)
-                    unm, src, dst = (torch.from_numpy(a) for a in (unm, src, dst))
-                xs, size = tome_merge_wavg(x[:, s0:s0 + tcur], size, unm, src, dst, r)
-                x = torch.cat([x[:, :s0], xs, x[:, s0 + tcur:]], dim=1)
-            L2 = x.shape[1]
-            z = seq_layernorm(x, p[f"{blk}/LayerNorm_1/scale"], p[f"{blk}/LayerNorm_1/bias"], cfg.layer_norm_eps)
-            h = torch.relu(dense(p, f"{blk}/MLPBlock_0/Dense_0", z))
-            if train:
-                keep = torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 2, B * L2, cfg.mlp_dim,
-                                                          sample_offset * L2, kp)).view(B, L2, -1)
-                h = torch.where(keep, h / kp, torch.zeros_like(h))
-            z = dense(p, f"{blk}/MLPBlock_0/Dense_1", h)
-            if train:
-                keep = torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 3, B * L2, D,
-                                                          sample_offset * L2, kp)).view(B, L2, D)
-                z = torch.where(keep, z / kp, torch.zeros_like(z))
-            x = self._q(x + z)
-        # ---- readouts (octo.py:122-124) and head (diffusion.py:88-143)
-        final = [(k, lens[i] - cfg.num_blocks * c, ts) for i, (k, _, ts, c) in enumerate(sequence)]
+            o = tr("o", torch.einsum("bhqk,bkhd->bqhd", a, v).reshape(B, L, D))
+        o = gb(dense(p, f"{blk}/SelfAttention_0/out", o))
+        if train:
+            keep = torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 1, B * L, D,
+                                                      sample_offset * L, kp)).view(B, L, D)
+            o = torch.where(keep, o / kp, torch.zeros_like(o))
+        x = self._q(x + o)
+        used = None
+        merged = [i for i, c in enumerate(sequence) if c[3] > 0]
+        if merged:
+            si = merged[0]
+            r = sequence[si][3]
+            s0 = sum(ln for _, ln, _ in cur[:si])
+            tcur = cur[si][1]
+            if tome_indices is not None:
+                unm, src, dst = tome_indices
+            else:  # canonical C matching on this restatement's own key metric (sum over heads)
+                from . import tome as T
+                km = k.detach().float()[:, s0:s0 + tcur].contiguous().numpy()
+                unm, src, dst, _ = T.canon_match(km, r)
+                unm, src, dst = (torch.from_numpy(a) for a in (unm, src, dst))
+            used = (unm, src, dst)
+            xs, size = tome_merge_wavg(x[:, s0:s0 + tcur], size, unm, src, dst, r)
+            x = torch.cat([x[:, :s0], xs, x[:, s0 + tcur:]], dim=1)
+        L2 = x.shape[1]
+        tr("x1", x)
+        z = tr("y1", rbg(seq_layernorm(x, p[f"{blk}/LayerNorm_1/scale"], p[f"{blk}/LayerNorm_1/bias"],
+                                       cfg.layer_norm_eps)))
+        h = torch.relu(gb(dense(p, f"{blk}/MLPBlock_0/Dense_0", z)))
+        if train:
+            keep = torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 2, B * L2, cfg.mlp_dim,
+                                                      sample_offset * L2, kp)).view(B, L2, -1)
+            h = torch.where(keep, h / kp, torch.zeros_like(h))
+        h = tr("h", rb(h))
+        z = gb(dense(p, f"{blk}/MLPBlock_0/Dense_1", h))
+        if train:
+            keep = torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 3, B * L2, D,
+                                                      sample_offset * L2, kp)).view(B, L2, D)
+            z = torch.where(keep, z / kp, torch.zeros_like(z))
+        return self._q(x + z), size, used
+
+    def readout_rows(self, sequence):
+        """Readout positions in the final (compressed) layout (octo.py:122-124)."""
+        nb = self.cfg.num_blocks
         idx, cur_pos = [], 0
-        for kind, n, _ in final:
+        for kind, n, _, c in sequence:
+            n = n - nb * c
             if kind == "readout":
                 idx.extend(range(cur_pos, cur_pos + n))
             cur_pos += n
-        e = x[:, idx].mean(dim=1)
+        return idx
+
+    def head_loss(self, x, sequence, actions, t, eps):
+        """Readout mean (diffusion.py:102) -> denoise_loss (diffusion.py:110-143)."""
+        cfg, p, dt = self.cfg, self.p, self.dtype
+        rb, gb, rbg = self.rb, self.gb, self.rbg
+        B = x.shape[0]
+        e = rbg(x[:, self.readout_rows(sequence)].mean(dim=1))
         hp = "diffusion_action_head/OctoDenoise_0"
         betas = cosine_beta_schedule(cfg.diffusion_steps)
         alphas = 1 - betas
@@ -328,16 +486,46 @@ class OctoRef:
         tt = torch.as_tensor(t).long().view(B, 1)
         eps_t = torch.as_tensor(eps).to(dt)
         ah = ahat[tt]
-        noisy = torch.sqrt(ah) * torch.as_tensor(actions).to(dt) + torch.sqrt(1 - ah) * eps_t
+        noisy = rb(torch.sqrt(ah) * torch.as_tensor(actions).to(dt) + torch.sqrt(1 - ah) * eps_t)
         w = p[f"{hp}/FourierFeatures_0/fourier_kernel"]                        # (F, 1)
         hh = 2 * math.pi * tt.to(dt) @ w.t()
-        feats = torch.cat([torch.cos(hh), torch.sin(hh)], dim=-1)
-        temb = dense(p, f"{hp}/FourierFeatures_0/MLPBlock_0/Dense_1",
-                     torch.relu(dense(p, f"{hp}/FourierFeatures_0/MLPBlock_0/Dense_0", feats)))
-        cat = torch.cat([noisy, temb, e], dim=-1)
-        pred = dense(p, f"{hp}/MLPBlock_0/Dense_1", torch.relu(dense(p, f"{hp}/MLPBlock_0/Dense_0", cat)))
+        feats = rbg(torch.cat([torch.cos(hh), torch.sin(hh)], dim=-1))
+        ht = rb(torch.relu(gb(dense(p, f"{hp}/FourierFeatures_0/MLPBlock_0/Dense_0", feats))))
+        temb = dense(p, f"{hp}/FourierFeatures_0/MLPBlock_0/Dense_1", ht)
+        cat = rbg(torch.cat([noisy, temb, e], dim=-1))
+        hd = rb(torch.relu(gb(dense(p, f"{hp}/MLPBlock_0/Dense_0", cat))))
+        pred = gb(dense(p, f"{hp}/MLPBlock_0/Dense_1", hd))
         loss = (0.5 * (pred - eps_t) ** 2).sum(-1).mean()
-        return loss, dict(pred=pred, e=e, x_final=x)
+        return loss, dict(pred=pred, e=e)
+
+    # ---------------------------------------------------------------------- whole step
+    def forward_loss(self, text_ids, images, actions, *, seed: int, step: int, positions,
+                     t, eps, tome_indices: Optional[List] = None, sequence=None,
+                     sample_offset: int = 0, train: bool = True, record: Optional[list] = None,
+                     trace: Optional[dict] = None):
+        """octo.py:91-126,139-145. Returns (loss, extras). sequence: list of (kind, n, timestep,
+        compressed_per_layer). record (list): receives per block the block input x
+        (retain_grad); extras["tome"] lists the ToMe index triples used. trace (dict): receives
+        detached intermediates by name (b{layer}/{x,y0,qkv,o,x1,y1,h}, txt, img)."""
+        images = torch.as_tensor(images)
+        B = images.shape[0]
+        img = self.stem(images, positions, trace)
+        txt = self.text(text_ids, trace)
+        x = self.assemble(img, txt, sequence, B)
+        size = None
+        used_tome = []
+        for layer in range(self.cfg.num_blocks):
+            if record is not None:
+                x.retain_grad()
+                record.append(x)
+            x, size, used = self.block(x, layer, sequence, size, seed=seed, step=step,
+                                       sample_offset=sample_offset, train=train,
+                                       tome_indices=None if tome_indices is None else tome_indices[layer],
+                                       trace=trace)
+            if used is not None:
+                used_tome.append(used)
+        loss, ex = self.head_loss(x, sequence, actions, t, eps)
+        return loss, dict(pred=ex["pred"], e=ex["e"], x_final=x, tome=used_tome)
 
 
 def sequence_spec(token_sequence_str: str, compression_str: Optional[str]):

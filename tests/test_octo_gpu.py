@@ -1,52 +1,109 @@
-"""GPU end-to-end parity: the HIP training step (forward loss + every parameter gradient) vs the
-fp32 CPU oracle (oracle/octo_ref.py) on identical inputs, identical dropout streams and the HIP
-run's own position tokens, diffusion (t, eps) and ToMe indices injected into the oracle.
+"""GPU end-to-end parity of the OCTO training step against the CPU restatement
+(oracle/octo_ref.py, bf16 storage points emulated; harness in oracle/parity.py).
 
-The oracle computes with the bf16-rounded Dense/attention kernels the HIP path actually multiplies
-(its bf16 shadow), fp32 everywhere else. Remaining differences come from bf16 activations
-(LayerNorm outputs, q/k/v, attention probabilities, MLP hidden, stem GroupNorm output, im2col
-pixels) and from relu gates that flip under the resulting forward perturbation. The end-to-end bar
-is set from the measured noise floor of that comparison (tools/parity_sweep.py, 12 runs over
-seeds x ToMe on/off x dropout on/off, profiles/r01_parity_sweep.txt: loss within 2.7 %, global
-gradient cosine >= 0.988, per-tensor >= 0.970 — the same with fp32 or bf16 LayerNorm input
-gradients), with margin, and is checked on two seeds:
-  loss: relative difference <= 4e-2
-  gradients: cosine similarity >= 0.96 per parameter tensor, >= 0.985 on the concatenation
-The per-op GPU tests (GEMM, attention, LayerNorm, ToMe, stem, sampler) carry the tight bars.
+Two kinds of comparison, because this model amplifies any bf16-level perturbation with depth
+(tools/parity_sweep.py, profiles/r02_parity_depth_sweep.txt: the oracle alone, bf16-emulating vs
+float64, with no HIP involved, drifts to the same ~0.8 gradient cosine at 12 blocks as the HIP
+run does — the floor is the network's sensitivity, not a kernel):
+
+* block-local at FULL depth (12 blocks, 12-layer T5, B = 2, both OCTO-small configs, every
+  layer's ToMe indices checked in situ bit-exact): each block gets the HIP block input and the
+  HIP gradient at its output, the head the HIP final sequence, the stem/assembly the HIP
+  gradient of the assembled sequence. Bar = SURVEY §8c: every parameter gradient cosine >= 0.999
+  with norm ratio in [0.98, 1.02], loss within 1e-3, block outputs within 5e-3 (relative L2),
+  input gradients cosine >= 0.999. Measured: min cosine 0.99936, ratios 0.997-1.003.
+* free-running (the whole step end to end, in-situ ToMe checks on every layer), octo-tiny at 2
+  blocks and both OCTO-small configs at 2 blocks and at full depth, against a floor measured in
+  the same test: the oracle's own bf16-emulating run vs its float64 run (CPU only). HIP may
+  deviate from the emulating oracle at most twice as much as that (plus 1e-3 / 2e-3 slack) in
+  loss, global gradient cosine and worst per-tensor cosine — i.e. it behaves like an honest
+  bf16 implementation of the same arithmetic (oracle/parity.py check_against_floor).
 """
+import numpy as np
 import pytest
+import torch
 
-from oracle.parity import check as _check, run_parity
+from oracle import parity as P
 
 pytestmark = pytest.mark.gpu
 
 
-def test_octo_tiny_parity(dev):
-    from multi_modal_transformers_tokenmerge_amd.models.octo.config import get_config
-    cfg = get_config("octo-tiny", num_blocks=2)
-    for seed in (0, 1):
-        _check(run_parity(cfg, 3, seed=seed))
-
-
-def test_octo_small_tome_parity(dev):
+def _cfg(name, **kw):
     from multi_modal_transformers_tokenmerge_amd.models.octo.config import get_config
     from multi_modal_transformers_tokenmerge_amd.tokenizers.text.t5_base import T5Config
-    cfg = get_config("octo-small-tome16", num_blocks=3, t5=T5Config(num_layers=2))
-    for seed in (0, 1):
-        _check(run_parity(cfg, 2, seed=seed))
+    t5 = kw.pop("t5_layers", None)
+    if t5 is not None:
+        kw["t5"] = T5Config(num_layers=t5)
+    return get_config(name, **kw)
+
+
+@pytest.mark.parametrize("name", ["octo-small-tome16", "octo-small"])
+def test_blockwise_full_depth(dev, name):
+    cfg = _cfg(name)
+    assert cfg.num_blocks == 12 and cfg.t5.num_layers == 12
+    res = P.hip_blockwise(cfg, 2, seed=0)
+    assert res["tome_layers_checked"] == (12 if cfg.tome_r else 0)
+    out = P.oracle_blockwise(cfg, res)
+    P.check_blockwise(out)
+
+
+def test_t5_layerwise_full_depth(dev):
+    """Each of the 12 frozen T5 layers, fed the HIP layer input, reproduces the HIP layer output
+    within 3e-3 relative L2 (the bf16 residual stream rounds once per sub-layer; measured
+    <= 1.6e-3), and the final RMS norm likewise."""
+    from multi_modal_transformers_tokenmerge_amd.tokenizers.text.t5_base import T5Config, T5Tokenizer
+    from oracle.octo_ref import t5_layer, t5_position_bias, t5_rms
+    c = T5Config()
+    t5 = T5Tokenizer(c).materialize(dev, 1)
+    B, T = 2, 32
+    ids = torch.from_numpy(np.random.default_rng(0).integers(0, c.vocab_size, (B, T), dtype=np.int32))
+    outs = []
+    final = t5(ids.to(dev), layer_outputs=outs).float().cpu()
+    tp = {p.name: p.bf16.float().cpu() for p in t5.store.params}
+    x = tp["T5Tokenizer_0/shared/embedding"][ids.long()]
+    bias = t5_position_bias(tp, T)
+    for i in range(c.num_layers):
+        y = t5_layer(tp, x, i, bias, c.num_heads, c.d_kv, c.layer_norm_epsilon, emulate_bf16=True)
+        want = outs[i].float().cpu()
+        rel = float((y - want).norm() / want.norm())
+        assert rel <= 3e-3, (i, rel)
+        x = want
+    y = t5_rms(x, tp["T5Tokenizer_0/final_layer_norm"], c.layer_norm_epsilon, True)
+    assert float((y - final).norm() / final.norm()) <= 3e-3
+
+
+E2E = [("octo-tiny", dict(num_blocks=2), 3, 0), ("octo-tiny", dict(num_blocks=2), 3, 1),
+       ("octo-small-tome16", dict(num_blocks=2, t5_layers=2), 2, 0),
+       ("octo-small-tome16", {}, 2, 0), ("octo-small", {}, 2, 0)]
+
+
+@pytest.mark.parametrize("name,kw,B,seed", E2E, ids=["tiny-d2-s0", "tiny-d2-s1", "small16-d2",
+                                                     "small16-full", "small-full"])
+def test_e2e_free_running(dev, name, kw, B, seed):
+    cfg = _cfg(name, **kw)
+    out = P.run_parity(cfg, B, seed=seed, floor=True)
+    assert out["tome_layers_checked"] == (cfg.num_blocks if cfg.tome_r else 0)
+    P.check_against_floor(out)
+
+
+def test_blockwise_base_2cam(dev):
+    """configs[3] geometry (D 768, 12 heads, two 256-token images per step, 2-step history,
+    L = 1064) at reduced depth (2 blocks, 2 T5 layers), B = 1, block-local bar."""
+    cfg = _cfg("octo-base-2cam", num_blocks=2, t5_layers=2)
+    res = P.hip_blockwise(cfg, 1, seed=0)
+    assert res["xs"][0].shape[1] == 1064
+    P.check_blockwise(P.oracle_blockwise(cfg, res))
 
 
 def test_staged_backward_matches_backward(dev):
     """The block-range stages used to overlap the gradient all-reduce (bench.py, N > 1) write
     the gradients of the one-piece backward (up to the order of the fp32 atomics some bias and
     embedding gradients use), and each stage's region is final after it."""
-    import torch
     from multi_modal_transformers_tokenmerge_amd.models.octo.config import get_config
     from multi_modal_transformers_tokenmerge_amd.models.octo.octo import Octo, create_octo_train_state
-    from oracle.parity import _inputs
     model = Octo(get_config("octo-tiny", num_blocks=4), dev, seed=0)
     state = create_octo_train_state(model, seed=5)
-    images, text, actions = _inputs(model, 3)
+    images, text, actions = P._inputs(model, 3)
     img, act = torch.from_numpy(images).to(dev), torch.from_numpy(actions).to(dev)
     model.store.zero_grad()
     _, st = model.compute_diffusion_denoise_loss(None, img, act, True, state.rng, 0)
