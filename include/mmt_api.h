@@ -40,6 +40,13 @@ enum {
 const char* mmt_last_error(void);
 int mmt_version(void);
 
+/* Bytes of caller-provided device workspace an entry point needs (the library
+ * allocates nothing; scratch comes from the caller). op / dims:
+ *   MMT_WS_TOME_MATCH  {n, t, c}  (mmt_tome_match)
+ * Returns the byte count, or a negative MMT_ERR_* code. */
+enum { MMT_WS_TOME_MATCH = 1 };
+int64_t mmt_workspace_size(int op, const int64_t* dims, int ndims);
+
 /* ------------------------------------------------------------------ ToMe
  * mmt_tome_match replaces tokenizers/token_compression.py:54-112 (bipartite_soft_matching)
  * for an r that the caller has already clamped to min(r, (t - protected) // 2) > 0
@@ -52,11 +59,13 @@ int mmt_version(void);
  * where ta = ceil(t/2) (indices into the a = x[::2] / b = x[1::2] halves, exactly as the
  * reference's edge_idx / node_idx). node_max[n][ta] (fp32) is optional (may be NULL).
  * Arithmetic is canonical (see DESIGN.md "ToMe canonical arithmetic") so indices are bit-exact
- * with oracle/tome_ref.c.
+ * with oracle/tome_ref.c. t <= 2048, c <= 512. workspace: >= mmt_workspace_size(
+ * MMT_WS_TOME_MATCH, {n, t, c}) bytes, 16-B aligned (normalised metric halves, node_max/idx).
  */
 int mmt_tome_match(const void* metric, int dtype, int n, int t, int heads, int c, int64_t s_n,
                    int64_t s_t, int64_t s_h, int r, int flags, int32_t* unm_idx, int32_t* src_idx,
-                   int32_t* dst_idx, float* node_max, mmt_stream_t stream);
+                   int32_t* dst_idx, float* node_max, void* workspace, int64_t ws_bytes,
+                   mmt_stream_t stream);
 
 /* mmt_tome_merge_wavg_fwd replaces token_compression.py:114-129 (merge_wavg) applied with the
  * merge closure of :90-109 (mode "sum"), fused with the surrounding sequence copy:

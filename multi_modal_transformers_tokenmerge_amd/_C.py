@@ -27,7 +27,8 @@ class Epilogue(ctypes.Structure):
 SIGNATURES: dict[str, list] = {
     "mmt_version": [],
     "mmt_tome_set_match_path": [I],
-    "mmt_tome_match": [P, I, I, I, I, I, L, L, L, I, I, P, P, P, P, P],
+    "mmt_workspace_size": [I, P, I],
+    "mmt_tome_match": [P, I, I, I, I, I, L, L, L, I, I, P, P, P, P, P, L, P],
     "mmt_tome_merge_wavg_fwd": [P, I, I, I, I, L, L, I, I, I, I, P, P, P, P, P, L, L, P, P, P],
     "mmt_tome_merge_wavg_bwd": [P, I, I, I, I, L, L, I, I, I, P, P, P, P, L, L, P],
     "mmt_topk_gather": [P, I, I, I, I, L, L, P, L, I, P, P, P, P, L, L, P, P],
@@ -66,6 +67,7 @@ SIGNATURES: dict[str, list] = {
     "mmt_step_advance": [P, P],
 }
 _VOID = {"mmt_tome_set_match_path", "mmt_gemm_set_variant"}
+_RESTYPE = {"mmt_workspace_size": L}      # returns a byte count (negative: error)
 
 
 class MMTError(RuntimeError):
@@ -85,7 +87,7 @@ def lib():
         for name, args in SIGNATURES.items():
             fn = getattr(h, name)
             fn.argtypes = args
-            fn.restype = None if name in _VOID else I
+            fn.restype = None if name in _VOID else _RESTYPE.get(name, I)
         _lib = h
         import os
         if os.environ.get("MMT_GEMM_VARIANT"):  # benchmarking knob (include/mmt_api.h)
@@ -97,6 +99,10 @@ def call(name: str, *args) -> int:
     rc = getattr(lib(), name)(*args)
     if name in _VOID:
         return 0
+    if name in _RESTYPE:
+        if rc < 0:
+            raise MMTError(f"{name} failed ({rc}): {lib().mmt_last_error().decode(errors='replace')}")
+        return rc
     if rc != 0:
         msg = lib().mmt_last_error().decode(errors="replace")
         raise MMTError(f"{name} failed ({rc}): {msg}")
@@ -105,6 +111,14 @@ def call(name: str, *args) -> int:
 
 def exported_symbols() -> list[str]:
     return ["mmt_last_error", *SIGNATURES.keys()]
+
+
+WS_TOME_MATCH = 1  # mmt_workspace_size op codes (include/mmt_api.h)
+
+
+def workspace_size(op: int, *dims: int) -> int:
+    arr = (ctypes.c_int64 * len(dims))(*dims)
+    return call("mmt_workspace_size", op, arr, len(dims))
 
 
 def ptr(t) -> int | None:

@@ -57,8 +57,9 @@ def tome_match(metric: torch.Tensor, r: int, flags: int = 0, return_node_max: bo
     src = torch.empty((n, r), dtype=torch.int32, device=dev)
     dst = torch.empty((n, r), dtype=torch.int32, device=dev)
     nmax = torch.empty((n, ta), dtype=torch.float32, device=dev) if return_node_max else None
+    ws = torch.empty(_C.workspace_size(_C.WS_TOME_MATCH, n, t, c), dtype=torch.uint8, device=dev)
     _C.call("mmt_tome_match", ptr(metric), _dtype_code(metric), n, t, heads, c, s_n, s_t, s_h, r,
-            flags, ptr(unm), ptr(src), ptr(dst), ptr(nmax), _C.stream_ptr())
+            flags, ptr(unm), ptr(src), ptr(dst), ptr(nmax), ptr(ws), ws.numel(), _C.stream_ptr())
     return (unm, src, dst, nmax) if return_node_max else (unm, src, dst)
 
 

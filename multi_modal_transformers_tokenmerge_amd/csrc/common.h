@@ -17,6 +17,9 @@ namespace mmt {
 // ---------------------------------------------------------------- errors
 void set_error(const char* fmt, ...);
 
+// workspace sizes (bytes) behind mmt_workspace_size
+int64_t tome_match_workspace(int64_t n, int64_t t, int64_t c);
+
 #define MMT_CHECK_ARG(cond, ...)              \
   do {                                        \
     if (!(cond)) {                            \

@@ -15,3 +15,17 @@ void set_error(const char* fmt, ...) {
 
 extern "C" const char* mmt_last_error(void) { return mmt::g_err; }
 extern "C" int mmt_version(void) { return 1; }
+
+extern "C" int64_t mmt_workspace_size(int op, const int64_t* dims, int ndims) {
+  switch (op) {
+    case MMT_WS_TOME_MATCH:
+      if (!dims || ndims != 3 || dims[0] <= 0 || dims[1] < 2 || dims[2] <= 0) {
+        mmt::set_error("mmt_workspace_size(TOME_MATCH): dims must be {n, t, c}");
+        return MMT_ERR_INVALID;
+      }
+      return mmt::tome_match_workspace(dims[0], dims[1], dims[2]);
+    default:
+      mmt::set_error("mmt_workspace_size: unknown op %d", op);
+      return MMT_ERR_INVALID;
+  }
+}

@@ -33,12 +33,6 @@ __device__ __forceinline__ uint32_t sort_key(float v) {
   return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }
 
-struct MatchSmem {
-  int ta, tb, ta_pad, tb_pad, cs;
-};
-
-constexpr int MATCH_NT = 512;  // 8 waves per batch row
-
 __device__ __forceinline__ void ld8f(const bf16_t* p, float* f) {
   const uint4 u = *reinterpret_cast<const uint4*>(p);
   const uint32_t w[4] = {u.x, u.y, u.z, u.w};
@@ -53,196 +47,230 @@ __device__ __forceinline__ void ld8f(const float* p, float* f) {
   f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
 }
 
-// One workgroup (8 waves) per batch row. LDS: a^ [ta_pad][c+1], b^ [tb_pad][c+1] fp32, per-a-row
-// node arrays and per-(b tile, a row) argmax partials [PJ][ta_pad].
-template <typename T, bool MFMA>
-__global__ __launch_bounds__(MATCH_NT) void tome_match_kernel(const T* __restrict__ metric, int t,
-                                                              int heads, int c, int64_t s_n,
-                                                              int64_t s_t, int64_t s_h, int r,
-                                                              int flags, int vec,
-                                                              int32_t* __restrict__ unm_idx,
-                                                              int32_t* __restrict__ src_idx,
-                                                              int32_t* __restrict__ dst_idx,
-                                                              float* __restrict__ node_max_out) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int n = blockIdx.x;
-  const int ta = (t + 1) / 2, tb = t / 2;
-  const int ta_pad = (ta + 31) & ~31, tb_pad = (tb + 31) & ~31;
-  const int n_it = ta_pad / 32, n_jt = tb_pad / 32;
-  const int PJ = n_jt > 4 ? n_jt : 4;
-  const int cs = c + 1;
-  float* A = smem;                    // normalised even tokens (the reference's a = m[::2])
-  float* Bm = A + ta_pad * cs;        // normalised odd tokens  (b = m[1::2])
-  float* nmax = Bm + tb_pad * cs;     // node_max [ta_pad]
-  int* nidx = (int*)(nmax + ta_pad);  // node_idx [ta_pad]
-  int* edge = nidx + ta_pad;          // edge_idx [ta_pad]
-  float* pbest = (float*)(edge + ta_pad);  // argmax partials [PJ][ta_pad]
-  int* pidx = (int*)(pbest + PJ * ta_pad);
+// The matching runs as three launches (all on the caller's stream, workspace from the caller):
+//   norm  : m = sum_h metric (fp32, h ascending), m / ||m||_2 with ||m|| = sqrt of a sequential
+//           fmaf chain over c (no eps, token_compression.py:72) -> A^ [n][ta][c], B^ [n][tb][c]
+//           (the reference's a = m[::2], b = m[1::2], :73), every token row in parallel;
+//   score : S = A^ B^T as k-ordered fmaf chains (:75), class/distill -inf (:77-80), first-index
+//           argmax per a row (:82-83) -> node_max / node_idx [n][ta]; one workgroup per
+//           (32 a rows, sample), the b rows streamed through LDS 4 tiles at a time;
+//   rank  : edge_idx = argsort(node_max)[::-1] (:84) as a rank count, src/unm/dst (:86-88).
+// Workspace: n*t*c fp32 (A^, B^) + n*ta (node_max fp32) + n*ta (node_idx int32).
+constexpr int NORM_NT = 256;
+constexpr int SCORE_NT = 256;
+constexpr int RANK_NT = 512;
 
-  const T* base = metric + (int64_t)n * s_n;
+// Vector path: LPR lanes per token row, lane q of a row owns c-chunk q (8 elements). The norm's
+// fmaf chain walks the chunks in order: chunk q continues from the partial sum of chunk q-1,
+// passed along the row's lanes by a shuffle.
+template <typename T, int LPR>
+__global__ __launch_bounds__(NORM_NT) void tome_norm_vec_kernel(
+    const T* __restrict__ metric, int n, int t, int heads, int c, int64_t s_n, int64_t s_t,
+    int64_t s_h, float* __restrict__ An, float* __restrict__ Bn) {
+  const int lane = threadIdx.x & 63;
+  const int lr = lane % LPR, rbase = lane - lr;
+  const int64_t row = ((int64_t)blockIdx.x * NORM_NT + threadIdx.x) / LPR;  // global token row
+  const bool live = row < (int64_t)n * t;
+  const int b = live ? (int)(row / t) : 0, tok = live ? (int)(row - (int64_t)b * t) : 0;
+  const int nch = c / 8;
+  const bool mine = live && lr < nch;
+  float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (mine) {
+    const T* p = metric + (int64_t)b * s_n + (int64_t)tok * s_t + lr * 8;
+    for (int h = 0; h < heads; ++h) {
+      float f[8];
+      ld8f(p + (int64_t)h * s_h, f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) m[q] = m[q] + f[q];
+    }
+  }
+  float ss = 0.f;
+  for (int j = 0; j < nch; ++j) {
+    if (lr == j) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ss = __fmaf_rn(m[q], m[q], ss);
+    }
+    ss = __shfl(ss, rbase + j, 64);
+  }
+  if (!mine) return;
+  const float nrm = __fsqrt_rn(ss);
+  const int ta = (t + 1) / 2, tb = t / 2;
+  float* o = (tok & 1) ? Bn + ((int64_t)b * tb + (tok >> 1)) * c : An + ((int64_t)b * ta + (tok >> 1)) * c;
+  o += lr * 8;
+  float v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = __fdiv_rn(m[q], nrm);
+  *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+// Scalar path (any c, any strides): one thread per token row, two passes over its output row.
+template <typename T>
+__global__ __launch_bounds__(NORM_NT) void tome_norm_scalar_kernel(
+    const T* __restrict__ metric, int n, int t, int heads, int c, int64_t s_n, int64_t s_t,
+    int64_t s_h, float* __restrict__ An, float* __restrict__ Bn) {
+  const int64_t row = (int64_t)blockIdx.x * NORM_NT + threadIdx.x;
+  if (row >= (int64_t)n * t) return;
+  const int b = (int)(row / t), tok = (int)(row - (int64_t)b * t);
+  const int ta = (t + 1) / 2, tb = t / 2;
+  float* o = (tok & 1) ? Bn + ((int64_t)b * tb + (tok >> 1)) * c : An + ((int64_t)b * ta + (tok >> 1)) * c;
+  const T* p = metric + (int64_t)b * s_n + (int64_t)tok * s_t;
+  float ss = 0.f;
+  for (int k = 0; k < c; ++k) {
+    float acc = 0.f;
+    for (int h = 0; h < heads; ++h) acc = acc + ld_f32(p + (int64_t)h * s_h + k);
+    o[k] = acc;
+    ss = __fmaf_rn(acc, acc, ss);
+  }
+  const float nrm = __fsqrt_rn(ss);
+  for (int k = 0; k < c; ++k) o[k] = __fdiv_rn(o[k], nrm);
+}
+
+__device__ __forceinline__ void keep_best(float v, int j, float& best, int& bidx) {
+  if (j >= 0 && (bidx < 0 || argmax_better(v, j, best, bidx))) {
+    best = v;
+    bidx = j;
+  }
+}
+
+// Stage rows [r0, r0 + 32) of a normalised half (rows >= nrows zero) into LDS [32][c+1].
+__device__ __forceinline__ void stage_tile(const float* __restrict__ src, int r0, int nrows, int c,
+                                           float* __restrict__ dst, int tid, int nthr) {
+  const int cs = c + 1;
+  const int per = 32 * c;
+  for (int e = tid; e < per; e += nthr) {
+    const int rr = e / c, k = e - rr * c;
+    dst[rr * cs + k] = (r0 + rr < nrows) ? src[(int64_t)(r0 + rr) * c + k] : 0.f;
+  }
+}
+
+template <bool MFMA>
+__global__ __launch_bounds__(SCORE_NT) void tome_score_kernel(const float* __restrict__ An,
+                                                              const float* __restrict__ Bn, int t,
+                                                              int c, int flags, int nb_tiles,
+                                                              float* __restrict__ nmax,
+                                                              int32_t* __restrict__ nidx) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int it = blockIdx.x, b = blockIdx.y;
+  const int ta = (t + 1) / 2, tb = t / 2;
+  const int cs = c + 1;
+  const int n_jt = (tb + 31) / 32;
+  float* As = smem;                          // [32][cs]
+  float* Bs = As + 32 * cs;                  // [nb_tiles][32][cs]
+  float* pb = Bs + nb_tiles * 32 * cs;       // partials [8][32]
+  int* pi = (int*)(pb + 8 * 32);
+  const float* Ab = An + (int64_t)b * ta * c;
+  const float* Bb = Bn + (int64_t)b * tb * c;
   const bool cls = flags & MMT_TOME_CLASS_TOKEN;
   const bool dis = flags & MMT_TOME_DISTILL_TOKEN;
-  const int rows_total = ta_pad + tb_pad;
-
-  // Phase 1a: metric = sum over heads (fp32, h ascending). Pad rows = 0. Vector path: 8
-  // contiguous c per work item, 16-B loads per head.
-  for (int i = threadIdx.x; i < PJ * ta_pad; i += blockDim.x) pidx[i] = -1;
-  const int cw = vec ? 8 : 1;
-  const int cchunks = c / cw;
-  for (int e = threadIdx.x; e < rows_total * cchunks; e += blockDim.x) {
-    const int row = e / cchunks, k = (e - row * cchunks) * cw;
-    int tok;
-    float* dstp;
-    if (row < ta_pad) {
-      tok = (row < ta) ? 2 * row : -1;
-      dstp = A + row * cs + k;
-    } else {
-      const int j = row - ta_pad;
-      tok = (j < tb) ? 2 * j + 1 : -1;
-      dstp = Bm + j * cs + k;
-    }
-    if (vec) {
-      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (tok >= 0) {
-        const T* p = base + (int64_t)tok * s_t + k;
-        for (int h = 0; h < heads; ++h) {
-          float f[8];
-          ld8f(p + (int64_t)h * s_h, f);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  stage_tile(Ab, it * 32, ta, c, As, threadIdx.x, SCORE_NT);
+  float best = 0.f;
+  int bidx = -1;
+  for (int g = 0; g < n_jt; g += nb_tiles) {
+    __syncthreads();  // previous group's reads of Bs are done (and As is staged)
+    for (int w = 0; w < nb_tiles && g + w < n_jt; ++w)
+      stage_tile(Bb, (g + w) * 32, tb, c, Bs + w * 32 * cs, threadIdx.x, SCORE_NT);
+    __syncthreads();
+    if (MFMA) {
+      // S^T tile (32 b rows x 32 a cols) = b^ . a^T with v_mfma_f32_32x32x2_f32, whose result
+      // is a k-ordered fmaf chain (f32 in / f32 accumulate, one rounding per step): a row on the
+      // lane, b rows in the 16 accumulator registers, the argmax over j lane-local.
+      const int jt = g + wave;
+      if (wave < nb_tiles && jt < n_jt) {
+        const int i = it * 32 + (lane & 31);
+        const float* bp = As + (lane & 31) * cs + (lane >> 5);
+        const float* ap = Bs + wave * 32 * cs + (lane & 31) * cs + (lane >> 5);
+        floatx16 acc;
 #pragma unroll
-          for (int q = 0; q < 8; ++q) acc[q] = acc[q] + f[q];
+        for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+        for (int s = 0; s < c / 2; ++s)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[2 * s], bp[2 * s], acc, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int jj = jt * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+          if (jj >= tb) continue;
+          float v = acc[q];
+          if ((cls && i == 0) || (dis && jj == 0)) v = -INFINITY;
+          keep_best(v, jj, best, bidx);
         }
       }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) dstp[q] = acc[q];
     } else {
-      float acc = 0.f;
-      if (tok >= 0) {
-        const T* p = base + (int64_t)tok * s_t + k;
-        for (int h = 0; h < heads; ++h) acc = acc + ld_f32(p + (int64_t)h * s_h);
-      }
-      *dstp = acc;
-    }
-  }
-  __syncthreads();
-
-  // Phase 1b: m / ||m||_2 per row; ||m|| = sqrt of a sequential fmaf chain over c (no eps,
-  // token_compression.py:72).
-  for (int row = threadIdx.x; row < rows_total; row += blockDim.x) {
-    const bool is_a = row < ta_pad;
-    const int lr = is_a ? row : row - ta_pad;
-    if (lr >= (is_a ? ta : tb)) continue;
-    float* rp = (is_a ? A : Bm) + lr * cs;
-    float ss = 0.f;
-    for (int k = 0; k < c; ++k) ss = __fmaf_rn(rp[k], rp[k], ss);
-    const float nrm = __fsqrt_rn(ss);
-    for (int k = 0; k < c; ++k) rp[k] = __fdiv_rn(rp[k], nrm);
-  }
-  __syncthreads();
-
-  // Phase 2: scores = a^ b^T (fmaf chain over c ascending); per (b tile, a row) argmax partials.
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
-  if (MFMA) {
-    // S^T tile (32 b rows x 32 a cols) = b^ . a^T with v_mfma_f32_32x32x2_f32, whose result is a
-    // k-ordered fmaf chain (f32 in / f32 accumulate, one rounding per step). a row i is on the
-    // lane, b rows in the 16 accumulator registers: the argmax over j is lane-local. The
-    // (a tile, b tile) pairs are spread over the 8 waves.
-    for (int pr = wave; pr < n_it * n_jt; pr += nwaves) {
-      const int it = pr / n_jt, jt = pr - it * n_jt;
-      const int i = it * 32 + (lane & 31);
-      const float* bp = A + (it * 32 + (lane & 31)) * cs + (lane >> 5);
-      const float* ap = Bm + (jt * 32 + (lane & 31)) * cs + (lane >> 5);
-      floatx16 acc;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-      for (int s = 0; s < c / 2; ++s)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[2 * s], bp[2 * s], acc, 0, 0, 0);
-      float best = 0.f;
-      int bidx = -1;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int jj = jt * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
-        if (jj >= tb) continue;
-        float v = acc[q];
-        if ((cls && i == 0) || (dis && jj == 0)) v = -INFINITY;
-        if (bidx < 0 || argmax_better(v, jj, best, bidx)) {
-          best = v;
-          bidx = jj;
-        }
-      }
-      const float ov = __shfl_xor(best, 32, 64);
-      const int oi = __shfl_xor(bidx, 32, 64);
-      if (oi >= 0 && (bidx < 0 || argmax_better(ov, oi, best, bidx))) {
-        best = ov;
-        bidx = oi;
-      }
-      if (lane < 32 && i < ta) {
-        pbest[jt * ta_pad + i] = best;
-        pidx[jt * ta_pad + i] = bidx;
-      }
-    }
-  } else {
-    // VALU path: (a row, one of PJ slices of the b rows) per thread, sequential __fmaf_rn.
-    const int cwj = (tb + PJ - 1) / PJ;
-    for (int e = threadIdx.x; e < ta * PJ; e += blockDim.x) {
-      const int i = e / PJ, jc = e - i * PJ;
-      const float* ap = A + i * cs;
-      float best = 0.f;
-      int bidx = -1;
-      const int j1 = min(tb, (jc + 1) * cwj);
-      for (int j = jc * cwj; j < j1; ++j) {
-        const float* bq = Bm + j * cs;
+      // VALU: thread (a row tid & 31, slice tid >> 5 of 8) walks the group's b rows with stride 8.
+      const int ar = threadIdx.x & 31, sl = threadIdx.x >> 5;
+      const int i = it * 32 + ar;
+      const float* ap = As + ar * cs;
+      const int rows = min(nb_tiles * 32, tb - g * 32);
+      for (int jr = sl; jr < rows; jr += 8) {
+        const float* bq = Bs + jr * cs;
         float acc = 0.f;
         for (int k = 0; k < c; ++k) acc = __fmaf_rn(ap[k], bq[k], acc);
-        if ((cls && i == 0) || (dis && j == 0)) acc = -INFINITY;
-        if (bidx < 0 || argmax_better(acc, j, best, bidx)) {
-          best = acc;
-          bidx = j;
-        }
-      }
-      pbest[jc * ta_pad + i] = best;
-      pidx[jc * ta_pad + i] = bidx;
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < ta; i += blockDim.x) {  // combine the partials (order-free)
-    float best = 0.f;
-    int bidx = -1;
-    for (int jc = 0; jc < PJ; ++jc) {
-      const int oi = pidx[jc * ta_pad + i];
-      const float ov = pbest[jc * ta_pad + i];
-      if (oi >= 0 && (bidx < 0 || argmax_better(ov, oi, best, bidx))) {
-        best = ov;
-        bidx = oi;
+        const int jj = g * 32 + jr;
+        if ((cls && i == 0) || (dis && jj == 0)) acc = -INFINITY;
+        keep_best(acc, jj, best, bidx);
       }
     }
-    nmax[i] = best;
-    nidx[i] = bidx;
+  }
+  // combine (argmax_better is a total order with index tie-break: order-free)
+  if (MFMA) {
+    const float ov = __shfl_xor(best, 32, 64);
+    const int oi = __shfl_xor(bidx, 32, 64);
+    keep_best(ov, oi, best, bidx);
+    if (lane < 32) {
+      pb[wave * 32 + lane] = best;
+      pi[wave * 32 + lane] = bidx;
+    }
+  } else {
+    pb[(threadIdx.x >> 5) * 32 + (threadIdx.x & 31)] = best;
+    pi[(threadIdx.x >> 5) * 32 + (threadIdx.x & 31)] = bidx;
   }
   __syncthreads();
+  if (threadIdx.x < 32) {
+    const int nparts = MFMA ? SCORE_NT / 64 : SCORE_NT / 32;
+    float bb = 0.f;
+    int bi = -1;
+    for (int w = 0; w < nparts; ++w) keep_best(pb[w * 32 + threadIdx.x], pi[w * 32 + threadIdx.x], bb, bi);
+    const int i = it * 32 + threadIdx.x;
+    if (i < ta) {
+      nmax[(int64_t)b * ta + i] = bb;
+      nidx[(int64_t)b * ta + i] = bi;
+    }
+  }
+}
 
-  // Phase 3: edge_idx = argsort(node_max)[::-1] (stable ascending sort, reversed) as a rank
-  // count: descending total-order key, ties -> higher index first (token_compression.py:84).
-  for (int i = threadIdx.x; i < ta; i += blockDim.x) {
-    const uint32_t kv = sort_key(nmax[i]);
+__global__ __launch_bounds__(RANK_NT) void tome_rank_kernel(const float* __restrict__ nmax,
+                                                            const int32_t* __restrict__ nidx,
+                                                            int ta, int r,
+                                                            int32_t* __restrict__ unm_idx,
+                                                            int32_t* __restrict__ src_idx,
+                                                            int32_t* __restrict__ dst_idx,
+                                                            float* __restrict__ node_max_out) {
+  __shared__ uint32_t keys[1024];
+  __shared__ int32_t edge[1024];
+  const int n = blockIdx.x;
+  const float* nm = nmax + (int64_t)n * ta;
+  for (int i = threadIdx.x; i < ta; i += RANK_NT) keys[i] = sort_key(nm[i]);
+  __syncthreads();
+  // descending total-order key, ties -> higher index first (stable ascending sort, reversed)
+  for (int i = threadIdx.x; i < ta; i += RANK_NT) {
+    const uint32_t kv = keys[i];
     int rank = 0;
     for (int j = 0; j < ta; ++j) {
-      const uint32_t kw = sort_key(nmax[j]);
+      const uint32_t kw = keys[j];
       rank += (kw > kv) || (kw == kv && j > i);
     }
     edge[rank] = i;
   }
   __syncthreads();
-
-  // Phase 4: src = edge[:r], unm = edge[r:], dst = node_idx[src] (token_compression.py:86-88).
-  for (int k = threadIdx.x; k < ta; k += blockDim.x) {
+  for (int k = threadIdx.x; k < ta; k += RANK_NT) {
     const int e = edge[k];
     if (k < r) {
       src_idx[(int64_t)n * r + k] = e;
-      dst_idx[(int64_t)n * r + k] = nidx[e];
+      dst_idx[(int64_t)n * r + k] = nidx[(int64_t)n * ta + e];
     } else {
       unm_idx[(int64_t)n * (ta - r) + (k - r)] = e;
     }
-    if (node_max_out) node_max_out[(int64_t)n * ta + k] = nmax[k];
+    if (node_max_out) node_max_out[(int64_t)n * ta + k] = nm[k];
   }
 }
 
@@ -506,54 +534,108 @@ __global__ __launch_bounds__(256) void tome_merge_bwd_kernel(
   }
 }
 
-size_t match_smem_bytes(int t, int c) {
-  const int ta = (t + 1) / 2, tb = t / 2;
-  const int ta_pad = (ta + 31) & ~31, tb_pad = (tb + 31) & ~31;
-  const int PJ = tb_pad / 32 > 4 ? tb_pad / 32 : 4;
-  return sizeof(float) * ((size_t)(ta_pad + tb_pad) * (c + 1) + ta_pad * 3 + 2 * PJ * ta_pad);
-}
-
 bool g_match_use_mfma = true;
 
+int pow2_at_least(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
 }  // namespace
+
+namespace mmt {
+int64_t tome_match_workspace(int64_t n, int64_t t, int64_t c) {
+  const int64_t ta = (t + 1) / 2;
+  auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
+  return al(n * ta * c * 4) + al(n * (t / 2) * c * 4) + al(n * ta * 4) + al(n * ta * 4);
+}
+}  // namespace mmt
 
 extern "C" void mmt_tome_set_match_path(int use_mfma) { g_match_use_mfma = use_mfma != 0; }
 
 extern "C" int mmt_tome_match(const void* metric, int dtype, int n, int t, int heads, int c,
                               int64_t s_n, int64_t s_t, int64_t s_h, int r, int flags,
                               int32_t* unm_idx, int32_t* src_idx, int32_t* dst_idx,
-                              float* node_max, mmt_stream_t stream) {
-  MMT_CHECK_ARG(metric && unm_idx && src_idx && dst_idx, "mmt_tome_match: null pointer");
+                              float* node_max, void* workspace, int64_t ws_bytes,
+                              mmt_stream_t stream) {
+  MMT_CHECK_ARG(metric && unm_idx && src_idx && dst_idx && workspace, "mmt_tome_match: null pointer");
   MMT_CHECK_ARG(n > 0 && t >= 2 && heads >= 1 && c >= 1, "mmt_tome_match: bad shape n=%d t=%d", n, t);
+  MMT_CHECK_ARG(t <= 2048 && c <= 512, "mmt_tome_match: t=%d c=%d beyond 2048 / 512", t, c);
   const int prot = ((flags & MMT_TOME_CLASS_TOKEN) ? 1 : 0) + ((flags & MMT_TOME_DISTILL_TOKEN) ? 1 : 0);
   MMT_CHECK_ARG(r > 0 && r <= (t - prot) / 2,
                 "mmt_tome_match: r=%d must be clamped to 1..(t-protected)//2=%d", r, (t - prot) / 2);
   MMT_CHECK_ARG(dtype == MMT_F32 || dtype == MMT_BF16, "mmt_tome_match: dtype %d", dtype);
-  const size_t smem = match_smem_bytes(t, c);
-  MMT_CHECK_ARG(smem <= 160 * 1024, "mmt_tome_match: t=%d c=%d needs %zu B of LDS (> 160 KiB)",
-                t, c, smem);
-  const bool mfma = g_match_use_mfma && (c % 2 == 0);
-  const int vw = dtype == MMT_BF16 ? 8 : 4;  // elements per 16 B
-  const int vec = (c % 8 == 0) && (s_n % vw == 0) && (s_t % vw == 0) && (s_h % vw == 0) &&
-                  ((uintptr_t)metric % 16 == 0);
+  const int64_t need = tome_match_workspace(n, t, c);
+  MMT_CHECK_ARG(ws_bytes >= need && (uintptr_t)workspace % 16 == 0,
+                "mmt_tome_match: workspace %lld B < %lld B (mmt_workspace_size) or not 16-B aligned",
+                (long long)ws_bytes, (long long)need);
+  const int ta = (t + 1) / 2, tb = t / 2;
+  auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
+  char* w = (char*)workspace;
+  float* An = (float*)w;
+  float* Bn = (float*)(w + al((int64_t)n * ta * c * 4));
+  float* nmax = (float*)((char*)Bn + al((int64_t)n * tb * c * 4));
+  int32_t* nidx = (int32_t*)((char*)nmax + al((int64_t)n * ta * 4));
   hipStream_t s = as_stream(stream);
-#define LAUNCH(T, M)                                                                         \
-  do {                                                                                       \
-    auto kfn = tome_match_kernel<T, M>;                                                      \
-    static const bool attr_set_ = (hipFuncSetAttribute((const void*)kfn,                    \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024), \
-                                   true);                                                    \
-    (void)attr_set_;                                                                         \
-    hipLaunchKernelGGL(kfn, dim3(n), dim3(MATCH_NT), smem, s, (const T*)metric, t, heads, c, s_n, \
-                       s_t, s_h, r, flags, vec, unm_idx, src_idx, dst_idx, node_max);       \
-  } while (0)
-  if (dtype == MMT_F32) {
-    if (mfma) LAUNCH(float, true); else LAUNCH(float, false);
-  } else {
-    if (mfma) LAUNCH(bf16_t, true); else LAUNCH(bf16_t, false);
+  // 1. per-token head sum + L2 normalisation
+  const int vw = dtype == MMT_BF16 ? 8 : 4;  // elements per 16 B
+  const bool vec = (c % 8 == 0) && (s_n % vw == 0) && (s_t % vw == 0) && (s_h % vw == 0) &&
+                   ((uintptr_t)metric % 16 == 0);
+  const int64_t rows = (int64_t)n * t;
+  if (vec) {
+    const int lpr = pow2_at_least(c / 8);
+#define NORMV(T, LPR)                                                                          \
+  hipLaunchKernelGGL((tome_norm_vec_kernel<T, LPR>), dim3((rows * LPR + NORM_NT - 1) / NORM_NT), \
+                     dim3(NORM_NT), 0, s, (const T*)metric, n, t, heads, c, s_n, s_t, s_h, An, Bn)
+#define NORMV_ALL(T)                                  \
+  switch (lpr) {                                      \
+    case 1: NORMV(T, 1); break;                       \
+    case 2: NORMV(T, 2); break;                       \
+    case 4: NORMV(T, 4); break;                       \
+    case 8: NORMV(T, 8); break;                       \
+    case 16: NORMV(T, 16); break;                     \
+    case 32: NORMV(T, 32); break;                     \
+    default: NORMV(T, 64); break;                     \
   }
-#undef LAUNCH
-  MMT_CHECK_LAUNCH("mmt_tome_match");
+    if (dtype == MMT_F32) { NORMV_ALL(float) } else { NORMV_ALL(bf16_t) }
+#undef NORMV_ALL
+#undef NORMV
+  } else {
+    const dim3 grid((rows + NORM_NT - 1) / NORM_NT);
+    if (dtype == MMT_F32)
+      hipLaunchKernelGGL(tome_norm_scalar_kernel<float>, grid, dim3(NORM_NT), 0, s,
+                         (const float*)metric, n, t, heads, c, s_n, s_t, s_h, An, Bn);
+    else
+      hipLaunchKernelGGL(tome_norm_scalar_kernel<bf16_t>, grid, dim3(NORM_NT), 0, s,
+                         (const bf16_t*)metric, n, t, heads, c, s_n, s_t, s_h, An, Bn);
+  }
+  MMT_CHECK_LAUNCH("mmt_tome_match(norm)");
+  // 2. scores + per-a-row argmax; as many 32-row b tiles per LDS group as fit (<= 4)
+  const int cs = c + 1;
+  const size_t tile = sizeof(float) * 32 * cs;
+  const size_t fixed = tile + sizeof(float) * 8 * 32 * 2;
+  int nbt = (int)((160 * 1024 - fixed) / tile);
+  nbt = nbt > 4 ? 4 : nbt;
+  MMT_CHECK_ARG(nbt >= 1, "mmt_tome_match: c=%d too large for the LDS tiles", c);
+  const size_t smem = fixed + nbt * tile;
+  const bool mfma = g_match_use_mfma && (c % 2 == 0);
+  const dim3 sgrid((ta + 31) / 32, n);
+#define SCORE(M)                                                                              \
+  do {                                                                                        \
+    static const bool attr_ = (hipFuncSetAttribute((const void*)tome_score_kernel<M>,        \
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024), true); \
+    (void)attr_;                                                                              \
+    hipLaunchKernelGGL(tome_score_kernel<M>, sgrid, dim3(SCORE_NT), smem, s, An, Bn, t, c,    \
+                       flags, nbt, nmax, nidx);                                               \
+  } while (0)
+  if (mfma) SCORE(true); else SCORE(false);
+#undef SCORE
+  MMT_CHECK_LAUNCH("mmt_tome_match(score)");
+  // 3. rank sort -> src / dst / unm
+  hipLaunchKernelGGL(tome_rank_kernel, dim3(n), dim3(RANK_NT), 0, s, nmax, nidx, ta, r, unm_idx,
+                     src_idx, dst_idx, node_max);
+  MMT_CHECK_LAUNCH("mmt_tome_match(rank)");
   return MMT_OK;
 }
 

@@ -3,6 +3,8 @@ import ctypes
 import re
 from pathlib import Path
 
+import pytest
+
 ROOT = Path(__file__).resolve().parents[1]
 
 
@@ -36,5 +38,17 @@ def test_version_and_error_without_gpu():
     from multi_modal_transformers_tokenmerge_amd import _C
     assert _C.lib().mmt_version() >= 1
     # argument validation happens before any HIP call: a bad shape returns an error, no abort
-    rc = _C.lib().mmt_tome_match(None, 0, 1, 8, 1, 4, 32, 4, 0, 2, 0, None, None, None, None, None)
+    rc = _C.lib().mmt_tome_match(None, 0, 1, 8, 1, 4, 32, 4, 0, 2, 0, None, None, None, None, None,
+                                 0, None)
     assert rc == -1 and b"null" in _C.lib().mmt_last_error()
+
+
+def test_workspace_size_without_gpu():
+    from multi_modal_transformers_tokenmerge_amd import _C
+    # normalised halves (n t c fp32) + node_max / node_idx (n ceil(t/2) each), 256-B aligned pieces
+    n, t, c = 16, 1024, 64
+    assert _C.workspace_size(_C.WS_TOME_MATCH, n, t, c) == 4 * n * t * c + 2 * 4 * n * 512
+    with pytest.raises(_C.MMTError):
+        _C.workspace_size(_C.WS_TOME_MATCH, 1, 8)
+    with pytest.raises(_C.MMTError):
+        _C.workspace_size(99, 1, 8, 4)

@@ -95,6 +95,17 @@ def test_blockwise_base_2cam(dev):
     P.check_blockwise(P.oracle_blockwise(cfg, res))
 
 
+def test_blockwise_base_hires_tome32(dev):
+    """configs[4] geometry (512 x 512 image = 1024 tokens, ToMe r = 32 per block, L0 = 1060,
+    D 768, 12 heads) at reduced depth (2 blocks, 2 T5 layers), B = 1, block-local bar, in-situ
+    ToMe check at t = 1024 and 992."""
+    cfg = _cfg("octo-base-hires-tome32", num_blocks=2, t5_layers=2)
+    res = P.hip_blockwise(cfg, 2, seed=0)
+    assert res["xs"][0].shape[1] == 1060 and res["xs"][1].shape[1] == 1028
+    assert res["tome_layers_checked"] == 2
+    P.check_blockwise(P.oracle_blockwise(cfg, res))
+
+
 def test_staged_backward_matches_backward(dev):
     """The block-range stages used to overlap the gradient all-reduce (bench.py, N > 1) write
     the gradients of the one-piece backward (up to the order of the fp32 atomics some bias and

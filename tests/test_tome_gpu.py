@@ -22,7 +22,11 @@ def match_path(request):
 
 CASES = [(4, 256, 64, 1, 16, 0), (3, 257, 64, 1, 16, 0), (2, 64, 32, 1, 8, 1), (2, 64, 32, 1, 8, 2),
          (2, 64, 32, 1, 8, 3), (2, 31, 6, 1, 7, 0), (5, 292, 64, 6, 16, 0), (2, 512, 64, 1, 32, 0),
-         (64, 256, 64, 6, 16, 0)]
+         (64, 256, 64, 6, 16, 0),
+         # hi-res config (configs[4]): t = 1024 image tokens, heads = 12, r = 32; the maximum t;
+         # Dh = 256 (ref-octo_base); a partial last a tile (t = 1000) and a tiny odd t
+         (4, 1024, 64, 12, 32, 0), (2, 2048, 64, 1, 64, 0), (2, 26, 256, 3, 5, 0),
+         (3, 1000, 64, 2, 100, 3), (2, 3, 8, 1, 1, 0)]
 
 
 @pytest.mark.parametrize("n,t,c,heads,r,flags", CASES)

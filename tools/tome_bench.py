@@ -48,9 +48,10 @@ def graph_time(fn, reps=20):
 
 def main():
     dev = torch.device("cuda")
-    L, s0, t, r, D, H, c = 292, 32, 256, 16, 384, 6, 64
     out = []
-    for n in (64, 256):
+    shapes = [(n, 292, 32, 256, 16, 384, 6, 64) for n in (64, 256)] + \
+        [(n, 1060, 32, 1024, 32, 768, 12, 64) for n in (16, 64)]      # OCTO-base hi-res block 0
+    for n, L, s0, t, r, D, H, c in shapes:
         g = torch.Generator(device="cpu").manual_seed(n)
         qkv = torch.randn((n, L, 3 * D), generator=g).bfloat16().to(dev)
         metric = qkv[:, s0:s0 + t, D:2 * D].view(n, t, H, c)     # strided K heads, in place
@@ -69,7 +70,7 @@ def main():
         for name, us, byts in (("match", us_m, b_match), ("merge_fwd", us_f, b_all),
                                ("merge_bwd", us_b, b_all)):
             gbs = byts / us / 1e3
-            out.append(dict(kernel=name, n=n, us=round(us, 2), bytes=byts, GBps=round(gbs, 1),
+            out.append(dict(kernel=name, n=n, t=t, us=round(us, 2), bytes=byts, GBps=round(gbs, 1),
                             hbm_frac=round(gbs / HBM_GBS, 3),
                             set_only_GBps=round((b_set if name != "match" else b_match) / us / 1e3, 1)))
             print(json.dumps(out[-1]), flush=True)
