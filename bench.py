@@ -11,8 +11,10 @@ Per-GPU batch 256 by default (measured 5.7k / 7.4k / 8.6k / 9.1k samples/s at B 
 One step = zero grads -> forward (frozen T5, image stem, 12 ToMe blocks, diffusion loss) ->
 backward -> [gradient all-reduce over RCCL] -> fused AdamW -> device step counter, on synthetic
 inputs resident in HBM (numpy default_rng(0) shapes of SURVEY §8d). The N=1 step is one HIP graph
-replay; with N>1 the forward/backward graph and the optimizer graph bracket an eager bucketed
-all-reduce. Timing: barrier + synchronize on both sides of exactly K steps, max over ranks.
+replay; with N>1 the backward runs as --overlap-stages block-range graphs, each stage's gradient
+region all-reduced asynchronously on the RCCL stream while the later stages compute, and the AdamW
+graph waits for them (distributed.DDPStep; --no-graph launches the same schedule eagerly).
+Timing: barrier + synchronize on both sides of exactly K steps, max over ranks.
 
 Printed on rank 0: ONE JSON line with the metric, a roofline object for the dominant kernel
 (MFMA GEMM of the MLP up-projection, measured here with HIP events on its own stream) and the
@@ -34,7 +36,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from multi_modal_transformers_tokenmerge_amd import _kernels as K  # noqa: E402
-from multi_modal_transformers_tokenmerge_amd.distributed import GradAllReducer, init_from_env  # noqa: E402
+from multi_modal_transformers_tokenmerge_amd.distributed import (  # noqa: E402
+    DDPStep, GradAllReducer, init_from_env)
 from multi_modal_transformers_tokenmerge_amd.models.octo.config import get_config  # noqa: E402
 from multi_modal_transformers_tokenmerge_amd.models.octo.octo import (  # noqa: E402
     Octo, create_octo_train_state)
@@ -217,92 +220,12 @@ def main():
     reducer = GradAllReducer(N) if di.enabled else None
     state = create_octo_train_state(model, seed=1234, allreduce=reducer, sample_offset=di.rank * B)
     txt, img, act = synthetic_inputs(model, B, di.rank, dev)
-    loss_buf = torch.zeros(1, device=dev)
-
-    def fwd_bwd():
-        model.store.zero_grad()
-        loss, st = model.compute_diffusion_denoise_loss(txt, img, act, True, state.rng,
-                                                        state.sample_offset)
-        model.backward(st)
-        loss_buf.copy_(loss)
-
-    # N > 1: the backward runs as S block-range stages; after each stage the gradient region it
-    # finalised is all-reduced asynchronously (RCCL stream) while the next stages compute, and
-    # AdamW waits for all of them
-    S = max(1, min(args.overlap_stages, cfg.num_blocks)) if reducer else 1
-    regions = model.grad_regions(S) if S > 1 else None
-    stage_state = {}
-
-    def fwd_stage(k):
-        if k == 0:
-            model.store.zero_grad()
-            loss, st = model.compute_diffusion_denoise_loss(txt, img, act, True, state.rng,
-                                                            state.sample_offset)
-            loss_buf.copy_(loss)
-            stage_state["st"] = st
-        model.backward_stage(stage_state["st"], k, S)
-
-    def opt():
-        state.apply_gradients()
-
     use_graph = not args.no_graph
-    graphs = []
-    if use_graph:
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(2):   # warm caches (T5 bias, constants) + allocator, outside capture
-                fwd_bwd()
-                if reducer:
-                    reducer(model.store.flat_grad)
-                opt()
-        torch.cuda.current_stream().wait_stream(side)
-        torch.cuda.synchronize()
-        pool = torch.cuda.graph_pool_handle()
-        if S > 1:
-            for k in range(S):   # one graph per backward stage (the first also holds the forward)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
-                    fwd_stage(k)
-                graphs.append(g)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
-                opt()
-            graphs.append(g)
-        else:
-            g1 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1, pool=pool):
-                fwd_bwd()
-                if not reducer:
-                    opt()
-            graphs.append(g1)
-            if reducer:
-                g2 = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g2, pool=pool):
-                    opt()
-                graphs.append(g2)
-
-    def step():
-        if use_graph and S > 1:
-            works = []
-            flat = model.store.flat_grad
-            for k in range(S):
-                graphs[k].replay()
-                lo, hi = regions[k]
-                works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
-            for w in works:
-                w.wait()
-            graphs[S].replay()
-        elif use_graph:
-            graphs[0].replay()
-            if reducer:
-                reducer(model.store.flat_grad)
-                graphs[1].replay()
-        else:
-            fwd_bwd()
-            if reducer:
-                reducer(model.store.flat_grad)
-            opt()
+    # N > 1: the backward runs as --overlap-stages block-range stages, each stage's gradient
+    # region all-reduced asynchronously while the later stages compute (distributed.DDPStep)
+    step = DDPStep(model, state, txt, img, act, reducer, stages=args.overlap_stages,
+                   use_graph=use_graph).build()
+    loss_buf = step.loss_buf
 
     for _ in range(args.warmup):
         step()

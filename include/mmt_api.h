@@ -279,6 +279,11 @@ int mmt_seq_assemble_bwd(int B, int L, int D, const int32_t* row_src, const void
                          void* dtext, int T, void* dimg, int NI, const int32_t* rtok,
                          const int32_t* ctok, const int32_t* img_rows, int Q, float* drow_emb,
                          float* dcol_emb, float* dreadout_pe, mmt_stream_t stream);
+/* AddPositionEmbedding standalone (tokenizers/readout/readout.py:18-33; also attention.py:71-85):
+ * out (B, L, D) fp32 = x + pe[None] (x may alias out). Backward: dx = dout; d(pe) = mmt_colsum of
+ * dout viewed as (B, L*D). The training step fuses this add into mmt_seq_assemble_fwd. */
+int mmt_add_position_embedding(const float* x, const float* pe, float* out, int B, int L, int D,
+                               mmt_stream_t stream);
 /* readout gather + mean (octo.py:122-124, diffusion.py:102): out[b] = mean_i x[b, rows[i]]. */
 int mmt_rows_mean_fwd(const void* x, int64_t xs_b, int64_t xs_t, int B, int D,
                       const int32_t* rows, int nrows, void* out, int64_t ld_out,
@@ -350,9 +355,10 @@ int mmt_embedding_gather(const int32_t* ids, int64_t n, int D, const void* table
  * Fused AdamW over the flat fp32 parameter buffer (the reference takes an optax tx from the
  * caller, octo.py:228,341; this is optax.adamw semantics), writing the bf16 shadow copy.
  * state = device {seed, step}: step+1 is the bias-correction count; mmt_step_advance
- * increments it (keys every random stream of the next step). */
+ * increments it (keys every random stream of the next step). Hyper-parameters in double (the
+ * caller's Python floats): 1 - beta and the bias corrections are formed in double. */
 int mmt_adamw(float* p, const float* g, float* m, float* v, void* shadow_bf16, int64_t n,
-              const int32_t* state, float lr, float b1, float b2, float eps, float wd,
+              const int32_t* state, double lr, double b1, double b2, double eps, double wd,
               float grad_scale, mmt_stream_t stream);
 int mmt_cast_f32_bf16(const float* a, void* b, int64_t n, mmt_stream_t stream);
 int mmt_step_advance(int32_t* state, mmt_stream_t stream);

@@ -14,6 +14,7 @@ _lib = None
 
 P, I, L, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
 U32, U64, Z = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
+D = ctypes.c_double
 
 class Epilogue(ctypes.Structure):
     """mmt_epilogue_t (include/mmt_api.h)."""
@@ -50,6 +51,7 @@ SIGNATURES: dict[str, list] = {
     "mmt_patch_positions": [P, U32, I, I, I, I, I, I, L, P, P, P],
     "mmt_seq_assemble_fwd": [I, I, I, P, P, I, P, I, P, P, P, P, P, P, P, P],
     "mmt_seq_assemble_bwd": [I, I, I, P, P, P, I, P, I, P, P, P, I, P, P, P, P],
+    "mmt_add_position_embedding": [P, P, P, I, I, I, P],
     "mmt_rows_mean_fwd": [P, L, L, I, I, P, I, P, L, P],
     "mmt_rows_mean_bwd": [P, L, I, I, I, P, I, P, P],
     "mmt_diffusion_prep": [P, I, I, I, L, P, P, P, I, P, P, P, P, P, L, P, P],
@@ -61,7 +63,7 @@ SIGNATURES: dict[str, list] = {
     "mmt_action_head": [I, P, L, I, I, P, P, I, F, F, P, P, P, P],
     "mmt_rmsnorm_fwd": [P, L, I, P, F, P, P],
     "mmt_embedding_gather": [P, L, I, P, I, P, P],
-    "mmt_adamw": [P, P, P, P, P, L, P, F, F, F, F, F, F, P],
+    "mmt_adamw": [P, P, P, P, P, L, P, D, D, D, D, D, F, P],
     "mmt_cast_f32_bf16": [P, P, L, P],
     "mmt_transpose_bf16_batched": [P, P, P, I, L, P],
     "mmt_step_advance": [P, P],

@@ -172,11 +172,14 @@ __device__ __forceinline__ bf16x8 pack_frag(const floatx16& x, int s) {
 // Transposed through LDS (`red`: the idle K/V staging buffers, >= waves x 32 ND x 33 floats; rows
 // padded to 33 so both phases are bank-conflict free), per-wave sums in `wsum` [waves][32 ND],
 // one global atomic per d per workgroup. Every thread of the workgroup must call it.
-static_assert(4 * KT * (64 + 8) * 2 >= 4 * 64 * 33 * 4, "colsum staging must fit the K/V buffers");
 template <int ND, int NTT>
 __device__ __forceinline__ void colsum_atomic(const floatx16 (&acc)[ND], float scale, float* red,
                                               float* wsum, float* gbias, int lane, int wave) {
   constexpr int ROWS = 32 * ND;
+  // `red` is the callers' smem[4 * KT * (32 ND + 8)] bf16 staging array: the (NTT / 64) waves'
+  // ROWS x 33 fp32 transposes must fit in it for every (Dh, workgroup size) instantiated
+  static_assert((NTT / 64) * ROWS * 33 * 4 <= 4 * KT * (32 * ND + 8) * 2,
+                "colsum staging exceeds the K/V LDS buffers for this Dh / workgroup size");
   float* rw = red + wave * (ROWS * 33);
   const int hh = lane >> 5, c = lane & 31;
 #pragma unroll

@@ -798,7 +798,8 @@ __device__ __forceinline__ void dma16(const void* base, int64_t bytes, void* lds
 template <int BN, int OUT, bool STASH, int NS>
 __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
-    int64_t ldb, void* __restrict__ Cv, int64_t ldc, int tiles_n, int n_tiles, Epi epi) {
+    int64_t ldb, void* __restrict__ Cv, int64_t ldc, int tiles_n, int n_tiles, int xcd_order,
+    Epi epi) {
   constexpr int W = BN / 2, NF = W / 16, Q = W / 4;
   constexpr int BSH = __builtin_ctz(Q);
   constexpr int A_BYTES = 256 * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
@@ -814,8 +815,22 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int nk = K / 64;
-  const int first = xcd_remap(blockIdx.x, gridDim.x), stride = gridDim.x;
-  const int n_mine = first < n_tiles ? (n_tiles - first + stride - 1) / stride : 0;
+  // Tile order. xcd_order: each XCD owns one contiguous eighth of the (row-panel major) tile
+  // range for the whole launch, its workgroups (dispatch is round-robin over the 8 XCDs, so
+  // blockIdx & 7 is the XCD) striding through it together: an A row panel is fetched into ONE
+  // XCD's L2 and consumed there by its tn column tiles. Otherwise: strided over the whole grid
+  // with the bijective remap (a panel can straddle two XCDs at every stride step).
+  int first, stride, limit = n_tiles;
+  if (xcd_order && (gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7, per = gridDim.x >> 3;
+    first = (int)((int64_t)n_tiles * xcd / 8) + (blockIdx.x >> 3);
+    limit = (int)((int64_t)n_tiles * (xcd + 1) / 8);
+    stride = per;
+  } else {
+    first = xcd_remap(blockIdx.x, gridDim.x);
+    stride = gridDim.x;
+  }
+  const int n_mine = first < limit ? (limit - first + stride - 1) / stride : 0;
   const int S = n_mine * nk;
   uint32_t key = 0;
   if (epi.rng) key = stream_key(epi.rng[0], epi.rng[1], epi.drop_layer, epi.drop_site);
@@ -1182,6 +1197,7 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
           n_cu <= 0)
         n_cu = 256;
     }
+    static const int g_nt_xcd_order = getenv("MMT_NT_ORDER") ? atoi(getenv("MMT_NT_ORDER")) : 1;
     const int tm256 = (M + 255) / 256;
     int bn = 0;
     if (g_variant == 5) bn = N % 256 == 0 ? 256 : 0;
@@ -1200,7 +1216,7 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
       const int grid = std::min(n_tiles, n_cu);
 #define GN(BNV, OUT, ST, NSV)                                                                     \
   hipLaunchKernelGGL((gemm_nt256_kernel<BNV, OUT, ST, NSV>), dim3(grid), dim3(NT3), 0, s, M, N, K, \
-                     (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, tn, n_tiles, epi)
+                     (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, tn, n_tiles, g_nt_xcd_order, epi)
       // the register stash fits 2 waves/SIMD for bf16 at BN <= 192 and fp32 at BN 128;
       // BN 128 has LDS for 3 stages (DMA two K-steps ahead)
       if (final_kind == 0) {

@@ -395,14 +395,20 @@ __global__ void embedding_gather_kernel(const int32_t* __restrict__ ids, int64_t
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                              float* __restrict__ m, float* __restrict__ v,
                              bf16_t* __restrict__ shadow, int64_t n, const int32_t* __restrict__ state,
-                             float lr, float b1, float b2, float eps, float wd, float grad_scale) {
+                             float lr, double b1d, double b2d, float eps, float wd, float grad_scale) {
   const int step = state[1] + 1;
-  const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
+  // the betas arrive in double (optax / torch hold them as Python floats): 1 - b and the bias
+  // corrections are formed in double and rounded once (fp32 1.f - 0.999f would differ from
+  // (float)0.001 by 1.3e-5 relative)
+  const float b1 = (float)b1d, b2 = (float)b2d;
+  const float bc1 = (float)(1.0 - pow(b1d, (double)step));
+  const float bc2 = (float)(1.0 - pow(b2d, (double)step));
+  const float omb1 = (float)(1.0 - b1d), omb2 = (float)(1.0 - b2d);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const float gi = g[i] * grad_scale;
-    const float mi = b1 * m[i] + (1.f - b1) * gi;
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    const float mi = b1 * m[i] + omb1 * gi;
+    const float vi = b2 * v[i] + omb2 * (gi * gi);
     m[i] = mi;
     v[i] = vi;
     const float upd = (mi / bc1) / (sqrtf(vi / bc2) + eps) + wd * p[i];
@@ -618,12 +624,13 @@ extern "C" int mmt_embedding_gather(const int32_t* ids, int64_t n, int D, const 
 }
 
 extern "C" int mmt_adamw(float* p, const float* g, float* m, float* v, void* shadow_bf16,
-                         int64_t n, const int32_t* state, float lr, float b1, float b2, float eps,
-                         float wd, float grad_scale, mmt_stream_t stream) {
+                         int64_t n, const int32_t* state, double lr, double b1, double b2,
+                         double eps, double wd, float grad_scale, mmt_stream_t stream) {
   MMT_CHECK_ARG(p && g && m && v && state && n > 0, "mmt_adamw: args");
   const int64_t blocks = std::min<int64_t>((n + 255) / 256, 256 * 8);
   hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), p, g, m, v,
-                     (bf16_t*)shadow_bf16, n, state, lr, b1, b2, eps, wd, grad_scale);
+                     (bf16_t*)shadow_bf16, n, state, (float)lr, b1, b2, (float)eps, (float)wd,
+                     grad_scale);
   MMT_CHECK_LAUNCH("mmt_adamw");
   return MMT_OK;
 }
@@ -641,5 +648,30 @@ extern "C" int mmt_step_advance(int32_t* state, mmt_stream_t stream) {
   MMT_CHECK_ARG(state, "mmt_step_advance: null");
   hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(1), 0, as_stream(stream), state);
   MMT_CHECK_LAUNCH("mmt_step_advance");
+  return MMT_OK;
+}
+
+// AddPositionEmbedding (tokenizers/readout/readout.py:18-33, attention.py:71-85): out[b, l, :] =
+// x[b, l, :] + pe[l, :] (fp32, float4 lanes; x may alias out). The backward is the identity for x
+// and mmt_colsum over the batch for pe.
+__global__ void add_pe_kernel(const float4* __restrict__ x, const float4* __restrict__ pe,
+                              float4* __restrict__ out, int64_t n4, int64_t per4) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 a = x[i], p = pe[i % per4];
+    out[i] = make_float4(a.x + p.x, a.y + p.y, a.z + p.z, a.w + p.w);
+  }
+}
+
+extern "C" int mmt_add_position_embedding(const float* x, const float* pe, float* out, int B, int L,
+                                          int D, mmt_stream_t stream) {
+  MMT_CHECK_ARG(x && pe && out && B > 0 && L > 0 && D > 0 && D % 4 == 0 &&
+                    (uintptr_t)x % 16 == 0 && (uintptr_t)pe % 16 == 0 && (uintptr_t)out % 16 == 0,
+                "mmt_add_position_embedding: args (D %% 4 == 0, 16-B aligned)");
+  const int64_t per4 = (int64_t)L * D / 4, n4 = per4 * B;
+  const int64_t blocks = std::min<int64_t>((n4 + 255) / 256, 256 * 8);
+  hipLaunchKernelGGL(add_pe_kernel, dim3(blocks), dim3(256), 0, as_stream(stream),
+                     (const float4*)x, (const float4*)pe, (float4*)out, n4, per4);
+  MMT_CHECK_LAUNCH("mmt_add_position_embedding");
   return MMT_OK;
 }

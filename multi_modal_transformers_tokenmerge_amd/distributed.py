@@ -68,3 +68,115 @@ class GradAllReducer:
         n = flat_grad.numel()
         for s in range(0, n, self.bucket_elems):
             dist.all_reduce(flat_grad[s:s + self.bucket_elems], op=dist.ReduceOp.SUM, group=self.group)
+
+
+class DDPStep:
+    """One data-parallel training step of an Octo model on this rank's shard, as bench.py runs it:
+    zero grads -> forward -> backward -> gradient all-reduce -> fused AdamW -> step counter.
+
+    * world size 1: the whole step is ONE HIP graph (no host work between kernels);
+    * world size N > 1 with stages S > 1: the backward runs as S block-range stages
+      (Octo.backward_stage; the heads and last blocks first). After stage k the flat-gradient
+      region it finalised (Octo.grad_regions) is all-reduced asynchronously on the collective
+      stream while the later stages compute; AdamW (its own graph) waits for all of them, so only
+      the last region (first blocks + stem/embeddings) is exposed;
+    * S = 1: one forward/backward graph, then a blocking bucketed all-reduce (GradAllReducer);
+    * use_graph False: the same schedules launched eagerly (the overlap still applies).
+    The 1/N average is AdamW's grad_scale (reducer.grad_scale)."""
+
+    def __init__(self, model, state, txt, img, act, reducer: GradAllReducer | None = None,
+                 stages: int = 3, use_graph: bool = True):
+        self.model, self.state = model, state
+        self.txt, self.img, self.act = txt, img, act
+        self.reducer = reducer
+        self.distributed = reducer is not None and reducer.world_size > 1
+        self.S = max(1, min(stages, model.cfg.num_blocks)) if self.distributed else 1
+        self.regions = model.grad_regions(self.S) if self.S > 1 else None
+        self.use_graph = use_graph
+        self.loss_buf = torch.zeros(1, device=model.device)
+        self.graphs = []
+        self._st = {}
+
+    # --------------------------------------------------------------- schedule pieces
+    def _fwd_bwd(self):
+        m, s = self.model, self.state
+        m.store.zero_grad()
+        loss, st = m.compute_diffusion_denoise_loss(self.txt, self.img, self.act, True, s.rng,
+                                                    s.sample_offset)
+        m.backward(st)
+        self.loss_buf.copy_(loss)
+
+    def _stage(self, k):
+        m, s = self.model, self.state
+        if k == 0:
+            m.store.zero_grad()
+            loss, st = m.compute_diffusion_denoise_loss(self.txt, self.img, self.act, True, s.rng,
+                                                        s.sample_offset)
+            self.loss_buf.copy_(loss)
+            self._st["st"] = st
+        m.backward_stage(self._st["st"], k, self.S)
+
+    def _opt(self):
+        self.state.apply_gradients()
+
+    def _reduce_async(self, k):
+        lo, hi = self.regions[k]
+        return dist.all_reduce(self.model.store.flat_grad[lo:hi], op=dist.ReduceOp.SUM,
+                               async_op=True, group=self.reducer.group)
+
+    # --------------------------------------------------------------------- capture
+    def build(self, warm: int = 2):
+        """Warm caches and the allocator outside capture, then capture the step's graphs."""
+        if not self.use_graph:
+            return self
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warm):
+                self._fwd_bwd()
+                if self.distributed:
+                    self.reducer(self.model.store.flat_grad)
+                self._opt()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        pool = torch.cuda.graph_pool_handle()
+
+        def cap(fn):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                fn()
+            self.graphs.append(g)
+        if self.S > 1:
+            for k in range(self.S):   # one graph per backward stage (the first holds the forward)
+                cap(lambda k=k: self._stage(k))
+            cap(self._opt)
+        elif self.distributed:
+            cap(self._fwd_bwd)
+            cap(self._opt)
+        else:
+            def whole():
+                self._fwd_bwd()
+                self._opt()
+            cap(whole)
+        return self
+
+    def __call__(self):
+        g = self.graphs
+        if self.S > 1:
+            works = []
+            for k in range(self.S):
+                g[k].replay() if self.use_graph else self._stage(k)
+                works.append(self._reduce_async(k))
+            for w in works:
+                w.wait()
+            g[self.S].replay() if self.use_graph else self._opt()
+        elif self.distributed:
+            g[0].replay() if self.use_graph else self._fwd_bwd()
+            self.reducer(self.model.store.flat_grad)
+            g[1].replay() if self.use_graph else self._opt()
+        else:
+            if self.use_graph:
+                g[0].replay()
+            else:
+                self._fwd_bwd()
+                self._opt()

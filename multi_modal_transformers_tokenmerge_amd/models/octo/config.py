@@ -38,6 +38,8 @@ class OctoConfig:
     layer_norm_eps: float = 1e-6
     t5: T5Config = field(default_factory=T5Config)
     text_tokens: int = 32
+    # ResNetV2Block hyper-parameters (gato_resnet.yaml:41-104); None = the build defaults
+    stem: Optional[dict] = None
 
     @property
     def tome_r(self) -> int:
@@ -72,6 +74,16 @@ PRESETS = {
 
 
 def get_config(name: str, **overrides) -> OctoConfig:
+    """A preset by name ("octo-small-tome16"), or a YAML config of the reference schema from
+    model_configs/ ("octo_small_tome16", "ref_octo_base", or a path ending in .yaml)."""
     if name not in PRESETS:
-        raise KeyError(f"unknown config {name!r}; known: {sorted(PRESETS)}")
+        from ...config_loader import CONFIG_DIR, load_octo_config
+        from pathlib import Path
+        p = Path(name)
+        if name.endswith(".yaml") and p.exists():
+            return replace(load_octo_config(p.name, p.parent), **overrides)
+        if (CONFIG_DIR / f"{name}.yaml").exists():
+            return replace(load_octo_config(name), **overrides)
+        raise KeyError(f"unknown config {name!r}; known: {sorted(PRESETS)} or "
+                       f"model_configs/*.yaml")
     return replace(PRESETS[name], **overrides)

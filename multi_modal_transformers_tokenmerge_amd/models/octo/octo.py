@@ -31,6 +31,7 @@ from ...attention_blocks.attention import LayerCtx, StackedEncoder1DBlock
 from ...layers import Dense
 from ...params import ParamStore, he_normal, normal
 from ...tokenizers.images.image_tokenizer import ImageTokenizer
+from ...tokenizers.readout.readout import AddPositionEmbedding
 from ...tokenizers.text.t5_base import T5Tokenizer
 from ...tokenizers.token_sequencer import Image, Readout, Text, TokenSequence
 from .config import OctoConfig, get_config
@@ -59,7 +60,8 @@ class Octo:
         store = self.store = ParamStore()
         # ---- tokenizers
         self.image_tokenizer = ImageTokenizer(store, "ImageTokenizer_0", cfg.image_size,
-                                              cfg.patch_size, True, cfg.position_interval, D)
+                                              cfg.patch_size, True, cfg.position_interval, D,
+                                              resnet=cfg.stem)
         NP = self.image_tokenizer.num_patches
         for ts in sets0:
             if isinstance(ts, Image) and ts.num_tokens != NP:
@@ -67,8 +69,10 @@ class Octo:
         self.text_proj = None
         if self.has_text and cfg.t5.d_model != D:
             self.text_proj = Dense(store, "TextProjection_0", cfg.t5.d_model, D)
-        self.readout_pe = store.add("AddPositionEmbedding_0/pos_embedding", (self.n_readout, D),
-                                    he_normal((1, self.n_readout, D)))
+        # readouts = AddPositionEmbedding(zeros) (octo.py:103-108); the add itself is fused into
+        # the sequence assembly kernel, the module owns the parameter
+        self.readout_encoder = AddPositionEmbedding(store, "AddPositionEmbedding_0", self.n_readout, D)
+        self.readout_pe = self.readout_encoder.pe
         # ---- backbone (posembed_input of StackedEncoder1DBlock, attention.py:97-100)
         self.pos_embed = store.add("StackedEncoder1DBlock_0/posembed_input/pos_embedding",
                                    (self.L0, D), normal(0.02))
@@ -366,6 +370,30 @@ class AdamW:
     weight_decay: float = 1e-4
 
 
+class OCTOMetrics:
+    """Reference octo.py:322-324 (``clu.metrics.Average.from_output("loss")``): running sum and
+    count kept on the device, merged without a host sync (the reference's wandb.log forces one
+    every step, :231-233). ``compute()`` is the average (a host read)."""
+
+    def __init__(self, device):
+        self.total = torch.zeros(1, dtype=torch.float64, device=device)
+        self.count = torch.zeros(1, dtype=torch.float64, device=device)
+
+    def merge(self, loss: torch.Tensor) -> "OCTOMetrics":
+        """single_from_model_output(loss=loss) merged in place (Average.merge: sums add)."""
+        self.total.add_(loss.detach().reshape(-1)[:1].double())
+        self.count.add_(1.0)
+        return self
+
+    def compute(self) -> float:
+        c = float(self.count.item())
+        return float(self.total.item()) / c if c else float("nan")
+
+    def reset(self):
+        self.total.zero_()
+        self.count.zero_()
+
+
 @dataclass
 class OCTOTrainState:
     """Reference octo.py:326-332: params (flat store), optimizer, rngs (device {seed, step}),
@@ -375,8 +403,8 @@ class OCTOTrainState:
     rng: torch.Tensor
     allreduce: Optional[Callable] = None        # DDP gradient all-reduce (distributed.py)
     sample_offset: int = 0
-    loss_sum: float = 0.0
-    loss_count: int = 0
+    metrics: Optional[OCTOMetrics] = None
+    last_loss: Optional[torch.Tensor] = None    # loss of the latest step (device)
 
     @property
     def params(self):
@@ -401,42 +429,50 @@ def create_octo_train_state(model: Octo, tx: AdamW | None = None, seed: int = 12
                             allreduce=None, sample_offset: int = 0) -> OCTOTrainState:
     """Reference octo.py:334-386 (parameters were initialised by Octo(...))."""
     rng = torch.tensor([seed, 0], dtype=torch.int32, device=model.device)
-    return OCTOTrainState(model, tx or AdamW(), rng, allreduce, sample_offset)
+    return OCTOTrainState(model, tx or AdamW(), rng, allreduce, sample_offset,
+                          metrics=OCTOMetrics(model.device))
 
 
-def _head_train_step(loss_fn, model: Octo, train_state: OCTOTrainState, text_tokens, images,
-                     actions):
+def grads_tree(model: Octo) -> Dict[str, torch.Tensor]:
+    """The step's gradients by parameter name (views into the flat fp32 gradient buffer, valid
+    until the next step zeroes it) — the ``grads`` the reference's train steps return."""
+    return {p.name: p.grad for p in model.store.params}
+
+
+def _train_step(loss_fn, model: Octo, train_state: OCTOTrainState, text_tokens, images, actions,
+                **kw):
+    """value_and_grad -> apply_gradients -> metrics merge (octo.py:216-239); returns
+    (train_state, grads). The step's loss stays on the device: train_state.last_loss."""
     model.store.zero_grad()
     loss, st = loss_fn(text_tokens, images, actions, True, train_state.rng,
-                       train_state.sample_offset)
+                       train_state.sample_offset, **kw)
     model.backward(st)
     if train_state.allreduce is not None:
         train_state.allreduce(model.store.flat_grad)
     train_state.apply_gradients()
-    return train_state, loss
+    train_state.last_loss = loss
+    if train_state.metrics is not None:
+        train_state.metrics.merge(loss)
+    return train_state, grads_tree(model)
 
 
 def continuous_train_step(model: Octo, train_state: OCTOTrainState, text_tokens, images, actions):
-    """Reference octo.py:242-280: value_and_grad of mean(compute_l2_loss), apply_gradients."""
-    return _head_train_step(model.compute_l2_loss, model, train_state, text_tokens, images, actions)
+    """Reference octo.py:242-280: value_and_grad of mean(compute_l2_loss), apply_gradients,
+    metrics merge. Returns (train_state, grads)."""
+    return _train_step(model.compute_l2_loss, model, train_state, text_tokens, images, actions)
 
 
 def categorical_train_step(model: Octo, train_state: OCTOTrainState, text_tokens, images, actions):
-    """Reference octo.py:282-320: value_and_grad of mean(compute_ce_loss), apply_gradients."""
-    return _head_train_step(model.compute_ce_loss, model, train_state, text_tokens, images, actions)
+    """Reference octo.py:282-320: value_and_grad of mean(compute_ce_loss), apply_gradients,
+    metrics merge. Returns (train_state, grads)."""
+    return _train_step(model.compute_ce_loss, model, train_state, text_tokens, images, actions)
 
 
 def diffusion_train_step(model: Octo, train_state: OCTOTrainState, text_tokens, images, actions,
                          inject: Optional[dict] = None):
-    """Reference octo.py:204-240: value_and_grad of the denoise loss, then apply_gradients.
-    Returns (train_state, loss_tensor); gradients stay in model.store.flat_grad (views:
-    ``p.grad`` of every model.store parameter)."""
-    model.store.zero_grad()
-    loss, st = model.compute_diffusion_denoise_loss(text_tokens, images, actions, True,
-                                                    train_state.rng, train_state.sample_offset,
-                                                    inject)
-    model.backward(st)
-    if train_state.allreduce is not None:
-        train_state.allreduce(model.store.flat_grad)
-    train_state.apply_gradients()
-    return train_state, loss
+    """Reference octo.py:204-240: value_and_grad of the denoise loss, apply_gradients, metrics
+    merge. Returns (train_state, grads) like the reference; grads are views of the flat gradient
+    buffer by parameter name, the loss is train_state.last_loss (device) and the running average
+    train_state.metrics."""
+    return _train_step(model.compute_diffusion_denoise_loss, model, train_state, text_tokens,
+                       images, actions, inject=inject)

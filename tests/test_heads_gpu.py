@@ -78,11 +78,13 @@ def test_octo_head_train_steps(dev, kind):
     images = torch.randint(0, 256, (B, model.n_images, 64, 64, 3), dtype=torch.uint8, device=dev)
     actions = (torch.rand((B, 8), device=dev) * 2 - 1).contiguous()
     step = O.continuous_train_step if kind == "continuous" else O.categorical_train_step
+    head = model.continuous_head if kind == "continuous" else model.categorical_head
     losses = []
     for _ in range(3):
-        state, loss = step(model, state, None, images, actions)
-        losses.append(float(loss))
-    head = model.continuous_head if kind == "continuous" else model.categorical_head
+        state, grads = step(model, state, None, images, actions)
+        losses.append(float(state.last_loss))
+        assert grads[head.dense.w.name].data_ptr() == head.dense.w.grad.data_ptr()
+    assert abs(state.metrics.compute() - np.mean(losses)) <= 1e-5 * abs(np.mean(losses))
     assert all(np.isfinite(losses)) and head.dense.w.grad.abs().sum() > 0
     assert model.stack.blocks[0].qkv.w.grad.abs().sum() > 0
     out = (model.predict_continuous_action(None, images, state.rng) if kind == "continuous"

@@ -1,0 +1,81 @@
+"""Optimizer and train-state pieces on the GPU:
+* mmt_adamw (the fused AdamW over the flat buffer, octo.py:228 apply_gradients with optax.adamw
+  semantics) vs torch.optim.AdamW in fp32 on the CPU over 3 steps, with the DDP 1/N grad_scale;
+  the bf16 shadow is exactly bf16(master);
+* diffusion_train_step returns (state, grads) and merges the loss into the running average
+  (octo.py:216-239);
+* AddPositionEmbedding (tokenizers/readout/readout.py:8-33) forward/backward vs torch fp32.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("grad_scale", [1.0, 0.5])
+def test_adamw_matches_torch(dev, grad_scale):
+    from multi_modal_transformers_tokenmerge_amd import _C
+    n = 100_003
+    g = torch.Generator().manual_seed(3)
+    p0 = torch.randn(n, generator=g)
+    lr, b1, b2, eps, wd = 3e-3, 0.9, 0.999, 1e-8, 1e-2
+    ref = p0.clone().requires_grad_()
+    opt = torch.optim.AdamW([ref], lr=lr, betas=(b1, b2), eps=eps, weight_decay=wd)
+    p = p0.to(dev)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    shadow = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    state = torch.tensor([1234, 0], dtype=torch.int32, device=dev)
+    for it in range(3):
+        grad = torch.randn(n, generator=g) * (it + 1)
+        ref.grad = grad * grad_scale
+        opt.step()
+        _C.call("mmt_adamw", _C.ptr(p), _C.ptr(grad.to(dev)), _C.ptr(m), _C.ptr(v), _C.ptr(shadow), n,
+                _C.ptr(state), lr, b1, b2, eps, wd, grad_scale, _C.stream_ptr())
+        _C.call("mmt_step_advance", _C.ptr(state), _C.stream_ptr())
+        torch.cuda.synchronize()
+        torch.testing.assert_close(p.cpu(), ref.detach(), rtol=2e-6, atol=2e-7)
+        st = opt.state[ref]
+        torch.testing.assert_close(m.cpu(), st["exp_avg"], rtol=2e-6, atol=1e-7)
+        torch.testing.assert_close(v.cpu(), st["exp_avg_sq"], rtol=2e-6, atol=1e-12)
+        assert torch.equal(shadow.cpu(), p.cpu().bfloat16())
+    assert int(state[1].item()) == 3
+
+
+def test_diffusion_train_step_returns_grads_and_metrics(dev):
+    from multi_modal_transformers_tokenmerge_amd.models.octo.config import get_config
+    from multi_modal_transformers_tokenmerge_amd.models.octo import octo as O
+    from oracle.parity import _inputs
+    model = O.Octo(get_config("octo-tiny", num_blocks=2), dev, seed=0)
+    state = O.create_octo_train_state(model, seed=7)
+    images, _, actions = _inputs(model, 3)
+    img, act = torch.from_numpy(images).to(dev), torch.from_numpy(actions).to(dev)
+    losses = []
+    for _ in range(3):
+        state, grads = O.diffusion_train_step(model, state, None, img, act)
+        losses.append(float(state.last_loss))
+    assert set(grads) == {p.name for p in model.store.params}
+    assert all(grads[p.name].data_ptr() == p.grad.data_ptr() for p in model.store.params)
+    assert float(sum(g.abs().sum() for g in grads.values())) > 0
+    assert state.step == 3
+    assert abs(state.metrics.compute() - np.mean(losses)) <= 1e-5 * abs(np.mean(losses))
+
+
+def test_add_position_embedding(dev):
+    from multi_modal_transformers_tokenmerge_amd.params import ParamStore
+    from multi_modal_transformers_tokenmerge_amd.tokenizers.readout.readout import AddPositionEmbedding
+    store = ParamStore()
+    mod = AddPositionEmbedding(store, "AddPositionEmbedding_0", 8, 64)
+    store.materialize(dev, 0)
+    x = torch.randn((3, 8, 64), device=dev)
+    y = mod(x)
+    torch.testing.assert_close(y, x + mod.pe.data[None], rtol=0, atol=0)
+    dout = torch.randn_like(x)
+    store.zero_grad()
+    dx = mod.backward(dout)
+    torch.cuda.synchronize()
+    assert dx is dout
+    torch.testing.assert_close(mod.pe.grad, dout.sum(0), rtol=1e-6, atol=1e-6)
+    with pytest.raises(ValueError):
+        mod(torch.zeros((8, 64), device=dev))

@@ -14,16 +14,22 @@ from tools.gemm_bench import timeit
 def main():
     dev = torch.device("cuda")
     B = 256
+    Ls = (292, 212, 132)
+    t5 = True
     for a in sys.argv[1:]:
         if a.startswith("--b="):
             B = int(a.split("=")[1])
+        if a.startswith("--L="):
+            Ls = tuple(int(v) for v in a.split("=")[1].split(","))
+            t5 = False
     rng = torch.tensor([7, 1], dtype=torch.int32, device=dev)
     cases = []
-    for L in (292, 212, 132):  # layers 0, 5, 10 of the ToMe r=16 schedule
+    for L in Ls:  # default: layers 0, 5, 10 of the ToMe r=16 schedule
         n_img = L - 36
         cases.append((f"octo-small L={L}", L, 6, 64,
                       K.SetTable([0, 32, 32 + n_img], [32, n_img, 4], [0b001, 0b011, 0b111]), True, False))
-    cases.append(("t5 L=32 (bias)", 32, 12, 64, None, False, True))
+    if t5:
+        cases.append(("t5 L=32 (bias)", 32, 12, 64, None, False, True))
     for name, L, H, Dh, table, drop, bias in cases:
         g = torch.Generator().manual_seed(L)
         qkv = torch.randn((B, L, 3 * H * Dh), generator=g).bfloat16().to(dev)
