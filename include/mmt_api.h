@@ -134,6 +134,7 @@ int mmt_topk_scatter_bwd(const void* dout, int dtype, int B, int K, int D, int64
  * v += residual[m][n] (bf16 or fp32 per res_dtype).
  */
 enum { MMT_ACT_NONE = 0, MMT_ACT_RELU = 1 };
+#define MMT_SET_CAUSAL 0x80000000u
 enum { MMT_OUT_BF16 = 0, MMT_OUT_F32 = 1, MMT_OUT_F32_ACCUM = 2 };
 
 typedef struct {
@@ -170,10 +171,12 @@ int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t lda, const 
  * qkv: bf16 rows (b, t) at qkv + b*s_b + t*s_t holding [q(H,Dh) | k(H,Dh) | v(H,Dh)].
  * Mask = token-set table: n_sets (<= 16) contiguous sets tiling [0, L) (set_start/set_len HOST
  * arrays) and set_vis[s] = bitmask of key sets that query set s attends to; n_sets = 0: no mask.
+ * Bit 31 of set_vis[s] (MMT_SET_CAUSAL) makes set s causal within itself: its query q sees its
+ * own set's keys k <= q only (Text sets, token_sequencer.py:76-82, nn.make_causal_mask).
  * drop_bits: (L, ceil(L/32)) uint32 keep bitmask from mmt_dropout_bits, or NULL (no dropout);
  * kept probabilities are scaled by 1/keep_prob. bias: optional fp32 (H, L, L) added to the
  * scaled logits (T5 relative position bias; forward only). o: bf16 (b, t) rows of (H, Dh);
- * lse: fp32 (B, H, L) natural-log softmax normaliser. Dh in {64, 128}.
+ * lse: fp32 (B, H, L) natural-log softmax normaliser. Dh in {64, 128, 256}.
  */
 int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, int L, int H, int Dh,
                  float scale, int n_sets, const int32_t* set_start, const int32_t* set_len,

@@ -214,14 +214,18 @@ class SetTable:
     """Host-side token-set table of one layer: contiguous sets tiling [0, L) and, per query set,
     the bitmask of key sets it attends to (the blockwise mask of token_sequencer.py:94-183)."""
 
-    def __init__(self, starts, lens, vis):
+    CAUSAL = 1 << 31  # MMT_SET_CAUSAL: causal within the set (Text, token_sequencer.py:76-82)
+
+    def __init__(self, starts, lens, vis, causal=None):
         n = len(starts)
         if n > 16:
             raise ValueError("at most 16 token sets")
         self.n = n
         self.starts = (_C.ctypes.c_int32 * max(n, 1))(*starts)
         self.lens = (_C.ctypes.c_int32 * max(n, 1))(*lens)
-        self.vis = (_C.ctypes.c_uint32 * max(n, 1))(*vis)
+        causal = causal or [False] * n
+        self.vis = (_C.ctypes.c_uint32 * max(n, 1))(*[(v & 0xFFFF) | (self.CAUSAL if c else 0)
+                                                     for v, c in zip(vis, causal)])
         self.L = int(sum(lens))
 
     @staticmethod

@@ -51,6 +51,8 @@ struct AttnMask {
   int start[MAX_SETS];
   int len[MAX_SETS];
   uint32_t vis[MAX_SETS];  // bit k: query set s sees key set k
+  uint32_t causal;         // bit s: inside set s, query q sees key k only if k <= q (Text sets,
+                           // token_sequencer.py:76-82: nn.make_causal_mask)
 };
 
 __device__ __forceinline__ int set_of(const AttnMask& m, int t) {
@@ -95,6 +97,32 @@ __device__ __forceinline__ uint64_t sets_bits(const AttnMask& m, uint32_t sel, i
     }
   }
   return r;
+}
+
+// Bits [a, e) of a 64-bit tile word (0 <= a < e <= 64)
+__device__ __forceinline__ uint64_t bit_range(int a, int e) {
+  const uint64_t hi = e >= 64 ? ~0ull : ((1ull << e) - 1ull);
+  return hi & ~((1ull << a) - 1ull);
+}
+// Causal set (query-on-lane view): query q of causal set sq does not see the keys of its own set
+// after it: clears keys (q, end(sq)) of the tile starting at kt.
+__device__ __forceinline__ uint64_t causal_keys(const AttnMask& m, int sq, int q, int kt,
+                                                uint64_t vm) {
+  if ((m.causal >> sq) & 1u) {
+    const int a = max(q + 1 - kt, 0), e = min(m.start[sq] + m.len[sq] - kt, KT);
+    if (a < e) vm &= ~bit_range(a, e);
+  }
+  return vm;
+}
+// Key-on-lane view: key k of causal set sk is not seen by the queries of its set before it:
+// clears queries [start(sk), k) of the tile starting at qt.
+__device__ __forceinline__ uint64_t causal_queries(const AttnMask& m, int sk, int k, int qt,
+                                                   uint64_t qm) {
+  if ((m.causal >> sk) & 1u) {
+    const int a = max(m.start[sk] - qt, 0), e = min(k - qt, KT);
+    if (a < e) qm &= ~bit_range(a, e);
+  }
+  return qm;
 }
 
 // Bit of accumulator register r of this lane inside a 32-row word pre-shifted by 4*(lane>>5):
@@ -246,7 +274,7 @@ struct Geo {
 
 // =============================================================================== forward
 template <int DH>
-__global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(Geo g, AttnMask mask,
+__global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(Geo g, AttnMask mask,
                                                       const uint32_t* __restrict__ drop_bits,
                                                       int drop_words, float drop_scale,
                                                       const float* __restrict__ bias,
@@ -272,7 +300,8 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(Geo g, AttnMask mask,
   const bf16_t* qrow = base + (int64_t)(qv ? q : 0) * g.s_t + h * DH;
 #pragma unroll
   for (int s = 0; s < NS; ++s) qf[s] = row_frag_global(qrow, qv, s, lane);
-  const uint32_t visq = qv ? mask.vis[set_of(mask, q)] : 0u;
+  const int sq = qv ? set_of(mask, q) : 0;
+  const uint32_t visq = qv ? mask.vis[sq] : 0u;
   const float* brow = bias ? bias + ((int64_t)h * L + (qv ? q : 0)) * L : nullptr;
   const float c = bias ? 1.f : g.scale * LOG2E;  // score -> log2 units (bias mode converts first)
 
@@ -309,7 +338,8 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(Geo g, AttnMask mask,
           sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<STR>(Ks, 32 * u, s, lane),
                                                             qf[s], sacc[u], 0, 0, 0);
       }
-      const uint64_t vm = sets_bits(mask, visq, kt);
+      uint64_t vm = sets_bits(mask, visq, kt);
+      if (mask.causal) vm = causal_keys(mask, sq, q, kt, vm);
       if (brow) {  // registers 4 r4 .. 4 r4 + 3 hold 4 consecutive keys: one float4 (L % 4 == 0)
 #pragma unroll
         for (int u = 0; u < 2; ++u)
@@ -400,7 +430,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(Geo g, AttnMask mask,
 
 // =============================================================================== bwd: dQ
 template <int DH, int NTT>
-__global__ __launch_bounds__(NTT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mask,
+__global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dq_kernel(Geo g, AttnMask mask,
                                                          const uint32_t* __restrict__ drop_bits,
                                                          int drop_words, float drop_scale,
                                                          const bf16_t* __restrict__ dout,
@@ -436,7 +466,8 @@ __global__ __launch_bounds__(NTT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mas
     qf[s] = row_frag_global(qrow, qv, s, lane);
     df[s] = row_frag_global(drow, qv, s, lane);
   }
-  const uint32_t visq = qv ? mask.vis[set_of(mask, q)] : 0u;
+  const int sq = qv ? set_of(mask, q) : 0;
+  const uint32_t visq = qv ? mask.vis[sq] : 0u;
   const int64_t row_bh = ((int64_t)b * g.H + h) * L;
   const float lse2 = qv ? lse[row_bh + q] * LOG2E : INFINITY;
   // delta = rowsum(dO * O) of this query (fp32), fused here: the lane pair (q, hh = 0/1) holds
@@ -477,7 +508,8 @@ __global__ __launch_bounds__(NTT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mas
     if (wave_live) {
       uint32_t dw[2];
       load_drop_words(drop_bits, drop_words, qv ? q : 0, qv, kt, dw);
-      const uint64_t vm = sets_bits(mask, visq, kt);
+      uint64_t vm = sets_bits(mask, visq, kt);
+      if (mask.causal) vm = causal_keys(mask, sq, q, kt, vm);
       floatx16 ds[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -543,7 +575,7 @@ __global__ __launch_bounds__(NTT, 2) void attn_bwd_dq_kernel(Geo g, AttnMask mas
 
 // =============================================================================== bwd: dK, dV
 template <int DH, int NTT>
-__global__ __launch_bounds__(NTT, 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask mask,
+__global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask mask,
                                                            const uint32_t* __restrict__ drop_bits_t,
                                                            int drop_words, float drop_scale,
                                                            const bf16_t* __restrict__ dout,
@@ -579,10 +611,9 @@ __global__ __launch_bounds__(NTT, 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask m
   }
   // query sets that see this key's set
   uint32_t selq = 0;
-  if (kv) {
-    const int ks = set_of(mask, key);
-    for (int i = 0; i < mask.n_sets; ++i) selq |= ((mask.vis[i] >> ks) & 1u) << i;
-  }
+  const int sk = kv ? set_of(mask, key) : 0;
+  if (kv)
+    for (int i = 0; i < mask.n_sets; ++i) selq |= ((mask.vis[i] >> sk) & 1u) << i;
   const int64_t row_bh = ((int64_t)b * g.H + h) * L;
   const float sl2 = g.scale * LOG2E;
   floatx16 dk[ND], dv[ND];
@@ -626,7 +657,8 @@ __global__ __launch_bounds__(NTT, 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask m
     if (wave_live) {
       uint32_t dw[2];
       load_drop_words(drop_bits_t, drop_words, kv ? key : 0, kv, qt, dw);
-      const uint64_t qm = sets_bits(mask, selq, qt);
+      uint64_t qm = sets_bits(mask, selq, qt);
+      if (mask.causal) qm = causal_queries(mask, sk, key, qt, qm);
 #pragma unroll 1
       for (int u = 0; u < 2; ++u) {  // 32-query sub-tiles (not unrolled: keeps 2 waves/SIMD)
         floatx16 sacc, pacc;
@@ -743,6 +775,7 @@ __global__ void dropout_bits_kernel(const uint32_t* __restrict__ rng, uint32_t l
 
 int fill_mask(AttnMask& m, int n_sets, const int32_t* starts, const int32_t* lens,
               const uint32_t* vis, int L) {
+  m.causal = 0;
   if (n_sets <= 0) {  // no mask: one set covering everything
     m.n_sets = 1;
     m.start[0] = 0;
@@ -762,7 +795,8 @@ int fill_mask(AttnMask& m, int n_sets, const int32_t* starts, const int32_t* len
     MMT_CHECK_ARG(starts[i] == expect && lens[i] >= 0, "attention: token sets must tile [0, L)");
     m.start[i] = starts[i];
     m.len[i] = lens[i];
-    m.vis[i] = vis[i];
+    m.vis[i] = vis[i] & ((1u << MAX_SETS) - 1u);
+    m.causal |= ((vis[i] >> 31) & 1u) << i;   // MMT_SET_CAUSAL
     expect += lens[i];
   }
   MMT_CHECK_ARG(expect == L, "attention: token sets cover %d of L=%d", expect, L);
@@ -780,7 +814,8 @@ int fill_mask(AttnMask& m, int n_sets, const int32_t* starts, const int32_t* len
   do {                                                           \
     if (Dh == 64) { constexpr int DH_ = 64; __VA_ARGS__; }       \
     else if (Dh == 128) { constexpr int DH_ = 128; __VA_ARGS__; } \
-    else { MMT_CHECK_ARG(false, "attention: head dim %d unsupported (64, 128)", Dh); } \
+    else if (Dh == 256) { constexpr int DH_ = 256; __VA_ARGS__; } \
+    else { MMT_CHECK_ARG(false, "attention: head dim %d unsupported (64, 128, 256)", Dh); } \
   } while (0)
 
 // Backward workgroup size: 2 waves (64 rows) when that fills the row blocks clearly better than

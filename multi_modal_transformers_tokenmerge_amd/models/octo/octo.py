@@ -136,9 +136,8 @@ class Octo:
                 t = sets.lens[tome_set]
                 if r > t // 2:
                     raise ValueError(f"layer {layer}: ToMe r={r} exceeds t//2={t // 2}")
-            if any(sets.causal):
-                raise NotImplementedError("causal Text sets are not supported by the attention kernel yet")
-            self.layer_sets.append((sets, K.SetTable(sets.starts, sets.lens, sets.vis), tome_set, r))
+            self.layer_sets.append((sets, K.SetTable(sets.starts, sets.lens, sets.vis, sets.causal),
+                                    tome_set, r))
         final = self.seq.set_table(cfg.num_blocks) if cfg.token_compression_sequence else self.seq.set_table(0)
         self.L_final = final.L
         rows = [s + j for s, n, m in zip(final.starts, final.lens, final.modalities) if m == "readouts"

@@ -16,12 +16,16 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
 
 
-def dense_mask(starts, lens, vis, L, dev):
+def dense_mask(starts, lens, vis, L, dev, causal=None):
     sid = torch.zeros(L, dtype=torch.long)
     for i, (s, n) in enumerate(zip(starts, lens)):
         sid[s:s + n] = i
     v = torch.tensor(vis, dtype=torch.long)
     m = ((v[sid][:, None] >> sid[None, :]) & 1).bool()
+    for i, c in enumerate(causal or []):
+        if c:  # nn.make_causal_mask inside the set
+            s, n = starts[i], lens[i]
+            m[s:s + n, s:s + n] &= torch.tril(torch.ones((n, n), dtype=torch.bool))
     return m.to(dev)
 
 
@@ -92,6 +96,42 @@ def test_attention_fwd_bwd(dev, B, L, H, Dh, masked, drop):
     # fused QKV bias gradient = column sums of dqkv (summed before the bf16 rounding of dqkv)
     torch.testing.assert_close(bgrad - 0.5, dqkv.float().sum((0, 1)), rtol=2e-2,
                                atol=2e-2 * float(dqkv.float().sum((0, 1)).abs().max()) + 1e-3)
+    for i in range(3):
+        assert rel(gk[:, :, i], gr[:, :, i]) < 2e-2, ("qkv"[i], rel(gk[:, :, i], gr[:, :, i]))
+
+
+@pytest.mark.parametrize("B,L,H,Dh,drop", [(2, 110, 3, 64, True), (2, 200, 2, 128, False),
+                                           (2, 74, 3, 256, True)])
+def test_attention_causal_text_sets(dev, B, L, H, Dh, drop):
+    """[Text{n}] [Image{m};Readout{4}]*2-like tables with CAUSAL Text sets (token_sequencer.py:
+    76-82): intra-set causal, the Text sets of both steps; Dh 64 / 128 / 256 (the reference's
+    octo_base has 3 heads of 256)."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    g = torch.Generator().manual_seed(L + Dh)
+    n_img = (L - 2 * 4 - 2 * 13) // 2
+    lens = [13, n_img, 4, 13, n_img, 4]
+    lens[-1] += L - sum(lens)
+    starts = [sum(lens[:i]) for i in range(len(lens))]
+    # Text_t sees Text/Image of t' <= t; Image_t same; Readout_t also itself
+    vis = [0b000001, 0b000011, 0b000111, 0b011011, 0b011011, 0b111011]
+    causal = [True, False, False, True, False, False]
+    table = K.SetTable(starts, lens, vis, causal)
+    mask = dense_mask(starts, lens, vis, L, dev, causal)
+    qkv = torch.randn((B, L, 3 * H * Dh), generator=g).bfloat16().to(dev)
+    scale = Dh ** -0.5
+    keep_prob = 0.9 if drop else 1.0
+    rng = torch.tensor([5, 2], dtype=torch.int32, device=dev)
+    bits = K.dropout_bits(rng, 1, 0, L, L, keep_prob) if drop else None
+    keep = bits_to_keep(bits[0], L).to(dev) if drop else None
+    o, lse = K.attn_fwd(qkv, H, scale, table, bits, keep_prob)
+    qf = qkv.float().requires_grad_()
+    ref = ref_attention(qf, H, scale, mask, keep, keep_prob)
+    assert rel(o, ref) < 1e-2
+    dout = torch.randn((B, L, H * Dh), generator=g).bfloat16().to(dev)
+    dqkv = K.attn_bwd(qkv, o, dout, lse, H, scale, table, bits, keep_prob)
+    ref.backward(dout.float())
+    gr = qf.grad.view(B, L, 3, H * Dh)
+    gk = dqkv.float().view(B, L, 3, H * Dh)
     for i in range(3):
         assert rel(gk[:, :, i], gr[:, :, i]) < 2e-2, ("qkv"[i], rel(gk[:, :, i], gr[:, :, i]))
 

@@ -106,6 +106,16 @@ def test_blockwise_base_hires_tome32(dev):
     P.check_blockwise(P.oracle_blockwise(cfg, res))
 
 
+def test_blockwise_causal_text(dev):
+    """A sequence with causal Text sets (token_sequencer.py:55-91: causal within the set, sees
+    earlier non-readout sets) over two observation steps, block-local bar."""
+    cfg = _cfg("octo-tiny", num_blocks=2, t5_layers=2, text_tokens=16,
+               input_sequence="[Text{8};Image{16};Readout{4}]*2", num_observation_blocks=2)
+    res = P.hip_blockwise(cfg, 2, seed=0)
+    assert any(res["model"].layer_sets[0][0].causal)
+    P.check_blockwise(P.oracle_blockwise(cfg, res))
+
+
 def test_staged_backward_matches_backward(dev):
     """The block-range stages used to overlap the gradient all-reduce (bench.py, N > 1) write
     the gradients of the one-piece backward (up to the order of the fp32 atomics some bias and
