@@ -273,45 +273,64 @@ struct Geo {
 };
 
 // =============================================================================== forward
-template <int DH>
-__global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(Geo g, AttnMask mask,
-                                                      const uint32_t* __restrict__ drop_bits,
-                                                      int drop_words, float drop_scale,
-                                                      const float* __restrict__ bias,
-                                                      bf16_t* __restrict__ o, int64_t o_s_b,
-                                                      int64_t o_s_t, float* __restrict__ lse) {
+// One workgroup = 4 waves over 128 NQ query rows of one (sample, head): wave w owns the NQ
+// 32-row query blocks w, w + 4, ..., each with its own Q fragments, O^T accumulators and
+// running max / sum. Every K/V tile is staged into LDS ONCE for all of them: with NQ = 3 one
+// workgroup covers L <= 384 rows, so K and V of a (sample, head) are read from HBM once (the
+// one-block-per-workgroup form read them once per 128 rows, 2.3x the algorithmic bytes at
+// L = 292) and each LDS tile feeds NQ x 16 MFMAs per wave instead of 16, which amortises the
+// per-tile barrier and the per-workgroup prologue.
+template <int DH, int NQ>
+__global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
+    Geo g, AttnMask mask, const uint32_t* __restrict__ drop_bits, int drop_words, float drop_scale,
+    const float* __restrict__ bias, bf16_t* __restrict__ o, int64_t o_s_b, int64_t o_s_t,
+    float* __restrict__ lse) {
   constexpr int STR = DH + 8;
   constexpr int NS = DH / 16;   // k-steps over the head dim
   constexpr int ND = DH / 32;   // 32-row d sub-tiles of O^T
   constexpr int TILE = KT * STR;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE];  // [buf][K | V]
+  // visibility word of every (query set, 64-key tile) pair, built once per workgroup
+  __shared__ uint64_t s_vis[MAX_SETS * (MAXL / KT)];
   const int b = blockIdx.z, h = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
   const int L = g.L, D = g.H * DH;
-  const int q0 = blockIdx.x * QB, q1 = min(L, q0 + QB);
-  const int q = q0 + wave * 32 + (lane & 31);
-  const bool qv = q < L;
-  const bool wave_live = q0 + wave * 32 < L;
+  const int q0 = blockIdx.x * (QB * NQ), q1 = min(L, q0 + QB * NQ);
   const bf16_t* base = g.qkv + (int64_t)b * g.s_b;
   const bf16_t* kbase = base + D + h * DH;
   const bf16_t* vbase = base + 2 * D + h * DH;
-
-  bf16x8 qf[NS];
-  const bf16_t* qrow = base + (int64_t)(qv ? q : 0) * g.s_t + h * DH;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) qf[s] = row_frag_global(qrow, qv, s, lane);
-  const int sq = qv ? set_of(mask, q) : 0;
-  const uint32_t visq = qv ? mask.vis[sq] : 0u;
-  const float* brow = bias ? bias + ((int64_t)h * L + (qv ? q : 0)) * L : nullptr;
   const float c = bias ? 1.f : g.scale * LOG2E;  // score -> log2 units (bias mode converts first)
 
-  floatx16 oacc[ND];
+  bf16x8 qf[NQ][NS];
+  floatx16 oacc[NQ][ND];
+  float m[NQ], l[NQ];
+  uint32_t visq[NQ];
+  int sq[NQ], qrow[NQ];
+  bool qv[NQ], live[NQ];
 #pragma unroll
-  for (int d = 0; d < ND; ++d)
+  for (int i = 0; i < NQ; ++i) {
+    const int qb = q0 + 32 * (wave + 4 * i);
+    qrow[i] = qb + (lane & 31);
+    qv[i] = qrow[i] < L;
+    live[i] = qb < L;  // wave-uniform
+    const bf16_t* qp = base + (int64_t)(qv[i] ? qrow[i] : 0) * g.s_t + h * DH;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
-  float m = -INFINITY, l = 0.f;
+    for (int s = 0; s < NS; ++s) qf[i][s] = row_frag_global(qp, qv[i], s, lane);
+    sq[i] = qv[i] ? set_of(mask, qrow[i]) : 0;
+    visq[i] = qv[i] ? mask.vis[sq[i]] : 0u;
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[i][d][r] = 0.f;
+    m[i] = -INFINITY;
+    l[i] = 0.f;
+  }
 
+  const int ntiles = (L + KT - 1) / KT;
+  for (int e = threadIdx.x; e < mask.n_sets * ntiles; e += NT) {
+    const int st = e / ntiles, t = e - st * ntiles;
+    s_vis[st * ntiles + t] = sets_bits(mask, mask.vis[st], t * KT);
+  }
   TilePair<DH> pf;
   int kt = next_key_tile(mask, q0, q1, 0, L);
   if (kt < L) {
@@ -325,9 +344,15 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(Geo g, A
     if (kn < L) pf.load(kbase, g.s_t, vbase, g.s_t, kn, L);
     const bf16_t* Ks = smem + buf * 2 * TILE;
     const bf16_t* Vs = Ks + TILE;
-    if (wave_live) {
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      if (!live[i]) continue;
+      uint64_t vm = qv[i] ? s_vis[sq[i] * ntiles + kt / KT] : 0ull;
+      if (mask.causal) vm = causal_keys(mask, sq[i], qrow[i], kt, vm);
+      if (__all(vm == 0ull)) continue;  // no query of this block sees the tile
+      const int q = qrow[i];
       uint32_t dw[2];
-      load_drop_words(drop_bits, drop_words, qv ? q : 0, qv, kt, dw);
+      load_drop_words(drop_bits, drop_words, qv[i] ? q : 0, qv[i], kt, dw);
       floatx16 sacc[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -336,11 +361,10 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(Geo g, A
 #pragma unroll
         for (int s = 0; s < NS; ++s)
           sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<STR>(Ks, 32 * u, s, lane),
-                                                            qf[s], sacc[u], 0, 0, 0);
+                                                            qf[i][s], sacc[u], 0, 0, 0);
       }
-      uint64_t vm = sets_bits(mask, visq, kt);
-      if (mask.causal) vm = causal_keys(mask, sq, q, kt, vm);
-      if (brow) {  // registers 4 r4 .. 4 r4 + 3 hold 4 consecutive keys: one float4 (L % 4 == 0)
+      if (bias) {  // registers 4 r4 .. 4 r4 + 3 hold 4 consecutive keys: one float4 (L % 4 == 0)
+        const float* brow = bias + ((int64_t)h * L + (qv[i] ? q : 0)) * L;
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -371,9 +395,9 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(Geo g, A
 #pragma unroll
         for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sacc[u][r]);
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mn = fmaxf(m, tmax);
+      const float mn = fmaxf(m[i], tmax);
       const float mnc = mn == -INFINITY ? 0.f : mn * c;
-      const float alpha = fast_exp2(m * c - mnc);  // m = -inf -> 0 (nothing accumulated yet)
+      const float alpha = fast_exp2(m[i] * c - mnc);  // m = -inf -> 0 (nothing accumulated yet)
       float rs = 0.f;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -386,23 +410,23 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(Geo g, A
         }
       }
       rs += __shfl_xor(rs, 32, 64);
-      l = l * alpha + rs;
-      m = mn;
+      l[i] = l[i] * alpha + rs;
+      m[i] = mn;
       if (!__all(alpha == 1.f)) {
 #pragma unroll
         for (int d = 0; d < ND; ++d)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+          for (int r = 0; r < 16; ++r) oacc[i][d][r] *= alpha;
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const bf16x8 p0 = pack_frag(sacc[u], 0), p1 = pack_frag(sacc[u], 1);
 #pragma unroll
         for (int d = 0; d < ND; ++d) {
-          oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trans_frag<STR>(Vs, 32 * u, 32 * d, lane),
-                                                            p0, oacc[d], 0, 0, 0);
-          oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              trans_frag<STR>(Vs, 32 * u + 16, 32 * d, lane), p1, oacc[d], 0, 0, 0);
+          oacc[i][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              trans_frag<STR>(Vs, 32 * u, 32 * d, lane), p0, oacc[i][d], 0, 0, 0);
+          oacc[i][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              trans_frag<STR>(Vs, 32 * u + 16, 32 * d, lane), p1, oacc[i][d], 0, 0, 0);
         }
       }
     }
@@ -411,8 +435,11 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(Geo g, A
     buf ^= 1;
     kt = kn;
   }
-  if (qv) {
-    const float inv = l > 0.f ? drop_scale / l : 0.f;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    if (!qv[i]) continue;
+    const int q = qrow[i];
+    const float inv = l[i] > 0.f ? drop_scale / l[i] : 0.f;
     bf16_t* orow = o + (int64_t)b * o_s_b + (int64_t)q * o_s_t + h * DH;
 #pragma unroll
     for (int d = 0; d < ND; ++d)
@@ -420,11 +447,12 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(Geo g, A
       for (int r4 = 0; r4 < 4; ++r4) {
         const int dd = 32 * d + 8 * r4 + 4 * hh;
         uint2 w;
-        w.x = (uint32_t)f2bf(oacc[d][4 * r4] * inv) | ((uint32_t)f2bf(oacc[d][4 * r4 + 1] * inv) << 16);
-        w.y = (uint32_t)f2bf(oacc[d][4 * r4 + 2] * inv) | ((uint32_t)f2bf(oacc[d][4 * r4 + 3] * inv) << 16);
+        w.x = (uint32_t)f2bf(oacc[i][d][4 * r4] * inv) | ((uint32_t)f2bf(oacc[i][d][4 * r4 + 1] * inv) << 16);
+        w.y = (uint32_t)f2bf(oacc[i][d][4 * r4 + 2] * inv) | ((uint32_t)f2bf(oacc[i][d][4 * r4 + 3] * inv) << 16);
         *reinterpret_cast<uint2*>(orow + dd) = w;
       }
-    if (lane < 32) lse[((int64_t)b * g.H + h) * L + q] = l > 0.f ? m * c * LN2 + logf(l) : -INFINITY;
+    if (lane < 32)
+      lse[((int64_t)b * g.H + h) * L + q] = l[i] > 0.f ? m[i] * c * LN2 + logf(l[i]) : -INFINITY;
   }
 }
 
@@ -810,6 +838,9 @@ int fill_mask(AttnMask& m, int n_sets, const int32_t* starts, const int32_t* len
 
 }  // namespace
 
+// forward query blocks per wave (0: automatic); MMT_ATTN_NQ=1..3 forces it (benchmarks)
+static const int g_attn_nq = getenv("MMT_ATTN_NQ") ? atoi(getenv("MMT_ATTN_NQ")) : 0;
+
 #define ATTN_DISPATCH(DH_, ...)                                  \
   do {                                                           \
     if (Dh == 64) { constexpr int DH_ = 64; __VA_ARGS__; }       \
@@ -868,11 +899,24 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   if (rc) return rc;
   Geo g{(const bf16_t*)qkv, s_b, s_t, L, H, scale};
   const int words = (L + 31) / 32;
-  dim3 grid((L + QB - 1) / QB, H, B);
   const float dscale = drop_bits ? 1.f / keep_prob : 1.f;
-  ATTN_DISPATCH(DH, hipLaunchKernelGGL(attn_fwd_kernel<DH>, grid, dim3(NT), 0, as_stream(stream),
-                                       g, m, drop_bits, words, dscale, bias, (bf16_t*)o,
-                                       o_s_b, o_s_t, lse));
+  // query blocks per wave: enough for one workgroup to cover L (K/V read once per (b, h)) at
+  // Dh 64; Dh 128 / 256 keep one (registers)
+  const int nqb = (L + 31) / 32;
+  int nq = g_attn_nq > 0 ? g_attn_nq : std::min(3, (nqb + 3) / 4);
+  if (Dh > 64) nq = 1;
+  dim3 grid((L + QB * nq - 1) / (QB * nq), H, B);
+#define FWD(DH_, NQ_)                                                                            \
+  hipLaunchKernelGGL((attn_fwd_kernel<DH_, NQ_>), grid, dim3(NT), 0, as_stream(stream), g, m,   \
+                     drop_bits, words, dscale, bias, (bf16_t*)o, o_s_b, o_s_t, lse)
+  if (Dh == 64) {
+    if (nq == 3) FWD(64, 3);
+    else if (nq == 2) FWD(64, 2);
+    else FWD(64, 1);
+  } else {
+    ATTN_DISPATCH(DH, FWD(DH, 1));
+  }
+#undef FWD
   MMT_CHECK_LAUNCH("mmt_attn_fwd");
   return MMT_OK;
 }
