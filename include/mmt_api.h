@@ -163,6 +163,20 @@ int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t lda, const 
              int64_t sB, int64_t sC, int split_k, const mmt_epilogue_t* epi, float* workspace,
              int64_t ws_elems, mmt_stream_t stream);
 
+/* FP8 weight path (BASELINE configs[4]; SURVEY §8c bar cosine >= 0.995): forward Dense products
+ * in OCP e4m3 with one fp32 scale per activation row and per weight row (output channel).
+ * mmt_quant_rows_fp8: scale[r] = amax|x[r,:]| / 448 (1 for a zero row), q[r,k] = e4m3(x[r,k] /
+ * scale[r]) rounded to nearest even; x bf16 rows (stride ld), q uint8 rows (stride ldq), K % 8 == 0.
+ * mmt_gemm_fp8: C = epilogue((A_q . B_q^T)[m][n] * sa[m] * sb[n]) with A_q [M][lda], B_q [N][ldb]
+ * e4m3 (the NT form of mmt_gemm: B is the weight W[out][in]), on the block-scaled
+ * v_mfma_scale_f32_32x32x64_f8f6f4 (unit block scales); same epilogue as mmt_gemm; c_mode
+ * MMT_OUT_BF16 or MMT_OUT_F32. K % 64 == 0, N % 8 == 0, 16-B aligned rows. */
+int mmt_quant_rows_fp8(const void* x, int64_t ld, int rows, int K, void* q, int64_t ldq,
+                       float* scale, mmt_stream_t stream);
+int mmt_gemm_fp8(int M, int N, int K, const void* A, int64_t lda, const float* sa, const void* B,
+                 int64_t ldb, const float* sb, void* C, int c_mode, int64_t ldc,
+                 const mmt_epilogue_t* epi, mmt_stream_t stream);
+
 /* ------------------------------------------------------------------ attention
  * Blockwise-causal MHA replacing flax.linen.SelfAttention / dot_product_attention as the
  * reference configures it (vanilla_decoder.yaml:19-31, mask token_sequencer.py:313-321,

@@ -177,6 +177,44 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
     return out
 
 
+def quant_rows_fp8(x2d: torch.Tensor, out=None, scale=None):
+    """bf16 (R, K) rows -> (e4m3 uint8 (R, K), fp32 scale (R,)): scale = amax / 448 per row."""
+    _dev(x2d)
+    if x2d.dtype != torch.bfloat16 or x2d.dim() != 2 or x2d.stride(1) != 1:
+        raise ValueError("quant_rows_fp8 takes bf16 (rows, K) with unit inner stride")
+    R, Kd = x2d.shape
+    out = torch.empty((R, Kd), dtype=torch.uint8, device=x2d.device) if out is None else out
+    scale = torch.empty(R, dtype=torch.float32, device=x2d.device) if scale is None else scale
+    _C.call("mmt_quant_rows_fp8", ptr(x2d), x2d.stride(0), R, Kd, ptr(out), out.stride(0),
+            ptr(scale), _C.stream_ptr())
+    return out, scale
+
+
+def gemm_fp8(aq: torch.Tensor, sa: torch.Tensor, bq: torch.Tensor, sb: torch.Tensor,
+             out: torch.Tensor | None = None, out_mode: int = OUT_BF16, **epi):
+    """(aq (M, K) e4m3 . bq (N, K)^T e4m3) * sa[m] * sb[n] with the GEMM epilogue."""
+    _dev(aq, sa, bq, sb, out)
+    if aq.dtype != torch.uint8 or bq.dtype != torch.uint8:
+        raise TypeError("gemm_fp8 operands are e4m3 bytes (uint8)")
+    M, Kd = aq.shape
+    N, Kb = bq.shape
+    if Kd != Kb or sa.numel() != M or sb.numel() != N:
+        raise ValueError("gemm_fp8 shapes")
+    if out_mode not in (OUT_BF16, OUT_F32):
+        raise ValueError("gemm_fp8 writes bf16 or fp32")
+    odt = torch.bfloat16 if out_mode == OUT_BF16 else torch.float32
+    if out is None:
+        out = torch.empty((M, N), dtype=odt, device=aq.device)
+    for name, dts in (("gate", (torch.bfloat16,)), ("residual", (torch.bfloat16, torch.float32))):
+        t = epi.get(name)
+        if t is not None and (tuple(t.shape) != (M, N) or t.dtype not in dts or t.stride(-1) != 1):
+            raise ValueError(f"gemm_fp8 {name} must be {dts} (M, N) with unit inner stride")
+    e = _epi(**epi)
+    _C.call("mmt_gemm_fp8", M, N, Kd, ptr(aq), aq.stride(0), ptr(sa), ptr(bq), bq.stride(0), ptr(sb),
+            ptr(out), out_mode, out.stride(0), _C.ctypes.byref(e), _C.stream_ptr())
+    return out
+
+
 # ----------------------------------------------------------------------------- top-k pruning
 def topk_gather(x: torch.Tensor, scores: torch.Tensor, tokenset_idx, tokenset_k):
     """x (B, L, D) fp32/bf16, scores (B, L) fp32; tokenset_idx [(start, num)], tokenset_k [k].

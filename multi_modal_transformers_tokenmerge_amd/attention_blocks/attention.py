@@ -59,9 +59,9 @@ class MLPBlock:
     """attention.py:20-39."""
 
     def __init__(self, store: ParamStore, name: str, in_f: int, hidden: int, out_f: int,
-                 dropout_rate: float = 0.1):
-        self.dense = Dense(store, f"{name}/Dense_0", in_f, hidden)
-        self.dense_out = Dense(store, f"{name}/Dense_1", hidden, out_f)
+                 dropout_rate: float = 0.1, fp8: bool = False):
+        self.dense = Dense(store, f"{name}/Dense_0", in_f, hidden, fp8=fp8)
+        self.dense_out = Dense(store, f"{name}/Dense_1", hidden, out_f, fp8=fp8)
         self.rate = dropout_rate
 
 
@@ -69,15 +69,18 @@ class Encoder1DBlock:
     """attention.py:41-69 (+ ToMe between the attention residual and LN1)."""
 
     def __init__(self, store: ParamStore, name: str, D: int, num_heads: int, mlp_dim: int,
-                 eps: float = 1e-6, dropout_rate: float = 0.1, attn_dropout_rate: float = 0.1):
+                 eps: float = 1e-6, dropout_rate: float = 0.1, attn_dropout_rate: float = 0.1,
+                 fp8: bool = False):
         if D % num_heads:
             raise ValueError("qkv_features must be divisible by num_heads")
         self.D, self.H, self.Dh, self.M = D, num_heads, D // num_heads, mlp_dim
         self.ln0 = SeqLayerNorm(store, f"{name}/LayerNorm_0", D, eps)
-        self.qkv = Dense(store, f"{name}/SelfAttention_0/qkv", D, 3 * D, kernel_init=he_normal((D, D)))
-        self.out = Dense(store, f"{name}/SelfAttention_0/out", D, D, kernel_init=he_normal((D, D)))
+        self.qkv = Dense(store, f"{name}/SelfAttention_0/qkv", D, 3 * D, kernel_init=he_normal((D, D)),
+                         fp8=fp8)
+        self.out = Dense(store, f"{name}/SelfAttention_0/out", D, D, kernel_init=he_normal((D, D)),
+                         fp8=fp8)
         self.ln1 = SeqLayerNorm(store, f"{name}/LayerNorm_1", D, eps)
-        self.mlp = MLPBlock(store, f"{name}/MLPBlock_0", D, mlp_dim, D, dropout_rate)
+        self.mlp = MLPBlock(store, f"{name}/MLPBlock_0", D, mlp_dim, D, dropout_rate, fp8=fp8)
         self.rate = dropout_rate
         self.attn_rate = attn_dropout_rate
         self.scale = self.Dh ** -0.5
@@ -178,9 +181,10 @@ class StackedEncoder1DBlock:
 
     def __init__(self, store: ParamStore, name: str, num_blocks: int, D: int, num_heads: int,
                  mlp_dim: int, eps: float = 1e-6, dropout_rate: float = 0.1,
-                 attn_dropout_rate: float = 0.1):
+                 attn_dropout_rate: float = 0.1, fp8: bool = False):
         self.blocks = [Encoder1DBlock(store, f"{name}/Block_{i}", D, num_heads, mlp_dim, eps,
-                                      dropout_rate, attn_dropout_rate) for i in range(num_blocks)]
+                                      dropout_rate, attn_dropout_rate, fp8)
+                       for i in range(num_blocks)]
 
     def forward(self, x, ctxs: List[LayerCtx]):
         saved = []

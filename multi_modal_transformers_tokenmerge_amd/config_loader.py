@@ -270,6 +270,7 @@ def octo_config_from_yaml(cfg: dict, name: str = "yaml"):
     # text: the sequence string fixes the number of text tokens (TaskDescriptionPrefix{n})
     m = re.findall(r"(?:TaskDescriptionPrefix|Text)\{(\d+)\}", kw["input_sequence"])
     kw["text_tokens"] = int(cfg.get("text_tokens", sum(int(v) for v in m)))
+    kw["fp8"] = bool(cfg.get("fp8_matmul", False))
     t5_layers = cfg.get("t5_num_layers")
     if t5_layers:
         kw["t5"] = T5Config(num_layers=int(t5_layers))

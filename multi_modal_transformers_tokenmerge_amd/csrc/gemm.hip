@@ -1125,6 +1125,160 @@ __global__ void splitk_epilogue_kernel(const float* __restrict__ ws, int split, 
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// FP8 (OCP e4m3) forward GEMM for the fp8 weight path (BASELINE configs[4]): C = epilogue(
+// (A_q . B_q^T) * sa[m] * sb[n]) with A_q [M][K] e4m3 (activation rows quantised with one scale
+// per row) and B_q [N][K] e4m3 (weight rows = output channels, one scale each). The products run
+// on v_mfma_scale_f32_32x32x64_f8f6f4 with unit E8M0 block scales (the row / channel scales are
+// applied exactly once in the epilogue, where they factor out of the K sum): twice the bf16 MFMA
+// rate. Operands swapped (acc = C^T) so a lane holds one output row and four runs of 4 columns.
+// Any consistent k order works for the MX operands (the hardware pairs byte j of lane half h of
+// A with byte j of lane half h of B): lane (r, h) takes bytes 32h .. 32h+31 of its row's 64-byte
+// K-step (tools/fp8_mfma_probe.hip checks the pairing with exact integers).
+// 128 x 128 tiles, 4 waves as 2 x 2 of 64 x 64, K-steps of 64 bytes, double-buffered LDS rows
+// padded to 80 bytes, register-staged loads one K-step ahead. Requires K % 64 == 0, N % 8 == 0.
+constexpr int F8_BM = 128, F8_BN = 128, F8_RS = 80;
+typedef int v8i __attribute__((ext_vector_type(8)));
+
+template <int OUT>
+__global__ __launch_bounds__(256, 2) void gemm_fp8_nt_kernel(
+    int M, int N, int K, const uint8_t* __restrict__ A, int64_t lda, const float* __restrict__ sa,
+    const uint8_t* __restrict__ B, int64_t ldb, const float* __restrict__ sb, void* __restrict__ Cv,
+    int64_t ldc, int tiles_n, int n_work, Epi epi) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2][2][F8_BM * F8_RS];  // [stage][A | B]
+  const int wi = xcd_remap(blockIdx.x, gridDim.x);
+  if (wi >= n_work) return;
+  const int tm = wi / tiles_n, tn = wi - tm * tiles_n;
+  const int m0 = tm * F8_BM, n0 = tn * F8_BN;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  uint32_t key = 0;
+  if (epi.rng) key = stream_key(epi.rng[0], epi.rng[1], epi.drop_layer, epi.drop_site);
+  // global -> register staging: 2 x 16 B of A and of B per thread per K-step (128 rows x 64 B)
+  uint4 ra[2], rb[2];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = threadIdx.x + 256 * q, row = c >> 2, ch = c & 3;
+      ra[q] = *reinterpret_cast<const uint4*>(A + (int64_t)min(m0 + row, M - 1) * lda + k0 + 16 * ch);
+      rb[q] = *reinterpret_cast<const uint4*>(B + (int64_t)min(n0 + row, N - 1) * ldb + k0 + 16 * ch);
+    }
+  };
+  auto lstore = [&](int st) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = threadIdx.x + 256 * q, row = c >> 2, ch = c & 3;
+      const uint32_t ma = m0 + row < M ? 0xffffffffu : 0u;
+      *reinterpret_cast<uint4*>(&smem[st][0][row * F8_RS + 16 * ch]) =
+          make_uint4(ra[q].x & ma, ra[q].y & ma, ra[q].z & ma, ra[q].w & ma);
+      *reinterpret_cast<uint4*>(&smem[st][1][row * F8_RS + 16 * ch]) = rb[q];
+    }
+  };
+  typedef float floatx16_t __attribute__((ext_vector_type(16)));
+  floatx16_t acc[2][2];  // [n sub-tile][m sub-tile]: C^T
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const int nk = K / 64;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * 64);
+    const uint8_t* As = smem[st][0];
+    const uint8_t* Bs = smem[st][1];
+    v8i xf[2], wf[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const uint8_t* pa = As + (wm * 64 + 32 * t + (lane & 31)) * F8_RS + 32 * (lane >> 5);
+      const uint8_t* pb = Bs + (wn * 64 + 32 * t + (lane & 31)) * F8_RS + 32 * (lane >> 5);
+      const uint4 a0 = *reinterpret_cast<const uint4*>(pa), a1 = *reinterpret_cast<const uint4*>(pa + 16);
+      const uint4 b0 = *reinterpret_cast<const uint4*>(pb), b1 = *reinterpret_cast<const uint4*>(pb + 16);
+      xf[t] = v8i{(int)a0.x, (int)a0.y, (int)a0.z, (int)a0.w, (int)a1.x, (int)a1.y, (int)a1.z, (int)a1.w};
+      wf[t] = v8i{(int)b0.x, (int)b0.y, (int)b0.z, (int)b0.w, (int)b1.x, (int)b1.y, (int)b1.z, (int)b1.w};
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[a], xf[b], acc[a][b], 0, 0, 0,
+                                                                     127, 0, 127);
+    if (kt + 1 < nk) {
+      // stage st^1 was last read in step kt-1, before the barrier that closed it
+      lstore(st ^ 1);
+      __syncthreads();
+    }
+  }
+  // epilogue: lane = output row m; registers 4 g .. 4 g + 3 = columns n + 8 g + 4 h .. + 3
+  const int hh = lane >> 5;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int gr = m0 + wm * 64 + 32 * b + (lane & 31);
+    if (gr >= M) continue;
+    const float s_row = sa[gr];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int gc = n0 + wn * 64 + 32 * a + 8 * g4 + 4 * hh;
+        if (gc >= N) continue;
+        float v[4];
+        const float4 sw = *reinterpret_cast<const float4*>(sb + gc);
+        v[0] = acc[a][b][4 * g4] * s_row * sw.x;
+        v[1] = acc[a][b][4 * g4 + 1] * s_row * sw.y;
+        v[2] = acc[a][b][4 * g4 + 2] * s_row * sw.z;
+        v[3] = acc[a][b][4 * g4 + 3] * s_row * sw.w;
+        epilogue_w<4>(epi, key, N, gr, gc, v);
+        store_w<OUT, 4>(Cv, (int64_t)gr * ldc + gc, epi.beta, v);
+      }
+  }
+}
+
+// Row-wise e4m3 quantisation: scale[r] = amax(|x[r, :]|) / 448 (1 for an all-zero row),
+// q[r, k] = e4m3(x[r, k] / scale[r]) with round-to-nearest-even (v_cvt_pk_fp8_f32, OCP).
+// One wave per row; bf16 input rows with stride ld (16-B aligned), K % 8 == 0.
+__global__ __launch_bounds__(256) void quant_rows_fp8_kernel(const bf16_t* __restrict__ x, int64_t ld,
+                                                             int rows, int K, uint8_t* __restrict__ q,
+                                                             int64_t ldq, float* __restrict__ scale) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const bf16_t* xr = x + (int64_t)row * ld;
+  float amax = 0.f;
+  for (int k = lane * 8; k < K; k += 512) {
+    const uint4 u = *reinterpret_cast<const uint4*>(xr + k);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      amax = fmaxf(amax, fmaxf(fabsf(__uint_as_float(w[e] << 16)), fabsf(__uint_as_float(w[e] & 0xffff0000u))));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+  const float sc = amax > 0.f ? __fdiv_rn(amax, 448.f) : 1.f;
+  if (lane == 0) scale[row] = sc;
+  uint8_t* qr = q + (int64_t)row * ldq;
+  for (int k = lane * 8; k < K; k += 512) {
+    const uint4 u = *reinterpret_cast<const uint4*>(xr + k);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+    uint32_t out[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float f0 = __fdiv_rn(__uint_as_float(w[2 * e] << 16), sc);
+      const float f1 = __fdiv_rn(__uint_as_float(w[2 * e] & 0xffff0000u), sc);
+      const float f2 = __fdiv_rn(__uint_as_float(w[2 * e + 1] << 16), sc);
+      const float f3 = __fdiv_rn(__uint_as_float(w[2 * e + 1] & 0xffff0000u), sc);
+      int pk = __builtin_amdgcn_cvt_pk_fp8_f32(f0, f1, 0, false);
+      pk = __builtin_amdgcn_cvt_pk_fp8_f32(f2, f3, pk, true);
+      out[e] = (uint32_t)pk;
+    }
+    *reinterpret_cast<uint2*>(qr + k) = make_uint2(out[0], out[1]);
+  }
+}
+
 }  // namespace
 
 extern "C" void mmt_gemm_set_variant(int v) { g_variant = v; }
@@ -1299,5 +1453,60 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
                          split_k, M, N, C, ldc, epi);
     MMT_CHECK_LAUNCH("mmt_gemm(split-K combine)");
   }
+  return MMT_OK;
+}
+
+extern "C" int mmt_quant_rows_fp8(const void* x, int64_t ld, int rows, int K, void* q, int64_t ldq,
+                                  float* scale, mmt_stream_t stream) {
+  MMT_CHECK_ARG(x && q && scale && rows > 0 && K > 0 && K % 8 == 0 && ld % 8 == 0 && ldq % 8 == 0 &&
+                    (uintptr_t)x % 16 == 0 && (uintptr_t)q % 8 == 0,
+                "mmt_quant_rows_fp8: args (K %% 8 == 0, 16-B aligned rows)");
+  hipLaunchKernelGGL(quant_rows_fp8_kernel, dim3((rows + 3) / 4), dim3(256), 0, as_stream(stream),
+                     (const bf16_t*)x, ld, rows, K, (uint8_t*)q, ldq, scale);
+  MMT_CHECK_LAUNCH("mmt_quant_rows_fp8");
+  return MMT_OK;
+}
+
+extern "C" int mmt_gemm_fp8(int M, int N, int K, const void* A, int64_t lda, const float* sa,
+                            const void* B, int64_t ldb, const float* sb, void* C, int c_mode,
+                            int64_t ldc, const mmt_epilogue_t* e, mmt_stream_t stream) {
+  MMT_CHECK_ARG(A && B && C && sa && sb && M > 0 && N > 0 && K > 0, "mmt_gemm_fp8: args");
+  MMT_CHECK_ARG(K % 64 == 0 && N % 8 == 0 && lda % 16 == 0 && ldb % 16 == 0 && ldc % 8 == 0 &&
+                    (uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0 && (uintptr_t)C % 16 == 0 &&
+                    (uintptr_t)sb % 16 == 0,
+                "mmt_gemm_fp8: K %% 64, N %% 8, 16-B aligned operands / rows / channel scales");
+  MMT_CHECK_ARG(c_mode == MMT_OUT_BF16 || c_mode == MMT_OUT_F32, "mmt_gemm_fp8: c_mode");
+  Epi epi{};
+  epi.alpha = 1.f;
+  if (e) {
+    epi.bias = e->bias;
+    epi.act = e->act;
+    epi.rng = e->rng;
+    epi.drop_layer = e->drop_layer;
+    epi.drop_site = e->drop_site;
+    MMT_CHECK_ARG(!e->rng || (e->keep_prob > 0.f && e->keep_prob <= 1.f), "mmt_gemm_fp8: keep_prob");
+    epi.keep_thresh16 = e->rng ? keep_threshold16(e->keep_prob) : 65536u;
+    epi.drop_scale = e->rng ? 1.f / e->keep_prob : 1.f;
+    epi.drop_row_offset = e->drop_row_offset;
+    epi.gate = (const bf16_t*)e->gate;
+    epi.ld_gate = e->ld_gate;
+    epi.gate_scale = e->gate_scale;
+    epi.residual = e->residual;
+    epi.res_f32 = e->res_dtype == MMT_F32;
+    epi.ld_res = e->ld_res;
+    epi.alpha = e->alpha;
+    epi.beta = e->beta;
+  }
+  const int tiles_n = (N + F8_BN - 1) / F8_BN, n_work = ((M + F8_BM - 1) / F8_BM) * tiles_n;
+  hipStream_t s = as_stream(stream);
+  if (c_mode == MMT_OUT_BF16)
+    hipLaunchKernelGGL(gemm_fp8_nt_kernel<0>, dim3(n_work), dim3(256), 0, s, M, N, K,
+                       (const uint8_t*)A, lda, sa, (const uint8_t*)B, ldb, sb, C, ldc, tiles_n,
+                       n_work, epi);
+  else
+    hipLaunchKernelGGL(gemm_fp8_nt_kernel<1>, dim3(n_work), dim3(256), 0, s, M, N, K,
+                       (const uint8_t*)A, lda, sa, (const uint8_t*)B, ldb, sb, C, ldc, tiles_n,
+                       n_work, epi);
+  MMT_CHECK_LAUNCH("mmt_gemm_fp8");
   return MMT_OK;
 }

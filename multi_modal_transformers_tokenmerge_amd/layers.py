@@ -33,13 +33,20 @@ class Dense:
     the NT GEMM y = x W^T and the GEMM reads both operands along the reduction)."""
 
     def __init__(self, store: ParamStore, name: str, in_f: int, out_f: int, use_bias: bool = True,
-                 kernel_init=None, bias_init=None):
+                 kernel_init=None, bias_init=None, fp8: bool = False):
         self.in_f, self.out_f = in_f, out_f
+        # fp8: the forward product runs in e4m3 (per-row activation scales, per-output-channel
+        # weight scales, csrc/gemm.hip gemm_fp8_nt_kernel); the backward stays bf16 (straight-through)
+        self.fp8 = fp8
         self.w = store.add(f"{name}/kernel", (out_f, in_f), kernel_init or he_normal((in_f, out_f)),
-                           transposed=True)
+                           transposed=True, fp8=fp8)
         self.b = store.add(f"{name}/bias", (out_f,), bias_init or normal(0.01)) if use_bias else None
 
     def fwd(self, x2d: torch.Tensor, out=None, out_mode=K.OUT_BF16, **epi) -> torch.Tensor:
+        if self.fp8:
+            xq, sx = K.quant_rows_fp8(x2d)
+            return K.gemm_fp8(xq, sx, self.w.q8, self.w.q8_scale, out=out, out_mode=out_mode,
+                              bias=self.b.data if self.b else None, **epi)
         return K.gemm(x2d, self.w.bf16, trans_b=True, bias=self.b.data if self.b else None,
                       out=out, out_mode=out_mode, **epi)
 

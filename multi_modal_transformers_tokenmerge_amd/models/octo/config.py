@@ -40,6 +40,8 @@ class OctoConfig:
     text_tokens: int = 32
     # ResNetV2Block hyper-parameters (gato_resnet.yaml:41-104); None = the build defaults
     stem: Optional[dict] = None
+    # fp8 weight path (BASELINE configs[4]): the encoder blocks' Dense forward products in e4m3
+    fp8: bool = False
 
     @property
     def tome_r(self) -> int:
@@ -65,11 +67,11 @@ PRESETS = {
         name="octo-base-2cam", token_embedding_dim=768, num_heads=12, mlp_dim=3072,
         input_sequence="[TaskDescriptionPrefix{32}] [Image{256};Image{256};Readout{4}]*2",
         num_observation_blocks=2),
-    # configs[4]: base hi-res 512^2, ToMe r=32 (bf16 here; the fp8 weight path is not built)
+    # configs[4]: base hi-res 512^2, ToMe r=32, fp8 weight path
     "octo-base-hires-tome32": OctoConfig(
         name="octo-base-hires-tome32", token_embedding_dim=768, num_heads=12, mlp_dim=3072,
         image_size=(512, 512, 3), input_sequence="[TaskDescriptionPrefix{32}] [Image{1024};Readout{4}]",
-        token_compression_sequence="[TaskDescriptionPrefix{0}] [Image{32};Readout{0}]"),
+        token_compression_sequence="[TaskDescriptionPrefix{0}] [Image{32};Readout{0}]", fp8=True),
 }
 
 

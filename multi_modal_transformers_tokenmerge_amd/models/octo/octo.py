@@ -78,7 +78,8 @@ class Octo:
                                    (self.L0, D), normal(0.02))
         self.stack = StackedEncoder1DBlock(store, "StackedEncoder1DBlock_0", cfg.num_blocks, D,
                                            cfg.num_heads, cfg.mlp_dim, cfg.layer_norm_eps,
-                                           cfg.dropout_rate, cfg.attention_dropout_rate)
+                                           cfg.dropout_rate, cfg.attention_dropout_rate,
+                                           fp8=cfg.fp8)
         # ---- head
         self.head = DiffusionActionHead(store, "diffusion_action_head", D, cfg.action_space_dim,
                                         cfg.diffusion_steps)
@@ -421,6 +422,7 @@ class OCTOTrainState:
                 tx.b2, tx.eps, tx.weight_decay, getattr(self.allreduce, "grad_scale", 1.0),
                 _C.stream_ptr())
         s.refresh_transposed()
+        s.refresh_fp8()
         _C.call("mmt_step_advance", _C.ptr(self.rng), _C.stream_ptr())
 
 

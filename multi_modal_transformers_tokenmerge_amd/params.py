@@ -80,6 +80,9 @@ class Param:
     bf16: torch.Tensor | None = None      # bf16 shadow view
     transposed: bool = False              # also keep a transposed bf16 shadow (2-D weights)
     bf16_t: torch.Tensor | None = None    # its (cols, rows) view
+    fp8: bool = False                     # also keep an e4m3 shadow with one scale per row
+    q8: torch.Tensor | None = None        # (rows, cols) uint8 e4m3 view
+    q8_scale: torch.Tensor | None = None  # (rows,) fp32
     grad: torch.Tensor | None = None      # fp32 grad view
 
     @property
@@ -94,12 +97,12 @@ class ParamStore:
         self.n = 0
         self.flat = self.flat_bf16 = self.flat_grad = self.m = self.v = None
 
-    def add(self, name: str, shape, init, transposed: bool = False) -> Param:
+    def add(self, name: str, shape, init, transposed: bool = False, fp8: bool = False) -> Param:
         if name in self.by_name:
             raise KeyError(f"duplicate parameter {name}")
-        if transposed and len(shape) != 2:
-            raise ValueError("only 2-D parameters keep a transposed shadow")
-        p = Param(name, tuple(int(s) for s in shape), init, transposed=transposed)
+        if (transposed or fp8) and len(shape) != 2:
+            raise ValueError("only 2-D parameters keep transposed / fp8 shadows")
+        p = Param(name, tuple(int(s) for s in shape), init, transposed=transposed, fp8=fp8)
         p.offset = self.n
         self.n += (p.numel + ALIGN - 1) // ALIGN * ALIGN
         self.params.append(p)
@@ -124,6 +127,11 @@ class ParamStore:
         tps = [p for p in self.params if p.transposed]
         self.flat_bf16_t = torch.zeros_like(self.flat_bf16) if tps else None
         self._t_desc, self._t_tiles = None, 0
+        # e4m3 shadows (+ one fp32 scale per row) of the fp8-path weights, same offsets
+        f8 = [p for p in self.params if p.fp8]
+        self.flat_fp8 = torch.zeros(self.n, dtype=torch.uint8, device=device) if f8 else None
+        n_rows = sum((p.shape[0] + 3) // 4 * 4 for p in f8)
+        self.fp8_scale = torch.ones(max(n_rows, 1), dtype=torch.float32, device=device) if f8 else None
         if tps:
             rows = []
             tiles = 0
@@ -135,7 +143,20 @@ class ParamStore:
             self._t_tiles = tiles
         self._bind()
         self.refresh_transposed()
+        self.refresh_fp8()
         return self
+
+    def refresh_fp8(self):
+        """Re-quantise the e4m3 weight shadows from the bf16 shadow (one launch per weight,
+        captured into the step graph after AdamW)."""
+        if self.flat_fp8 is None:
+            return
+        if not self.flat_bf16.is_cuda:
+            raise RuntimeError("fp8 shadows live on the device")
+        from . import _kernels as K
+        for p in self.params:
+            if p.fp8:
+                K.quant_rows_fp8(p.bf16, out=p.q8, scale=p.q8_scale)
 
     def refresh_transposed(self):
         """Re-derive the transposed bf16 shadows from the bf16 shadow (one batched launch; on a
@@ -159,6 +180,12 @@ class ParamStore:
             p.grad = self.flat_grad[sl].view(p.shape)
             if p.transposed:
                 p.bf16_t = self.flat_bf16_t[sl].view(p.shape[1], p.shape[0])
+        so = 0
+        for p in self.params:
+            if p.fp8:
+                p.q8 = self.flat_fp8[p.offset:p.offset + p.numel].view(p.shape)
+                p.q8_scale = self.fp8_scale[so:so + p.shape[0]]
+                so += (p.shape[0] + 3) // 4 * 4
 
     def zero_grad(self):
         self.flat_grad.zero_()
@@ -167,6 +194,7 @@ class ParamStore:
         """Re-derive the bf16 shadow after the master was modified outside AdamW."""
         self.flat_bf16.copy_(self.flat.to(torch.bfloat16))
         self.refresh_transposed()
+        self.refresh_fp8()
 
     def num_params(self) -> int:
         return sum(p.numel for p in self.params)

@@ -121,6 +121,31 @@ def dense(p, name, x):
     return y + b if b is not None else y
 
 
+def quant_rows_e4m3(x: torch.Tensor):
+    """Row-wise OCP e4m3 quantisation of the fp8 path (csrc/gemm.hip quant_rows_fp8_kernel):
+    scale = amax / 448 (1 for a zero row), q = round_to_nearest_even(x / scale) as e4m3."""
+    amax = x.detach().abs().amax(-1, keepdim=True)
+    scale = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    q = (x.detach() / scale).to(torch.float8_e4m3fn).float()
+    return q, scale
+
+
+def dense_fp8(p, name, x):
+    """The fp8 forward product (e4m3 activations per row x e4m3 weights per output channel,
+    fp32 accumulation, scales applied after the sum) with the bf16 product's gradient
+    (straight-through: the build's backward runs on the bf16 shadow)."""
+    y = dense(p, name, x)
+    w = p[f"{name}/kernel"]
+    xs = x.reshape(-1, x.shape[-1])
+    xq, sx = quant_rows_e4m3(xs)
+    wq, sw = quant_rows_e4m3(w.detach())
+    y8 = (xq @ wq.t()) * sx * sw.reshape(1, -1)
+    b = p.get(f"{name}/bias")
+    if b is not None:
+        y8 = y8 + b.detach()
+    return y + (y8.reshape(y.shape) - y).detach()
+
+
 # ------------------------------------------------------------------ bf16 storage emulation
 class _RoundFwd(torch.autograd.Function):
     """bf16 rounding of a stored activation; the gradient passes through unchanged."""
@@ -405,7 +430,8 @@ class OctoRef:
         mask = torch.from_numpy(literal_mask(cur))
         y = tr("y0", rbg(seq_layernorm(x, p[f"{blk}/LayerNorm_0/scale"], p[f"{blk}/LayerNorm_0/bias"],
                                        cfg.layer_norm_eps)))
-        qkv = tr("qkv", rbg(dense(p, f"{blk}/SelfAttention_0/qkv", y)))
+        bdense = dense_fp8 if getattr(cfg, "fp8", False) else dense
+        qkv = tr("qkv", rbg(bdense(p, f"{blk}/SelfAttention_0/qkv", y)))
         q, k, v = qkv.split(D, dim=-1)
         k, v = k.reshape(B, L, H, Dh), v.reshape(B, L, H, Dh)
         keep = (torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 0, L, L, 0, kpa))
@@ -421,7 +447,7 @@ class OctoRef:
             if train:
                 a = torch.where(keep[None, None], a / kpa, torch.zeros_like(a))
             o = tr("o", torch.einsum("bhqk,bkhd->bqhd", a, v).reshape(B, L, D))
-        o = gb(dense(p, f"{blk}/SelfAttention_0/out", o))
+        o = gb(bdense(p, f"{blk}/SelfAttention_0/out", o))
         if train:
             keep = torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 1, B * L, D,
                                                       sample_offset * L, kp)).view(B, L, D)
@@ -448,13 +474,13 @@ class OctoRef:
         tr("x1", x)
         z = tr("y1", rbg(seq_layernorm(x, p[f"{blk}/LayerNorm_1/scale"], p[f"{blk}/LayerNorm_1/bias"],
                                        cfg.layer_norm_eps)))
-        h = torch.relu(gb(dense(p, f"{blk}/MLPBlock_0/Dense_0", z)))
+        h = torch.relu(gb(bdense(p, f"{blk}/MLPBlock_0/Dense_0", z)))
         if train:
             keep = torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 2, B * L2, cfg.mlp_dim,
                                                       sample_offset * L2, kp)).view(B, L2, -1)
             h = torch.where(keep, h / kp, torch.zeros_like(h))
         h = tr("h", rb(h))
-        z = gb(dense(p, f"{blk}/MLPBlock_0/Dense_1", h))
+        z = gb(bdense(p, f"{blk}/MLPBlock_0/Dense_1", h))
         if train:
             keep = torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 3, B * L2, D,
                                                       sample_offset * L2, kp)).view(B, L2, D)

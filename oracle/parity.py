@@ -238,15 +238,33 @@ def oracle_blockwise(cfg, res):
     out["act"]["assembly"] = _cos_ratio(res["xs"][0], x0.detach())
     x0.backward(res["dins"][0])
     out["cos"], out["ratio"] = {}, {}
+    ga, gb = [], []
     for name, v in params.items():
         g = v.grad.numpy() if v.grad is not None else np.zeros(v.shape, np.float32)
         c, r, _ = _cos_ratio(res["grads"][name], g)
         out["cos"][name], out["ratio"][name] = c, r
+        ga.append(np.asarray(res["grads"][name], np.float64).ravel())
+        gb.append(np.asarray(g, np.float64).ravel())
+    out["cos_all"] = _cos_ratio(np.concatenate(ga), np.concatenate(gb))[0]
     return out
 
 
-def check_blockwise(out, cos_min=COS_MIN, ratio=NORM_RATIO, loss_rel=1e-3, act_rel=5e-3):
+# fp8 weight path (configs[4]): e4m3 keeps 3 mantissa bits and one scale per row, so a 1-ulp bf16
+# difference upstream (fp32 summation order) can move a row's amax or an element across an e4m3
+# rounding boundary (a 6 % step): block outputs agree to ~2e-2 and per-tensor gradient cosines to
+# ~0.995 (measured min 0.9948 at 2 blocks, B = 2). Bar: SURVEY §8c's fp8 cosine >= 0.995 on the
+# global gradient, >= 0.99 per tensor, block outputs within 3e-2.
+FP8_BAR = dict(cos_min=0.99, ratio=(0.95, 1.05), act_rel=3e-2, cos_all_min=0.995)
+
+
+def check_blockwise(out, cos_min=COS_MIN, ratio=NORM_RATIO, loss_rel=1e-3, act_rel=5e-3,
+                    cos_all_min=0.998):
+    """Block-local bar: every tensor's gradient cosine >= 0.999 with its norm ratio in
+    [0.98, 1.02], and the concatenation's cosine >= 0.998 (the per-tensor norm
+    ratios, each within 0.3 %, do not all lie on one line, which costs the global cosine a
+    little: hi-res at B = 2 measures per tensor >= 0.99927, global 0.99891)."""
     assert abs(out["loss"] - out["ref_loss"]) <= loss_rel * abs(out["ref_loss"]), (out["loss"], out["ref_loss"])
+    assert out["cos_all"] >= cos_all_min, out["cos_all"]
     bad = {k: v for k, v in out["act"].items() if v[2] > act_rel}
     assert not bad, f"block outputs differ: {bad}"
     bad = {k: v for k, v in out["dinp"].items() if v[0] < cos_min or not ratio[0] <= v[1] <= ratio[1]}
@@ -257,7 +275,7 @@ def check_blockwise(out, cos_min=COS_MIN, ratio=NORM_RATIO, loss_rel=1e-3, act_r
 
 
 def report_blockwise(out, n=10) -> str:
-    lines = [f"loss {out['loss']:.6f} ref {out['ref_loss']:.6f}"]
+    lines = [f"loss {out['loss']:.6f} ref {out['ref_loss']:.6f} cos_all {out['cos_all']:.6f}"]
     worst_act = max(out["act"].items(), key=lambda kv: kv[1][2])
     worst_din = min(out["dinp"].items(), key=lambda kv: kv[1][0])
     lines.append(f"  worst activation rel {worst_act[1][2]:.2e} ({worst_act[0]}); "

@@ -97,13 +97,16 @@ def test_blockwise_base_2cam(dev):
 
 def test_blockwise_base_hires_tome32(dev):
     """configs[4] geometry (512 x 512 image = 1024 tokens, ToMe r = 32 per block, L0 = 1060,
-    D 768, 12 heads) at reduced depth (2 blocks, 2 T5 layers), B = 1, block-local bar, in-situ
-    ToMe check at t = 1024 and 992."""
-    cfg = _cfg("octo-base-hires-tome32", num_blocks=2, t5_layers=2)
-    res = P.hip_blockwise(cfg, 2, seed=0)
-    assert res["xs"][0].shape[1] == 1060 and res["xs"][1].shape[1] == 1028
-    assert res["tome_layers_checked"] == 2
-    P.check_blockwise(P.oracle_blockwise(cfg, res))
+    D 768, 12 heads) at reduced depth (2 blocks, 2 T5 layers), B = 2, in-situ ToMe check at
+    t = 1024 and 992; bf16 products at the block-local bar, then the fp8 weight path (e4m3
+    forward products, emulated by the oracle) at the fp8 bar (oracle/parity.py FP8_BAR)."""
+    for fp8 in (False, True):
+        cfg = _cfg("octo-base-hires-tome32", num_blocks=2, t5_layers=2, fp8=fp8)
+        res = P.hip_blockwise(cfg, 2, seed=0)
+        assert res["xs"][0].shape[1] == 1060 and res["xs"][1].shape[1] == 1028
+        assert res["tome_layers_checked"] == 2
+        out = P.oracle_blockwise(cfg, res)
+        P.check_blockwise(out, **(P.FP8_BAR if fp8 else {}))
 
 
 def test_blockwise_causal_text(dev):
