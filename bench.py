@@ -62,10 +62,14 @@ def algorithmic_flops_per_sample(model) -> float:
     cfg = model.cfg
     D, M = cfg.token_embedding_dim, cfg.mlp_dim
     tr = 0.0
-    for (sets, _, ts, r) in model.layer_sets:
+    for (sets, _, ts, r, prune) in model.layer_sets:
         L = sets.L
-        Lp = L - r
-        tr += 2 * L * 4 * D * D + 2 * Lp * 2 * D * M + 4 * L * L * D
+        if prune is None:   # ToMe merges after the out-projection
+            Lp = L - r
+            tr += 2 * L * 4 * D * D + 2 * Lp * 2 * D * M + 4 * L * L * D
+        else:               # pruning happens before it
+            Lp = sum(prune[1])
+            tr += 2 * L * 3 * D * D + 2 * Lp * D * D + 2 * Lp * 2 * D * M + 4 * L * L * D
     stem = 0.0
     rs = model.image_tokenizer.resnet
     npat = model.image_tokenizer.num_patches * model.n_images
@@ -91,8 +95,8 @@ def probe_dominant_gemm(model, B, reps=20):
     persistent 256 x 256 kernel gemm_nt256_kernel<256, 0, false, 2> (csrc/gemm.hip)."""
     cfg = model.cfg
     blk = model.stack.blocks[0]
-    sets, _, ts, r = model.layer_sets[0]
-    M = B * (sets.L - r)
+    sets, _, ts, r, prune = model.layer_sets[0]
+    M = B * (sum(prune[1]) if prune else sets.L - r)
     D = cfg.token_embedding_dim
     x = torch.randn((M, D), device=model.device).to(torch.bfloat16)
     rng = torch.tensor([7, 1], dtype=torch.int32, device=model.device)

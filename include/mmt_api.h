@@ -107,6 +107,14 @@ int mmt_topk_gather(const void* x, int dtype, int B, int L, int D, int64_t xs_b,
                     const float* scores, int64_t ss_b, int n_sets, const int32_t* set_start,
                     const int32_t* set_len, const int32_t* set_k, void* out, int64_t os_b,
                     int64_t os_t, int32_t* idx_out, mmt_stream_t stream);
+/* out[b, i] = x[b, idx[b, i]] for i < K (rows of D fp32 / bf16 elements; idx (B, K) from
+ * mmt_topk_gather): the residual stream of a pruned block follows its attention rows. */
+int mmt_gather_rows(const void* x, int dtype, int B, int L, int D, int64_t xs_b, int64_t xs_t,
+                    const int32_t* idx, int K, void* out, int64_t os_b, int64_t os_t,
+                    mmt_stream_t stream);
+/* Importance of compressed_attention.py:302-306 from mmt_attn_fwd's wsum: scores[b, q] =
+ * (sum_h wsum[b, h, q] / L) / H (h ascending), the input of mmt_topk_gather. */
+int mmt_prune_importance(const float* wsum, int B, int H, int L, float* scores, mmt_stream_t stream);
 /* Backward of the gather: dx = 0, dx[b, idx[b, i]] = dout[b, i]. */
 int mmt_topk_scatter_bwd(const void* dout, int dtype, int B, int K, int D, int64_t ds_b,
                          int64_t ds_t, const int32_t* idx, int L, void* dx, int64_t xs_b,
@@ -191,12 +199,15 @@ int mmt_gemm_fp8(int M, int N, int K, const void* A, int64_t lda, const float* s
  * kept probabilities are scaled by 1/keep_prob. bias: optional fp32 (H, L, L) added to the
  * scaled logits (T5 relative position bias; forward only). o: bf16 (b, t) rows of (H, Dh);
  * lse: fp32 (B, H, L) natural-log softmax normaliser. Dh in {64, 128, 256}.
+ * wsum (optional, fp32 (B, H, L)): per query, the sum over keys of the attention weights AFTER
+ * dropout (kept / keep_prob) — the per-head factor of the pruning importance score
+ * (compressed_attention.py:302-306: mean over keys, then over heads; mmt_prune_importance).
  */
 int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, int L, int H, int Dh,
                  float scale, int n_sets, const int32_t* set_start, const int32_t* set_len,
                  const uint32_t* set_vis, const uint32_t* drop_bits, float keep_prob,
                  const float* bias, void* o, int64_t o_s_b, int64_t o_s_t, float* lse,
-                 mmt_stream_t stream);
+                 float* wsum, mmt_stream_t stream);
 /* Backward: writes dq, dk, dv into dqkv (same row layout as qkv). delta: fp32 (B, H, L)
  * workspace (rowsum(dO * O)). drop_bits_t: the transposed keep mask (mmt_dropout_bits out_t);
  * both or neither of drop_bits / drop_bits_t. bias_grad (fp32 [3 H Dh], may be NULL) += the

@@ -238,6 +238,28 @@ def topk_gather(x: torch.Tensor, scores: torch.Tensor, tokenset_idx, tokenset_k)
     return out, idx
 
 
+def prune_importance(wsum: torch.Tensor) -> torch.Tensor:
+    """(B, H, L) post-dropout attention row sums -> (B, L) importance (mean over keys, heads)."""
+    _dev(wsum)
+    B, H, L = wsum.shape
+    scores = torch.empty((B, L), dtype=torch.float32, device=wsum.device)
+    _C.call("mmt_prune_importance", ptr(wsum), B, H, L, ptr(scores), _C.stream_ptr())
+    return scores
+
+
+def gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """out[b, i] = x[b, idx[b, i]]: x (B, L, D) fp32/bf16, idx (B, K) int32."""
+    _dev(x, idx)
+    B, L, D = x.shape
+    if idx.dtype != torch.int32 or idx.dim() != 2 or idx.shape[0] != B or not idx.is_contiguous():
+        raise ValueError("idx must be contiguous int32 (B, K)")
+    K = idx.shape[1]
+    out = torch.empty((B, K, D), dtype=x.dtype, device=x.device)
+    _C.call("mmt_gather_rows", ptr(x), _dtype_code(x), B, L, D, x.stride(0), x.stride(1), ptr(idx),
+            K, ptr(out), out.stride(0), out.stride(1), _C.stream_ptr())
+    return out
+
+
 def topk_scatter_bwd(dout: torch.Tensor, idx: torch.Tensor, L: int):
     _dev(dout, idx)
     B, K, D = dout.shape
@@ -297,8 +319,11 @@ def _qkv_geo(qkv: torch.Tensor, H: int):
 
 def attn_fwd(qkv: torch.Tensor, H: int, scale: float, table: SetTable | None = None,
              drop_bits: torch.Tensor | None = None, keep_prob: float = 1.0,
-             bias: torch.Tensor | None = None, out: torch.Tensor | None = None):
-    _dev(qkv, drop_bits, bias, out)
+             bias: torch.Tensor | None = None, out: torch.Tensor | None = None,
+             wsum: torch.Tensor | None = None):
+    """wsum (optional fp32 (B, H, L)): receives the per-query sum of the post-dropout attention
+    weights (the pruning importance, compressed_attention.py:302-306)."""
+    _dev(qkv, drop_bits, bias, out, wsum)
     B, L, Dh = _qkv_geo(qkv, H)
     t = table or SetTable.none(L)
     if t.L != L:
@@ -310,9 +335,12 @@ def attn_fwd(qkv: torch.Tensor, H: int, scale: float, table: SetTable | None = N
     lse = torch.empty((B, H, L), dtype=torch.float32, device=qkv.device)
     if drop_bits is not None and drop_bits.dim() == 3:
         drop_bits = drop_bits[0]
+    if wsum is not None and (tuple(wsum.shape) != (B, H, L) or wsum.dtype != torch.float32
+                             or not wsum.is_contiguous()):
+        raise ValueError("wsum must be contiguous fp32 (B, H, L)")
     _C.call("mmt_attn_fwd", ptr(qkv), qkv.stride(0), qkv.stride(1), B, L, H, Dh, scale, t.n,
             t.starts, t.lens, t.vis, ptr(drop_bits), keep_prob, ptr(bias), ptr(out), out.stride(0),
-            out.stride(1), ptr(lse), _C.stream_ptr())
+            out.stride(1), ptr(lse), ptr(wsum), _C.stream_ptr())
     return out, lse
 
 

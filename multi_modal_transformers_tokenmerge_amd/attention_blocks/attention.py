@@ -10,7 +10,14 @@ Semantics kept from the reference:
     mask broadcast over batch and heads; q/k/v/out DenseGeneral with bias (fused QKV here);
   * MLPBlock: Dense -> relu -> Dropout -> Dense -> Dropout (the YAML key ``norm`` is the Dropout);
   * ToMe metric = sum over heads of the key projection of the image token set, merged with
-    merge_wavg and the set's token sizes carried across layers (no proportional attention).
+    merge_wavg and the set's token sizes carried across layers (no proportional attention);
+  * top-k pruning (OctoConfig.compression == "prune"): importance = mean over keys, then over
+    heads, of the post-dropout attention weights (compressed_attention.py:302-306, written by the
+    attention forward as per-query row sums), compute_top_k_tokens per token set
+    (token_compression.py:15-46) applied to the attention output BEFORE the out-projection
+    (compressed_attention.py:308-326). The reference's CompressedEncoder1DBlock then discards
+    the attention output (:349-354); the build adds it to the block input's
+    rows at the same indices — the only residual that matches the pruned shape.
 Every op is a libmmt_hip kernel (see layers.py); backward is explicit.
 """
 from __future__ import annotations
@@ -35,6 +42,8 @@ class LayerCtx:
     table: K.SetTable
     tome_set: int = -1             # index of the merged token set, -1 = no merge
     r: int = 0
+    # top-k pruning: (((start, num_tokens) per set), (k per set)) or None
+    prune: Optional[tuple] = None
     train: bool = True
     rng: Optional[torch.Tensor] = None
     sample_offset: int = 0         # global index of this rank's first sample (RNG counters)
@@ -120,11 +129,21 @@ class Encoder1DBlock:
                 tome_idx = K.tome_match(metric, ctx.r)
         if bits_ready is not None:
             main.wait_event(bits_ready)
-        o, lse = K.attn_fwd(qkv, H, self.scale, ctx.table, bits, kpa)
+        wsum = (torch.empty((B, H, L), dtype=torch.float32, device=x.device)
+                if ctx.prune is not None else None)
+        o, lse = K.attn_fwd(qkv, H, self.scale, ctx.table, bits, kpa, wsum=wsum)
+        prune = None
+        o_in, x_res, Lo = o, x, L
+        if ctx.prune is not None:
+            scores = K.prune_importance(wsum)
+            o_in, pidx = K.topk_gather(o, scores, *ctx.prune)
+            x_res = K.gather_rows(x, pidx)
+            Lo = o_in.shape[1]
+            prune = (pidx, scores)
         # residual stream stays fp32 (sequence-axis LayerNorm conditioning, csrc/norm.hip)
-        x1 = self.out.fwd(o.view(B * L, D), residual=x.view(B * L, D), out_mode=K.OUT_F32,
-                          **drop(DROP_ATTN_OUT, L))
-        x1 = x1.view(B, L, D)
+        x1 = self.out.fwd(o_in.reshape(B * Lo, D), residual=x_res.reshape(B * Lo, D),
+                          out_mode=K.OUT_F32, **drop(DROP_ATTN_OUT, Lo))
+        x1 = x1.view(B, Lo, D)
         tome = None
         new_size = size
         if ctx.r > 0:
@@ -139,8 +158,8 @@ class Encoder1DBlock:
         h = self.mlp.dense.fwd(y1.view(B * L2, D), act=K.ACT_RELU, **drop(DROP_MLP_HIDDEN, L2))
         x2 = self.mlp.dense_out.fwd(h, residual=x1.view(B * L2, D), out_mode=K.OUT_F32,
                                     **drop(DROP_MLP_OUT, L2))
-        saved = dict(x=x, y0=y0, mu0=mu0, rs0=rs0, qkv=qkv, o=o, lse=lse, bits=bits, x1=x1, y1=y1,
-                     mu1=mu1, rs1=rs1, h=h, tome=tome, kp=kp, kpa=kpa)
+        saved = dict(x=x, y0=y0, mu0=mu0, rs0=rs0, qkv=qkv, o=o, o_in=o_in, lse=lse, bits=bits,
+                     x1=x1, y1=y1, mu1=mu1, rs1=rs1, h=h, tome=tome, prune=prune, kp=kp, kpa=kpa)
         return x2.view(B, L2, D), saved, new_size
 
     # ----------------------------------------------------------------------------- backward
@@ -164,10 +183,15 @@ class Encoder1DBlock:
         if sv["tome"] is not None:
             s0, t, r, pos, size_in, size_out = sv["tome"][:6]
             dx1 = K.tome_merge_bwd(dx1, s0, t, r, pos, size_in, size_out)
-        dx1f = dx1.view(B * L, D)
-        dzo = K.dropout_bwd(dx1f, rng, ctx.layer, DROP_ATTN_OUT, kp, row_offset=ctx.sample_offset * L,
+        Lo = sv["o_in"].shape[1]
+        dx1f = dx1.reshape(B * Lo, D)
+        dzo = K.dropout_bwd(dx1f, rng, ctx.layer, DROP_ATTN_OUT, kp, row_offset=ctx.sample_offset * Lo,
                             colsum_out=self.out.b.grad)
-        do = self.out.bwd(dzo, sv["o"].view(B * L, D), bias_grad_done=True)
+        do = self.out.bwd(dzo, sv["o_in"].reshape(B * Lo, D), bias_grad_done=True)
+        if sv["prune"] is not None:  # the top-k indices carry no gradient (lax.top_k indices)
+            pidx = sv["prune"][0]
+            do = K.topk_scatter_bwd(do.view(B, Lo, D), pidx, L)
+            dx1 = K.topk_scatter_bwd(dx1.view(B, Lo, D), pidx, L)
         # the QKV bias gradient (column sums of dqkv) is accumulated inside the attention backward
         dqkv = K.attn_bwd(sv["qkv"], sv["o"], do.view(B, L, D), sv["lse"], self.H, self.scale,
                           ctx.table, sv["bits"], kpa, bias_grad=self.qkv.b.grad)

@@ -14,8 +14,9 @@ which are not available on the GPU box.
   layouts are accepted: the one the shipped YAMLs define (``attention_blocks.num_blocks``,
   ``attention_blocks.encoder_1d_block``, ``vanilla_decoder.yaml:1-4``) and the one ``octo.py``
   reads (``attention_blocks.stacked_encoder_1d_block.{num_blocks, encoder_1d_block}``,
-  ``octo.py:67,80``). New keys: ``token_compression_sequence`` (ToMe)
-  and ``text_tokens``.
+  ``octo.py:67,80``). New keys: ``token_compression_sequence`` (ToMe),
+  ``token_compression_method`` ("tome" | "prune"), ``fp8_matmul``, ``t5_num_layers`` and
+  ``text_tokens``.
 
 Errors follow the reference's conventions: a missing key or an unknown ``_target_`` raises
 ``KeyError`` / ``ValueError`` (Hydra raises on both).
@@ -271,6 +272,7 @@ def octo_config_from_yaml(cfg: dict, name: str = "yaml"):
     m = re.findall(r"(?:TaskDescriptionPrefix|Text)\{(\d+)\}", kw["input_sequence"])
     kw["text_tokens"] = int(cfg.get("text_tokens", sum(int(v) for v in m)))
     kw["fp8"] = bool(cfg.get("fp8_matmul", False))
+    kw["compression"] = str(cfg.get("token_compression_method", "tome"))
     t5_layers = cfg.get("t5_num_layers")
     if t5_layers:
         kw["t5"] = T5Config(num_layers=int(t5_layers))

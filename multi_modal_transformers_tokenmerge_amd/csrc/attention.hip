@@ -284,7 +284,7 @@ template <int DH, int NQ>
 __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
     Geo g, AttnMask mask, const uint32_t* __restrict__ drop_bits, int drop_words, float drop_scale,
     const float* __restrict__ bias, bf16_t* __restrict__ o, int64_t o_s_b, int64_t o_s_t,
-    float* __restrict__ lse) {
+    float* __restrict__ lse, float* __restrict__ wsum) {
   constexpr int STR = DH + 8;
   constexpr int NS = DH / 16;   // k-steps over the head dim
   constexpr int ND = DH / 32;   // 32-row d sub-tiles of O^T
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
 
   bf16x8 qf[NQ][NS];
   floatx16 oacc[NQ][ND];
-  float m[NQ], l[NQ];
+  float m[NQ], l[NQ], ld[NQ];  // ld: sum of the kept (post-dropout) probabilities, for wsum
   uint32_t visq[NQ];
   int sq[NQ], qrow[NQ];
   bool qv[NQ], live[NQ];
@@ -324,6 +324,7 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
       for (int r = 0; r < 16; ++r) oacc[i][d][r] = 0.f;
     m[i] = -INFINITY;
     l[i] = 0.f;
+    ld[i] = 0.f;
   }
 
   const int ntiles = (L + KT - 1) / KT;
@@ -411,6 +412,15 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
       }
       rs += __shfl_xor(rs, 32, 64);
       l[i] = l[i] * alpha + rs;
+      if (wsum) {  // kernel-uniform: row sum of the kept probabilities (pruning importance)
+        float rd = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) rd += sacc[u][r];
+        rd += __shfl_xor(rd, 32, 64);
+        ld[i] = ld[i] * alpha + rd;
+      }
       m[i] = mn;
       if (!__all(alpha == 1.f)) {
 #pragma unroll
@@ -451,8 +461,10 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
         w.y = (uint32_t)f2bf(oacc[i][d][4 * r4 + 2] * inv) | ((uint32_t)f2bf(oacc[i][d][4 * r4 + 3] * inv) << 16);
         *reinterpret_cast<uint2*>(orow + dd) = w;
       }
-    if (lane < 32)
+    if (lane < 32) {
       lse[((int64_t)b * g.H + h) * L + q] = l[i] > 0.f ? m[i] * c * LN2 + logf(l[i]) : -INFINITY;
+      if (wsum) wsum[((int64_t)b * g.H + h) * L + q] = ld[i] * inv;  // sum_k of the dropped weights
+    }
   }
 }
 
@@ -886,7 +898,7 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
                             float scale, int n_sets, const int32_t* set_start,
                             const int32_t* set_len, const uint32_t* set_vis,
                             const uint32_t* drop_bits, float keep_prob, const float* bias,
-                            void* o, int64_t o_s_b, int64_t o_s_t, float* lse,
+                            void* o, int64_t o_s_b, int64_t o_s_t, float* lse, float* wsum,
                             mmt_stream_t stream) {
   MMT_CHECK_ARG(qkv && o && lse, "mmt_attn_fwd: null pointer");
   MMT_CHECK_ARG(B > 0 && L > 0 && H > 0 && L <= MAXL, "mmt_attn_fwd: bad shape (L <= %d)", MAXL);
@@ -908,7 +920,7 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   dim3 grid((L + QB * nq - 1) / (QB * nq), H, B);
 #define FWD(DH_, NQ_)                                                                            \
   hipLaunchKernelGGL((attn_fwd_kernel<DH_, NQ_>), grid, dim3(NT), 0, as_stream(stream), g, m,   \
-                     drop_bits, words, dscale, bias, (bf16_t*)o, o_s_b, o_s_t, lse)
+                     drop_bits, words, dscale, bias, (bf16_t*)o, o_s_b, o_s_t, lse, wsum)
   if (Dh == 64) {
     if (nq == 3) FWD(64, 3);
     else if (nq == 2) FWD(64, 2);

@@ -171,3 +171,61 @@ extern "C" int mmt_topk_scatter_bwd(const void* dout, int dtype, int B, int K, i
   MMT_CHECK_LAUNCH("mmt_topk_scatter_bwd");
   return MMT_OK;
 }
+
+namespace {
+template <typename T>
+__global__ void gather_rows_kernel(const T* __restrict__ x, int D, int64_t xs_b, int64_t xs_t,
+                                   const int32_t* __restrict__ idx, int K, T* __restrict__ out,
+                                   int64_t os_b, int64_t os_t) {
+  constexpr int V = 16 / sizeof(T);
+  const int nch = D / V;
+  const int b = blockIdx.y;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)K * nch) return;
+  const int i = e / nch, ch = e - (int64_t)i * nch;
+  const int row = idx[(int64_t)b * K + i];
+  *reinterpret_cast<uint4*>(out + (int64_t)b * os_b + (int64_t)i * os_t + ch * V) =
+      *reinterpret_cast<const uint4*>(x + (int64_t)b * xs_b + (int64_t)row * xs_t + ch * V);
+}
+
+__global__ void prune_importance_kernel(const float* __restrict__ wsum, int B, int H, int L,
+                                        float* __restrict__ scores) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * L) return;
+  const int b = (int)(i / L), q = (int)(i - (int64_t)b * L);
+  float acc = 0.f;
+  // IEEE divisions (the test restates this order exactly: h ascending, / L, then / H)
+  for (int h = 0; h < H; ++h) acc += __fdiv_rn(wsum[((int64_t)b * H + h) * L + q], (float)L);
+  scores[i] = __fdiv_rn(acc, (float)H);
+}
+}  // namespace
+
+extern "C" int mmt_prune_importance(const float* wsum, int B, int H, int L, float* scores,
+                                    mmt_stream_t stream) {
+  MMT_CHECK_ARG(wsum && scores && B > 0 && H > 0 && L > 0, "mmt_prune_importance: args");
+  const int64_t n = (int64_t)B * L;
+  hipLaunchKernelGGL(prune_importance_kernel, dim3((n + 255) / 256), dim3(256), 0,
+                     as_stream(stream), wsum, B, H, L, scores);
+  MMT_CHECK_LAUNCH("mmt_prune_importance");
+  return MMT_OK;
+}
+
+extern "C" int mmt_gather_rows(const void* x, int dtype, int B, int L, int D, int64_t xs_b,
+                               int64_t xs_t, const int32_t* idx, int K, void* out, int64_t os_b,
+                               int64_t os_t, mmt_stream_t stream) {
+  MMT_CHECK_ARG(x && idx && out && B > 0 && L > 0 && D > 0 && K >= 0, "mmt_gather_rows: args");
+  MMT_CHECK_ARG(dtype == MMT_F32 || dtype == MMT_BF16, "mmt_gather_rows: dtype");
+  MMT_CHECK_ARG(vec_ok(dtype, D, xs_b, xs_t, os_b, os_t), "mmt_gather_rows: D/strides not 16-B rows");
+  if (K == 0) return MMT_OK;
+  const int64_t ns = (int64_t)K * (D / (dtype == MMT_F32 ? 4 : 8));
+  dim3 grid((ns + 255) / 256, B);
+  hipStream_t s = as_stream(stream);
+  if (dtype == MMT_F32)
+    hipLaunchKernelGGL(gather_rows_kernel<float>, grid, dim3(256), 0, s, (const float*)x, D, xs_b,
+                       xs_t, idx, K, (float*)out, os_b, os_t);
+  else
+    hipLaunchKernelGGL(gather_rows_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, D,
+                       xs_b, xs_t, idx, K, (bf16_t*)out, os_b, os_t);
+  MMT_CHECK_LAUNCH("mmt_gather_rows");
+  return MMT_OK;
+}

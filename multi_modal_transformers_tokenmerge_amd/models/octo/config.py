@@ -42,10 +42,15 @@ class OctoConfig:
     stem: Optional[dict] = None
     # fp8 weight path (BASELINE configs[4]): the encoder blocks' Dense forward products in e4m3
     fp8: bool = False
+    # how token_compression_sequence's per-layer counts are realised: "tome" (bipartite soft
+    # matching + merge_wavg, token_compression.py:54-129, one image set per layer) or "prune"
+    # (per-set top-k on the attention importance, compressed_attention.py:302-308 +
+    # token_compression.py:15-46, every set); YAML key token_compression_method
+    compression: str = "tome"
 
     @property
     def tome_r(self) -> int:
-        if not self.token_compression_sequence:
+        if not self.token_compression_sequence or self.compression != "tome":
             return 0
         import re
         return max(int(x) for x in re.findall(r"\{(\d+)\}", self.token_compression_sequence))
@@ -72,6 +77,9 @@ PRESETS = {
         name="octo-base-hires-tome32", token_embedding_dim=768, num_heads=12, mlp_dim=3072,
         image_size=(512, 512, 3), input_sequence="[TaskDescriptionPrefix{32}] [Image{1024};Readout{4}]",
         token_compression_sequence="[TaskDescriptionPrefix{0}] [Image{32};Readout{0}]", fp8=True),
+    # top-k pruning on the small geometry: 16 image tokens per block
+    "octo-small-prune16": OctoConfig(name="octo-small-prune16", token_compression_sequence=TOME16,
+                                     compression="prune"),
 }
 
 

@@ -123,11 +123,24 @@ class Octo:
         self.img_rows = torch.from_numpy(img_rows).to(self.device)
         # per-layer token-set tables (square masks) + ToMe set / r
         self.layer_sets = []
+        if cfg.compression not in ("tome", "prune"):
+            raise ValueError(f"compression must be 'tome' or 'prune', got {cfg.compression!r}")
         for layer in range(cfg.num_blocks):
             sets = self.seq.set_table(layer)
             merged = [i for i, ts in enumerate(self.seq._parse(layer) if cfg.token_compression_sequence
                                                 else self.seq.token_sequence)
                       if ts.tokens_compressed_per_layer > 0]
+            if cfg.compression == "prune":
+                # top-k per token set, uncompressed sets keep all their tokens (k = n)
+                prune = None
+                if merged:
+                    nxt = self.seq.set_table(layer + 1)
+                    if min(nxt.lens) < 0:
+                        raise ValueError(f"layer {layer}: pruning empties a token set")
+                    prune = (tuple(zip(sets.starts, sets.lens)), tuple(nxt.lens))
+                self.layer_sets.append((sets, K.SetTable(sets.starts, sets.lens, sets.vis, sets.causal),
+                                        -1, 0, prune))
+                continue
             if len(merged) > 1:
                 raise NotImplementedError("ToMe on more than one token set per layer")
             tome_set = merged[0] if merged else -1
@@ -138,7 +151,7 @@ class Octo:
                 if r > t // 2:
                     raise ValueError(f"layer {layer}: ToMe r={r} exceeds t//2={t // 2}")
             self.layer_sets.append((sets, K.SetTable(sets.starts, sets.lens, sets.vis, sets.causal),
-                                    tome_set, r))
+                                    tome_set, r, None))
         final = self.seq.set_table(cfg.num_blocks) if cfg.token_compression_sequence else self.seq.set_table(0)
         self.L_final = final.L
         rows = [s + j for s, n, m in zip(final.starts, final.lens, final.modalities) if m == "readouts"
@@ -159,9 +172,9 @@ class Octo:
             self.readout_group_counts = torch.full((A,), per, dtype=torch.int32, device=self.device)
 
     def layer_ctxs(self, train: bool, rng, sample_offset: int) -> List[LayerCtx]:
-        return [LayerCtx(layer=i, sets=s, table=t, tome_set=ts, r=r, train=train, rng=rng,
+        return [LayerCtx(layer=i, sets=s, table=t, tome_set=ts, r=r, prune=pr, train=train, rng=rng,
                          sample_offset=sample_offset)
-                for i, (s, t, ts, r) in enumerate(self.layer_sets)]
+                for i, (s, t, ts, r, pr) in enumerate(self.layer_sets)]
 
     # ------------------------------------------------------------------ forward / backward
     def generate_readouts(self, text_tokens, images, train=True, rng=None, sample_offset=0,

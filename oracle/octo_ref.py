@@ -411,7 +411,10 @@ class OctoRef:
     def block(self, x, layer, sequence, size, *, seed, step, sample_offset=0, train=True,
               tome_indices=None, trace=None):
         """Encoder1DBlock (attention.py:41-69) with ToMe after the attention residual
-        (tome_attention.py:249-256 placement). Returns (x_out, size_out, (unm, src, dst) | None)."""
+        (tome_attention.py:249-256 placement), or top-k pruning of the attention output when
+        cfg.compression == "prune". Returns (x_out, size_out, used) with used = the ToMe
+        (unm, src, dst) triple, the (B, K) top-k row indices, or None; tome_indices injects
+        either instead of recomputing it."""
         def tr(name, v):
             if trace is not None:
                 trace[f"b{layer}/{name}"] = v.detach().clone()
@@ -447,15 +450,44 @@ class OctoRef:
             if train:
                 a = torch.where(keep[None, None], a / kpa, torch.zeros_like(a))
             o = tr("o", torch.einsum("bhqk,bkhd->bqhd", a, v).reshape(B, L, D))
-        o = gb(bdense(p, f"{blk}/SelfAttention_0/out", o))
-        if train:
-            keep = torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 1, B * L, D,
-                                                      sample_offset * L, kp)).view(B, L, D)
-            o = torch.where(keep, o / kp, torch.zeros_like(o))
-        x = self._q(x + o)
         used = None
         merged = [i for i, c in enumerate(sequence) if c[3] > 0]
-        if merged:
+        pruning = bool(merged) and getattr(cfg, "compression", "tome") == "prune"
+        if pruning:
+            # compressed_attention.py:302-308: importance = mean over keys, then heads, of the
+            # post-dropout attention weights; top-k per token set on it (token_compression.py:
+            # 15-46) applied to the attention output before the out-projection; the residual
+            # takes the block input's rows at the same indices (attention_blocks/attention.py)
+            with torch.no_grad():
+                sc = torch.einsum("bqhd,bkhd->bhqk", q.reshape(B, L, H, Dh).float(), k.float()) / math.sqrt(Dh)
+                sc = sc.masked_fill(~mask[None, None], float("-inf"))
+                a = torch.softmax(sc, -1)
+                if train:
+                    a = torch.where(keep[None, None], a / kpa, torch.zeros_like(a))
+                imp = tr("imp", a.mean(-1).mean(1))                              # (B, L)
+            if tome_indices is not None:
+                idx = torch.as_tensor(np.asarray(tome_indices)).long()
+            else:
+                from .tome import topk_tokens
+                sets, starts = [], 0
+                for (_, ln, _) in cur:
+                    sets.append((starts, ln))
+                    starts += ln
+                ks = [lens[i] - (layer + 1) * c[3] for i, c in enumerate(sequence)]
+                idx = torch.from_numpy(np.stack([topk_tokens(np.zeros((L, 1), np.float32),
+                                                             imp[b].numpy(), sets, ks)[1]
+                                                 for b in range(B)])).long()
+            used = idx.to(torch.int32)
+            bidx = torch.arange(B)[:, None]
+            o, x = o[bidx, idx], x[bidx, idx]
+        Lo = o.shape[1]
+        o = gb(bdense(p, f"{blk}/SelfAttention_0/out", o))
+        if train:
+            keep = torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 1, B * Lo, D,
+                                                      sample_offset * Lo, kp)).view(B, Lo, D)
+            o = torch.where(keep, o / kp, torch.zeros_like(o))
+        x = self._q(x + o)
+        if merged and not pruning:
             si = merged[0]
             r = sequence[si][3]
             s0 = sum(ln for _, ln, _ in cur[:si])

@@ -4,6 +4,10 @@ End-to-end parity harness: run one HIP training step (forward loss + every param
 and the CPU restatement (oracle/octo_ref.py, bf16 storage points emulated) on identical inputs,
 identical dropout streams and the HIP run's own position tokens and diffusion (t, eps).
 
+Top-k pruning (cfg.compression == "prune"): likewise, the rows each pruning layer kept must
+equal the literal compute_top_k_tokens restatement on the step's own importance scores, and the
+scores must agree with the oracle's (block-local bar) before the rows are injected.
+
 ToMe: the HIP run's index triples are checked IN SITU first — for every merging layer,
 canon_match (oracle/tome_ref.c) on the layer's own K projection (the bf16 qkv buffer the step
 wrote, summed over heads) must reproduce the indices the step used, bit for bit. Only then are
@@ -67,6 +71,43 @@ def insitu_tome_check(model, st):
     return checked
 
 
+def insitu_prune_check(model, st):
+    """For every pruning layer: the literal compute_top_k_tokens restatement (oracle/tome.py
+    topk_tokens) on the step's own importance scores must equal the rows the step kept."""
+    from oracle.tome import topk_tokens
+    checked = 0
+    for layer, sv in enumerate(st["stack_sv"]):
+        if sv.get("prune") is None:
+            continue
+        sets, ks = st["ctxs"][layer].prune
+        idx, scores = (a.cpu().numpy() for a in sv["prune"])
+        for b in range(idx.shape[0]):
+            _, want = topk_tokens(np.zeros((scores.shape[1], 1), np.float32), scores[b], sets, ks)
+            if not np.array_equal(idx[b], want):
+                bad = np.argwhere(idx[b] != want)[:4].ravel().tolist()
+                raise AssertionError(f"layer {layer} sample {b}: in-situ top-k differs at {bad}")
+        checked += 1
+    return checked
+
+
+def _used(sv, f=lambda a: a.cpu()):
+    """The compression indices a block used: the ToMe (unm, src, dst) triple, the top-k rows, or
+    None."""
+    if sv["tome"] is not None:
+        return tuple(f(a) for a in sv["tome"][6:9])
+    if sv.get("prune") is not None:
+        return f(sv["prune"][0])
+    return None
+
+
+def _inject(x):
+    if x is None:
+        return None
+    if isinstance(x, tuple):
+        return tuple(torch.from_numpy(np.asarray(a)) for a in x)
+    return torch.from_numpy(np.asarray(x))
+
+
 TRACE_KEYS = ("x", "y0", "qkv", "o", "x1", "y1", "h")
 
 
@@ -98,11 +139,12 @@ def hip_step(cfg, B, seed=0, check_tome=True, trace_layers=None):
     model.backward(st)
     torch.cuda.synchronize()
     n_tome = insitu_tome_check(model, st) if check_tome else 0
+    n_prune = insitu_prune_check(model, st) if check_tome else 0
     res = dict(B=B, seed=seed, loss=float(loss.item()),
                rt=st["rt"].cpu().numpy(), ct=st["ct"].cpu().numpy(),
                t=st["head_sv"]["t"].cpu().numpy(), eps=st["head_sv"]["eps"].cpu().numpy(),
-               tome=[None if sv["tome"] is None else tuple(a.cpu().numpy() for a in sv["tome"][6:9])
-                     for sv in st["stack_sv"]],
+               tome=[_used(sv, lambda a: a.cpu().numpy()) for sv in st["stack_sv"]],
+               prune_layers_checked=n_prune,
                grads={p.name: p.grad.detach().cpu().numpy().copy() for p in model.store.params},
                tome_layers_checked=n_tome, model=model)
     if trace_layers is not None:
@@ -131,7 +173,7 @@ def oracle_step(cfg, res, model=None, emulate_bf16=True):
     images, text, actions = _inputs(model, res["B"], res["seed"])
     params, t5p = oracle_params(model)
     ref = OctoRef(cfg, params, t5p, emulate_bf16=emulate_bf16)
-    tome = [None if x is None else tuple(torch.from_numpy(np.asarray(a)) for a in x) for x in res["tome"]]
+    tome = [_inject(x) for x in res["tome"]]
     rloss, _ = ref.forward_loss(text, images.astype(np.float32), actions, seed=1234, step=0,
                                 positions=(res["rt"], res["ct"]), t=res["t"], eps=res["eps"],
                                 tome_indices=tome,
@@ -194,11 +236,14 @@ def hip_blockwise(cfg, B, seed=0):
     model._backward_tokens(st, g)
     torch.cuda.synchronize()
     n_tome = insitu_tome_check(model, st)
+    n_prune = insitu_prune_check(model, st)
     f = lambda a: None if a is None else a.detach().float().cpu()  # noqa: E731
     return dict(model=model, B=B, seed=seed, loss=float(loss.item()),
                 xs=[f(sv["x"]) for sv in svs], xL=f(st["xL"]), dxL=f(dxL), douts=douts, dins=dins,
                 size_in=[None if sv["tome"] is None else f(sv["tome"][4]) for sv in svs],
-                tome=[None if sv["tome"] is None else tuple(a.cpu() for a in sv["tome"][6:9]) for sv in svs],
+                tome=[_used(sv) for sv in svs],
+                prune_scores=[None if sv.get("prune") is None else f(sv["prune"][1]) for sv in svs],
+                prune_layers_checked=n_prune,
                 t5_out=f(st.get("t5_out")), rt=st["rt"].cpu().numpy(), ct=st["ct"].cpu().numpy(),
                 t=st["head_sv"]["t"].cpu().numpy(), eps=st["head_sv"]["eps"].cpu().numpy(),
                 grads={p.name: p.grad.detach().cpu().numpy().copy() for p in model.store.params},
@@ -222,7 +267,11 @@ def oracle_blockwise(cfg, res):
         x_in = res["xs"][i].clone().requires_grad_()
         size = res["size_in"][i]
         size = None if size is None else size.unsqueeze(-1)
-        xo, _, _ = ref.block(x_in, i, seq, size, seed=1234, step=0, tome_indices=res["tome"][i])
+        trace = {}
+        xo, _, _ = ref.block(x_in, i, seq, size, seed=1234, step=0, tome_indices=res["tome"][i],
+                             trace=trace)
+        if res.get("prune_scores", [None] * nb)[i] is not None:
+            out["act"][f"importance{i}"] = _cos_ratio(res["prune_scores"][i], trace[f"b{i}/imp"])
         want = res["xs"][i + 1] if i + 1 < nb else res["xL"]
         out["act"][f"block{i}"] = _cos_ratio(want, xo.detach())
         xo.backward(res["douts"][i])
@@ -249,6 +298,34 @@ def oracle_blockwise(cfg, res):
     return out
 
 
+def blockwise_floor(cfg, res, blocks):
+    """CPU only: for the given blocks, the bf16-emulating block (fp32) against the same block in
+    float64 without emulation, both fed the HIP block input and output gradient. Per-parameter
+    (cos, ratio) of that comparison: how much of a block-local gradient difference the bf16
+    storage points alone explain."""
+    from oracle.octo_ref import OctoRef, sequence_spec
+    model = res["model"]
+    seq = sequence_spec(cfg.input_sequence, cfg.token_compression_sequence)
+    out = {}
+    for i in blocks:
+        grads = []
+        for emu, dt in ((True, torch.float32), (False, torch.float64)):
+            params, t5p = oracle_params(model)
+            params = {k: v.detach().to(dt).requires_grad_() for k, v in params.items()}
+            ref = OctoRef(cfg, params, t5p, dtype=dt, emulate_bf16=emu)
+            x_in = res["xs"][i].to(dt).requires_grad_()
+            size = res["size_in"][i]
+            size = None if size is None else size.unsqueeze(-1).to(dt)
+            xo, _, _ = ref.block(x_in, i, seq, size, seed=1234, step=0, tome_indices=res["tome"][i])
+            xo.backward(res["douts"][i].to(dt))
+            pre = f"StackedEncoder1DBlock_0/Block_{i}/"
+            grads.append({k: v.grad.double().numpy() for k, v in params.items()
+                          if k.startswith(pre) and v.grad is not None})
+        for k in grads[0]:
+            out[k] = _cos_ratio(grads[0][k], grads[1][k])[:2]
+    return out
+
+
 # fp8 weight path (configs[4]): e4m3 keeps 3 mantissa bits and one scale per row, so a 1-ulp bf16
 # difference upstream (fp32 summation order) can move a row's amax or an element across an e4m3
 # rounding boundary (a 6 % step): block outputs agree to ~2e-2 and per-tensor gradient cosines to
@@ -258,11 +335,17 @@ FP8_BAR = dict(cos_min=0.99, ratio=(0.95, 1.05), act_rel=3e-2, cos_all_min=0.995
 
 
 def check_blockwise(out, cos_min=COS_MIN, ratio=NORM_RATIO, loss_rel=1e-3, act_rel=5e-3,
-                    cos_all_min=0.998):
+                    cos_all_min=0.998, cfg=None, res=None):
     """Block-local bar: every tensor's gradient cosine >= 0.999 with its norm ratio in
     [0.98, 1.02], and the concatenation's cosine >= 0.998 (the per-tensor norm
     ratios, each within 0.3 %, do not all lie on one line, which costs the global cosine a
-    little: hi-res at B = 2 measures per tensor >= 0.99927, global 0.99891)."""
+    little: hi-res at B = 2 measures per tensor >= 0.99927, global 0.99891).
+
+    With cfg and res: a block parameter below 0.999 is still accepted when the HIP-vs-oracle
+    deviation is no larger than the bf16 floor of that tensor in that block (blockwise_floor:
+    the emulating oracle vs float64 on the same block inputs) — the bias gradients of the
+    first blocks are column sums over ~550 rows with heavy cancellation, where the bf16 storage
+    points alone cost ~2e-3 of cosine (octo-small-prune16 seed 0: floor 0.99829, HIP 0.99874)."""
     assert abs(out["loss"] - out["ref_loss"]) <= loss_rel * abs(out["ref_loss"]), (out["loss"], out["ref_loss"])
     assert out["cos_all"] >= cos_all_min, out["cos_all"]
     bad = {k: v for k, v in out["act"].items() if v[2] > act_rel}
@@ -271,6 +354,14 @@ def check_blockwise(out, cos_min=COS_MIN, ratio=NORM_RATIO, loss_rel=1e-3, act_r
     assert not bad, f"input gradients differ: {bad}"
     bad = {k: (v, out["ratio"][k]) for k, v in out["cos"].items()
            if v < cos_min or not ratio[0] <= out["ratio"][k] <= ratio[1]}
+    if bad and cfg is not None and res is not None:
+        import re
+        blocks = sorted({int(m.group(1)) for k in bad for m in [re.search(r"/Block_(\d+)/", k)] if m})
+        fl = blockwise_floor(cfg, res, blocks) if blocks else {}
+        out["floor_accepted"] = {k: (v, fl[k]) for k, v in bad.items()
+                                 if k in fl and 1 - v[0] <= 1 - fl[k][0]
+                                 and ratio[0] <= v[1] <= ratio[1]}
+        bad = {k: v for k, v in bad.items() if k not in out["floor_accepted"]}
     assert not bad, f"parameter gradients differ: {dict(list(sorted(bad.items(), key=lambda kv: kv[1][0]))[:8])}"
 
 
@@ -292,7 +383,7 @@ def bf16_floor(cfg, res, model):
     of the free-running end-to-end bar (the network amplifies bf16 noise with depth)."""
     from oracle.octo_ref import OctoRef, sequence_spec
     images, text, actions = _inputs(model, res["B"], res["seed"])
-    tome = [None if x is None else tuple(torch.from_numpy(np.asarray(a)) for a in x) for x in res["tome"]]
+    tome = [_inject(x) for x in res["tome"]]
     seq = sequence_spec(cfg.input_sequence, cfg.token_compression_sequence)
     outs = []
     for emu, dt in ((True, torch.float32), (False, torch.float64)):
@@ -313,6 +404,7 @@ def run_parity(cfg, B, seed=0, floor=False):
     ref_loss, ref_grads = oracle_step(cfg, res, model=res["model"])
     out = compare(res, ref_loss, ref_grads)
     out["tome_layers_checked"] = res["tome_layers_checked"]
+    out["prune_layers_checked"] = res["prune_layers_checked"]
     if floor:
         out["floor"] = bf16_floor(cfg, res, res["model"])
     return out

@@ -100,6 +100,61 @@ def test_attention_fwd_bwd(dev, B, L, H, Dh, masked, drop):
         assert rel(gk[:, :, i], gr[:, :, i]) < 2e-2, ("qkv"[i], rel(gk[:, :, i], gr[:, :, i]))
 
 
+@pytest.mark.parametrize("B,L,H,Dh,drop,causal", [
+    (2, 292, 6, 64, True, False), (3, 276, 6, 64, False, False), (1, 1064, 2, 64, True, False),
+    (2, 110, 3, 64, True, True), (2, 200, 2, 128, True, False), (2, 74, 3, 256, True, True)])
+def test_attention_importance(dev, B, L, H, Dh, drop, causal):
+    """Pruning importance (compressed_attention.py:302-306): the forward's optional per-query row
+    sums of the post-dropout weights vs fp32 torch (rel 1e-4 per element, fp32 exp sums), the
+    importance kernel = mean over keys then heads, and O unchanged (bit-exact) by the extra
+    output."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    g = torch.Generator().manual_seed(L * 7 + Dh)
+    if causal:
+        n_img = (L - 2 * 4 - 2 * 13) // 2
+        lens = [13, n_img, 4, 13, n_img, 4]
+        lens[-1] += L - sum(lens)
+        starts = [sum(lens[:i]) for i in range(len(lens))]
+        vis = [0b000001, 0b000011, 0b000111, 0b011011, 0b011011, 0b111011]
+        cz = [True, False, False, True, False, False]
+    elif L == 1064:
+        starts = [0, 32, 288, 544, 548, 804, 1060]
+        lens = [32, 256, 256, 4, 256, 256, 4]
+        vis = [0b0000001, 0b0000111, 0b0000111, 0b0001111, 0b0110111, 0b0110111, 0b1110111]
+        cz = None
+    else:
+        (starts, lens, vis), cz = octo_small_table(32, L - 36, 4), None
+    table = K.SetTable(starts, lens, vis, cz)
+    mask = dense_mask(starts, lens, vis, L, dev, cz)
+    qkv = torch.randn((B, L, 3 * H * Dh), generator=g).bfloat16().to(dev)
+    scale = Dh ** -0.5
+    keep_prob = 0.9 if drop else 1.0
+    rng = torch.tensor([11, 3], dtype=torch.int32, device=dev)
+    bits = K.dropout_bits(rng, 2, 0, L, L, keep_prob) if drop else None
+    keep = bits_to_keep(bits[0], L).to(dev) if drop else None
+    o0, lse0 = K.attn_fwd(qkv, H, scale, table, bits, keep_prob)
+    wsum = torch.full((B, H, L), float("nan"), device=dev)
+    o, lse = K.attn_fwd(qkv, H, scale, table, bits, keep_prob, wsum=wsum)
+    assert torch.equal(o, o0) and torch.equal(lse, lse0)
+    q, k, _ = qkv.float().view(B, L, 3, H, Dh).unbind(2)
+    s = torch.einsum("bqhd,bkhd->bhqk", q, k) * scale
+    s = torch.where(mask[None, None], s, torch.finfo(torch.float32).min)
+    p = torch.softmax(s, dim=-1)
+    if keep is not None:
+        p = torch.where(keep[None, None], p / keep_prob, torch.zeros_like(p))
+    want = p.sum(-1)
+    torch.testing.assert_close(wsum, want, rtol=1e-4, atol=1e-6)
+    imp = K.prune_importance(wsum)
+    torch.testing.assert_close(imp, p.mean(-1).mean(1), rtol=1e-4, atol=1e-8)
+    # the kernel's own arithmetic (h ascending, IEEE / L then / H) exactly; tensor divisors,
+    # since torch turns a division by a Python scalar into a multiply by its reciprocal
+    ref = torch.zeros((B, L), device=dev)
+    Lt, Ht = torch.full_like(ref, L), torch.full_like(ref, H)
+    for h in range(H):
+        ref = ref + wsum[:, h] / Lt
+    assert torch.equal(imp, ref / Ht)
+
+
 @pytest.mark.parametrize("B,L,H,Dh,drop", [(2, 110, 3, 64, True), (2, 200, 2, 128, False),
                                            (2, 74, 3, 256, True)])
 def test_attention_causal_text_sets(dev, B, L, H, Dh, drop):

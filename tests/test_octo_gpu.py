@@ -119,6 +119,35 @@ def test_blockwise_causal_text(dev):
     P.check_blockwise(P.oracle_blockwise(cfg, res))
 
 
+def test_blockwise_prune_full_depth(dev):
+    """Top-k pruning as the compressor (octo-small-prune16: 16 image tokens per block removed by
+    attention importance, every token set passed through compute_top_k_tokens): at full depth,
+    every layer's kept rows checked in situ against the literal top-k restatement on the step's
+    own importance scores, the scores against the oracle's (relative L2 <= 5e-3), then the
+    block-local bar with the rows injected (per tensor: >= 0.999, or no further from the
+    emulating oracle than that oracle is from float64 on the same block — measured for block 0's
+    LN1/Dense_0 bias: HIP 0.99874, floor 0.99829)."""
+    cfg = _cfg("octo-small-prune16")
+    assert cfg.compression == "prune" and cfg.tome_r == 0
+    res = P.hip_blockwise(cfg, 2, seed=0)
+    assert res["prune_layers_checked"] == 12
+    assert res["xs"][1].shape[1] == 292 - 16 and res["xL"].shape[1] == 292 - 12 * 16
+    out = P.oracle_blockwise(cfg, res)
+    assert sum(k.startswith("importance") for k in out["act"]) == 12
+    P.check_blockwise(out, cfg=cfg, res=res)
+    # at most the cancellation-heavy reductions of a few blocks may need the floor
+    assert len(out.get("floor_accepted", {})) <= 6, out["floor_accepted"]
+
+
+def test_e2e_free_running_prune(dev):
+    """octo-tiny with pruning on both sets at 2 blocks, free running, floor-relative bar."""
+    cfg = _cfg("octo-tiny", num_blocks=2, token_compression_sequence="[Image{2};Readout{1}]",
+               compression="prune")
+    out = P.run_parity(cfg, 3, seed=0, floor=True)
+    assert out["prune_layers_checked"] == 2
+    P.check_against_floor(out)
+
+
 def test_staged_backward_matches_backward(dev):
     """The block-range stages used to overlap the gradient all-reduce (bench.py, N > 1) write
     the gradients of the one-piece backward (up to the order of the fp32 atomics some bias and

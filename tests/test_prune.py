@@ -63,3 +63,16 @@ def test_topk_backward_scatter(dev):
     for b in range(2):
         ref[b, idx[b].long()] = gout[b]
     torch.testing.assert_close(x.grad, ref, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gather_rows_bit_exact(dev, dt):
+    """mmt_gather_rows (the pruned block's residual rows) == torch advanced indexing."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn((3, 292, 384), generator=g).to(dt).to(dev)
+    idx = torch.stack([torch.randperm(292, generator=g)[:276] for _ in range(3)]).int().to(dev)
+    out = K.gather_rows(x, idx)
+    want = x[torch.arange(3, device=dev)[:, None], idx.long()]
+    assert torch.equal(out, want)

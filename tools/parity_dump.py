@@ -35,9 +35,11 @@ def save(path, cfg_args, res, grads=True):
     d = dict(meta=json.dumps(dict(cfg_args, B=res["B"], seed=res["seed"])), loss=res["loss"],
              rt=res["rt"], ct=res["ct"], t=res["t"], eps=res["eps"])
     for i, tr in enumerate(res["tome"]):
-        if tr is not None:
+        if isinstance(tr, tuple):
             for k, a in zip(("unm", "src", "dst"), tr):
                 d[f"tome_{i}_{k}"] = a
+        elif tr is not None:          # top-k pruning rows
+            d[f"tome_{i}_topk"] = np.asarray(tr)
     for name, a in res.get("trace", {}).items():
         d["tr/" + name] = a.astype(np.float32)
     for name, g in (res["grads"].items() if grads else ()):
@@ -67,6 +69,8 @@ def load(path):
     for i in range(max(nb, 0)):
         if f"tome_{i}_unm" in z.files:
             res["tome"].append(tuple(z[f"tome_{i}_{k}"] for k in ("unm", "src", "dst")))
+        elif f"tome_{i}_topk" in z.files:
+            res["tome"].append(z[f"tome_{i}_topk"])
         else:
             res["tome"].append(None)
     return meta, res
