@@ -88,25 +88,9 @@ def algorithmic_flops_per_sample(model) -> float:
 PROBE_KERNEL = "gemm_nt256_kernel<256, 0, false, 2>"
 
 
-def probe_dominant_gemm(model, B, reps=20):
-    """Average duration (HIP events on the launching stream) of the MLP up-projection GEMM of
-    block 0 at the step's exact shape: M = B*L1, N = mlp_dim, K = D (bias+relu+dropout fused);
-    the library's automatic choice for this NT shape (N >= 1152, N % 256 == 0, K <= 512) is the
-    persistent 256 x 256 kernel gemm_nt256_kernel<256, 0, false, 2> (csrc/gemm.hip)."""
-    cfg = model.cfg
-    blk = model.stack.blocks[0]
-    sets, _, ts, r, prune = model.layer_sets[0]
-    M = B * (sum(prune[1]) if prune else sets.L - r)
-    D = cfg.token_embedding_dim
-    x = torch.randn((M, D), device=model.device).to(torch.bfloat16)
-    rng = torch.tensor([7, 1], dtype=torch.int32, device=model.device)
-    out = torch.empty((M, cfg.mlp_dim), dtype=torch.bfloat16, device=model.device)
-
-    def launch():
-        blk.mlp.dense.fwd(x, out=out, act=K.ACT_RELU, rng=rng, drop_layer=0, drop_site=2,
-                          keep_prob=0.9)
-    # reps launches captured in one HIP graph (as in the training step: no host launch gaps),
-    # timed with HIP events recorded on the stream the graph replays on
+def _graph_time_us(launch, reps):
+    """Average duration of `launch` (µs): reps launches captured in one HIP graph (no host gaps,
+    as in the training step), timed with HIP events recorded on the stream the graph replays on."""
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
@@ -126,24 +110,126 @@ def probe_dominant_gemm(model, B, reps=20):
     g.replay()
     e1.record(s)
     e1.synchronize()
-    avg_ms = e0.elapsed_time(e1) / reps
-    flops = 2.0 * M * cfg.mlp_dim * D
-    return dict(kernel=PROBE_KERNEL + " (MLP Dense_0 fwd, bias+relu+dropout epilogue)",
-                shape=[M, cfg.mlp_dim, D], avg_us=avg_ms * 1e3, flops=flops,
-                tflops=flops / (avg_ms * 1e-3) / 1e12)
+    return e0.elapsed_time(e1) / reps * 1e3
 
 
-def gemm_traffic(shape):
-    """HBM bytes per launch of the probe GEMM from the committed rocprofv3 PMC passes
-    (profiles/*_gemm_pmc.json, written by tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE,
-    the gfx950 correction of MI355X_MICROARCH.md "HBM"), or None when no pass matches."""
+def _gemm_bytes(M, N, K, out_bytes=2, extra=0):
+    return 2 * (M * K + N * K) + out_bytes * M * N + extra
+
+
+def kernel_probes(model, B, reps=20):
+    """The step's heaviest kernels at their exact block-0 shapes (B per GPU), each launched alone:
+    per probe the kernel name (rocprofv3 substring), the average launch duration and the
+    algorithmic work per launch (flops for MFMA-bound kernels, bytes for HBM-bound ones; DESIGN.md
+    §3 states each figure). Covers the top of the step's trace: the nt256 GEMM (MLP up), the
+    direct-to-LDS NT GEMM (MLP input gradient, N = 384, K = 1536), the split-K weight-gradient
+    GEMM (MLP Dense_0 dW), attention forward and backward (dQ + dK/dV), ToMe merge forward and
+    the sequence-axis LayerNorm backward."""
+    from multi_modal_transformers_tokenmerge_amd.layers import split_k_for
+    cfg = model.cfg
+    dev = model.device
+    blk = model.stack.blocks[0]
+    sets, table, ts, r, prune = model.layer_sets[0]
+    L = sets.L
+    L1 = sum(prune[1]) if prune else L - r
+    D, Mh, H = cfg.token_embedding_dim, cfg.mlp_dim, cfg.num_heads
+    Dh = D // H
+    g = torch.Generator(device="cpu").manual_seed(0)
+
+    def rnd(*shape, dt=torch.bfloat16):
+        return torch.randn(shape, generator=g).to(dt).to(dev)
+
+    rng = torch.tensor([7, 1], dtype=torch.int32, device=dev)
+    out = []
+
+    def add(name, kernel, launch, bound, work, note, alg_bytes=None):
+        us = _graph_time_us(launch, reps)
+        if bound == "mfma":
+            ach = work / (us * 1e-6) / 1e12
+            out.append(dict(name=name, kernel=kernel, bound="mfma", avg_launch_us=round(us, 2),
+                            flops_per_launch=work, achieved=round(ach, 2),
+                            peak=MFMA_BF16_PEAK_TFLOPS, unit="TFLOP/s",
+                            frac=round(ach / MFMA_BF16_PEAK_TFLOPS, 4), note=note,
+                            algorithmic_bytes_per_launch=alg_bytes))
+        else:
+            ach = work / (us * 1e-6) / 1e9
+            out.append(dict(name=name, kernel=kernel, bound="hbm", avg_launch_us=round(us, 2),
+                            bytes_per_launch=work, achieved=round(ach, 1), peak=HBM_PEAK_GBS,
+                            unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4), note=note))
+
+    # 1. MLP up-projection (bias + relu + dropout epilogue): the dominant kernel
+    M = B * L1
+    y1 = rnd(M, D)
+    h = torch.empty((M, Mh), dtype=torch.bfloat16, device=dev)
+    add("mlp_up_fwd", PROBE_KERNEL,
+        lambda: blk.mlp.dense.fwd(y1, out=h, act=K.ACT_RELU, rng=rng, drop_layer=0, drop_site=2,
+                                  keep_prob=0.9),
+        "mfma", 2.0 * M * Mh * D, f"M={M} N={Mh} K={D}, 2MNK", _gemm_bytes(M, Mh, D, extra=4 * Mh))
+    # 2. MLP input gradient dy1 = dz1 . W1 (NT on the transposed shadow): N = 384, K = 1536
+    dz1 = rnd(M, Mh)
+    dy1 = torch.empty((M, D), dtype=torch.bfloat16, device=dev)
+    add("mlp_dx", "gemm_glds_nt_kernel<0>",
+        lambda: K.gemm(dz1, blk.mlp.dense.w.bf16_t, trans_b=True, out=dy1),
+        "mfma", 2.0 * M * D * Mh, f"M={M} N={D} K={Mh}, 2MNK", _gemm_bytes(M, D, Mh))
+    # 3. MLP Dense_0 weight gradient dW += dz1^T . y1 (TN, split-K fp32 slabs + combine)
+    wgrad = torch.zeros((Mh, D), dtype=torch.float32, device=dev)
+    add("mlp_dw", "gemm_big_kernel<true, false, 2>",
+        lambda: K.gemm(dz1, y1, trans_a=True, out=wgrad, out_mode=K.OUT_F32_ACCUM,
+                       split_k=split_k_for(Mh, D, M)),
+        "mfma", 2.0 * M * D * Mh,
+        f"M={Mh} N={D} K={M}, 2MNK (split-K GEMM + its combine kernel together)",
+        2 * (M * Mh + M * D) + 8 * Mh * D)
+    # 4./5. attention forward and backward of block 0 (token-set mask, dropout)
+    qkv = rnd(B, L, 3 * D)
+    kpa = 1.0 - cfg.attention_dropout_rate
+    bits = K.dropout_bits(rng, 0, 0, L, L, kpa)
+    scale = Dh ** -0.5
+    o, lse = K.attn_fwd(qkv, H, scale, table, bits, kpa)
+    fwd_flops = 4.0 * L * L * Dh * H * B
+    add("attn_fwd", "attn_fwd_kernel",
+        lambda: K.attn_fwd(qkv, H, scale, table, bits, kpa), "mfma", fwd_flops,
+        f"B={B} L={L} H={H} Dh={Dh}: 4 L^2 Dh H B (dense count, masked tiles included)",
+        B * L * (3 * D + D) * 2 + B * H * L * 4)
+    do = rnd(B, L, D)
+    bgrad = torch.zeros(3 * D, dtype=torch.float32, device=dev)
+    add("attn_bwd", "attn_bwd_dkdv_kernel",
+        lambda: K.attn_bwd(qkv, o, do, lse, H, scale, table, bits, kpa, bias_grad=bgrad),
+        "mfma", 2.5 * fwd_flops,
+        "dQ + dK/dV kernels together: 2.5 x the forward count (flash-attention convention)",
+        B * L * (3 * D + 2 * D + 3 * D) * 2 + B * H * L * 8)
+    # 6. ToMe merge forward of block 0 (fp32 residual stream, image set)
+    if r > 0:
+        s0, t = sets.starts[ts], sets.lens[ts]
+        x1 = rnd(B, L, D, dt=torch.float32)
+        unm, src, dst = K.tome_match(qkv.view(B, L, 3, H, Dh)[:, s0:s0 + t, 1], r)
+        torch.cuda.synchronize()
+        add("tome_merge_fwd", "tome_merge_fwd_kernel",
+            lambda: K.tome_merge_fwd(x1, s0, t, r, unm, src, dst, size_in=None), "hbm",
+            B * L * D * 4 + B * (L - r) * D * 4 + B * (t - r) * 4,
+            "read the fp32 sequence, write the merged sequence and the token sizes")
+    # 7. sequence-axis LayerNorm backward (fp32 x, bf16 dy, fp32 addend and dx)
+    x = rnd(B, L1, D, dt=torch.float32)
+    _, mu, rs = blk.ln1.fwd(x)
+    dy = rnd(B, L1, D)
+    addend = rnd(B, L1, D, dt=torch.float32)
+    add("seqnorm_bwd", "seqnorm_bwd_kernel",
+        lambda: blk.ln1.bwd(dy, x, mu, rs, addend=addend), "hbm", B * L1 * D * (4 + 2 + 4 + 4),
+        "read x (fp32), dy (bf16), the addend (fp32); write dx (fp32)")
+    return out
+
+
+def probe_traffic():
+    """HBM bytes per launch of each probe from the committed rocprofv3 PMC passes
+    (profiles/*_probe_pmc.json, written by tools/pmc_traffic.py from a FETCH_SIZE and a WRITE_SIZE
+    pass over `bench.py --probe-only`: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
+    MI355X_MICROARCH.md "HBM"); {} when none is committed."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_gemm_pmc.json")), reverse=True):
-        with open(f) as fh:
-            d = json.load(fh)
-        if list(d.get("shape_MNK", [])) == list(shape) and d.get("kernel") == PROBE_KERNEL:
-            return d["hbm_bytes_per_launch"]
-    return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_probe_pmc.json")))
+    if not files:
+        return {}
+    with open(files[-1]) as fh:
+        d = json.load(fh)
+    return {k: v["hbm_bytes_per_launch"] for k, v in d.get("probes", {}).items()}
 
 
 def cpu_baseline(cfg_name, model, budget_s=15.0, B=2):
@@ -214,9 +300,8 @@ def main():
     cfg = get_config(args.config)
     B = args.batch
     model = Octo(cfg, dev, seed=0)
-    if args.probe_only:
-        probe = probe_dominant_gemm(model, B, reps=50)
-        print(json.dumps(dict(probe_only=True, **probe)), flush=True)
+    if args.probe_only:  # for rocprofv3 --pmc traffic passes (tools/pmc_traffic.py)
+        print(json.dumps(dict(probe_only=True, probes=kernel_probes(model, B))), flush=True)
         return
     if di.enabled:  # identical initial parameters on every rank (broadcast from rank 0)
         dist.broadcast(model.store.flat, 0)
@@ -253,16 +338,21 @@ def main():
     if di.rank == 0:
         ms = elapsed / args.steps * 1e3
         value = N * B * args.steps / elapsed
-        probe = probe_dominant_gemm(model, B)
-        roof = dict(bound="mfma", achieved=round(probe["tflops"], 2), peak=MFMA_BF16_PEAK_TFLOPS,
-                    unit="TFLOP/s", frac=round(probe["tflops"] / MFMA_BF16_PEAK_TFLOPS, 4),
-                    traffic=gemm_traffic(probe["shape"]), kernel=probe["kernel"], shape_MNK=probe["shape"],
-                    avg_launch_us=round(probe["avg_us"], 2),
-                    flops_per_launch=probe["flops"],
-                    algorithmic_bytes_per_launch=2 * (probe["shape"][0] * probe["shape"][2]
-                                                      + probe["shape"][1] * probe["shape"][2]
-                                                      + probe["shape"][0] * probe["shape"][1])
-                    + 4 * probe["shape"][1])
+        probes = kernel_probes(model, B)
+        traffic = probe_traffic()
+        for pr in probes:
+            pr["traffic"] = traffic.get(pr["name"])
+        top = probes[0]
+        sets0, _, _, r0, pr0 = model.layer_sets[0]
+        M_ = B * (sum(pr0[1]) if pr0 else sets0.L - r0)
+        N_, K_ = cfg.mlp_dim, cfg.token_embedding_dim
+        roof = dict(bound="mfma", achieved=top["achieved"], peak=MFMA_BF16_PEAK_TFLOPS,
+                    unit="TFLOP/s", frac=top["frac"], traffic=top["traffic"],
+                    kernel=top["kernel"] + " (MLP Dense_0 fwd, bias+relu+dropout epilogue)",
+                    shape_MNK=[M_, N_, K_], avg_launch_us=top["avg_launch_us"],
+                    flops_per_launch=top["flops_per_launch"],
+                    algorithmic_bytes_per_launch=_gemm_bytes(M_, N_, K_, extra=4 * N_),
+                    kernels=probes[1:])
         fps = algorithmic_flops_per_sample(model)
         cpu = None
         if N == 1 and not args.no_cpu_baseline:

@@ -851,9 +851,6 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
     voff[p] = row * (int)((p < GA ? lda : ldb) * 2) + c * 16;
   }
   auto piece = [&](int m0, int n0, int k0, int st, int p) {
-#ifdef NT_NO_LOAD  // tools/nt_trace: time the kernel without its operand DMA (wrong results)
-    return;
-#endif
     char* S0 = smem + st * STAGE;
     if (p < GA)
       dma16(A + (int64_t)m0 * lda, (int64_t)(M - m0) * lda * 2, S0 + (wave * GA + p) * 1024,
@@ -906,14 +903,9 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
     if (gr < M) {
       const int64_t off = (int64_t)gr * ldc + sgc + (OUT == 0 ? 8 : 4) * c;
       const uint4 u = make_uint4(stash[ci][0], stash[ci][1], stash[ci][2], stash[ci][3]);
-#ifdef NT_NO_STORE
-      if (u.x == 0x12345u)
-#endif
-      {
-        // plain stores: non-temporal ones (MMT_NT_STORE experiment) doubled this kernel's time
-        if (OUT == 0) *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(Cv) + off) = u;
-        else *reinterpret_cast<uint4*>(reinterpret_cast<float*>(Cv) + off) = u;
-      }
+      // plain stores: non-temporal ones measured twice this kernel's time
+      if (OUT == 0) *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(Cv) + off) = u;
+      else *reinterpret_cast<uint4*>(reinterpret_cast<float*>(Cv) + off) = u;
     }
   };
 
@@ -931,34 +923,17 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
     for (int h = 0; h < 2; ++h) {
       const int c = 4 * h + lq;
       bf16x8 af[4], bfr[NF];
-#ifdef NT_NO_DSREAD  // tools/nt_trace: MFMAs on register operands, no LDS reads (wrong results)
-#pragma unroll
-      for (int mf = 0; mf < 4; ++mf) {
-        uint4 u = make_uint4(lane + mf, c, 3, 4);
-        asm volatile("" : "+v"(u.x), "+v"(u.y), "+v"(u.z), "+v"(u.w));
-        af[mf] = __builtin_bit_cast(bf16x8, u);
-      }
-#pragma unroll
-      for (int nf = 0; nf < NF; ++nf) {
-        uint4 u = make_uint4(lane + nf, c, 5, 6);
-        asm volatile("" : "+v"(u.x), "+v"(u.y), "+v"(u.z), "+v"(u.w));
-        bfr[nf] = __builtin_bit_cast(bf16x8, u);
-      }
-#else
 #pragma unroll
       for (int mf = 0; mf < 4; ++mf)
         af[mf] = *reinterpret_cast<const bf16x8*>(S0 + a_off[mf] + ((c ^ a_sw[mf]) << 4));
 #pragma unroll
       for (int nf = 0; nf < NF; ++nf)
         bfr[nf] = *reinterpret_cast<const bf16x8*>(S0 + b_off[nf] + ((c ^ b_sw[nf]) << 4));
-#endif
 #pragma unroll
       for (int mf = 0; mf < 4; ++mf) {
-#ifndef NT_NO_MFMA
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf)
           acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nf], af[mf], acc[mf][nf], 0, 0, 0);
-#endif
         if (h == hl && nxt) {
           if (2 * mf < G) piece(nm0, nn0, nk0, nst, 2 * mf);
           if (2 * mf + 1 < G) piece(nm0, nn0, nk0, nst, 2 * mf + 1);
@@ -1015,9 +990,6 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
             }
             continue;
           }
-#ifdef NT_NO_STORE  // tools/nt_trace: time the kernel without its output stores
-          if (v[0] == 12345.f)
-#endif
           store_w<OUT, 8>(Cv, (int64_t)gr * ldc + gc0 + 8 * c8, epi.beta, v);
         }
       }

@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
 """Turn two rocprofv3 --pmc passes over `bench.py --probe-only` into the per-launch HBM traffic
-of the probe GEMM (the `roofline.traffic` field of bench.py).
+of every kernel probe (the `traffic` fields of bench.py's roofline).
 
+    python bench.py --probe-only > gpurun_out/probes.json
     rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --probe-only
     rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --probe-only
-    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write --shape M N K --out profiles/r01_nt256_gemm_pmc.json
+    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write --probes gpurun_out/probes.json --out profiles/r02_probe_pmc.json
 
 FETCH_SIZE and WRITE_SIZE are in KB. gfx950 correction (MI355X_MICROARCH.md, "HBM"): FETCH_SIZE
 counts half of the bytes of 16 B/lane streaming reads, so reads = 2 x FETCH_SIZE; WRITE_SIZE is
-exact for 16 B/lane stores.
+exact for 16 B/lane stores. A probe whose launch is several kernels (attention backward = dQ +
+dK/dV, split-K GEMM + combine) is matched by its main kernel only.
 """
 from __future__ import annotations
 
@@ -18,6 +20,7 @@ import glob
 import json
 import os
 import statistics
+
 
 def per_dispatch(d: str, counter: str, kernel: str) -> list[float]:
     files = glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True)
@@ -31,8 +34,6 @@ def per_dispatch(d: str, counter: str, kernel: str) -> list[float]:
                     continue
                 key = f"{f}:{row.get('Dispatch_Id')}"
                 vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
-    if not vals:
-        raise SystemExit(f"no {counter} rows for {kernel} under {d}")
     return list(vals.values())
 
 
@@ -40,25 +41,30 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
-    ap.add_argument("--shape", type=int, nargs=3, required=True)
+    ap.add_argument("--probes", required=True, help="the JSON line of bench.py --probe-only")
     ap.add_argument("--out", required=True)
-    ap.add_argument("--kernel", default="gemm_nt256_kernel<256, 0, false, 2>",
-                    help="substring of the demangled kernel name (bench.py PROBE_KERNEL)")
     a = ap.parse_args()
-    fetch = per_dispatch(a.fetch_dir, "FETCH_SIZE", a.kernel)
-    write = per_dispatch(a.write_dir, "WRITE_SIZE", a.kernel)
-    f_kb, w_kb = statistics.median(fetch), statistics.median(write)
-    M, N, K = a.shape
-    alg = 2 * (M * K + N * K + M * N) + 4 * N
-    hbm = 2 * f_kb * 1024 + w_kb * 1024
-    out = dict(kernel=a.kernel, shape_MNK=[M, N, K], dispatches=[len(fetch), len(write)],
-               fetch_size_kb_median=f_kb, write_size_kb_median=w_kb,
-               read_bytes_corrected=2 * f_kb * 1024, write_bytes=w_kb * 1024,
-               hbm_bytes_per_launch=round(hbm), algorithmic_bytes_per_launch=alg,
-               ratio_to_algorithmic=round(hbm / alg, 3))
+    with open(a.probes) as fh:
+        line = [ln for ln in fh if ln.startswith("{")][-1]
+    probes = json.loads(line)["probes"]
+    res = {}
+    for p in probes:
+        fetch = per_dispatch(a.fetch_dir, "FETCH_SIZE", p["kernel"])
+        write = per_dispatch(a.write_dir, "WRITE_SIZE", p["kernel"])
+        if not fetch or not write:
+            print(f"no counter rows for {p['kernel']}")
+            continue
+        f_kb, w_kb = statistics.median(fetch), statistics.median(write)
+        hbm = 2 * f_kb * 1024 + w_kb * 1024
+        alg = p.get("bytes_per_launch") or p.get("algorithmic_bytes_per_launch")
+        res[p["name"]] = dict(kernel=p["kernel"], dispatches=[len(fetch), len(write)],
+                              fetch_size_kb_median=f_kb, write_size_kb_median=w_kb,
+                              read_bytes_corrected=2 * f_kb * 1024, write_bytes=w_kb * 1024,
+                              hbm_bytes_per_launch=round(hbm), algorithmic_bytes_per_launch=alg,
+                              ratio_to_algorithmic=round(hbm / alg, 3) if alg else None)
     with open(a.out, "w") as fh:
-        json.dump(out, fh, indent=1)
-    print(json.dumps(out))
+        json.dump(dict(probes=res), fh, indent=1)
+    print(json.dumps(res))
 
 
 if __name__ == "__main__":
