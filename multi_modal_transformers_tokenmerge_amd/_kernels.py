@@ -295,12 +295,15 @@ class SetTable:
 
 def dropout_bits(rng: torch.Tensor, layer: int, site: int, rows: int, cols: int, keep_prob: float,
                  out: torch.Tensor | None = None):
-    """Keep bitmask words (rows, ceil(cols/32)) int32; for a square (attention) mask the result
-    is (2, L, W): [0] row-major, [1] transposed (what the dK/dV kernel reads)."""
+    """Keep bitmask words (rows, ceil(cols/32)) int32, bit j of word (r, w) = keep(r, 32w + j).
+    For a square (attention) mask the result is (2, W, LP), LP = roundup(L, 64): [0] the query-word
+    image (bit j of word (w, pos(k)) = keep(32w + j, k), read by the forward and dQ kernels),
+    [1] the key-word image (bit j of word (w, pos(q)) = keep(q, 32w + j), read by dK/dV), with
+    pos(8g + 4h + i) = 8g + 2i + h (csrc/attention.hip TileMasks: SGPR lane masks)."""
     words = (cols + 31) // 32
     square = rows == cols
     if out is None:
-        shape = (2, rows, words) if square else (rows, words)
+        shape = (2, words, (rows + 63) // 64 * 64) if square else (rows, words)
         out = torch.empty(shape, dtype=torch.int32, device=rng.device)
     out_t = ptr(out[1]) if square else None
     _C.call("mmt_dropout_bits", ptr(rng), layer, site, rows, cols, keep_prob,
@@ -315,6 +318,13 @@ def _qkv_geo(qkv: torch.Tensor, H: int):
     if three_d % (3 * H):
         raise ValueError("qkv last dim must be 3*H*Dh")
     return B, L, three_d // (3 * H)
+
+
+def _check_attn_bits(bits: torch.Tensor, L: int):
+    want = (2, (L + 31) // 32, (L + 63) // 64 * 64)
+    if tuple(bits.shape) != want or bits.dtype != torch.int32 or not bits.is_contiguous():
+        raise ValueError(f"attention dropout needs the square mask of dropout_bits(.., L, L, ..): "
+                         f"contiguous int32 {want}, got {tuple(bits.shape)}")
 
 
 def attn_fwd(qkv: torch.Tensor, H: int, scale: float, table: SetTable | None = None,
@@ -333,7 +343,8 @@ def attn_fwd(qkv: torch.Tensor, H: int, scale: float, table: SetTable | None = N
     if out is None:
         out = torch.empty((B, L, H * Dh), dtype=torch.bfloat16, device=qkv.device)
     lse = torch.empty((B, H, L), dtype=torch.float32, device=qkv.device)
-    if drop_bits is not None and drop_bits.dim() == 3:
+    if drop_bits is not None:
+        _check_attn_bits(drop_bits, L)
         drop_bits = drop_bits[0]
     if wsum is not None and (tuple(wsum.shape) != (B, H, L) or wsum.dtype != torch.float32
                              or not wsum.is_contiguous()):
@@ -356,8 +367,8 @@ def attn_bwd(qkv, o, dout, lse, H: int, scale: float, table: SetTable | None = N
     if dqkv is None:
         dqkv = torch.empty_like(qkv)
     delta = torch.empty((B, H, L), dtype=torch.float32, device=qkv.device)
-    if drop_bits is not None and (drop_bits.dim() != 3 or drop_bits.shape[0] != 2):
-        raise ValueError("attn_bwd needs the (2, L, W) mask of dropout_bits (row-major + transposed)")
+    if drop_bits is not None:
+        _check_attn_bits(drop_bits, L)
     bits, bits_t = (None, None) if drop_bits is None else (drop_bits[0], drop_bits[1])
     if bias_grad is not None and (bias_grad.dtype != torch.float32 or bias_grad.numel() != 3 * H * Dh
                                   or not bias_grad.is_contiguous()):

@@ -12,9 +12,9 @@
 // waves whose 32 rows lie past L skip the math. T5 mode: an additive fp32 (H, L, L) bias, scale 1.
 //
 // Layout: qkv rows (b, t) hold [q(H, Dh) | k(H, Dh) | v(H, Dh)] (the fused QKV GEMM output);
-// o rows (b, t) hold (H, Dh); lse / delta are (B, H, L) fp32. Dropout keep bits: (L, W) words,
-// bit k of word (q, k/32); the backward also takes the transposed (L, W) words (bit q of
-// word (k, q/32)) so the key-on-lane dK/dV kernel reads one word per 32 queries.
+// o rows (b, t) hold (H, Dh); lse / delta are (B, H, L) fp32. Dropout keep bits: the two
+// word-major images of mmt_dropout_bits (query words for the forward / dQ, key words for dK/dV),
+// read as SGPR lane masks (TileMasks).
 //
 // Forward and dQ: one wave = 32 queries ON THE LANES; S^T = K . Q^T so every score of a query is
 // lane-local (registers) and the row max / sum need one cross-half exchange; the S^T accumulator
@@ -33,6 +33,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short short4v __attribute__((ext_vector_type(4)));
 typedef short short8v __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float float2v __attribute__((ext_vector_type(2)));
 
 namespace {
 
@@ -171,20 +172,35 @@ __device__ __forceinline__ bf16x8 row_frag_global(const bf16_t* rowp, bool valid
   return __builtin_bit_cast(bf16x8, make_uint4(v.x & m, v.y & m, v.z & m, v.w & m));
 }
 
-// Dropout keep words t0/32 and t0/32 + 1 of one row (all ones past the last word, for an invalid
-// row, or without dropout). Branch-free loads from clamped addresses, for the reason above;
-// `row` must be a valid row index.
-__device__ __forceinline__ void load_drop_words(const uint32_t* bits, int words, int row,
-                                                bool valid, int t0, uint32_t dw[2]) {
-  dw[0] = dw[1] = 0xffffffffu;
-  if (bits) {  // kernel-uniform
-    const int w0 = t0 >> 5, w1 = min(w0 + 1, words - 1);
-    const uint32_t* p = bits + (int64_t)row * words;
-    const uint32_t a = p[w0], c = p[w1];
-    dw[0] = valid ? a : 0xffffffffu;
-    dw[1] = (valid && w0 + 1 < words) ? c : 0xffffffffu;
-  }
+// Dropout keep masks as SGPR lane masks. mmt_dropout_bits stores the square (L, L) keep mask
+// twice, word-major with interleaved positions, rows padded to LP = roundup(L, 64) zero words:
+//   QF[w][pos(k)]: bit j = keep(32 w + j, k)   (query words: the query-on-lane kernels)
+//   KF[w][pos(q)]: bit j = keep(q, 32 w + j)   (key words: the key-on-lane dK/dV kernel)
+// pos(8g + 4h + i) = 8g + 2i + h. For a 64-wide tile at t0 (a multiple of 64), the 64-bit pair
+// 16u + r of the 64 words X[w][t0 .. t0 + 63] is the lane mask of accumulator register r of the
+// 32-wide sub-tile u: element offset 32u + rbit(r) for lanes 0-31 (the 32 lane rows of word w) in
+// its low half, offset 32u + rbit(r) + 4 for lanes 32-63 in its high half. So the mask of one
+// score is one v_cndmask with its condition read from an SGPR pair (scalar loads of the tile's
+// 256 B per wave), instead of a bit extraction per score.
+__host__ __device__ __forceinline__ int lp_of(int L) { return (L + 63) & ~63; }
+__device__ __forceinline__ int key_of_pos(int p) { return (p & ~7) | ((p & 1) << 2) | ((p >> 1) & 3); }
+__device__ __forceinline__ float sel_keep(float v, uint64_t m) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(v), "s"(m));
+  return r;
 }
+// The N lane masks of one (word, tile or 32-wide sub-tile at t0): wave-uniform address, so
+// these are scalar loads (indices into m[] must be compile-time constants to stay in SGPRs).
+template <int N>
+struct TileMasks {
+  uint64_t m[N];
+  __device__ __forceinline__ void load(const uint32_t* bits, int lp, int w, int t0) {
+    const uint64_t* p = reinterpret_cast<const uint64_t*>(
+        bits + (int64_t)__builtin_amdgcn_readfirstlane(w) * lp + __builtin_amdgcn_readfirstlane(t0));
+#pragma unroll
+    for (int j = 0; j < N; ++j) m[j] = p[j];
+  }
+};
 
 // Pack accumulator registers 8s..8s+7 to a bf16 operand fragment.
 __device__ __forceinline__ bf16x8 pack_frag(const floatx16& x, int s) {
@@ -280,9 +296,9 @@ struct Geo {
 // one-block-per-workgroup form read them once per 128 rows, 2.3x the algorithmic bytes at
 // L = 292) and each LDS tile feeds NQ x 16 MFMAs per wave instead of 16, which amortises the
 // per-tile barrier and the per-workgroup prologue.
-template <int DH, int NQ>
+template <int DH, int NQ, bool WS>
 __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
-    Geo g, AttnMask mask, const uint32_t* __restrict__ drop_bits, int drop_words, float drop_scale,
+    Geo g, AttnMask mask, const uint32_t* __restrict__ drop_q, int drop_lp, float drop_scale,
     const float* __restrict__ bias, bf16_t* __restrict__ o, int64_t o_s_b, int64_t o_s_t,
     float* __restrict__ lse, float* __restrict__ wsum) {
   constexpr int STR = DH + 8;
@@ -293,7 +309,8 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
   // visibility word of every (query set, 64-key tile) pair, built once per workgroup
   __shared__ uint64_t s_vis[MAX_SETS * (MAXL / KT)];
   const int b = blockIdx.z, h = blockIdx.y;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int L = g.L, D = g.H * DH;
   const int q0 = blockIdx.x * (QB * NQ), q1 = min(L, q0 + QB * NQ);
   const bf16_t* base = g.qkv + (int64_t)b * g.s_b;
@@ -352,8 +369,6 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
       if (mask.causal) vm = causal_keys(mask, sq[i], qrow[i], kt, vm);
       if (__all(vm == 0ull)) continue;  // no query of this block sees the tile
       const int q = qrow[i];
-      uint32_t dw[2];
-      load_drop_words(drop_bits, drop_words, qv[i] ? q : 0, qv[i], kt, dw);
       floatx16 sacc[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -399,25 +414,34 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
       const float mn = fmaxf(m[i], tmax);
       const float mnc = mn == -INFINITY ? 0.f : mn * c;
       const float alpha = fast_exp2(m[i] * c - mnc);  // m = -inf -> 0 (nothing accumulated yet)
-      float rs = 0.f;
+      // p = 2^(s c - m) in packed pairs (v_pk_fma / v_pk_add), the row sum before dropout, the
+      // dropout keep mask as one v_cndmask per score from the SGPR lane masks
+      float2v rs2 = {0.f, 0.f}, rd2 = {0.f, 0.f};
+      const float2v cc = {c, c}, mm = {-mnc, -mnc};
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const uint32_t w = dw[u] >> (4 * hh);
+        TileMasks<16> dm;  // dropout lane masks of (query word, key sub-tile): scalar loads
+        if (drop_q) dm.load(drop_q, drop_lp, (q0 >> 5) + wave + 4 * i, kt + 32 * u);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = fast_exp2(fmaf(sacc[u][r], c, -mnc));
-          rs += p;
-          sacc[u][r] = __int_as_float(__float_as_int(p) & bitmask_of(w, rbit(r)));
+        for (int r = 0; r < 16; r += 2) {
+          float2v a = {sacc[u][r], sacc[u][r + 1]};
+          a = __builtin_elementwise_fma(a, cc, mm);
+          float2v pp = {fast_exp2(a.x), fast_exp2(a.y)};
+          rs2 += pp;
+          if (drop_q) {
+            pp.x = sel_keep(pp.x, dm.m[r]);
+            pp.y = sel_keep(pp.y, dm.m[r + 1]);
+          }
+          if (WS) rd2 += pp;
+          sacc[u][r] = pp.x;
+          sacc[u][r + 1] = pp.y;
         }
       }
+      float rs = rs2.x + rs2.y;
       rs += __shfl_xor(rs, 32, 64);
       l[i] = l[i] * alpha + rs;
-      if (wsum) {  // kernel-uniform: row sum of the kept probabilities (pruning importance)
-        float rd = 0.f;
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) rd += sacc[u][r];
+      if (WS) {  // row sum of the kept probabilities (pruning importance)
+        float rd = rd2.x + rd2.y;
         rd += __shfl_xor(rd, 32, 64);
         ld[i] = ld[i] * alpha + rd;
       }
@@ -463,7 +487,7 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
       }
     if (lane < 32) {
       lse[((int64_t)b * g.H + h) * L + q] = l[i] > 0.f ? m[i] * c * LN2 + logf(l[i]) : -INFINITY;
-      if (wsum) wsum[((int64_t)b * g.H + h) * L + q] = ld[i] * inv;  // sum_k of the dropped weights
+      if (WS) wsum[((int64_t)b * g.H + h) * L + q] = ld[i] * inv;  // sum_k of the dropped weights
     }
   }
 }
@@ -471,8 +495,8 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
 // =============================================================================== bwd: dQ
 template <int DH, int NTT>
 __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dq_kernel(Geo g, AttnMask mask,
-                                                         const uint32_t* __restrict__ drop_bits,
-                                                         int drop_words, float drop_scale,
+                                                         const uint32_t* __restrict__ drop_q,
+                                                         int drop_lp, float drop_scale,
                                                          const bf16_t* __restrict__ dout,
                                                          int64_t d_s_b, int64_t d_s_t,
                                                          const float* __restrict__ lse,
@@ -489,7 +513,8 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dq_kernel(Geo 
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE];  // [buf][K | V]
   __shared__ float s_wsum[NTT / 64 * DH];
   const int b = blockIdx.z, h = blockIdx.y;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int L = g.L, D = g.H * DH;
   const int q0 = blockIdx.x * (NTT / 2), q1 = min(L, q0 + NTT / 2);
   const int q = q0 + wave * 32 + (lane & 31);
@@ -546,13 +571,14 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dq_kernel(Geo 
     const bf16_t* Ks = smem + buf * 2 * TILE;
     const bf16_t* Vs = Ks + TILE;
     if (wave_live) {
-      uint32_t dw[2];
-      load_drop_words(drop_bits, drop_words, qv ? q : 0, qv, kt, dw);
       uint64_t vm = sets_bits(mask, visq, kt);
       if (mask.causal) vm = causal_keys(mask, sq, q, kt, vm);
+      const bool full = __all(vm == ~0ull);  // wave-uniform: no visibility masking needed
       floatx16 ds[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
+        TileMasks<16> dm;  // dropout lane masks of (query word, key sub-tile): scalar loads
+        if (drop_q) dm.load(drop_q, drop_lp, (q0 >> 5) + wave, kt + 32 * u);
         floatx16 sacc, pacc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -567,13 +593,26 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dq_kernel(Geo 
                                                          pacc, 0, 0, 0);
         }
         const uint32_t wv = (uint32_t)(vm >> (32 * u)) >> (4 * hh);
-        const uint32_t wd = dw[u] >> (4 * hh);
+        const float2v sl = {sl2, sl2}, ml = {-lse2, -lse2}, dd = {drop_scale, drop_scale},
+                      dl = {dlt, dlt};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = __int_as_float(__float_as_int(fast_exp2(fmaf(sacc[r], sl2, -lse2))) &
-                                         bitmask_of(wv, rbit(r)));
-          const float t = __int_as_float(__float_as_int(pacc[r] * drop_scale) & bitmask_of(wd, rbit(r)));
-          ds[u][r] = p * (t - dlt);
+        for (int r = 0; r < 16; r += 2) {
+          float2v a = {sacc[r], sacc[r + 1]};
+          a = __builtin_elementwise_fma(a, sl, ml);
+          float2v pp = {fast_exp2(a.x), fast_exp2(a.y)};
+          if (!full) {
+            pp.x = __int_as_float(__float_as_int(pp.x) & bitmask_of(wv, rbit(r)));
+            pp.y = __int_as_float(__float_as_int(pp.y) & bitmask_of(wv, rbit(r + 1)));
+          }
+          float2v t = {pacc[r], pacc[r + 1]};
+          t *= dd;
+          if (drop_q) {
+            t.x = sel_keep(t.x, dm.m[r]);
+            t.y = sel_keep(t.y, dm.m[r + 1]);
+          }
+          const float2v dsp = pp * (t - dl);
+          ds[u][r] = dsp.x;
+          ds[u][r + 1] = dsp.y;
         }
       }
 #pragma unroll
@@ -616,8 +655,8 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dq_kernel(Geo 
 // =============================================================================== bwd: dK, dV
 template <int DH, int NTT>
 __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask mask,
-                                                           const uint32_t* __restrict__ drop_bits_t,
-                                                           int drop_words, float drop_scale,
+                                                           const uint32_t* __restrict__ drop_k,
+                                                           int drop_lp, float drop_scale,
                                                            const bf16_t* __restrict__ dout,
                                                            int64_t d_s_b, int64_t d_s_t,
                                                            const float* __restrict__ lse,
@@ -633,7 +672,8 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dkdv_kernel(Ge
   __shared__ __attribute__((aligned(16))) float s_rows[2][2][KT];  // [buf][lse*log2e | delta]
   __shared__ float s_wsum[NTT / 64 * DH];
   const int b = blockIdx.z, h = blockIdx.y;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int L = g.L, D = g.H * DH;
   const int kb0 = blockIdx.x * (NTT / 2), kb1 = min(L, kb0 + NTT / 2);
   const int key = kb0 + wave * 32 + (lane & 31);
@@ -695,12 +735,13 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dkdv_kernel(Ge
     const bf16_t* Qs = smem + buf * 2 * TILE;
     const bf16_t* Ds = Qs + TILE;
     if (wave_live) {
-      uint32_t dw[2];
-      load_drop_words(drop_bits_t, drop_words, kv ? key : 0, kv, qt, dw);
       uint64_t qm = sets_bits(mask, selq, qt);
       if (mask.causal) qm = causal_queries(mask, sk, key, qt, qm);
+      const bool full = __all(qm == ~0ull);  // wave-uniform: no visibility masking needed
 #pragma unroll 1
       for (int u = 0; u < 2; ++u) {  // 32-query sub-tiles (not unrolled: keeps 2 waves/SIMD)
+        TileMasks<16> dm;  // dropout lane masks of (key word, query sub-tile): scalar loads
+        if (drop_k) dm.load(drop_k, drop_lp, (kb0 >> 5) + wave, qt + 32 * u);
         floatx16 sacc, pacc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -724,16 +765,32 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dkdv_kernel(Ge
           dr[4 * j] = d.x; dr[4 * j + 1] = d.y; dr[4 * j + 2] = d.z; dr[4 * j + 3] = d.w;
         }
         const uint32_t wv = (uint32_t)(qm >> (32 * u)) >> (4 * hh);
-        const uint32_t wd = dw[u] >> (4 * hh);
         floatx16 pd, dsv;
+        const float2v sl = {sl2, sl2}, dd = {drop_scale, drop_scale};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = __int_as_float(__float_as_int(fast_exp2(fmaf(sacc[r], sl2, -lr[r]))) &
-                                         bitmask_of(wv, rbit(r)));
-          const int keep = bitmask_of(wd, rbit(r));
-          pd[r] = __int_as_float(__float_as_int(p) & keep);  // drop_scale applied to dV at the end
-          const float t = __int_as_float(__float_as_int(pacc[r] * drop_scale) & keep);
-          dsv[r] = p * (t - dr[r]);
+        for (int r = 0; r < 16; r += 2) {
+          float2v a = {sacc[r], sacc[r + 1]};
+          const float2v ml = {-lr[r], -lr[r + 1]}, dl = {dr[r], dr[r + 1]};
+          a = __builtin_elementwise_fma(a, sl, ml);
+          float2v pp = {fast_exp2(a.x), fast_exp2(a.y)};
+          if (!full) {
+            pp.x = __int_as_float(__float_as_int(pp.x) & bitmask_of(wv, rbit(r)));
+            pp.y = __int_as_float(__float_as_int(pp.y) & bitmask_of(wv, rbit(r + 1)));
+          }
+          float2v t = {pacc[r], pacc[r + 1]};
+          t *= dd;
+          float2v pk = pp;  // drop_scale applied to dV at the end
+          if (drop_k) {
+            pk.x = sel_keep(pp.x, dm.m[r]);
+            pk.y = sel_keep(pp.y, dm.m[r + 1]);
+            t.x = sel_keep(t.x, dm.m[r]);
+            t.y = sel_keep(t.y, dm.m[r + 1]);
+          }
+          const float2v dsp = pp * (t - dl);
+          pd[r] = pk.x;
+          pd[r + 1] = pk.y;
+          dsv[r] = dsp.x;
+          dsv[r + 1] = dsp.y;
         }
         const bf16x8 pd0 = pack_frag(pd, 0), pd1 = pack_frag(pd, 1);
         const bf16x8 ds0 = pack_frag(dsv, 0), ds1 = pack_frag(dsv, 1);
@@ -785,32 +842,38 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dkdv_kernel(Ge
 }
 
 // =============================================================================== dropout bits
-// idx < rows*words: word (r, w) of the row-major mask; idx >= rows*words (square masks, out_t
-// given): word (c, w) of the transposed mask, bit j = keep(r = 32w + j, c).
+// Non-square masks (out_t == null): row-major words (rows, W), bit j of word (r, w) = keep(r,
+// 32 w + j). Square attention masks: the two word-major interleaved images QF (out) and KF
+// (out_t) described at TileMasks, W x LP words each, zero past L.
 __global__ void dropout_bits_kernel(const uint32_t* __restrict__ rng, uint32_t layer, uint32_t site,
                                     int rows, int cols, int words, uint32_t thresh,
                                     uint32_t* __restrict__ out, uint32_t* __restrict__ out_t) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t n = (int64_t)rows * words;
-  if (idx >= (out_t ? 2 * n : n)) return;
   const uint32_t key = stream_key(rng[0], rng[1], layer, site);
   uint32_t bits = 0;
-  if (idx < n) {
+  if (!out_t) {
+    if (idx >= (int64_t)rows * words) return;
     const int r = idx / words, w = idx % words;
     for (int j = 0; j < 32; ++j) {
       const int c = w * 32 + j;
       if (c < cols && keep_elem(key, (uint32_t)((int64_t)r * cols + c), thresh)) bits |= 1u << j;
     }
     out[idx] = bits;
-  } else {
-    const int64_t t = idx - n;
-    const int c = t / words, w = t % words;
-    for (int j = 0; j < 32; ++j) {
-      const int r = w * 32 + j;
-      if (r < rows && keep_elem(key, (uint32_t)((int64_t)r * cols + c), thresh)) bits |= 1u << j;
-    }
-    out_t[t] = bits;
+    return;
   }
+  const int L = rows, lp = lp_of(L);
+  const int64_t n = (int64_t)words * lp;
+  if (idx >= 2 * n) return;
+  const bool kimg = idx >= n;
+  const int64_t t = kimg ? idx - n : idx;
+  const int w = t / lp, x = key_of_pos((int)(t % lp));
+  if (x < L)
+    for (int j = 0; j < 32; ++j) {
+      const int y = w * 32 + j;  // QF: row y, column x; KF: row x, column y
+      const int r = kimg ? x : y, c = kimg ? y : x;
+      if (y < L && keep_elem(key, (uint32_t)((int64_t)r * cols + c), thresh)) bits |= 1u << j;
+    }
+  (kimg ? out_t : out)[t] = bits;
 }
 
 int fill_mask(AttnMask& m, int n_sets, const int32_t* starts, const int32_t* lens,
@@ -873,10 +936,10 @@ inline int bwd_threads(int L) {
 #define ATTN_BWD_LAUNCH(DH_, NTT_)                                                                \
   do {                                                                                            \
     hipLaunchKernelGGL((attn_bwd_dq_kernel<DH_, NTT_>), grid, dim3(NTT_), 0, s, g, m, drop_bits,  \
-                       words, dscale, (const bf16_t*)dout, d_s_b, d_s_t, lse, (const bf16_t*)o,   \
+                       lp, dscale, (const bf16_t*)dout, d_s_b, d_s_t, lse, (const bf16_t*)o,   \
                        o_s_b, o_s_t, delta, (bf16_t*)dqkv, dq_s_b, dq_s_t, bias_grad);            \
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DH_, NTT_>), grid, dim3(NTT_), 0, s, g, m,           \
-                       drop_bits_t, words, dscale, (const bf16_t*)dout, d_s_b, d_s_t, lse, delta,  \
+                       drop_bits_t, lp, dscale, (const bf16_t*)dout, d_s_b, d_s_t, lse, delta,  \
                        (bf16_t*)dqkv, dq_s_b, dq_s_t, bias_grad);                                  \
   } while (0)
 
@@ -887,7 +950,7 @@ extern "C" int mmt_dropout_bits(const uint32_t* rng, uint32_t layer, uint32_t si
                 "mmt_dropout_bits: bad args");
   MMT_CHECK_ARG(!out_t || rows == cols, "mmt_dropout_bits: the transposed mask needs rows == cols");
   const int words = (cols + 31) / 32;
-  const int64_t n = (int64_t)rows * words * (out_t ? 2 : 1);
+  const int64_t n = out_t ? 2 * (int64_t)words * lp_of(rows) : (int64_t)rows * words;
   hipLaunchKernelGGL(dropout_bits_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream),
                      rng, layer, site, rows, cols, words, keep_threshold16(keep_prob), out, out_t);
   MMT_CHECK_LAUNCH("mmt_dropout_bits");
@@ -910,7 +973,7 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   int rc = fill_mask(m, n_sets, set_start, set_len, set_vis, L);
   if (rc) return rc;
   Geo g{(const bf16_t*)qkv, s_b, s_t, L, H, scale};
-  const int words = (L + 31) / 32;
+  const int lp = lp_of(L);
   const float dscale = drop_bits ? 1.f / keep_prob : 1.f;
   // query blocks per wave: enough for one workgroup to cover L (K/V read once per (b, h)) at
   // Dh 64; Dh 128 / 256 keep one (registers)
@@ -918,9 +981,14 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   int nq = g_attn_nq > 0 ? g_attn_nq : std::min(3, (nqb + 3) / 4);
   if (Dh > 64) nq = 1;
   dim3 grid((L + QB * nq - 1) / (QB * nq), H, B);
-#define FWD(DH_, NQ_)                                                                            \
-  hipLaunchKernelGGL((attn_fwd_kernel<DH_, NQ_>), grid, dim3(NT), 0, as_stream(stream), g, m,   \
-                     drop_bits, words, dscale, bias, (bf16_t*)o, o_s_b, o_s_t, lse, wsum)
+#define FWD1(DH_, NQ_, WS_)                                                                       \
+  hipLaunchKernelGGL((attn_fwd_kernel<DH_, NQ_, WS_>), grid, dim3(NT), 0, as_stream(stream), g, m, \
+                     drop_bits, lp, dscale, bias, (bf16_t*)o, o_s_b, o_s_t, lse, wsum)
+#define FWD(DH_, NQ_)          \
+  do {                         \
+    if (wsum) FWD1(DH_, NQ_, true); \
+    else FWD1(DH_, NQ_, false);     \
+  } while (0)
   if (Dh == 64) {
     if (nq == 3) FWD(64, 3);
     else if (nq == 2) FWD(64, 2);
@@ -929,6 +997,7 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
     ATTN_DISPATCH(DH, FWD(DH, 1));
   }
 #undef FWD
+#undef FWD1
   MMT_CHECK_LAUNCH("mmt_attn_fwd");
   return MMT_OK;
 }
@@ -952,7 +1021,7 @@ extern "C" int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   int rc = fill_mask(m, n_sets, set_start, set_len, set_vis, L);
   if (rc) return rc;
   Geo g{(const bf16_t*)qkv, s_b, s_t, L, H, scale};
-  const int words = (L + 31) / 32;
+  const int lp = lp_of(L);
   const float dscale = drop_bits ? 1.f / keep_prob : 1.f;
   hipStream_t s = as_stream(stream);
   if (bwd_threads(L) == 128) {

@@ -34,10 +34,24 @@ def octo_small_table(n_text=32, n_img=256, n_read=4):
     return [0, n_text, n_text + n_img], [n_text, n_img, n_read], [0b001, 0b011, 0b111]
 
 
-def bits_to_keep(bits, L):
-    b = bits.cpu().numpy().view(np.uint32)
-    keep = ((b[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(b.shape[0], -1)[:, :L]
-    return torch.from_numpy(keep.astype(bool))
+def _pos_to_index(LP):
+    p = np.arange(LP)
+    return (p & ~7) | ((p & 1) << 2) | ((p >> 1) & 3)
+
+
+def bits_to_keep(bits, L, which=0):
+    """(L, L) bool keep mask from one image of K.dropout_bits' square layout (2, W, LP):
+    which 0 = query-word image (bit j of (w, pos(k)) = keep(32w + j, k)), 1 = key-word image
+    (bit j of (w, pos(q)) = keep(q, 32w + j))."""
+    b = bits[which].cpu().numpy().view(np.uint32)                  # (W, LP)
+    W, LP = b.shape
+    ex = ((b[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).astype(bool)   # (W, LP, 32)
+    idx = _pos_to_index(LP)
+    m = np.zeros((W * 32, LP), dtype=bool)                         # [word-row y][element x]
+    m[:, idx] = ex.transpose(0, 2, 1).reshape(W * 32, LP)
+    m = m[:L, :L]
+    keep = m if which == 0 else m.T                                 # keep[q, k]
+    return torch.from_numpy(np.ascontiguousarray(keep))
 
 
 def ref_attention(qkv, H, scale, mask, keep, keep_prob, bias=None):
@@ -78,11 +92,11 @@ def test_attention_fwd_bwd(dev, B, L, H, Dh, masked, drop):
     keep_prob = 0.9 if drop else 1.0
     rng = torch.tensor([77, 5], dtype=torch.int32, device=dev)
     bits = K.dropout_bits(rng, 3, 7, L, L, keep_prob) if drop else None
-    keep = bits_to_keep(bits[0], L).to(dev) if drop else None
+    keep = bits_to_keep(bits, L).to(dev) if drop else None
     if drop:  # the bitmask is the oracle's stream; [1] is its transpose
         ref_keep = R.dropout_mask_2d(77, 5, 3, 7, L, L, 0, 0.9)
         assert (keep.cpu().numpy() == ref_keep).all()
-        assert (bits_to_keep(bits[1], L).numpy() == ref_keep.T).all()
+        assert (bits_to_keep(bits, L, which=1).numpy() == ref_keep).all()
     o, lse = K.attn_fwd(qkv, H, scale, table, bits, keep_prob)
     qf = qkv.float().requires_grad_()
     ref = ref_attention(qf, H, scale, mask, keep, keep_prob)
@@ -131,7 +145,7 @@ def test_attention_importance(dev, B, L, H, Dh, drop, causal):
     keep_prob = 0.9 if drop else 1.0
     rng = torch.tensor([11, 3], dtype=torch.int32, device=dev)
     bits = K.dropout_bits(rng, 2, 0, L, L, keep_prob) if drop else None
-    keep = bits_to_keep(bits[0], L).to(dev) if drop else None
+    keep = bits_to_keep(bits, L).to(dev) if drop else None
     o0, lse0 = K.attn_fwd(qkv, H, scale, table, bits, keep_prob)
     wsum = torch.full((B, H, L), float("nan"), device=dev)
     o, lse = K.attn_fwd(qkv, H, scale, table, bits, keep_prob, wsum=wsum)
@@ -177,7 +191,7 @@ def test_attention_causal_text_sets(dev, B, L, H, Dh, drop):
     keep_prob = 0.9 if drop else 1.0
     rng = torch.tensor([5, 2], dtype=torch.int32, device=dev)
     bits = K.dropout_bits(rng, 1, 0, L, L, keep_prob) if drop else None
-    keep = bits_to_keep(bits[0], L).to(dev) if drop else None
+    keep = bits_to_keep(bits, L).to(dev) if drop else None
     o, lse = K.attn_fwd(qkv, H, scale, table, bits, keep_prob)
     qf = qkv.float().requires_grad_()
     ref = ref_attention(qf, H, scale, mask, keep, keep_prob)
