@@ -271,6 +271,21 @@ int mmt_maxpool_patch(const void* conv, int64_t npatch, int win, int C, void* po
                       uint8_t* argmax, mmt_stream_t stream);
 int mmt_maxpool_patch_bwd(const void* dpooled, const uint8_t* argmax, int64_t npatch, int win,
                           int C, void* G, mmt_stream_t stream);
+/* General stem maps (pooled map larger than 1 x 1: the reference's patch 56, 23 x 23 conv map,
+ * image_tokenizer.py:156-176 with gato_resnet.yaml:45-92):
+ * max_pool KP x KP stride 1 VALID over (npatch, OH, OW, C) fp32 -> (npatch, OH-KP+1, OW-KP+1, C)
+ * plus the first-maximum window slot; its backward writes the bf16 (npatch, OH, OW, C) operand of
+ * the conv weight gradient (gather over the windows, deterministic). */
+int mmt_maxpool2d(const void* x, int64_t npatch, int OH, int OW, int C, int KP, void* y,
+                  uint8_t* argmax, mmt_stream_t stream);
+int mmt_maxpool2d_bwd(const void* dy, const uint8_t* argmax, int64_t npatch, int OH, int OW, int C,
+                      int KP, void* G, mmt_stream_t stream);
+/* KS x KS stride-1 SAME convolution as im2col (bf16 (npatch, H, W, C) -> (npatch*H*W, KS*KS*C) in
+ * Flax HWIO (ky, kx, c) order, zero padding) + GEMM; col2im sums the fp32 column gradient back. */
+int mmt_im2col_same(const void* x, int64_t npatch, int H, int W, int C, int KS, void* cols,
+                    mmt_stream_t stream);
+int mmt_col2im_same(const float* dcols, int64_t npatch, int H, int W, int C, int KS, float* dx,
+                    mmt_stream_t stream);
 /* flax GroupNorm(num_groups=G, eps) over every non-batch axis + gelu(tanh approx)
  * (gato_resnet.yaml:77-86, image_tokenizer.py:165-167): x (B, R, C) fp32 -> y bf16 (the next
  * conv's GEMM operand); statistics in fp32. */

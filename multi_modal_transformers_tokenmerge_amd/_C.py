@@ -41,6 +41,10 @@ SIGNATURES: dict[str, list] = {
     "mmt_attn_fwd": [P, L, L, I, I, I, I, F, I, P, P, P, P, F, P, P, L, L, P, P, P],
     "mmt_prune_importance": [P, I, I, I, P, P],
     "mmt_gather_rows": [P, I, I, I, I, L, L, P, I, P, L, L, P],
+    "mmt_maxpool2d": [P, L, I, I, I, I, P, P, P],
+    "mmt_maxpool2d_bwd": [P, P, L, I, I, I, I, P, P],
+    "mmt_im2col_same": [P, L, I, I, I, I, P, P],
+    "mmt_col2im_same": [P, L, I, I, I, I, P, P],
     "mmt_attn_bwd": [P, L, L, I, I, I, I, F, I, P, P, P, P, P, F, P, L, L, P, L, L, P, P, P, L, L, P, P],
     "mmt_dropout_bits": [P, U32, U32, I, I, F, P, P, P],
     "mmt_seqnorm_fwd": [P, I, L, L, I, I, I, P, P, F, P, L, L, P, P, P],

@@ -481,6 +481,47 @@ def maxpool_patch_bwd(dpooled: torch.Tensor, arg: torch.Tensor, win: int, out=No
     return out
 
 
+def maxpool2d(x: torch.Tensor, npatch: int, OH: int, OW: int, KP: int):
+    """x fp32 (npatch*OH*OW, C) -> pooled fp32 (npatch*PH*PW, C) (KP x KP, stride 1, VALID) and
+    the window slot of the first maximum (uint8)."""
+    _f32(x, "conv output")
+    C = x.shape[-1]
+    if x.numel() != npatch * OH * OW * C:
+        raise ValueError("maxpool2d: x is not (npatch*OH*OW, C)")
+    rows = npatch * (OH - KP + 1) * (OW - KP + 1)
+    y = torch.empty((rows, C), dtype=torch.float32, device=x.device)
+    arg = torch.empty((rows, C), dtype=torch.uint8, device=x.device)
+    _C.call("mmt_maxpool2d", ptr(x), npatch, OH, OW, C, KP, ptr(y), ptr(arg), _C.stream_ptr())
+    return y, arg
+
+
+def maxpool2d_bwd(dy: torch.Tensor, arg: torch.Tensor, npatch: int, OH: int, OW: int, KP: int):
+    """-> bf16 (npatch*OH*OW, C): the gradient routed to each window's first maximum."""
+    _f32(dy, "dpooled")
+    C = dy.shape[-1]
+    G = torch.empty((npatch * OH * OW, C), dtype=torch.bfloat16, device=dy.device)
+    _C.call("mmt_maxpool2d_bwd", ptr(dy), ptr(arg), npatch, OH, OW, C, KP, ptr(G), _C.stream_ptr())
+    return G
+
+
+def im2col_same(x: torch.Tensor, npatch: int, H: int, W: int, KS: int):
+    """x bf16 (npatch*H*W, C) -> (npatch*H*W, KS*KS*C) bf16 columns of a SAME KS x KS conv."""
+    _dev(x)
+    C = x.shape[-1]
+    if x.dtype != torch.bfloat16 or x.numel() != npatch * H * W * C or not x.is_contiguous():
+        raise ValueError("im2col_same: x must be contiguous bf16 (npatch*H*W, C)")
+    cols = torch.empty((npatch * H * W, KS * KS * C), dtype=torch.bfloat16, device=x.device)
+    _C.call("mmt_im2col_same", ptr(x), npatch, H, W, C, KS, ptr(cols), _C.stream_ptr())
+    return cols
+
+
+def col2im_same(dcols: torch.Tensor, npatch: int, H: int, W: int, C: int, KS: int):
+    _f32(dcols, "column gradient")
+    dx = torch.empty((npatch * H * W, C), dtype=torch.float32, device=dcols.device)
+    _C.call("mmt_col2im_same", ptr(dcols), npatch, H, W, C, KS, ptr(dx), _C.stream_ptr())
+    return dx
+
+
 def groupnorm_gelu_fwd(x: torch.Tensor, groups: int, gamma, beta, eps: float, out=None):
     """x (B, R, C) fp32 contiguous -> gelu(GroupNorm(x)) bf16."""
     _f32(x, "groupnorm input")

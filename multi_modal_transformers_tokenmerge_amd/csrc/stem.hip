@@ -183,6 +183,99 @@ __global__ void maxpool_patch_bwd_kernel(const float* __restrict__ dpooled,
   *reinterpret_cast<uint4*>(G + (p * win + s) * C + c) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// ---- general stem maps (patch sizes whose pooled map is larger than 1 x 1, e.g. the reference's
+// own patch 56: 23 x 23 conv map -> 21 x 21 pooled map, gato_resnet.yaml:45-92)
+// max_pool KP x KP, stride 1, VALID over (npatch, OH, OW, C) fp32 -> (npatch, PH, PW, C), with the
+// window slot of the first maximum (lax.reduce_window max routes the gradient to one input).
+__global__ void maxpool2d_kernel(const float* __restrict__ x, int64_t npatch, int OH, int OW, int C,
+                                 int KP, float* __restrict__ y, uint8_t* __restrict__ arg) {
+  const int PH = OH - KP + 1, PW = OW - KP + 1;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= npatch * PH * PW * C) return;
+  const int c = idx % C;
+  const int64_t o = idx / C;
+  const int px = o % PW, py = (o / PW) % PH;
+  const int64_t p = o / ((int64_t)PW * PH);
+  const float* src = x + ((p * OH + py) * OW + px) * C + c;
+  float best = src[0];
+  int bi = 0;
+  for (int dy = 0; dy < KP; ++dy)
+    for (int dx = 0; dx < KP; ++dx) {
+      const float v = src[((int64_t)dy * OW + dx) * C];
+      if (v > best) {
+        best = v;
+        bi = dy * KP + dx;
+      }
+    }
+  y[idx] = best;
+  arg[idx] = (uint8_t)bi;
+}
+
+// G[p, y, x, c] = sum of dpooled[p, py, px, c] over the windows (py, px) whose first maximum is
+// (y, x) (gather form, windows in raster order: deterministic), bf16 — the operand of dW_conv.
+__global__ void maxpool2d_bwd_kernel(const float* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                     int64_t npatch, int OH, int OW, int C, int KP,
+                                     bf16_t* __restrict__ G) {
+  const int PH = OH - KP + 1, PW = OW - KP + 1;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= npatch * OH * OW * C) return;
+  const int c = idx % C;
+  const int64_t o = idx / C;
+  const int x = o % OW, yy = (o / OW) % OH;
+  const int64_t p = o / ((int64_t)OW * OH);
+  float acc = 0.f;
+  for (int py = max(0, yy - KP + 1); py <= min(yy, PH - 1); ++py)
+    for (int px = max(0, x - KP + 1); px <= min(x, PW - 1); ++px) {
+      const int64_t q = ((p * PH + py) * PW + px) * C + c;
+      if (arg[q] == (uint8_t)((yy - py) * KP + (x - px))) acc += dy[q];
+    }
+  G[idx] = f2bf(acc);
+}
+
+// im2col of a KS x KS stride-1 SAME convolution (zero padding KS/2) over (npatch, H, W, C) bf16:
+// cols[(p, y, x)][(ky, kx, c)] = X[p, y + ky - KS/2, x + kx - KS/2, c] (Flax HWIO order), one
+// thread per 8-channel chunk (C % 8 == 0).
+__global__ void im2col_same_kernel(const bf16_t* __restrict__ X, int64_t npatch, int H, int W, int C,
+                                   int KS, bf16_t* __restrict__ cols) {
+  const int c8 = C / 8, K = KS * KS * C;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= npatch * H * W * KS * KS * c8) return;
+  const int ch = idx % c8;
+  const int tap = (idx / c8) % (KS * KS);
+  const int64_t row = idx / ((int64_t)c8 * KS * KS);
+  const int x = row % W, y = (row / W) % H;
+  const int64_t p = row / ((int64_t)W * H);
+  const int yy = y + tap / KS - KS / 2, xx = x + tap % KS - KS / 2;
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+    v = *reinterpret_cast<const uint4*>(X + ((p * H + yy) * W + xx) * C + ch * 8);
+  *reinterpret_cast<uint4*>(cols + row * K + tap * C + ch * 8) = v;
+}
+
+// col2im (gather): dX[p, y, x, c] = sum over taps of dcols[(p, y - ky + KS/2, x - kx + KS/2)]
+// [(ky, kx, c)] in tap order, fp32.
+__global__ void col2im_same_kernel(const float* __restrict__ dcols, int64_t npatch, int H, int W, int C,
+                                   int KS, float* __restrict__ dX) {
+  const int K = KS * KS * C;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= npatch * H * W * C) return;
+  const int c = idx % C;
+  const int64_t o = idx / C;
+  const int x = o % W, y = (o / W) % H;
+  const int64_t p = o / ((int64_t)W * H);
+  float acc = 0.f;
+  for (int ky = 0; ky < KS; ++ky) {
+    const int sy = y - ky + KS / 2;
+    if (sy < 0 || sy >= H) continue;
+    for (int kx = 0; kx < KS; ++kx) {
+      const int sx = x - kx + KS / 2;
+      if (sx < 0 || sx >= W) continue;
+      acc += dcols[((p * H + sy) * W + sx) * K + (ky * KS + kx) * C + c];
+    }
+  }
+  dX[idx] = acc;
+}
+
 __device__ __forceinline__ float gelu_tanh(float z) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   return 0.5f * z * (1.f + tanhf(k0 * (z + k1 * z * z * z)));
@@ -663,5 +756,49 @@ extern "C" int mmt_patch_positions(const uint32_t* rng, uint32_t site, int B, in
                      as_stream(stream), rng, site, B, I, Himg, P, Q, train, sample_offset, row_tok,
                      col_tok);
   MMT_CHECK_LAUNCH("mmt_patch_positions");
+  return MMT_OK;
+}
+
+extern "C" int mmt_maxpool2d(const void* x, int64_t npatch, int OH, int OW, int C, int KP, void* y,
+                             uint8_t* argmax, mmt_stream_t stream) {
+  MMT_CHECK_ARG(x && y && argmax && npatch > 0 && C > 0 && KP > 0 && KP * KP <= 255 && OH >= KP &&
+                    OW >= KP, "mmt_maxpool2d: args");
+  const int64_t n = npatch * (OH - KP + 1) * (OW - KP + 1) * C;
+  hipLaunchKernelGGL(maxpool2d_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream),
+                     (const float*)x, npatch, OH, OW, C, KP, (float*)y, argmax);
+  MMT_CHECK_LAUNCH("mmt_maxpool2d");
+  return MMT_OK;
+}
+
+extern "C" int mmt_maxpool2d_bwd(const void* dy, const uint8_t* argmax, int64_t npatch, int OH,
+                                 int OW, int C, int KP, void* G, mmt_stream_t stream) {
+  MMT_CHECK_ARG(dy && argmax && G && npatch > 0 && C > 0 && KP > 0 && OH >= KP && OW >= KP,
+                "mmt_maxpool2d_bwd: args");
+  const int64_t n = npatch * OH * OW * C;
+  hipLaunchKernelGGL(maxpool2d_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream),
+                     (const float*)dy, argmax, npatch, OH, OW, C, KP, (bf16_t*)G);
+  MMT_CHECK_LAUNCH("mmt_maxpool2d_bwd");
+  return MMT_OK;
+}
+
+extern "C" int mmt_im2col_same(const void* x, int64_t npatch, int H, int W, int C, int KS,
+                               void* cols, mmt_stream_t stream) {
+  MMT_CHECK_ARG(x && cols && npatch > 0 && H > 0 && W > 0 && C > 0 && C % 8 == 0 && KS > 0 &&
+                    KS % 2 == 1, "mmt_im2col_same: args (C %% 8 == 0, odd KS)");
+  const int64_t n = npatch * H * W * KS * KS * (C / 8);
+  hipLaunchKernelGGL(im2col_same_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream),
+                     (const bf16_t*)x, npatch, H, W, C, KS, (bf16_t*)cols);
+  MMT_CHECK_LAUNCH("mmt_im2col_same");
+  return MMT_OK;
+}
+
+extern "C" int mmt_col2im_same(const float* dcols, int64_t npatch, int H, int W, int C, int KS,
+                               float* dx, mmt_stream_t stream) {
+  MMT_CHECK_ARG(dcols && dx && npatch > 0 && H > 0 && W > 0 && C > 0 && KS > 0 && KS % 2 == 1,
+                "mmt_col2im_same: args");
+  const int64_t n = npatch * H * W * C;
+  hipLaunchKernelGGL(col2im_same_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream),
+                     dcols, npatch, H, W, C, KS, dx);
+  MMT_CHECK_LAUNCH("mmt_col2im_same");
   return MMT_OK;
 }

@@ -8,8 +8,12 @@ patchify/normalise/im2col, conv-as-GEMM, per-patch max-pool, GroupNorm+gelu (x2)
 convolutions reduced to their centre tap (the pooled map is 1x1 at patch 16), residual add fused
 into a GEMM epilogue, and the output Dense. Position tokens are drawn on the device.
 
-Supported geometry: stem output map 1x1 (patch 16 with the 12x12/s2 conv and 3x3 pool, every
-OCTO config of SURVEY §8.0 except ref-octo_base's patch 56, which raises NotImplementedError).
+Geometry: the pooled map is 1x1 at patch 16 (every BASELINE config; the centre-tap form above).
+Larger maps — the reference's own patch 56 (23x23 conv map, 21x21 pooled) — take the general
+form: max_pool 3x3 s1 over the map, the 3x3 SAME convs as im2col + GEMM (+ col2im backward),
+GroupNorm over all patches x positions of a sample, flatten (h, w, c) and the output Dense over
+PH*PW*C features (image_tokenizer.py:156-176). Its Conv_{1,2} kernels are the full (3, 3, C, C)
+(stored (9C, C)); the 1x1 form stores only the centre tap (C, C).
 """
 from __future__ import annotations
 
@@ -58,10 +62,12 @@ class ResNetV2Block:
         self.kh, self.kw, self.stride = kh, kw, conv_stride
         self.oh = (patch_size - kh) // conv_stride + 1
         self.ow = (patch_size - kw) // conv_stride + 1
-        if (self.oh - pool[0] + 1, self.ow - pool[1] + 1) != (1, 1):
-            raise NotImplementedError(
-                f"stem output map {(self.oh - pool[0] + 1, self.ow - pool[1] + 1)} != 1x1 "
-                f"(patch {patch_size}); only the 1x1 stem of patch 16 is built (SURVEY §8.0)")
+        if pool[0] != pool[1] or self.oh < pool[0] or self.ow < pool[1]:
+            raise ValueError(f"pool {pool} on a {self.oh}x{self.ow} conv map")
+        self.kp = pool[0]
+        self.ph, self.pw = self.oh - pool[0] + 1, self.ow - pool[1] + 1
+        self.general = (self.ph, self.pw) != (1, 1)   # else the 1x1 centre-tap form
+        self.ks = 3                                   # resnet_conv 3x3 SAME (gato_resnet.yaml:88-92)
         self.win = self.oh * self.ow
         self.C, self.G, self.eps = features, num_groups, gn_eps
         self.num_blocks = num_blocks
@@ -73,14 +79,19 @@ class ResNetV2Block:
         for i in range(num_blocks):
             self.gn.append((store.add(f"{name}/GroupNorm_{i}/scale", (features,), const(1.0)),
                             store.add(f"{name}/GroupNorm_{i}/bias", (features,), const(0.0))))
-            # 3x3 SAME conv on a 1x1 map: only the centre tap acts (fan_in of the full kernel)
-            self.convs.append(Dense(store, f"{name}/Conv_{i + 1}", features, features,
+            # 3x3 SAME conv: the full (9C, C) kernel on a larger map; on a 1x1 map only the centre
+            # tap acts (fan_in of the full kernel either way)
+            cin = 9 * features if self.general else features
+            self.convs.append(Dense(store, f"{name}/Conv_{i + 1}", cin, features,
                                     kernel_init=he_normal((9 * features, features))))
-        self.out = Dense(store, f"{name}/Dense_0", features, embedding_dim,
-                         kernel_init=he_normal((features, embedding_dim)))
+        flat = self.ph * self.pw * features                 # flatten (h, w, c) (:174-175)
+        self.out = Dense(store, f"{name}/Dense_0", flat, embedding_dim,
+                         kernel_init=he_normal((flat, embedding_dim)))
 
     def forward(self, A: torch.Tensor, B: int, R: int):
         """A: im2col rows (B*R*win, K_in). Returns tokens (B*R, D) bf16 and the saved state."""
+        if self.general:
+            return self._forward_general(A, B, R)
         # pre-normalisation tensors are fp32 (GroupNorm spans all patches of a sample: same
         # conditioning argument as the sequence LayerNorm, csrc/norm.hip)
         conv = self.conv.fwd(A, out_mode=K.OUT_F32)               # (B*R*win, C)
@@ -101,6 +112,8 @@ class ResNetV2Block:
         return tok, dict(A=A, arg=arg, pooled=pooled, hs=hs, zs=zs, stats=stats, r=r16, B=B, R=R)
 
     def backward(self, dtok: torch.Tensor, sv: dict):
+        if self.general:
+            return self._backward_general(dtok, sv)
         B, R = sv["B"], sv["R"]
         dz = self.out.bwd(dtok, sv["r"], out_mode=K.OUT_F32)     # d(residual sum) (B*R, C) fp32
         dpooled = dz.clone()                                     # residual branch
@@ -118,6 +131,53 @@ class ResNetV2Block:
                                           rs, g.grad, b.grad).view(B * R, self.C)
         G = K.maxpool_patch_bwd(dpooled, sv["arg"], self.win)    # (B*R*win, C)
         K.colsum(dpooled, self.conv.b.grad)                      # bias added before the max
+        self.conv.bwd(G, sv["A"], need_dx=False, bias_grad_done=True)
+
+
+    # ---------------------------------------------------------------- general maps (patch 56)
+    def _forward_general(self, A: torch.Tensor, B: int, R: int):
+        n, C, PH, PW, ks = B * R, self.C, self.ph, self.pw, self.ks
+        conv = self.conv.fwd(A, out_mode=K.OUT_F32)               # (n*OH*OW, C)
+        pooled, arg = K.maxpool2d(conv, n, self.oh, self.ow, self.kp)   # (n*PH*PW, C) fp32
+        hs, cols, zs, stats = [], [], [], []
+        z = pooled
+        for i in range(self.num_blocks):
+            g, b = self.gn[i]
+            # GroupNorm over every non-batch axis: the R patches x PH x PW positions of a sample
+            h, mu, rs = K.groupnorm_gelu_fwd(z.view(B, R * PH * PW, C), self.G, g.data, b.data, self.eps)
+            col = K.im2col_same(h.view(n * PH * PW, C), n, PH, PW, ks)
+            residual = pooled if i == self.num_blocks - 1 else None
+            zn = self.convs[i].fwd(col, residual=residual, out_mode=K.OUT_F32)
+            cols.append(col)
+            zs.append(z)
+            stats.append((mu, rs))
+            z = zn
+        r16 = K.cast_f32_bf16(z, torch.empty(z.shape, dtype=torch.bfloat16, device=z.device))
+        tok = self.out.fwd(r16.view(n, PH * PW * C))               # flatten (h, w, c)
+        return tok, dict(A=A, arg=arg, cols=cols, zs=zs, stats=stats, r=r16, B=B, R=R)
+
+    def _backward_general(self, dtok: torch.Tensor, sv: dict):
+        B, R = sv["B"], sv["R"]
+        n, C, PH, PW, ks = B * R, self.C, self.ph, self.pw, self.ks
+        dz = self.out.bwd(dtok, sv["r"].view(n, PH * PW * C), out_mode=K.OUT_F32)
+        dz = dz.view(n * PH * PW, C)
+        dpooled = dz.clone()                                       # residual branch
+        for i in reversed(range(self.num_blocks)):
+            g, b = self.gn[i]
+            dz16 = K.cast_f32_bf16(dz, torch.empty(dz.shape, dtype=torch.bfloat16, device=dz.device))
+            dcol = self.convs[i].bwd(dz16, sv["cols"][i], out_mode=K.OUT_F32)   # (rows, 9C)
+            dh = K.col2im_same(dcol, n, PH, PW, C, ks)
+            mu, rs = sv["stats"][i]
+            zin = sv["zs"][i].view(B, R * PH * PW, C)
+            if i == 0:
+                K.groupnorm_gelu_bwd(dh.view(B, R * PH * PW, C), zin, self.G, g.data, b.data, mu, rs,
+                                     g.grad, b.grad, dx=dpooled.view(B, R * PH * PW, C),
+                                     accumulate=True)
+            else:
+                dz = K.groupnorm_gelu_bwd(dh.view(B, R * PH * PW, C), zin, self.G, g.data, b.data,
+                                          mu, rs, g.grad, b.grad).view(n * PH * PW, C)
+        G = K.maxpool2d_bwd(dpooled, sv["arg"], n, self.oh, self.ow, self.kp)
+        K.colsum(dpooled, self.conv.b.grad)                        # bias added before the max
         self.conv.bwd(G, sv["A"], need_dx=False, bias_grad_done=True)
 
 

@@ -359,14 +359,21 @@ class OctoRef:
         name = "ImageTokenizer_0/ResNetV2Block_0"
         wc = p[f"{name}/Conv_0/kernel"].view(64, 12, 12, 3).permute(0, 3, 1, 2)
         x = gb(F.conv2d(x, wc, None, stride=2)) + p[f"{name}/Conv_0/bias"].view(1, -1, 1, 1)
-        x = F.max_pool2d(x, 3, stride=1)                                       # (N, 64, 1, 1)
-        x = x.reshape(B, I * NP, 64)
+        x = F.max_pool2d(x, 3, stride=1)                                       # (N, 64, PH, PW)
+        PH, PW = x.shape[2], x.shape[3]
+        x = x.permute(0, 2, 3, 1).reshape(B, I * NP * PH * PW, 64)            # NHWC rows
         residual = x
         for k in range(2):
             x = groupnorm(x, 32, p[f"{name}/GroupNorm_{k}/scale"], p[f"{name}/GroupNorm_{k}/bias"], 1e-6)
             x = rb(gelu_tanh(x))
-            x = gb(dense(p, f"{name}/Conv_{k + 1}", x))   # 3x3 SAME conv on a 1x1 map = centre tap
-        x = x + residual
+            if PH * PW == 1:   # 3x3 SAME conv on a 1x1 map = centre tap
+                x = gb(dense(p, f"{name}/Conv_{k + 1}", x))
+            else:              # full 3x3 SAME conv (image_tokenizer.py:164-167)
+                w3 = p[f"{name}/Conv_{k + 1}/kernel"].view(64, 3, 3, 64).permute(0, 3, 1, 2)
+                xn = x.reshape(B * I * NP, PH, PW, 64).permute(0, 3, 1, 2)
+                y = F.conv2d(xn, w3, p[f"{name}/Conv_{k + 1}/bias"], padding=1)
+                x = gb(y.permute(0, 2, 3, 1).reshape(B, I * NP * PH * PW, 64))
+        x = (x + residual).reshape(B, I * NP, PH * PW * 64)                    # flatten (h, w, c)
         img = self.rbg(dense(p, f"{name}/Dense_0", rb(x)))                      # (B, I*NP, D)
         if trace is not None:
             trace["img"] = img.detach().clone()

@@ -109,6 +109,19 @@ def test_blockwise_base_hires_tome32(dev):
         P.check_blockwise(out, **(P.FP8_BAR if fp8 else {}))
 
 
+def test_blockwise_ref_octo_base(dev):
+    """The reference's own octo_base.yaml geometry (model_configs/ref_octo_base.yaml: 280x280
+    images with patch 56 -> the general stem: 23x23 conv map, 3x3 max-pool to 21x21, two full
+    3x3 SAME convs, flatten 21*21*64 -> Dense 768; D 768 as 3 heads of 256; 1 block; 2-step
+    history), T5 reduced to 2 layers (checked on its own above), B = 2, block-local bar."""
+    cfg = _cfg("ref_octo_base", t5_layers=2)
+    assert cfg.patch_size == 56 and cfg.token_embedding_dim // cfg.num_heads == 256
+    res = P.hip_blockwise(cfg, 2, seed=0)
+    assert res["model"].image_tokenizer.resnet.general
+    out = P.oracle_blockwise(cfg, res)
+    P.check_blockwise(out, cfg=cfg, res=res)
+
+
 def test_blockwise_causal_text(dev):
     """A sequence with causal Text sets (token_sequencer.py:55-91: causal within the set, sees
     earlier non-readout sets) over two observation steps, block-local bar."""

@@ -93,3 +93,41 @@ def test_fourier_bwd(dev, B, F):
     d = dfeats.double().numpy()
     want = 0.25 + (tt * (np.cos(h) * d[:, F:] - np.sin(h) * d[:, :F])).sum(0)
     np.testing.assert_allclose(dwd.cpu().double().numpy(), want, rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("npatch,OH,C", [(3, 23, 64), (4, 5, 16)])
+def test_maxpool2d_general(dev, npatch, OH, C):
+    """max_pool 3x3 s1 VALID on a larger map (the reference's patch 56: 23x23 -> 21x21) vs torch
+    max_pool2d; backward (first-maximum routing, gather over overlapping windows) vs autograd on
+    tie-free data, bf16-rounded like the kernel's output."""
+    g = torch.Generator().manual_seed(OH)
+    x = torch.randn((npatch, OH, OH, C), generator=g)
+    y, arg = K.maxpool2d(x.reshape(-1, C).contiguous().to(dev), npatch, OH, OH, 3)
+    xt = x.permute(0, 3, 1, 2).clone().requires_grad_()
+    ref = torch.nn.functional.max_pool2d(xt, 3, stride=1)
+    PH = OH - 2
+    torch.testing.assert_close(y.cpu().view(npatch, PH, PH, C), ref.detach().permute(0, 2, 3, 1),
+                               rtol=0, atol=0)
+    dy = torch.randn((npatch, PH, PH, C), generator=g)
+    ref.backward(dy.permute(0, 3, 1, 2))
+    G = K.maxpool2d_bwd(dy.reshape(-1, C).contiguous().to(dev), arg, npatch, OH, OH, 3)
+    want = xt.grad.permute(0, 2, 3, 1).reshape(-1, C)
+    torch.testing.assert_close(G.float().cpu(), want.bfloat16().float(), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("npatch,H,C", [(2, 21, 64), (3, 4, 16)])
+def test_same_conv_im2col_col2im(dev, npatch, H, C):
+    """3x3 SAME conv as im2col + GEMM vs torch conv2d(padding=1), and col2im as the adjoint of
+    im2col (<im2col(x), c> == <x, col2im(c)>) in fp32."""
+    g = torch.Generator().manual_seed(H)
+    x = torch.randn((npatch, H, H, C), generator=g).bfloat16()
+    w = torch.randn((C, 3, 3, C), generator=g) * 0.05          # (out, ky, kx, in)
+    cols = K.im2col_same(x.reshape(-1, C).contiguous().to(dev), npatch, H, H, 3)
+    y = cols.float() @ w.reshape(C, 9 * C).t().to(dev)
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), padding=1)
+    torch.testing.assert_close(y.cpu().view(npatch, H, H, C), ref.permute(0, 2, 3, 1), rtol=1e-4, atol=1e-4)
+    c = torch.randn((npatch * H * H, 9 * C), generator=g)
+    dx = K.col2im_same(c.to(dev), npatch, H, H, C, 3)
+    lhs = float((cols.float().cpu().double() * c.double()).sum())
+    rhs = float((x.float().reshape(-1, C).double() * dx.cpu().double()).sum())
+    assert abs(lhs - rhs) <= 1e-6 * max(1.0, abs(lhs)), (lhs, rhs)
