@@ -25,6 +25,8 @@
 // LDS and prefetched through registers one tile ahead: one barrier per tile.
 #include <math.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 using namespace mmt;
@@ -296,7 +298,7 @@ struct Geo {
 // one-block-per-workgroup form read them once per 128 rows, 2.3x the algorithmic bytes at
 // L = 292) and each LDS tile feeds NQ x 16 MFMAs per wave instead of 16, which amortises the
 // per-tile barrier and the per-workgroup prologue.
-template <int DH, int NQ, bool WS>
+template <int DH, int NQ, bool WS, bool DROP>
 __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
     Geo g, AttnMask mask, const uint32_t* __restrict__ drop_q, int drop_lp, float drop_scale,
     const float* __restrict__ bias, bf16_t* __restrict__ o, int64_t o_s_b, int64_t o_s_t,
@@ -421,14 +423,14 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         TileMasks<16> dm;  // dropout lane masks of (query word, key sub-tile): scalar loads
-        if (drop_q) dm.load(drop_q, drop_lp, (q0 >> 5) + wave + 4 * i, kt + 32 * u);
+        if constexpr (DROP) dm.load(drop_q, drop_lp, (q0 >> 5) + wave + 4 * i, kt + 32 * u);
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
           float2v a = {sacc[u][r], sacc[u][r + 1]};
           a = __builtin_elementwise_fma(a, cc, mm);
           float2v pp = {fast_exp2(a.x), fast_exp2(a.y)};
           rs2 += pp;
-          if (drop_q) {
+          if constexpr (DROP) {
             pp.x = sel_keep(pp.x, dm.m[r]);
             pp.y = sel_keep(pp.y, dm.m[r + 1]);
           }
@@ -493,7 +495,7 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
 }
 
 // =============================================================================== bwd: dQ
-template <int DH, int NTT>
+template <int DH, int NTT, bool DROP>
 __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dq_kernel(Geo g, AttnMask mask,
                                                          const uint32_t* __restrict__ drop_q,
                                                          int drop_lp, float drop_scale,
@@ -512,11 +514,15 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dq_kernel(Geo 
   constexpr int TILE = KT * STR;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE];  // [buf][K | V]
   __shared__ float s_wsum[NTT / 64 * DH];
-  const int b = blockIdx.z, h = blockIdx.y;
+  // 1-D grid of (sample, head, query block) items, XCD-contiguous: the query blocks of one
+  // (sample, head) share an XCD, so its K/V tiles are fetched into one L2 once
+  const int nqb = (g.L + NTT / 2 - 1) / (NTT / 2);
+  const int item = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = item / nqb, b = bh / g.H, h = bh - b * g.H;
   const int lane = threadIdx.x & 63, hh = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int L = g.L, D = g.H * DH;
-  const int q0 = blockIdx.x * (NTT / 2), q1 = min(L, q0 + NTT / 2);
+  const int q0 = (item - bh * nqb) * (NTT / 2), q1 = min(L, q0 + NTT / 2);
   const int q = q0 + wave * 32 + (lane & 31);
   const bool qv = q < L;
   const bool wave_live = q0 + wave * 32 < L;
@@ -578,7 +584,7 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dq_kernel(Geo 
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         TileMasks<16> dm;  // dropout lane masks of (query word, key sub-tile): scalar loads
-        if (drop_q) dm.load(drop_q, drop_lp, (q0 >> 5) + wave, kt + 32 * u);
+        if constexpr (DROP) dm.load(drop_q, drop_lp, (q0 >> 5) + wave, kt + 32 * u);
         floatx16 sacc, pacc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -595,25 +601,32 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dq_kernel(Geo 
         const uint32_t wv = (uint32_t)(vm >> (32 * u)) >> (4 * hh);
         const float2v sl = {sl2, sl2}, ml = {-lse2, -lse2}, dd = {drop_scale, drop_scale},
                       dl = {dlt, dlt};
+        // one wave-uniform branch between the fully visible form and the masked one (a per-pair
+        // branch would be emitted around every inline-asm select otherwise)
+        auto scores = [&](auto full_t) {
+          constexpr bool FULL = decltype(full_t)::value;
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          float2v a = {sacc[r], sacc[r + 1]};
-          a = __builtin_elementwise_fma(a, sl, ml);
-          float2v pp = {fast_exp2(a.x), fast_exp2(a.y)};
-          if (!full) {
-            pp.x = __int_as_float(__float_as_int(pp.x) & bitmask_of(wv, rbit(r)));
-            pp.y = __int_as_float(__float_as_int(pp.y) & bitmask_of(wv, rbit(r + 1)));
+          for (int r = 0; r < 16; r += 2) {
+            float2v a = {sacc[r], sacc[r + 1]};
+            a = __builtin_elementwise_fma(a, sl, ml);
+            float2v pp = {fast_exp2(a.x), fast_exp2(a.y)};
+            if constexpr (!FULL) {
+              pp.x = __int_as_float(__float_as_int(pp.x) & bitmask_of(wv, rbit(r)));
+              pp.y = __int_as_float(__float_as_int(pp.y) & bitmask_of(wv, rbit(r + 1)));
+            }
+            float2v t = {pacc[r], pacc[r + 1]};
+            t *= dd;
+            if constexpr (DROP) {
+              t.x = sel_keep(t.x, dm.m[r]);
+              t.y = sel_keep(t.y, dm.m[r + 1]);
+            }
+            const float2v dsp = pp * (t - dl);
+            ds[u][r] = dsp.x;
+            ds[u][r + 1] = dsp.y;
           }
-          float2v t = {pacc[r], pacc[r + 1]};
-          t *= dd;
-          if (drop_q) {
-            t.x = sel_keep(t.x, dm.m[r]);
-            t.y = sel_keep(t.y, dm.m[r + 1]);
-          }
-          const float2v dsp = pp * (t - dl);
-          ds[u][r] = dsp.x;
-          ds[u][r + 1] = dsp.y;
-        }
+        };
+        if (full) scores(std::true_type{});
+        else scores(std::false_type{});
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -653,7 +666,7 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dq_kernel(Geo 
 }
 
 // =============================================================================== bwd: dK, dV
-template <int DH, int NTT>
+template <int DH, int NTT, bool DROP>
 __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dkdv_kernel(Geo g, AttnMask mask,
                                                            const uint32_t* __restrict__ drop_k,
                                                            int drop_lp, float drop_scale,
@@ -671,11 +684,15 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dkdv_kernel(Ge
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE];  // [buf][Q | dO]
   __shared__ __attribute__((aligned(16))) float s_rows[2][2][KT];  // [buf][lse*log2e | delta]
   __shared__ float s_wsum[NTT / 64 * DH];
-  const int b = blockIdx.z, h = blockIdx.y;
+  // 1-D grid of (sample, head, key block) items, XCD-contiguous: the key blocks of one
+  // (sample, head) share an XCD, so its Q/dO tiles are fetched into one L2 once
+  const int nkb = (g.L + NTT / 2 - 1) / (NTT / 2);
+  const int item = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = item / nkb, b = bh / g.H, h = bh - b * g.H;
   const int lane = threadIdx.x & 63, hh = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int L = g.L, D = g.H * DH;
-  const int kb0 = blockIdx.x * (NTT / 2), kb1 = min(L, kb0 + NTT / 2);
+  const int kb0 = (item - bh * nkb) * (NTT / 2), kb1 = min(L, kb0 + NTT / 2);
   const int key = kb0 + wave * 32 + (lane & 31);
   const bool kv = key < L;
   const bool wave_live = kb0 + wave * 32 < L;
@@ -741,7 +758,7 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dkdv_kernel(Ge
 #pragma unroll 1
       for (int u = 0; u < 2; ++u) {  // 32-query sub-tiles (not unrolled: keeps 2 waves/SIMD)
         TileMasks<16> dm;  // dropout lane masks of (key word, query sub-tile): scalar loads
-        if (drop_k) dm.load(drop_k, drop_lp, (kb0 >> 5) + wave, qt + 32 * u);
+        if constexpr (DROP) dm.load(drop_k, drop_lp, (kb0 >> 5) + wave, qt + 32 * u);
         floatx16 sacc, pacc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -780,7 +797,7 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dkdv_kernel(Ge
           float2v t = {pacc[r], pacc[r + 1]};
           t *= dd;
           float2v pk = pp;  // drop_scale applied to dV at the end
-          if (drop_k) {
+          if constexpr (DROP) {
             pk.x = sel_keep(pp.x, dm.m[r]);
             pk.y = sel_keep(pp.y, dm.m[r + 1]);
             t.x = sel_keep(t.x, dm.m[r]);
@@ -933,14 +950,20 @@ inline int bwd_threads(int L) {
   return f64 > f128 + 0.10 ? 128 : 256;
 }
 
-#define ATTN_BWD_LAUNCH(DH_, NTT_)                                                                \
+#define ATTN_BWD_LAUNCH2(DH_, NTT_, DR_)                                                          \
   do {                                                                                            \
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<DH_, NTT_>), grid, dim3(NTT_), 0, s, g, m, drop_bits,  \
-                       lp, dscale, (const bf16_t*)dout, d_s_b, d_s_t, lse, (const bf16_t*)o,   \
-                       o_s_b, o_s_t, delta, (bf16_t*)dqkv, dq_s_b, dq_s_t, bias_grad);            \
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DH_, NTT_>), grid, dim3(NTT_), 0, s, g, m,           \
-                       drop_bits_t, lp, dscale, (const bf16_t*)dout, d_s_b, d_s_t, lse, delta,  \
-                       (bf16_t*)dqkv, dq_s_b, dq_s_t, bias_grad);                                  \
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DH_, NTT_, DR_>), grid, dim3(NTT_), 0, s, g, m,        \
+                       drop_bits, lp, dscale, (const bf16_t*)dout, d_s_b, d_s_t, lse,             \
+                       (const bf16_t*)o, o_s_b, o_s_t, delta, (bf16_t*)dqkv, dq_s_b, dq_s_t,      \
+                       bias_grad);                                                                \
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DH_, NTT_, DR_>), grid, dim3(NTT_), 0, s, g, m,      \
+                       drop_bits_t, lp, dscale, (const bf16_t*)dout, d_s_b, d_s_t, lse, delta,    \
+                       (bf16_t*)dqkv, dq_s_b, dq_s_t, bias_grad);                                 \
+  } while (0)
+#define ATTN_BWD_LAUNCH(DH_, NTT_)                     \
+  do {                                                 \
+    if (drop_bits) ATTN_BWD_LAUNCH2(DH_, NTT_, true);  \
+    else ATTN_BWD_LAUNCH2(DH_, NTT_, false);           \
   } while (0)
 
 extern "C" int mmt_dropout_bits(const uint32_t* rng, uint32_t layer, uint32_t site, int rows,
@@ -981,13 +1004,18 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   int nq = g_attn_nq > 0 ? g_attn_nq : std::min(3, (nqb + 3) / 4);
   if (Dh > 64) nq = 1;
   dim3 grid((L + QB * nq - 1) / (QB * nq), H, B);
-#define FWD1(DH_, NQ_, WS_)                                                                       \
-  hipLaunchKernelGGL((attn_fwd_kernel<DH_, NQ_, WS_>), grid, dim3(NT), 0, as_stream(stream), g, m, \
-                     drop_bits, lp, dscale, bias, (bf16_t*)o, o_s_b, o_s_t, lse, wsum)
-#define FWD(DH_, NQ_)          \
-  do {                         \
-    if (wsum) FWD1(DH_, NQ_, true); \
-    else FWD1(DH_, NQ_, false);     \
+#define FWD1(DH_, NQ_, WS_, DR_)                                                                 \
+  hipLaunchKernelGGL((attn_fwd_kernel<DH_, NQ_, WS_, DR_>), grid, dim3(NT), 0, as_stream(stream), \
+                     g, m, drop_bits, lp, dscale, bias, (bf16_t*)o, o_s_b, o_s_t, lse, wsum)
+#define FWD(DH_, NQ_)                                          \
+  do {                                                         \
+    if (drop_bits) {                                           \
+      if (wsum) FWD1(DH_, NQ_, true, true);                    \
+      else FWD1(DH_, NQ_, false, true);                        \
+    } else {                                                   \
+      if (wsum) FWD1(DH_, NQ_, true, false);                   \
+      else FWD1(DH_, NQ_, false, false);                       \
+    }                                                          \
   } while (0)
   if (Dh == 64) {
     if (nq == 3) FWD(64, 3);
@@ -1025,10 +1053,10 @@ extern "C" int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   const float dscale = drop_bits ? 1.f / keep_prob : 1.f;
   hipStream_t s = as_stream(stream);
   if (bwd_threads(L) == 128) {
-    dim3 grid((L + 63) / 64, H, B);
+    dim3 grid(((L + 63) / 64) * H * B);
     ATTN_DISPATCH(DH, ATTN_BWD_LAUNCH(DH, 128));
   } else {
-    dim3 grid((L + 127) / 128, H, B);
+    dim3 grid(((L + 127) / 128) * H * B);
     ATTN_DISPATCH(DH, ATTN_BWD_LAUNCH(DH, 256));
   }
   MMT_CHECK_LAUNCH("mmt_attn_bwd");

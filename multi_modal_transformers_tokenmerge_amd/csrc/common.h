@@ -116,6 +116,14 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// XCD-aware bijective remap: workgroups b and b+8 share an XCD (round-robin dispatch), so give
+// each XCD a contiguous range of work ids: items that share operands (a GEMM's A row panel, the
+// key/query blocks of one attention (sample, head)) then meet in one L2. Speed only.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
 inline hipStream_t as_stream(mmt_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace mmt

@@ -270,12 +270,6 @@ __device__ __forceinline__ void store_w(void* Cv, int64_t off, float beta, const
   }
 }
 
-// XCD-aware bijective remap: blocks b and b+8 share an XCD (round-robin dispatch), so give each
-// XCD a contiguous range of tile ids (guide §5.5 T1, bijective form). Speed only.
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-}
 
 // One output tile of one batch entry / K-split ("work item").
 struct Work {
