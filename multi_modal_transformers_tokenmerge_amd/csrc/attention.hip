@@ -293,11 +293,10 @@ struct Geo {
 // =============================================================================== forward
 // One workgroup = 4 waves over 128 NQ query rows of one (sample, head): wave w owns the NQ
 // 32-row query blocks w, w + 4, ..., each with its own Q fragments, O^T accumulators and
-// running max / sum. Every K/V tile is staged into LDS ONCE for all of them: with NQ = 3 one
-// workgroup covers L <= 384 rows, so K and V of a (sample, head) are read from HBM once (the
-// one-block-per-workgroup form read them once per 128 rows, 2.3x the algorithmic bytes at
-// L = 292) and each LDS tile feeds NQ x 16 MFMAs per wave instead of 16, which amortises the
-// per-tile barrier and the per-workgroup prologue.
+// running max / sum. Every K/V tile is staged into LDS ONCE for all of them: with NQ = 2 one
+// workgroup covers L <= 256 rows, so K and V of a (sample, head) are read from HBM once and each
+// LDS tile feeds NQ x 16 MFMAs per wave instead of 16, which amortises the per-tile barrier and
+// the per-workgroup prologue (the launch picks NQ per L, mmt_attn_fwd).
 template <int DH, int NQ, bool WS, bool DROP>
 __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
     Geo g, AttnMask mask, const uint32_t* __restrict__ drop_q, int drop_lp, float drop_scale,
@@ -930,7 +929,7 @@ int fill_mask(AttnMask& m, int n_sets, const int32_t* starts, const int32_t* len
 
 }  // namespace
 
-// forward query blocks per wave (0: automatic); MMT_ATTN_NQ=1..3 forces it (benchmarks)
+// forward query blocks per wave (0: automatic); MMT_ATTN_NQ=1..2 forces it (benchmarks)
 static const int g_attn_nq = getenv("MMT_ATTN_NQ") ? atoi(getenv("MMT_ATTN_NQ")) : 0;
 
 #define ATTN_DISPATCH(DH_, ...)                                  \
@@ -998,10 +997,11 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   Geo g{(const bf16_t*)qkv, s_b, s_t, L, H, scale};
   const int lp = lp_of(L);
   const float dscale = drop_bits ? 1.f / keep_prob : 1.f;
-  // query blocks per wave: enough for one workgroup to cover L (K/V read once per (b, h)) at
-  // Dh 64; Dh 128 / 256 keep one (registers)
-  const int nqb = (L + 31) / 32;
-  int nq = g_attn_nq > 0 ? g_attn_nq : std::min(3, (nqb + 3) / 4);
+  // query blocks per wave (Dh 64): two when one workgroup then covers L (K/V read once per
+  // (b, h)); beyond 256 rows one (3 blocks per wave spill registers; measured at B = 256:
+  // L = 292 117.6 / 150.5 / 122.6 us for 1 / 2 / 3 blocks, L = 212 73.1 / 71.5 / 78.2,
+  // L = 132 48.1 / 44.0 / 48.8). Dh 128 / 256 keep one (registers).
+  int nq = g_attn_nq > 0 ? std::min(g_attn_nq, 2) : (L <= 2 * QB ? 2 : 1);
   if (Dh > 64) nq = 1;
   dim3 grid((L + QB * nq - 1) / (QB * nq), H, B);
 #define FWD1(DH_, NQ_, WS_, DR_)                                                                 \
@@ -1018,8 +1018,7 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
     }                                                          \
   } while (0)
   if (Dh == 64) {
-    if (nq == 3) FWD(64, 3);
-    else if (nq == 2) FWD(64, 2);
+    if (nq == 2) FWD(64, 2);
     else FWD(64, 1);
   } else {
     ATTN_DISPATCH(DH, FWD(DH, 1));
