@@ -195,8 +195,8 @@ int mmt_gemm_fp8(int M, int N, int K, const void* A, int64_t lda, const float* s
  * arrays) and set_vis[s] = bitmask of key sets that query set s attends to; n_sets = 0: no mask.
  * Bit 31 of set_vis[s] (MMT_SET_CAUSAL) makes set s causal within itself: its query q sees its
  * own set's keys k <= q only (Text sets, token_sequencer.py:76-82, nn.make_causal_mask).
- * drop_bits: (L, ceil(L/32)) uint32 keep bitmask from mmt_dropout_bits, or NULL (no dropout);
- * kept probabilities are scaled by 1/keep_prob. bias: optional fp32 (H, L, L) added to the
+ * drop_bits: the query-word image of mmt_dropout_bits(.., L, L, ..) (its `out`), or NULL (no
+ * dropout); kept probabilities are scaled by 1/keep_prob. bias: optional fp32 (H, L, L) added to the
  * scaled logits (T5 relative position bias; forward only). o: bf16 (b, t) rows of (H, Dh);
  * lse: fp32 (B, H, L) natural-log softmax normaliser. Dh in {64, 128, 256}.
  * wsum (optional, fp32 (B, H, L)): per query, the sum over keys of the attention weights AFTER
@@ -209,8 +209,8 @@ int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, int L, int H,
                  const float* bias, void* o, int64_t o_s_b, int64_t o_s_t, float* lse,
                  float* wsum, mmt_stream_t stream);
 /* Backward: writes dq, dk, dv into dqkv (same row layout as qkv). delta: fp32 (B, H, L)
- * workspace (rowsum(dO * O)). drop_bits_t: the transposed keep mask (mmt_dropout_bits out_t);
- * both or neither of drop_bits / drop_bits_t. bias_grad (fp32 [3 H Dh], may be NULL) += the
+ * workspace (rowsum(dO * O)). drop_bits / drop_bits_t: the query-word and key-word images of
+ * mmt_dropout_bits (`out` / `out_t`); both or neither. bias_grad (fp32 [3 H Dh], may be NULL) += the
  * column sums of dq | dk | dv over (B, L): the bias gradient of the fused QKV projection. */
 int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, int L, int H, int Dh,
                  float scale, int n_sets, const int32_t* set_start, const int32_t* set_len,
@@ -218,11 +218,16 @@ int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, int L, int H,
                  float keep_prob, const void* o, int64_t o_s_b, int64_t o_s_t, const void* dout,
                  int64_t d_s_b, int64_t d_s_t, const float* lse, float* delta, void* dqkv,
                  int64_t dq_s_b, int64_t dq_s_t, float* bias_grad, mmt_stream_t stream);
-/* Keep bitmask (rows, ceil(cols/32)) of a dropout stream (flax Dropout keep-mask, broadcast over
- * batch and heads for attention): bit c of word (r, c/32) set iff keep_elem(key(rng, layer,
- * site), r*cols + c), i.e. the 16-bit half (idx & 1) of mix32(key ^ (idx >> 1)) is below
- * floor(keep_prob * 65536). out_t (optional, rows == cols): the transposed mask, bit r of word
- * (c, r/32). */
+/* Keep mask of a dropout stream (flax Dropout keep-mask, broadcast over batch and heads for
+ * attention): keep(r, c) iff keep_elem(key(rng, layer, site), r*cols + c), i.e. the 16-bit half
+ * (idx & 1) of mix32(key ^ (idx >> 1)) is below floor(keep_prob * 65536).
+ * out_t == NULL: row-major words (rows, ceil(cols/32)), bit j of word (r, w) = keep(r, 32w + j).
+ * out_t != NULL (attention, rows == cols == L): two word-major images of W = ceil(L/32) rows of
+ * LP = roundup(L, 64) words, positions interleaved pos(8g + 4h + i) = 8g + 2i + h, zero past L:
+ *   out   (query words): bit j of word (w, pos(k)) = keep(32w + j, k)
+ *   out_t (key words):   bit j of word (w, pos(q)) = keep(q, 32w + j)
+ * so that the 64-bit pair 16u + r of a 64-aligned tile's words is the wave lane mask of MFMA
+ * accumulator register r of the tile's 32-wide half u (read into SGPRs by the attention kernels). */
 int mmt_dropout_bits(const uint32_t* rng, uint32_t layer, uint32_t site, int rows, int cols,
                      float keep_prob, uint32_t* out, uint32_t* out_t, mmt_stream_t stream);
 
