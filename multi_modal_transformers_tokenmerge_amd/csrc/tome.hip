@@ -238,6 +238,140 @@ __global__ __launch_bounds__(SCORE_NT) void tome_score_kernel(const float* __res
   }
 }
 
+// Fused match, one 1024-thread workgroup per sample, when both normalised halves fit in LDS (t <=
+// 512 at c = 64; every OCTO-small/base layer): (1) the per-token head sums and normalisation (the
+// arithmetic of tome_norm_vec_kernel) are written straight into LDS; (2) the (a tile, b tile)
+// pairs are spread over the 16 waves, each running the k-ordered f32 MFMA chain and first-index
+// argmax of tome_score_kernel, partial maxima per (b tile, a row) in LDS, combined per a row
+// (argmax_better is a total order: the combination order does not matter); (3) the rank sort of
+// tome_rank_kernel and the src / dst / unm outputs. K is read from the QKV buffer once; nothing
+// round-trips through HBM and the three launches become one.
+constexpr int FUSED_NT = 1024;
+__host__ __device__ __forceinline__ size_t fused_match_lds(int t, int c) {
+  const int ta = (t + 1) / 2, tb = t / 2;
+  const int pa = (ta + 31) / 32 * 32, pbr = (tb + 31) / 32 * 32;
+  return sizeof(float) * (size_t)(pa + pbr) * (c + 1)   // normalised halves
+         + (size_t)(pbr / 32) * pa * 8                  // partial (max, idx) per (b tile, a row)
+         + (size_t)ta * 12;                             // node max / idx / rank slot
+}
+template <typename T, int LPR>
+__global__ __launch_bounds__(FUSED_NT) void tome_match_fused_kernel(
+    const T* __restrict__ metric, int t, int heads, int c, int64_t s_n, int64_t s_t, int64_t s_h,
+    int r, int flags, int32_t* __restrict__ unm_idx, int32_t* __restrict__ src_idx,
+    int32_t* __restrict__ dst_idx, float* __restrict__ node_max_out) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int b = blockIdx.x;
+  const int ta = (t + 1) / 2, tb = t / 2, cs = c + 1;
+  const int pa = (ta + 31) / 32 * 32, pbr = (tb + 31) / 32 * 32;
+  const int n_at = pa / 32, n_bt = pbr / 32;
+  float* As = smem;                                   // [pa][cs]
+  float* Bs = As + pa * cs;                           // [pbr][cs]
+  float* pmax = Bs + pbr * cs;                        // [n_bt][pa]
+  int* pidx = reinterpret_cast<int*>(pmax + n_bt * pa);
+  float* nm = reinterpret_cast<float*>(pidx + n_bt * pa);   // [ta]
+  int* ni = reinterpret_cast<int*>(nm + ta);                // [ta]
+  uint32_t* keys = reinterpret_cast<uint32_t*>(ni + ta);    // [ta] (reused as edge[] after)
+  for (int e = threadIdx.x; e < (pa - ta) * cs; e += FUSED_NT) As[ta * cs + e] = 0.f;
+  for (int e = threadIdx.x; e < (pbr - tb) * cs; e += FUSED_NT) Bs[tb * cs + e] = 0.f;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // (1) head sum + L2 normalisation into LDS
+  const int lr = lane % LPR, rbase = lane - lr;
+  const int nch = c / 8;
+  const T* mb = metric + (int64_t)b * s_n;
+  for (int r0 = 0; r0 < t; r0 += FUSED_NT / LPR) {  // uniform trip count: the shuffles below
+    const int tok = r0 + threadIdx.x / LPR;
+    const bool mine = tok < t && lr < nch;
+    float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (mine) {
+      const T* p = mb + (int64_t)tok * s_t + lr * 8;
+      for (int h = 0; h < heads; ++h) {
+        float f[8];
+        ld8f(p + (int64_t)h * s_h, f);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) m[q] = m[q] + f[q];
+      }
+    }
+    float ss = 0.f;
+    for (int j = 0; j < nch; ++j) {
+      if (lr == j) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) ss = __fmaf_rn(m[q], m[q], ss);
+      }
+      ss = __shfl(ss, rbase + j, 64);
+    }
+    if (mine) {
+      const float nrm = __fsqrt_rn(ss);
+      float* o = ((tok & 1) ? Bs : As) + (tok >> 1) * cs + lr * 8;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = __fdiv_rn(m[q], nrm);
+    }
+  }
+  __syncthreads();
+  // (2) scores: (a tile, b tile) pairs over the waves
+  const bool cls = flags & MMT_TOME_CLASS_TOKEN;
+  const bool dis = flags & MMT_TOME_DISTILL_TOKEN;
+  for (int pr = wave; pr < n_at * n_bt; pr += FUSED_NT / 64) {
+    const int at = pr % n_at, jt = pr / n_at;
+    const int i = at * 32 + (lane & 31);
+    const float* bp = As + i * cs + (lane >> 5);
+    const float* ap = Bs + (jt * 32 + (lane & 31)) * cs + (lane >> 5);
+    floatx16 acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+    for (int s2 = 0; s2 < c / 2; ++s2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[2 * s2], bp[2 * s2], acc, 0, 0, 0);
+    float best = 0.f;
+    int bidx = -1;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int jj = jt * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+      if (jj >= tb) continue;
+      float v = acc[q];
+      if ((cls && i == 0) || (dis && jj == 0)) v = -INFINITY;
+      keep_best(v, jj, best, bidx);
+    }
+    const float ov = __shfl_xor(best, 32, 64);
+    const int oi = __shfl_xor(bidx, 32, 64);
+    keep_best(ov, oi, best, bidx);
+    if (lane < 32) {
+      pmax[jt * pa + i] = best;
+      pidx[jt * pa + i] = bidx;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < ta; i += FUSED_NT) {
+    float bb = 0.f;
+    int bi = -1;
+    for (int jt = 0; jt < n_bt; ++jt) keep_best(pmax[jt * pa + i], pidx[jt * pa + i], bb, bi);
+    nm[i] = bb;
+    ni[i] = bi;
+    keys[i] = sort_key(bb);
+  }
+  __syncthreads();
+  // (3) descending total-order rank, ties -> higher index first (tome_rank_kernel)
+  int* edge = pidx;  // the partials are consumed
+  for (int i = threadIdx.x; i < ta; i += FUSED_NT) {
+    const uint32_t kv = keys[i];
+    int rank = 0;
+    for (int j = 0; j < ta; ++j) {
+      const uint32_t kw = keys[j];
+      rank += (kw > kv) || (kw == kv && j > i);
+    }
+    edge[rank] = i;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < ta; k += FUSED_NT) {
+    const int e = edge[k];
+    if (k < r) {
+      src_idx[(int64_t)b * r + k] = e;
+      dst_idx[(int64_t)b * r + k] = ni[e];
+    } else {
+      unm_idx[(int64_t)b * (ta - r) + (k - r)] = e;
+    }
+    if (node_max_out) node_max_out[(int64_t)b * ta + k] = nm[k];
+  }
+}
+
 __global__ __launch_bounds__(RANK_NT) void tome_rank_kernel(const float* __restrict__ nmax,
                                                             const int32_t* __restrict__ nidx,
                                                             int ta, int r,
@@ -578,10 +712,39 @@ extern "C" int mmt_tome_match(const void* metric, int dtype, int n, int t, int h
   float* nmax = (float*)((char*)Bn + al((int64_t)n * tb * c * 4));
   int32_t* nidx = (int32_t*)((char*)nmax + al((int64_t)n * ta * 4));
   hipStream_t s = as_stream(stream);
-  // 1. per-token head sum + L2 normalisation
   const int vw = dtype == MMT_BF16 ? 8 : 4;  // elements per 16 B
   const bool vec = (c % 8 == 0) && (s_n % vw == 0) && (s_t % vw == 0) && (s_h % vw == 0) &&
                    ((uintptr_t)metric % 16 == 0);
+  const size_t fused_lds = fused_match_lds(t, c);
+  if (vec && g_match_use_mfma && fused_lds <= 160 * 1024 && c / 8 <= 64) {
+    // one launch: norm + score + rank with both halves in LDS
+    const int lpr = pow2_at_least(c / 8);
+#define FUSED(T, LPR)                                                                            \
+  do {                                                                                           \
+    static const bool attr_ = (hipFuncSetAttribute((const void*)tome_match_fused_kernel<T, LPR>, \
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024), true);    \
+    (void)attr_;                                                                                 \
+    hipLaunchKernelGGL((tome_match_fused_kernel<T, LPR>), dim3(n), dim3(FUSED_NT), fused_lds, s, \
+                       (const T*)metric, t, heads, c, s_n, s_t, s_h, r, flags, unm_idx, src_idx, \
+                       dst_idx, node_max);                                                       \
+  } while (0)
+#define FUSED_ALL(T)                                  \
+  switch (lpr) {                                      \
+    case 1: FUSED(T, 1); break;                       \
+    case 2: FUSED(T, 2); break;                       \
+    case 4: FUSED(T, 4); break;                       \
+    case 8: FUSED(T, 8); break;                       \
+    case 16: FUSED(T, 16); break;                     \
+    case 32: FUSED(T, 32); break;                     \
+    default: FUSED(T, 64); break;                     \
+  }
+    if (dtype == MMT_F32) { FUSED_ALL(float) } else { FUSED_ALL(bf16_t) }
+#undef FUSED_ALL
+#undef FUSED
+    MMT_CHECK_LAUNCH("mmt_tome_match(fused)");
+    return MMT_OK;
+  }
+  // 1. per-token head sum + L2 normalisation
   const int64_t rows = (int64_t)n * t;
   if (vec) {
     const int lpr = pow2_at_least(c / 8);
