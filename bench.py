@@ -123,8 +123,8 @@ def kernel_probes(model, B, reps=20):
     algorithmic work per launch (flops for MFMA-bound kernels, bytes for HBM-bound ones; DESIGN.md
     §3 states each figure). Covers the top of the step's trace: the nt256 GEMM (MLP up), the
     direct-to-LDS NT GEMM (MLP input gradient, N = 384, K = 1536), the split-K weight-gradient
-    GEMM (MLP Dense_0 dW), attention forward and backward (dQ + dK/dV), ToMe merge forward and
-    the sequence-axis LayerNorm backward."""
+    GEMM (MLP Dense_0 dW), attention forward and backward (dQ + dK/dV), ToMe matching and merge
+    forward and the sequence-axis LayerNorm backward."""
     from multi_modal_transformers_tokenmerge_amd.layers import split_k_for
     cfg = model.cfg
     dev = model.device
@@ -197,11 +197,16 @@ def kernel_probes(model, B, reps=20):
         "mfma", 2.5 * fwd_flops,
         "dQ + dK/dV kernels together: 2.5 x the forward count (flash-attention convention)",
         B * L * (3 * D + 2 * D + 3 * D) * 2 + B * H * L * 8)
-    # 6. ToMe merge forward of block 0 (fp32 residual stream, image set)
+    # 6. ToMe matching and merge forward of block 0 (metric = K of the image set, fp32 residual)
     if r > 0:
         s0, t = sets.starts[ts], sets.lens[ts]
         x1 = rnd(B, L, D, dt=torch.float32)
-        unm, src, dst = K.tome_match(qkv.view(B, L, 3, H, Dh)[:, s0:s0 + t, 1], r)
+        metric = qkv.view(B, L, 3, H, Dh)[:, s0:s0 + t, 1]
+        add("tome_match", "tome_match_fused_kernel",
+            lambda: K.tome_match(metric, r), "hbm",
+            B * t * H * Dh * 2 + B * ((t + 1) // 2) * 4,
+            "read the K rows of the set (all heads), write src/dst/unm indices")
+        unm, src, dst = K.tome_match(metric, r)
         torch.cuda.synchronize()
         add("tome_merge_fwd", "tome_merge_fwd_kernel",
             lambda: K.tome_merge_fwd(x1, s0, t, r, unm, src, dst, size_in=None), "hbm",

@@ -47,7 +47,24 @@ __device__ __forceinline__ void ld8f(const float* p, float* f) {
   f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
 }
 
-// The matching runs as three launches (all on the caller's stream, workspace from the caller):
+// m[0..7] += the 8 metric elements at p of every head, h ascending (fp32 adds, the canonical
+// order). Loads go out 8 heads at a time from clamped addresses (branch-free, so all of them are
+// in flight before the first add; a per-head load + add loop waited for every load in turn).
+template <typename T>
+__device__ __forceinline__ void head_sum(const T* p, int heads, int64_t s_h, float* m) {
+  for (int h0 = 0; h0 < heads; h0 += 8) {
+    float f[8][8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) ld8f(p + (int64_t)min(h0 + u, heads - 1) * s_h, f[u]);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (h0 + u < heads)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) m[q] = m[q] + f[u][q];
+  }
+}
+
+// The matching runs as three launches// The matching runs as three launches (all on the caller's stream, workspace from the caller):
 //   norm  : m = sum_h metric (fp32, h ascending), m / ||m||_2 with ||m|| = sqrt of a sequential
 //           fmaf chain over c (no eps, token_compression.py:72) -> A^ [n][ta][c], B^ [n][tb][c]
 //           (the reference's a = m[::2], b = m[1::2], :73), every token row in parallel;
@@ -75,15 +92,7 @@ __global__ __launch_bounds__(NORM_NT) void tome_norm_vec_kernel(
   const int nch = c / 8;
   const bool mine = live && lr < nch;
   float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (mine) {
-    const T* p = metric + (int64_t)b * s_n + (int64_t)tok * s_t + lr * 8;
-    for (int h = 0; h < heads; ++h) {
-      float f[8];
-      ld8f(p + (int64_t)h * s_h, f);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) m[q] = m[q] + f[q];
-    }
-  }
+  if (mine) head_sum(metric + (int64_t)b * s_n + (int64_t)tok * s_t + lr * 8, heads, s_h, m);
   float ss = 0.f;
   for (int j = 0; j < nch; ++j) {
     if (lr == j) {
@@ -282,15 +291,7 @@ __global__ __launch_bounds__(FUSED_NT) void tome_match_fused_kernel(
     const int tok = r0 + threadIdx.x / LPR;
     const bool mine = tok < t && lr < nch;
     float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (mine) {
-      const T* p = mb + (int64_t)tok * s_t + lr * 8;
-      for (int h = 0; h < heads; ++h) {
-        float f[8];
-        ld8f(p + (int64_t)h * s_h, f);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) m[q] = m[q] + f[q];
-      }
-    }
+    if (mine) head_sum(mb + (int64_t)tok * s_t + lr * 8, heads, s_h, m);
     float ss = 0.f;
     for (int j = 0; j < nch; ++j) {
       if (lr == j) {
@@ -318,7 +319,19 @@ __global__ __launch_bounds__(FUSED_NT) void tome_match_fused_kernel(
     floatx16 acc;
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-    for (int s2 = 0; s2 < c / 2; ++s2)
+    // operands read 8 k-steps ahead of their MFMAs (one LDS latency per group, not per step)
+    int s2 = 0;
+    for (; s2 + 8 <= c / 2; s2 += 8) {
+      float av[8], bv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        av[u] = ap[2 * (s2 + u)];
+        bv[u] = bp[2 * (s2 + u)];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+    }
+    for (; s2 < c / 2; ++s2)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[2 * s2], bp[2 * s2], acc, 0, 0, 0);
     float best = 0.f;
     int bidx = -1;
@@ -348,16 +361,22 @@ __global__ __launch_bounds__(FUSED_NT) void tome_match_fused_kernel(
     keys[i] = sort_key(bb);
   }
   __syncthreads();
-  // (3) descending total-order rank, ties -> higher index first (tome_rank_kernel)
+  // (3) descending total-order rank, ties -> higher index first (tome_rank_kernel); 8 lanes per
+  // row each count over an eighth of the keys, summed with xor shuffles (uniform trip count)
   int* edge = pidx;  // the partials are consumed
-  for (int i = threadIdx.x; i < ta; i += FUSED_NT) {
-    const uint32_t kv = keys[i];
+  for (int i0 = 0; i0 < ta; i0 += FUSED_NT / 8) {
+    const int i = i0 + (threadIdx.x >> 3), part = threadIdx.x & 7;
+    const uint32_t kv = i < ta ? keys[i] : 0u;
     int rank = 0;
-    for (int j = 0; j < ta; ++j) {
-      const uint32_t kw = keys[j];
-      rank += (kw > kv) || (kw == kv && j > i);
-    }
-    edge[rank] = i;
+    if (i < ta)
+      for (int j = part; j < ta; j += 8) {
+        const uint32_t kw = keys[j];
+        rank += (kw > kv) || (kw == kv && j > i);
+      }
+    rank += __shfl_xor(rank, 1, 64);
+    rank += __shfl_xor(rank, 2, 64);
+    rank += __shfl_xor(rank, 4, 64);
+    if (i < ta && part == 0) edge[rank] = i;
   }
   __syncthreads();
   for (int k = threadIdx.x; k < ta; k += FUSED_NT) {
