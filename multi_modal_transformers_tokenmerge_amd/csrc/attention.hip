@@ -297,8 +297,8 @@ struct Geo {
 // workgroup covers L <= 256 rows, so K and V of a (sample, head) are read from HBM once and each
 // LDS tile feeds NQ x 16 MFMAs per wave instead of 16, which amortises the per-tile barrier and
 // the per-workgroup prologue (the launch picks NQ per L, mmt_attn_fwd).
-template <int DH, int NQ, bool WS, bool DROP>
-__global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
+template <int DH, int NQ, bool WS, bool DROP, int NW = 4>
+__global__ __launch_bounds__(64 * NW, DH > 128 ? 1 : 2) void attn_fwd_kernel(
     Geo g, AttnMask mask, const uint32_t* __restrict__ drop_q, int drop_lp, float drop_scale,
     const float* __restrict__ bias, bf16_t* __restrict__ o, int64_t o_s_b, int64_t o_s_t,
     float* __restrict__ lse, float* __restrict__ wsum) {
@@ -313,7 +313,8 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
   const int lane = threadIdx.x & 63, hh = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int L = g.L, D = g.H * DH;
-  const int q0 = blockIdx.x * (QB * NQ), q1 = min(L, q0 + QB * NQ);
+  constexpr int NTF = 64 * NW, QBF = 32 * NW;  // threads / query rows per block slot
+  const int q0 = blockIdx.x * (QBF * NQ), q1 = min(L, q0 + QBF * NQ);
   const bf16_t* base = g.qkv + (int64_t)b * g.s_b;
   const bf16_t* kbase = base + D + h * DH;
   const bf16_t* vbase = base + 2 * D + h * DH;
@@ -327,7 +328,7 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
   bool qv[NQ], live[NQ];
 #pragma unroll
   for (int i = 0; i < NQ; ++i) {
-    const int qb = q0 + 32 * (wave + 4 * i);
+    const int qb = q0 + 32 * (wave + NW * i);
     qrow[i] = qb + (lane & 31);
     qv[i] = qrow[i] < L;
     live[i] = qb < L;  // wave-uniform
@@ -346,11 +347,11 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
   }
 
   const int ntiles = (L + KT - 1) / KT;
-  for (int e = threadIdx.x; e < mask.n_sets * ntiles; e += NT) {
+  for (int e = threadIdx.x; e < mask.n_sets * ntiles; e += NTF) {
     const int st = e / ntiles, t = e - st * ntiles;
     s_vis[st * ntiles + t] = sets_bits(mask, mask.vis[st], t * KT);
   }
-  TilePair<DH> pf;
+  TilePair<DH, NTF> pf;
   int kt = next_key_tile(mask, q0, q1, 0, L);
   if (kt < L) {
     pf.load(kbase, g.s_t, vbase, g.s_t, kt, L);
@@ -422,7 +423,7 @@ __global__ __launch_bounds__(NT, DH > 128 ? 1 : 2) void attn_fwd_kernel(
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         TileMasks<16> dm;  // dropout lane masks of (query word, key sub-tile): scalar loads
-        if constexpr (DROP) dm.load(drop_q, drop_lp, (q0 >> 5) + wave + 4 * i, kt + 32 * u);
+        if constexpr (DROP) dm.load(drop_q, drop_lp, (q0 >> 5) + wave + NW * i, kt + 32 * u);
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
           float2v a = {sacc[u][r], sacc[u][r + 1]};
@@ -1001,12 +1002,25 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   // (b, h)); beyond 256 rows one (3 blocks per wave spill registers; measured at B = 256:
   // L = 292 117.6 / 150.5 / 122.6 us for 1 / 2 / 3 blocks, L = 212 73.1 / 71.5 / 78.2,
   // L = 132 48.1 / 44.0 / 48.8). Dh 128 / 256 keep one (registers).
-  int nq = g_attn_nq > 0 ? std::min(g_attn_nq, 2) : (L <= 2 * QB ? 2 : 1);
+  int nq = g_attn_nq > 0 ? std::min(g_attn_nq, 2) : (L <= 32 ? 1 : L <= 2 * QB ? 2 : 1);
   if (Dh > 64) nq = 1;
   dim3 grid((L + QB * nq - 1) / (QB * nq), H, B);
 #define FWD1(DH_, NQ_, WS_, DR_)                                                                 \
-  hipLaunchKernelGGL((attn_fwd_kernel<DH_, NQ_, WS_, DR_>), grid, dim3(NT), 0, as_stream(stream), \
-                     g, m, drop_bits, lp, dscale, bias, (bf16_t*)o, o_s_b, o_s_t, lse, wsum)
+  do {                                                                                            \
+    bool one_wave = false;                                                                        \
+    if constexpr (DH_ <= 64 && NQ_ == 1) {                                                        \
+      if (L <= 32) { /* one 32-row block (the T5 text): one-wave workgroups */                    \
+        one_wave = true;                                                                          \
+        hipLaunchKernelGGL((attn_fwd_kernel<DH_, NQ_, WS_, DR_, 1>), dim3(1, H, B), dim3(64), 0,  \
+                           as_stream(stream), g, m, drop_bits, lp, dscale, bias, (bf16_t*)o,      \
+                           o_s_b, o_s_t, lse, wsum);                                              \
+      }                                                                                           \
+    }                                                                                             \
+    if (!one_wave)                                                                                \
+      hipLaunchKernelGGL((attn_fwd_kernel<DH_, NQ_, WS_, DR_>), grid, dim3(NT), 0,                \
+                         as_stream(stream), g, m, drop_bits, lp, dscale, bias, (bf16_t*)o, o_s_b,  \
+                         o_s_t, lse, wsum);                                                       \
+  } while (0)
 #define FWD(DH_, NQ_)                                          \
   do {                                                         \
     if (drop_bits) {                                           \

@@ -71,7 +71,8 @@ def ref_attention(qkv, H, scale, mask, keep, keep_prob, bias=None):
 
 @pytest.mark.parametrize("B,L,H,Dh,masked,drop", [
     (2, 292, 6, 64, True, True), (3, 292, 6, 64, True, False), (2, 130, 2, 64, False, False),
-    (1, 1064, 2, 64, True, True), (2, 33, 3, 128, False, True), (4, 276, 6, 64, True, True)])
+    (1, 1064, 2, 64, True, True), (2, 33, 3, 128, False, True), (4, 276, 6, 64, True, True),
+    (3, 24, 4, 64, False, True), (2, 32, 3, 64, False, False)])
 def test_attention_fwd_bwd(dev, B, L, H, Dh, masked, drop):
     from multi_modal_transformers_tokenmerge_amd import _kernels as K
     g = torch.Generator().manual_seed(B * 100 + L + H)
