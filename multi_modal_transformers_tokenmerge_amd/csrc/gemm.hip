@@ -776,6 +776,9 @@ __global__ __launch_bounds__(NT2, 1) void gemm_big_kernel(
 // Requires K % 64 == 0 and N % BN == 0 (checked by mmt_gemm); rows past M are clamped on load
 // and not stored.
 constexpr int NT3 = 512;
+#ifndef NT_SH256  // stashed output chunks of the bf16 256-wide tile (0: all stored by the epilogue;
+#define NT_SH256 0  // measured: 4 and 8 slower at M = 70656, K = 384 and 1536)
+#endif
 
 // buffer_load_dwordx4 ... lds of 16 B per lane: byte voffset + soffset inside [base, base + bytes)
 // (out-of-range lanes read zeros) into the wave-uniform LDS address lds (+ 16 * lane).
@@ -789,21 +792,24 @@ __device__ __forceinline__ void dma16(const void* base, int64_t bytes, void* lds
 #endif
 }
 
-template <int BN, int OUT, bool STASH, int NS>
+template <int BN, int OUT, int SHV, int NS>
 __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
     int64_t ldb, void* __restrict__ Cv, int64_t ldc, int tiles_n, int n_tiles, int xcd_order,
     Epi epi) {
   constexpr int W = BN / 2, NF = W / 16, Q = W / 4;
-  constexpr int BSH = __builtin_ctz(Q);
+  static_assert(NF % 2 == 0, "column fragments come in pairs");
   constexpr int A_BYTES = 256 * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
   constexpr int GA = 4, GB = BN / 64, G = GA + GB;  // DMA instructions per wave per K-step
-  // 16-B output chunks per lane per tile (CPM per 16-row fragment); with STASH they are held in
-  // registers and stored SPS per K-step during the next tile (NSTEPS K-steps)
+  // 16-B output chunks per lane per tile (CPM per 16-row fragment). The last SH of them (SHV; -1:
+  // all) are held in registers (the stash) and stored SPS per K-step during the next tile
+  // (NSTEPS K-steps); the first EI are stored by the epilogue itself.
   constexpr int CPM = OUT == 0 ? Q / 8 : Q / 4, E = 4 * CPM;
-  constexpr int SPS = 4, NSTEPS = E / SPS;
-  static_assert(E % SPS == 0, "stash chunks");
-  static_assert(NS == 2 || (NS == 3 && STASH), "3 stages only with the stash");
+  constexpr int SH = SHV < 0 ? E : SHV, EI = E - SH;
+  constexpr bool STASH = SH > 0;
+  constexpr int SPS = 4, NSTEPS = SH / SPS;
+  static_assert(SH % SPS == 0 && SH <= E && EI % 2 == 0, "stash chunks");
+  static_assert(NS == 2 || (NS == 3 && STASH && EI == 0), "3 stages only with the full stash");
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -830,7 +836,7 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
   if (epi.rng) key = stream_key(epi.rng[0], epi.rng[1], epi.drop_layer, epi.drop_site);
 
   auto fA = [](int r) { return r & 6; };
-  auto fB = [](int r) { return (r & 2) | (((r >> BSH) & 1) << 2); };
+  auto fB = [](int r) { return (r & 2) | (((r >> 3) & 1) << 2); };
   // one DMA piece (1 KB per wave) of K-step position (m0, n0, k0) into stage st:
   // pieces 0..GA-1 are A rows 8j..8j+7 (j = wave*GA + p), the rest B rows. buffer_load ... lds
   // with the tile's panel as the buffer: the per-lane byte offsets (row, swizzled chunk) are
@@ -880,22 +886,23 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
   }
 #pragma unroll
   for (int nf = 0; nf < NF; ++nf) {
-    const int r = wn * W + (l15 >> 2) * Q + 4 * nf + (l15 & 3);
+    const int r = wn * W + 32 * (nf >> 1) + 8 * (l15 >> 2) + 4 * (nf & 1) + (l15 & 3);
     b_off[nf] = A_BYTES + r * 128;
     b_sw[nf] = fB(r);
   }
 
   // Output stash (STASH): the finished tile's epilogue values, bf16-packed (OUT 0) or fp32, as
-  // 16-B chunks ci = mf * CPM + c; chunk ci covers row srow + 16 mf, columns sgc + 8c (bf16) /
-  // sgc + 4c (fp32).
-  uint32_t stash[E][4];
+  // 16-B chunks ci = mf * CPM + c; chunk ci covers row srow + 16 mf, columns sgc + 32c (bf16) /
+  // sgc + 32(c >> 1) + 4(c & 1) (fp32): the four lq lanes of a row store 64 contiguous bytes
+  // (bf16) or 128 (fp32) per instruction.
+  uint32_t stash[STASH ? SH : 1][4];
   int sk = NSTEPS;            // next K-step's store group (NSTEPS: nothing left to store)
   int srow = 0, sgc = 0;      // this lane's first row / first column of the stashed tile
-  auto stash_store = [&](int ci) {
-    const int mf = ci / CPM, c = ci - mf * CPM;
+  auto stash_store = [&](int ci) {  // stash entry ci = output chunk EI + ci
+    const int mf = (EI + ci) / CPM, c = EI + ci - mf * CPM;
     const int gr = srow + 16 * mf;
     if (gr < M) {
-      const int64_t off = (int64_t)gr * ldc + sgc + (OUT == 0 ? 8 : 4) * c;
+      const int64_t off = (int64_t)gr * ldc + sgc + (OUT == 0 ? 32 * c : 32 * (c >> 1) + 4 * (c & 1));
       const uint4 u = make_uint4(stash[ci][0], stash[ci][1], stash[ci][2], stash[ci][3]);
       // plain stores: non-temporal ones measured twice this kernel's time
       if (OUT == 0) *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(Cv) + off) = u;
@@ -942,10 +949,13 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
     }
   };
 
-  // lane (row l15 of fragment mf, group lq) holds columns lq*Q + 4*nf + r: one contiguous run
+  // lane (row l15 of fragment mf, group lq) holds columns 32 (nf >> 1) + 8 lq + 4 (nf & 1) + r of
+  // the wave's W: runs of 8 columns, the four lq lanes' runs adjacent (B-fragment row order
+  // above), so each store instruction writes 64 contiguous bytes per row instead of four 16-B
+  // pieces at a 64-B stride
   auto epilogue = [&](int tile) {
     const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
-    const int gc0 = tn * BN + wn * W + lq * Q;
+    const int gc0 = tn * BN + wn * W + 8 * lq;
     if (STASH) {  // store what is left of the previous stash (K-loops shorter than NSTEPS)
 #pragma unroll
       for (int j = 0; j < NSTEPS; ++j)
@@ -965,26 +975,27 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
           float v[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = acc[mf][(8 * c8 + e) >> 2][e & 3];
-          epilogue_w<8>(epi, key, N, gr, gc0 + 8 * c8, v);
-          if (STASH) {
+          epilogue_w<8>(epi, key, N, gr, gc0 + 32 * c8, v);
+          if (STASH && mf * CPM + (OUT == 0 ? c8 : 2 * c8) >= EI) {
+            const int ci = mf * CPM + (OUT == 0 ? c8 : 2 * c8) - EI;  // stash entry
             if (OUT == 1 && epi.beta != 0.f) {
               float o[8];
-              ldw<8>(reinterpret_cast<const float*>(Cv) + (int64_t)gr * ldc + gc0 + 8 * c8, o);
+              ldw<8>(reinterpret_cast<const float*>(Cv) + (int64_t)gr * ldc + gc0 + 32 * c8, o);
 #pragma unroll
               for (int e = 0; e < 8; ++e) v[e] += epi.beta * o[e];
             }
             if (OUT == 0) {
-              uint32_t* d = stash[mf * CPM + c8];
+              uint32_t* d = stash[ci];
 #pragma unroll
               for (int q = 0; q < 4; ++q)
                 d[q] = (uint32_t)f2bf(v[2 * q]) | ((uint32_t)f2bf(v[2 * q + 1]) << 16);
             } else {
 #pragma unroll
-              for (int q = 0; q < 8; ++q) stash[mf * CPM + 2 * c8 + (q >> 2)][q & 3] = __float_as_uint(v[q]);
+              for (int q = 0; q < 8; ++q) stash[ci + (q >> 2)][q & 3] = __float_as_uint(v[q]);
             }
             continue;
           }
-          store_w<OUT, 8>(Cv, (int64_t)gr * ldc + gc0 + 8 * c8, epi.beta, v);
+          store_w<OUT, 8>(Cv, (int64_t)gr * ldc + gc0 + 32 * c8, epi.beta, v);
         }
       }
 #pragma unroll
@@ -1008,6 +1019,8 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
     else if (n == G) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
     else if (n == G + SPS) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G + SPS) : "memory");
     else if (n == G + 2 * SPS) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G + 2 * SPS) : "memory");
+    else if (n == EI && EI > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EI) : "memory");
+    else if (n == EI + SPS && EI > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EI + SPS) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
 
@@ -1027,7 +1040,10 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
       NT_TRACE(i - 1, 2);
       pend = false;
       counted = (ptile / tiles_n) * 256 + 256 <= M;
-      if (STASH) wait_vm(NS == 2 ? sc1 : (s + 1 < S ? G : 0) + sc1 + sc2);  // see below
+      // younger than K-step s's DMA: the previous K-step's stash stores and this epilogue's EI
+      // immediate stores (exact only for a full tile)
+      if (STASH) wait_vm(EI > 0 ? (counted ? EI + sc1 : 0)
+                                : NS == 2 ? sc1 : (s + 1 < S ? G : 0) + sc1 + sc2);  // see below
       else if (counted) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(E) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if (STASH) {
@@ -1060,7 +1076,7 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
   epilogue(ptile);
   if (STASH)
 #pragma unroll
-    for (int ci = 0; ci < E; ++ci) stash_store(ci);
+    for (int ci = 0; ci < SH; ++ci) stash_store(ci);
   NT_TRACE(n_mine - 1, 2);
   NT_CLK(1);
 }
@@ -1340,13 +1356,13 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
       // the register stash fits 2 waves/SIMD for bf16 at BN <= 192 and fp32 at BN 128;
       // BN 128 has LDS for 3 stages (DMA two K-steps ahead)
       if (final_kind == 0) {
-        if (bn == 256) GN(256, 0, false, 2);
-        else if (bn == 192) GN(192, 0, true, 2);
-        else GN(128, 0, true, 3);
+        if (bn == 256) GN(256, 0, NT_SH256, 2);
+        else if (bn == 192) GN(192, 0, -1, 2);
+        else GN(128, 0, -1, 3);
       } else {
-        if (bn == 256) GN(256, 1, false, 2);
-        else if (bn == 192) GN(192, 1, false, 2);
-        else GN(128, 1, true, 3);
+        if (bn == 256) GN(256, 1, 0, 2);
+        else if (bn == 192) GN(192, 1, 0, 2);
+        else GN(128, 1, -1, 3);
       }
 #undef GN
       MMT_CHECK_LAUNCH("mmt_gemm(nt256)");

@@ -39,12 +39,18 @@ def _cfg(name, **kw):
 
 @pytest.mark.parametrize("name", ["octo-small-tome16", "octo-small"])
 def test_blockwise_full_depth(dev, name):
+    """Every block at full depth, teacher-forced, at the block-local bar; as in the prune test,
+    a tensor under 0.999 passes only when the HIP deviation is within that tensor's bf16 floor
+    (the emulating oracle vs float64 on the same block inputs): block 0's LN1 / Dense_0 bias
+    gradients of octo-small (no merge, 292 rows of cancellation) sit at ~0.9987 and move by
+    ~1e-4 between runs with the order of the fp32 bias-gradient atomics."""
     cfg = _cfg(name)
     assert cfg.num_blocks == 12 and cfg.t5.num_layers == 12
     res = P.hip_blockwise(cfg, 2, seed=0)
     assert res["tome_layers_checked"] == (12 if cfg.tome_r else 0)
     out = P.oracle_blockwise(cfg, res)
-    P.check_blockwise(out)
+    P.check_blockwise(out, cfg=cfg, res=res)
+    assert len(out.get("floor_accepted", {})) <= 6, out["floor_accepted"]
 
 
 def test_t5_layerwise_full_depth(dev):
