@@ -290,6 +290,40 @@ struct Geo {
   float scale;
 };
 
+// A wave's 32 x DH bf16 output rows from O^T-layout accumulators (lane = row r0 + (lane & 31),
+// register r of d-subtile d = column 32 d + 8 (r >> 2) + 4 (lane >> 5) + (r & 3)), each row scaled
+// by its lane's sc: written to the wave's LDS region `so` (32 x STR, 8 B per lane), read back as
+// 16-B row chunks and stored so that every store instruction writes whole 2*DH-byte rows (8 B per
+// lane at a row stride would touch 32 rows per instruction). Rows >= L are not stored.
+template <int DH, int STR>
+__device__ __forceinline__ void store_rows_lds(const floatx16* acc, float sc, bf16_t* so,
+                                               bf16_t* base, int64_t row_stride, int r0, int L,
+                                               int lane) {
+  const int hh = lane >> 5;
+#pragma unroll
+  for (int d = 0; d < DH / 32; ++d)
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4) {
+      const int dd = 32 * d + 8 * r4 + 4 * hh;
+      uint2 w;
+      w.x = (uint32_t)f2bf(acc[d][4 * r4] * sc) | ((uint32_t)f2bf(acc[d][4 * r4 + 1] * sc) << 16);
+      w.y = (uint32_t)f2bf(acc[d][4 * r4 + 2] * sc) | ((uint32_t)f2bf(acc[d][4 * r4 + 3] * sc) << 16);
+      *reinterpret_cast<uint2*>(so + (lane & 31) * STR + dd) = w;
+    }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  constexpr int CPR = DH / 8;  // 16-B chunks per row
+#pragma unroll
+  for (int j = 0; j < 32 * CPR / 64; ++j) {
+    const int ci = lane + 64 * j, row = ci / CPR, ch = ci - row * CPR;
+    if (r0 + row < L)
+      *reinterpret_cast<uint4*>(base + (int64_t)(r0 + row) * row_stride + ch * 8) =
+          *reinterpret_cast<const uint4*>(so + row * STR + ch * 8);
+  }
+  __builtin_amdgcn_wave_barrier();  // the region may be rewritten next
+}
+
 // =============================================================================== forward
 // One workgroup = 4 waves over 128 NQ query rows of one (sample, head): wave w owns the NQ
 // 32-row query blocks w, w + 4, ..., each with its own Q fragments, O^T accumulators and
@@ -471,23 +505,33 @@ __global__ __launch_bounds__(64 * NW, DH > 128 ? 1 : 2) void attn_fwd_kernel(
     buf ^= 1;
     kt = kn;
   }
+  // O, scaled and rounded to bf16: with NQ = 2 through LDS (the idle K/V buffers: one 32-row
+  // region per wave and query block) as whole-row stores (L = 212: 71.2 -> 67.9 us)
+  static_assert(NW * NQ * 32 <= 4 * KT, "O staging regions must fit the K/V buffers");
 #pragma unroll
   for (int i = 0; i < NQ; ++i) {
-    if (!qv[i]) continue;
-    const int q = qrow[i];
+    if (!live[i]) continue;  // wave-uniform
     const float inv = l[i] > 0.f ? drop_scale / l[i] : 0.f;
-    bf16_t* orow = o + (int64_t)b * o_s_b + (int64_t)q * o_s_t + h * DH;
+    if constexpr (NQ == 1) {  // measured faster as direct stores at NQ = 1 (L = 292: 117 vs 137 us)
+      if (!qv[i]) continue;
+      bf16_t* orow = o + (int64_t)b * o_s_b + (int64_t)qrow[i] * o_s_t + h * DH;
 #pragma unroll
-    for (int d = 0; d < ND; ++d)
+      for (int d = 0; d < ND; ++d)
 #pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        const int dd = 32 * d + 8 * r4 + 4 * hh;
-        uint2 w;
-        w.x = (uint32_t)f2bf(oacc[i][d][4 * r4] * inv) | ((uint32_t)f2bf(oacc[i][d][4 * r4 + 1] * inv) << 16);
-        w.y = (uint32_t)f2bf(oacc[i][d][4 * r4 + 2] * inv) | ((uint32_t)f2bf(oacc[i][d][4 * r4 + 3] * inv) << 16);
-        *reinterpret_cast<uint2*>(orow + dd) = w;
-      }
-    if (lane < 32) {
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const int dd = 32 * d + 8 * r4 + 4 * hh;
+          uint2 w;
+          w.x = (uint32_t)f2bf(oacc[i][d][4 * r4] * inv) | ((uint32_t)f2bf(oacc[i][d][4 * r4 + 1] * inv) << 16);
+          w.y = (uint32_t)f2bf(oacc[i][d][4 * r4 + 2] * inv) | ((uint32_t)f2bf(oacc[i][d][4 * r4 + 3] * inv) << 16);
+          *reinterpret_cast<uint2*>(orow + dd) = w;
+        }
+    } else {
+      store_rows_lds<DH, STR>(oacc[i], inv, smem + (wave * NQ + i) * 32 * STR,
+                              o + (int64_t)b * o_s_b + h * DH, o_s_t, q0 + 32 * (wave + NW * i), L,
+                              lane);
+    }
+    if (qv[i] && lane < 32) {
+      const int q = qrow[i];
       lse[((int64_t)b * g.H + h) * L + q] = l[i] > 0.f ? m[i] * c * LN2 + logf(l[i]) : -INFINITY;
       if (WS) wsum[((int64_t)b * g.H + h) * L + q] = ld[i] * inv;  // sum_k of the dropped weights
     }
@@ -648,21 +692,9 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dq_kernel(Geo 
   if (bgrad)  // kernel-uniform; the loop's last barrier freed the staging buffers
     colsum_atomic<ND, NTT>(dqacc, g.scale, reinterpret_cast<float*>(smem), s_wsum,
                            bgrad + h * DH, lane, wave);
-  if (qv) {
-    bf16_t* orow = dqkv + (int64_t)b * dq_s_b + (int64_t)q * dq_s_t + h * DH;
-#pragma unroll
-    for (int d = 0; d < ND; ++d)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        const int dd = 32 * d + 8 * r4 + 4 * hh;
-        uint2 w;
-        w.x = (uint32_t)f2bf(dqacc[d][4 * r4] * g.scale) |
-              ((uint32_t)f2bf(dqacc[d][4 * r4 + 1] * g.scale) << 16);
-        w.y = (uint32_t)f2bf(dqacc[d][4 * r4 + 2] * g.scale) |
-              ((uint32_t)f2bf(dqacc[d][4 * r4 + 3] * g.scale) << 16);
-        *reinterpret_cast<uint2*>(orow + dd) = w;
-      }
-  }
+  // the loop's last barrier (or colsum_atomic's) freed the staging buffers
+  store_rows_lds<DH, STR>(dqacc, g.scale, smem + wave * 32 * STR, dqkv + (int64_t)b * dq_s_b + h * DH,
+                          dq_s_t, q - (lane & 31), L, lane);
 }
 
 // =============================================================================== bwd: dK, dV
@@ -838,24 +870,11 @@ __global__ __launch_bounds__(NTT, DH > 128 ? 1 : 2) void attn_bwd_dkdv_kernel(Ge
     colsum_atomic<ND, NTT>(dv, drop_scale, reinterpret_cast<float*>(smem), s_wsum,
                            bgrad + 2 * D + h * DH, lane, wave);
   }
-  if (kv) {
-    bf16_t* krow_o = dqkv + (int64_t)b * dq_s_b + (int64_t)key * dq_s_t + D + h * DH;
-#pragma unroll
-    for (int d = 0; d < ND; ++d)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        const int dd = 32 * d + 8 * r4 + 4 * hh;
-        uint2 wk, wv;
-        wk.x = (uint32_t)f2bf(dk[d][4 * r4] * g.scale) | ((uint32_t)f2bf(dk[d][4 * r4 + 1] * g.scale) << 16);
-        wk.y = (uint32_t)f2bf(dk[d][4 * r4 + 2] * g.scale) | ((uint32_t)f2bf(dk[d][4 * r4 + 3] * g.scale) << 16);
-        wv.x = (uint32_t)f2bf(dv[d][4 * r4] * drop_scale) |
-               ((uint32_t)f2bf(dv[d][4 * r4 + 1] * drop_scale) << 16);
-        wv.y = (uint32_t)f2bf(dv[d][4 * r4 + 2] * drop_scale) |
-               ((uint32_t)f2bf(dv[d][4 * r4 + 3] * drop_scale) << 16);
-        *reinterpret_cast<uint2*>(krow_o + dd) = wk;
-        *reinterpret_cast<uint2*>(krow_o + D + dd) = wv;
-      }
-  }
+  bf16_t* kbase_o = dqkv + (int64_t)b * dq_s_b + D + h * DH;
+  store_rows_lds<DH, STR>(dk, g.scale, smem + wave * 32 * STR, kbase_o, dq_s_t, key - (lane & 31),
+                          L, lane);
+  store_rows_lds<DH, STR>(dv, drop_scale, smem + wave * 32 * STR, kbase_o + D, dq_s_t,
+                          key - (lane & 31), L, lane);
 }
 
 // =============================================================================== dropout bits

@@ -423,6 +423,32 @@ def check_against_floor(out, k=2.0, slack_all=1e-3, slack_min=2e-3):
     assert 1 - hmin <= k * (1 - fmin) + slack_min, (hmin, fmin)
 
 
+def check_against_floor_seeds(outs, k_loss=4.0, k_cos=2.0, slack=2e-3):
+    """Free-running bar at full depth, over seeds. There the bf16 storage noise alone (the
+    emulating oracle vs float64: the floor) moves the loss by 0.03 % .. 16 % and the global
+    gradient cosine down to 0.58 .. 0.90 depending on the seed (sequence-axis LayerNorms over
+    12 blocks amplify it; the merge indices are the HIP run's, injected), so one seed's HIP/floor
+    ratio is a ratio of two random draws. The bar compares medians over the seeds instead: HIP vs the emulating
+    oracle within k_loss x the floor's median loss deviation and k_cos x its median cosine
+    deficits (global and worst tensor). HIP carries noise sources the emulation does not
+    (MFMA accumulation order, fp32 atomics, exp2), measured at ~3x the floor's loss median
+    (octo-small-tome16 seeds 0-5: 5.4e-2 vs 1.8e-2)."""
+    import statistics as st
+
+    def med(f):
+        return st.median(f(o) for o in outs)
+    lr = med(lambda o: abs(o["loss"] / o["ref_loss"] - 1))
+    flr = med(lambda o: abs(o["floor"]["loss"] / o["floor"]["ref_loss"] - 1))
+    assert lr <= k_loss * flr + slack, (lr, flr)
+    ca = med(lambda o: 1 - o["cos_all"])
+    fca = med(lambda o: 1 - o["floor"]["cos_all"])
+    assert ca <= k_cos * fca + slack, (ca, fca)
+    cm = med(lambda o: 1 - min(o["cos"].values()))
+    fcm = med(lambda o: 1 - min(o["floor"]["cos"].values()))
+    assert cm <= k_cos * fcm + slack, (cm, fcm)
+    return dict(loss=(lr, flr), cos_all=(ca, fca), min_cos=(cm, fcm))
+
+
 def check(res, cos_min=COS_MIN, cos_all_min=COS_ALL_MIN, loss_rel=LOSS_RTOL, ratio=NORM_RATIO):
     assert abs(res["loss"] - res["ref_loss"]) <= loss_rel * abs(res["ref_loss"]), \
         (res["loss"], res["ref_loss"])

@@ -79,17 +79,30 @@ def test_t5_layerwise_full_depth(dev):
 
 
 E2E = [("octo-tiny", dict(num_blocks=2), 3, 0), ("octo-tiny", dict(num_blocks=2), 3, 1),
-       ("octo-small-tome16", dict(num_blocks=2, t5_layers=2), 2, 0),
-       ("octo-small-tome16", {}, 2, 0), ("octo-small", {}, 2, 0)]
+       ("octo-small-tome16", dict(num_blocks=2, t5_layers=2), 2, 0)]
 
 
-@pytest.mark.parametrize("name,kw,B,seed", E2E, ids=["tiny-d2-s0", "tiny-d2-s1", "small16-d2",
-                                                     "small16-full", "small-full"])
+@pytest.mark.parametrize("name,kw,B,seed", E2E, ids=["tiny-d2-s0", "tiny-d2-s1", "small16-d2"])
 def test_e2e_free_running(dev, name, kw, B, seed):
+    """Shallow free-running step: HIP vs the emulating oracle within 2x the bf16 floor."""
     cfg = _cfg(name, **kw)
     out = P.run_parity(cfg, B, seed=seed, floor=True)
     assert out["tome_layers_checked"] == (cfg.num_blocks if cfg.tome_r else 0)
     P.check_against_floor(out)
+
+
+@pytest.mark.parametrize("name", ["octo-small-tome16", "octo-small"])
+def test_e2e_free_running_full_depth(dev, name):
+    """Full depth (12 blocks, 12 T5 layers), B = 2, seeds 0-5: the median-over-seeds bar of
+    oracle/parity.check_against_floor_seeds (one seed's floor ranges over 3e-4 .. 0.16 in loss,
+    so a single-seed ratio is not a test); every layer's merge checked in situ on every seed."""
+    cfg = _cfg(name)
+    outs = []
+    for seed in range(6):
+        out = P.run_parity(cfg, 2, seed=seed, floor=True)
+        assert out["tome_layers_checked"] == (cfg.num_blocks if cfg.tome_r else 0)
+        outs.append(out)
+    print(P.check_against_floor_seeds(outs))
 
 
 def test_blockwise_base_2cam(dev):
