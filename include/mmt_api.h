@@ -159,6 +159,11 @@ typedef struct {
   int64_t ld_res;
   float alpha, beta;
   int res_dtype;              /* MMT_BF16 / MMT_F32 */
+  float* colsum;              /* [mmt_gemm_colsum_rows(...)][N] fp32 or NULL: row p = the column
+                                 sums of C rows [256 p, 256 p + 256) as stored (bf16), written
+                                 (not accumulated) — the bias gradient of the next Dense backward
+                                 (layers.py:59 colsum) without re-reading C; only where
+                                 mmt_gemm_colsum_rows is nonzero, else mmt_gemm fails */
 } mmt_epilogue_t;
 
 /* Tuning knob (benchmarks): 0 = 128x128 register-staged, double-buffered LDS; 1 = same, single
@@ -166,6 +171,9 @@ typedef struct {
  * waves; 4 = direct-to-LDS (global_load_lds) 128x128 kernel for NT; -1 = automatic (default).
  * Process-wide, not thread-safe. */
 void mmt_gemm_set_variant(int variant);
+/* Rows of the epilogue's colsum slab for this launch shape (ceil(M / 256)), 0 when the kernel the
+ * launch would use cannot write it (then take the column sums with mmt_colsum). */
+int mmt_gemm_colsum_rows(int M, int N, int K, int transA, int transB, int c_mode, int split_k);
 int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t lda, const void* B,
              int transB, int64_t ldb, void* C, int c_mode, int64_t ldc, int batch, int64_t sA,
              int64_t sB, int64_t sC, int split_k, const mmt_epilogue_t* epi, float* workspace,

@@ -21,7 +21,7 @@ class Epilogue(ctypes.Structure):
     _fields_ = [("bias", P), ("act", I), ("rng", P), ("drop_layer", U32), ("drop_site", U32),
                 ("keep_prob", F), ("drop_row_offset", L), ("gate", P), ("ld_gate", L),
                 ("gate_scale", F), ("residual", P), ("ld_res", L), ("alpha", F), ("beta", F),
-                ("res_dtype", I)]
+                ("res_dtype", I), ("colsum", P)]
 
 
 # name -> argtypes (every entry point returns int status unless listed in _VOID)
@@ -35,6 +35,7 @@ SIGNATURES: dict[str, list] = {
     "mmt_topk_gather": [P, I, I, I, I, L, L, P, L, I, P, P, P, P, L, L, P, P],
     "mmt_topk_scatter_bwd": [P, I, I, I, I, L, L, P, I, P, L, L, P],
     "mmt_gemm_set_variant": [I],
+    "mmt_gemm_colsum_rows": [I, I, I, I, I, I, I],
     "mmt_gemm": [I, I, I, P, I, L, P, I, L, P, I, L, I, L, L, L, I, P, P, L, P],
     "mmt_quant_rows_fp8": [P, L, I, I, P, L, P, P],
     "mmt_gemm_fp8": [I, I, I, P, L, P, P, L, P, P, I, L, P, P],
@@ -77,7 +78,8 @@ SIGNATURES: dict[str, list] = {
     "mmt_step_advance": [P, P],
 }
 _VOID = {"mmt_tome_set_match_path", "mmt_gemm_set_variant"}
-_RESTYPE = {"mmt_workspace_size": L}      # returns a byte count (negative: error)
+_RESTYPE = {"mmt_workspace_size": L,      # returns a byte count (negative: error)
+            "mmt_gemm_colsum_rows": I}    # returns a row count
 
 
 class MMTError(RuntimeError):

@@ -110,8 +110,10 @@ ACT_NONE, ACT_RELU = 0, 1
 
 
 def _epi(bias=None, act=ACT_NONE, rng=None, drop_layer=0, drop_site=0, keep_prob=1.0,
-         drop_row_offset=0, gate=None, gate_scale=1.0, residual=None, alpha=1.0, beta=0.0):
+         drop_row_offset=0, gate=None, gate_scale=1.0, residual=None, alpha=1.0, beta=0.0,
+         colsum=None):
     e = _C.Epilogue()
+    e.colsum = ptr(colsum)
     e.bias = ptr(bias)
     e.act = act
     e.rng = ptr(rng)
@@ -165,6 +167,12 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
     bias = epi.get("bias")
     if bias is not None and (bias.numel() != N or bias.dtype != torch.float32):
         raise ValueError("gemm bias must be fp32 [N]")
+    cs = epi.get("colsum")
+    if cs is not None:
+        rows = gemm_colsum_rows(M, N, K, trans_a, trans_b, out_mode, 1 if split_k is None else split_k)
+        if not rows or cs.dtype != torch.float32 or tuple(cs.shape) != (rows, N) or not cs.is_contiguous():
+            raise ValueError(f"gemm colsum must be fp32 ({rows}, {N}) and this launch must support it")
+        split_k = 1
     e = _epi(**epi)
     if split_k is None:
         split_k = auto_split_k(M, N, K)
@@ -175,6 +183,13 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
             b.stride(0), ptr(out), out_mode, out.stride(0), 1, 0, 0, 0, split_k,
             _C.ctypes.byref(e), ptr(ws), 0 if ws is None else ws.numel(), _C.stream_ptr())
     return out
+
+
+def gemm_colsum_rows(M: int, N: int, K: int, trans_a: bool = False, trans_b: bool = True,
+                     out_mode: int = OUT_BF16, split_k: int = 1) -> int:
+    """Rows of the (rows, N) fp32 slab a gemm(..., colsum=slab) fills with the column sums of
+    each 256-row panel of its bf16 output; 0 when that launch cannot (use colsum instead)."""
+    return _C.call("mmt_gemm_colsum_rows", M, N, K, int(trans_a), int(trans_b), out_mode, split_k)
 
 
 def quant_rows_fp8(x2d: torch.Tensor, out=None, scale=None):

@@ -174,11 +174,16 @@ class Encoder1DBlock:
         # fused with the bias gradient (column sum)
         dz2 = K.dropout_bwd(dx2f, rng, ctx.layer, DROP_MLP_OUT, kp, row_offset=ctx.sample_offset * L2,
                             colsum_out=self.mlp.dense_out.b.grad)
-        # dh gated by (h > 0): relu + hidden-dropout backward fused into the dX GEMM epilogue
+        # dh gated by (h > 0): relu + hidden-dropout backward fused into the dX GEMM epilogue,
+        # which also writes per-256-row column sums of dz1 (Dense_0's bias gradient) where the
+        # launch supports it
+        Mh = self.mlp.dense.out_f
+        rows = K.gemm_colsum_rows(B * L2, Mh, D)
+        cs = torch.empty((rows, Mh), dtype=torch.float32, device=dz2.device) if rows else None
         dz1 = self.mlp.dense_out.bwd(dz2, sv["h"], bias_grad_done=True, gate=sv["h"],
-                                     gate_scale=(1.0 / kp) if dropping else 1.0)
+                                     gate_scale=(1.0 / kp) if dropping else 1.0, colsum=cs)
         # dX of the LN-fed Dense in bf16 (the LN backward accumulates in fp32): halves its traffic
-        dy1 = self.mlp.dense.bwd(dz1, sv["y1"].view(B * L2, D))
+        dy1 = self.mlp.dense.bwd(dz1, sv["y1"].view(B * L2, D), dy_colsum=cs)
         dx1 = self.ln1.bwd(dy1.view(B, L2, D), sv["x1"], sv["mu1"], sv["rs1"], addend=dx2)
         if sv["tome"] is not None:
             s0, t, r, pos, size_in, size_out = sv["tome"][:6]

@@ -104,6 +104,7 @@ struct Epi {
   int res_f32;
   int64_t ld_res;
   float alpha, beta;
+  float* colsum;  // nt256 only: per-256-row-panel column sums of the stored (bf16) C, or null
 };
 
 // global -> registers for one 128 x 64 (K-contig) or 64 x 128 (MN-contig) operand tile.
@@ -792,7 +793,7 @@ __device__ __forceinline__ void dma16(const void* base, int64_t bytes, void* lds
 #endif
 }
 
-template <int BN, int OUT, int SHV, int NS>
+template <int BN, int OUT, int SHV, int NS, bool CS = false>
 __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
     int64_t ldb, void* __restrict__ Cv, int64_t ldc, int tiles_n, int n_tiles, int xcd_order,
@@ -810,7 +811,9 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
   constexpr int SPS = 4, NSTEPS = SH / SPS;
   static_assert(SH % SPS == 0 && SH <= E && EI % 2 == 0, "stash chunks");
   static_assert(NS == 2 || (NS == 3 && STASH && EI == 0), "3 stages only with the full stash");
+  static_assert(!CS || OUT == 0, "column sums of bf16 outputs only");
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+  __shared__ float s_cs[CS ? 4 : 1][CS ? BN : 1];  // per-wave-row column sums (CS)
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -956,6 +959,10 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
   auto epilogue = [&](int tile) {
     const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
     const int gc0 = tn * BN + wn * W + 8 * lq;
+    float cs[CS ? Q : 1];  // CS: this lane's column sums over its rows of the tile
+    if constexpr (CS)
+#pragma unroll
+      for (int j = 0; j < Q; ++j) cs[j] = 0.f;
     if (STASH) {  // store what is left of the previous stash (K-loops shorter than NSTEPS)
 #pragma unroll
       for (int j = 0; j < NSTEPS; ++j)
@@ -976,6 +983,9 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = acc[mf][(8 * c8 + e) >> 2][e & 3];
           epilogue_w<8>(epi, key, N, gr, gc0 + 32 * c8, v);
+          if constexpr (CS)  // the values as stored (bf16)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cs[8 * c8 + e] += __uint_as_float((uint32_t)f2bf(v[e]) << 16);
           if (STASH && mf * CPM + (OUT == 0 ? c8 : 2 * c8) >= EI) {
             const int ci = mf * CPM + (OUT == 0 ? c8 : 2 * c8) - EI;  // stash entry
             if (OUT == 1 && epi.beta != 0.f) {
@@ -1000,6 +1010,26 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
       }
 #pragma unroll
       for (int nf = 0; nf < NF; ++nf) acc[mf][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    if constexpr (CS) {
+      // sum over the 16 row lanes (l15) of each DPP row: xor 1, xor 2, half-row and row mirrors
+#pragma unroll
+      for (int j = 0; j < Q; ++j) {
+        float x = cs[j];
+        x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xf, 0xf, false));
+        x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xf, 0xf, false));
+        x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xf, 0xf, false));
+        x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xf, 0xf, false));
+        cs[j] = x;
+      }
+      if (l15 == 0)
+#pragma unroll
+        for (int j = 0; j < Q; ++j) s_cs[wm][wn * W + 32 * (j >> 3) + 8 * lq + (j & 7)] = cs[j];
+      // LDS only (no fence: the epilogue's global stores stay in flight)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (threadIdx.x < BN)
+        epi.colsum[(int64_t)tm * N + tn * BN + threadIdx.x] =
+            s_cs[0][threadIdx.x] + s_cs[1][threadIdx.x] + s_cs[2][threadIdx.x] + s_cs[3][threadIdx.x];
     }
   };
 
@@ -1261,7 +1291,44 @@ __global__ __launch_bounds__(256) void quant_rows_fp8_kernel(const bf16_t* __res
   }
 }
 
+int cu_count() {
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n_cu <= 0)
+      n_cu = 256;
+  }
+  return n_cu;
+}
+
+// Tile width of the persistent 256 x BN NT kernel for this launch, 0 when another kernel runs.
+int nt_bn(int M, int N, int K, int transA, int transB, int batch, int out_kind, int final_kind) {
+  if (transA || !transB || batch != 1 || out_kind == 2 || K % 64 != 0 ||
+      !(g_variant < 0 || g_variant >= 5))
+    return 0;
+  const int tm256 = (M + 255) / 256;
+  if (g_variant == 5) return N % 256 == 0 ? 256 : 0;
+  if (g_variant == 6) return N % 192 == 0 ? 192 : 0;
+  if (g_variant == 7) return N % 128 == 0 ? 128 : 0;
+  // measured (tools/gemm_bench.py --variant=5/6/7 and gpu_exp/t5g.py, graph-timed): 256-wide
+  // tiles at K <= 512 where N allows (MLP up 70656 x 1536 x 384: 125 us vs 141 at 192), 192-wide
+  // otherwise (QKV 74752 x 1152 x 384; the T5 projections 8192 x 2304 / 3072 x 768: 45.9 / 50.2 us
+  // vs 54.8 / 68.8 on the 128 x 128 kernels and 50.0 / 52.7 at 256); the narrow (N = 768 and
+  // 384) and fp32 residual-stream shapes stay on the 128 x 128 kernels, faster there
+  if (final_kind != 0 || N < 1152 || K > 768) return 0;
+  const int bn = (K <= 512 && N % 256 == 0) ? 256 : N % 192 == 0 ? 192 : N % 256 == 0 ? 256 : 0;
+  return bn && tm256 * (N / bn) >= cu_count() ? bn : 0;
+}
+
 }  // namespace
+
+extern "C" int mmt_gemm_colsum_rows(int M, int N, int K, int transA, int transB, int c_mode,
+                                    int split_k) {
+  if (M <= 0 || N <= 0 || K <= 0 || c_mode != MMT_OUT_BF16 || split_k != 1) return 0;
+  return nt_bn(M, N, K, transA, transB, 1, 0, 0) == 256 ? (M + 255) / 256 : 0;
+}
 
 extern "C" void mmt_gemm_set_variant(int v) { g_variant = v; }
 
@@ -1303,6 +1370,7 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     epi.ld_res = e->ld_res;
     epi.alpha = e->alpha;
     epi.beta = e->beta;
+    epi.colsum = e->colsum;
     MMT_CHECK_ARG((!e->gate || (e->ld_gate % 8 == 0 && (uintptr_t)e->gate % 16 == 0)) &&
                       (!e->residual || (e->ld_res % 8 == 0 && (uintptr_t)e->residual % 16 == 0)),
                   "mmt_gemm: gate/residual must be 16-byte aligned with ld % 8 == 0");
@@ -1323,31 +1391,11 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     out_kind = 2;
   }
   // Persistent 256 x BN NT kernel (variant -1 auto, 5/6/7 force BN 256/192/128)
-  if (!transA && transB && batch == 1 && out_kind != 2 && K % 64 == 0 &&
-      (g_variant < 0 || g_variant >= 5)) {
-    static int n_cu = 0;
-    if (!n_cu) {
-      int dev = 0;
-      hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-          n_cu <= 0)
-        n_cu = 256;
-    }
+  const int bn = nt_bn(M, N, K, transA, transB, batch, out_kind, final_kind);
+  if (bn) {
     static const int g_nt_xcd_order = getenv("MMT_NT_ORDER") ? atoi(getenv("MMT_NT_ORDER")) : 1;
-    const int tm256 = (M + 255) / 256;
-    int bn = 0;
-    if (g_variant == 5) bn = N % 256 == 0 ? 256 : 0;
-    else if (g_variant == 6) bn = N % 192 == 0 ? 192 : 0;
-    else if (g_variant == 7) bn = N % 128 == 0 ? 128 : 0;
-    else if (final_kind == 0 && N >= 1152 && K <= 512 && (N % 256 == 0 || N % 192 == 0) &&
-             tm256 * (N / (N % 256 == 0 ? 256 : 192)) >= n_cu)
-      // measured (tools/gemm_bench.py --variant=5/6/7, graph-timed, B = 256): 256-wide tiles
-      // where N allows (MLP up with bias+relu+dropout 153 -> 135 us, plain 145 -> 143 us), else
-      // 192 (QKV N = 1152: 111 -> 100 us); the narrow (N = 384) and fp32 residual-stream shapes
-      // stay on the 128 x 128 kernels, which are faster there, and so do the deep-K T5
-      // projections (K = 768: 2304 x 768 measured slower on the 256-row tiles)
-      bn = N % 256 == 0 ? 256 : 192;
-    if (bn) {
+    const int n_cu = cu_count();
+    {
       const int tn = N / bn, n_tiles = ((M + 255) / 256) * tn;
       const int grid = std::min(n_tiles, n_cu);
 #define GN(BNV, OUT, ST, NSV)                                                                     \
@@ -1355,7 +1403,13 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
                      (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, tn, n_tiles, g_nt_xcd_order, epi)
       // the register stash fits 2 waves/SIMD for bf16 at BN <= 192 and fp32 at BN 128;
       // BN 128 has LDS for 3 stages (DMA two K-steps ahead)
-      if (final_kind == 0) {
+      if (epi.colsum) {
+        MMT_CHECK_ARG(final_kind == 0 && bn == 256, "mmt_gemm: colsum needs the 256-wide bf16 nt path "
+                      "(mmt_gemm_colsum_rows)");
+        hipLaunchKernelGGL((gemm_nt256_kernel<256, 0, NT_SH256, 2, true>), dim3(grid), dim3(NT3), 0, s,
+                           M, N, K, (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, tn,
+                           n_tiles, g_nt_xcd_order, epi);
+      } else if (final_kind == 0) {
         if (bn == 256) GN(256, 0, NT_SH256, 2);
         else if (bn == 192) GN(192, 0, -1, 2);
         else GN(128, 0, -1, 3);
@@ -1369,6 +1423,7 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
       return MMT_OK;
     }
   }
+  MMT_CHECK_ARG(!epi.colsum, "mmt_gemm: colsum needs the 256-wide bf16 nt path (mmt_gemm_colsum_rows)");
   const int k_chunk = ((K + split_k - 1) / split_k + 63) / 64 * 64;
   if (out_kind == 2) split_k = (K + k_chunk - 1) / k_chunk;  // no empty K-splits
   const int n_work = tiles_m * tiles_n * batch * split_k;

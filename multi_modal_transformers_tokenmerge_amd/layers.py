@@ -51,12 +51,15 @@ class Dense:
                       out=out, out_mode=out_mode, **epi)
 
     def bwd(self, dy2d: torch.Tensor, x2d: torch.Tensor, need_dx: bool = True,
-            bias_grad_done: bool = False, dx_out=None, **dx_epi):
+            bias_grad_done: bool = False, dx_out=None, dy_colsum=None, **dx_epi):
+        """dy_colsum: the (panels, out) slab of per-256-row column sums of dy that the GEMM
+        producing dy wrote in its epilogue (gemm colsum=); the bias gradient then sums the slab
+        instead of re-reading dy."""
         M = dy2d.shape[0]
         K.gemm(dy2d, x2d, trans_a=True, out=self.w.grad, out_mode=K.OUT_F32_ACCUM,
                split_k=split_k_for(self.out_f, self.in_f, M))
         if self.b is not None and not bias_grad_done:
-            K.colsum(dy2d, self.b.grad)
+            K.colsum(dy_colsum if dy_colsum is not None else dy2d, self.b.grad)
         if need_dx:
             # dX = dY . W as an NT product on the transposed shadow W^T (in, out)
             return K.gemm(dy2d, self.w.bf16_t, trans_b=True, out=dx_out, **dx_epi)

@@ -95,3 +95,32 @@ def test_nt256_auto_matches_reference_path(dev):
     # identical accumulation order is not guaranteed across kernels: compare within 1 bf16 ulp
     _close_bf16(o_new, torch.relu(a.float() @ w.float().t() + bias))
     assert ((o_new.float() - o_old.float()).abs() <= o_old.float().abs() * 2 ** -7 + 1e-6).all()
+
+
+@pytest.mark.parametrize("M", [300, 70656])
+def test_nt256_colsum_slab(dev, variant, M):
+    """gemm(..., colsum=slab) on the gated dX shape (N = 1536, K = 384): the slab rows are the
+    column sums of each 256-row panel of the bf16 output exactly as stored (fp32 sums of bf16
+    values; summation order differs from torch's), the output itself unchanged."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    g = torch.Generator().manual_seed(M)
+    N, K = 1536, 384
+    a, w = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    gate = _mk((M, N), dev, g)
+    if M < 5000:  # too few tiles for the automatic choice of the 256-wide kernel: force it
+        assert Kn.gemm_colsum_rows(M, N, K) == 0
+        variant(256)
+    rows = Kn.gemm_colsum_rows(M, N, K)
+    assert rows == (M + 255) // 256
+    slab = torch.full((rows, N), float("nan"), dtype=torch.float32, device=dev)
+    out = Kn.gemm(a, w, False, True, gate=gate, gate_scale=1.25, colsum=slab)
+    plain = Kn.gemm(a, w, False, True, gate=gate, gate_scale=1.25)
+    assert torch.equal(out, plain)
+    pad = torch.zeros((rows * 256, N), dtype=torch.float64, device=dev)
+    pad[:M] = out.double()
+    want = pad.view(rows, 256, N).sum(1)
+    torch.testing.assert_close(slab.double(), want, rtol=1e-5, atol=1e-4 * want.abs().max().item())
+    # shapes the 256-wide kernel does not take report 0 rows and reject a slab
+    assert Kn.gemm_colsum_rows(M, 384, K) == 0 and Kn.gemm_colsum_rows(M, N, K, out_mode=Kn.OUT_F32) == 0
+    with pytest.raises(ValueError):
+        Kn.gemm(a, w[:384], False, True, colsum=torch.zeros((rows, 384), device=dev))
