@@ -217,11 +217,15 @@ def test_attention_bias_mode(dev):
     assert rel(o, ref) < 1e-2
 
 
-@pytest.mark.parametrize("B,L,D", [(4, 292, 384), (2, 74, 768), (3, 20, 192), (2, 1, 64)])
-def test_seqnorm(dev, B, L, D):
+@pytest.mark.parametrize("B,L,D,xdt", [(4, 292, 384, torch.bfloat16), (2, 74, 768, torch.bfloat16),
+                                        (3, 20, 192, torch.bfloat16), (2, 1, 64, torch.bfloat16),
+                                        (4, 292, 384, torch.float32), (2, 400, 384, torch.float32),
+                                        (2, 1064, 768, torch.float32)])
+def test_seqnorm(dev, B, L, D, xdt):
+    """bf16 and fp32 (the step's residual stream) inputs, L from 1 to 1064, against fp32 torch."""
     from multi_modal_transformers_tokenmerge_amd import _kernels as K
     g = torch.Generator().manual_seed(B + L + D)
-    x = (torch.randn((B, L, D), generator=g) * 2 + 0.5).bfloat16().to(dev)
+    x = (torch.randn((B, L, D), generator=g) * 2 + 0.5).to(xdt).to(dev)
     gamma = torch.randn(D, generator=g).to(dev)
     beta = torch.randn(D, generator=g).to(dev)
     y, mean, rstd = K.seqnorm_fwd(x, gamma, beta, 1e-6)
@@ -231,7 +235,7 @@ def test_seqnorm(dev, B, L, D):
     ref = (xf - mu) * (torch.rsqrt(var + 1e-6) * gamma) + beta
     assert rel(y, ref) < 1e-2
     dy = torch.randn((B, L, D), generator=g).bfloat16().to(dev)
-    add = torch.randn((B, L, D), generator=g).bfloat16().to(dev)
+    add = torch.randn((B, L, D), generator=g).to(xdt).to(dev)
     dg = torch.zeros(D, device=dev)
     db = torch.zeros(D, device=dev)
     dx = K.seqnorm_bwd(dy, x, mean, rstd, gamma, dg, db, addend=add)
