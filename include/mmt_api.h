@@ -335,6 +335,17 @@ int mmt_seq_assemble_bwd(int B, int L, int D, const int32_t* row_src, const void
                          void* dtext, int T, void* dimg, int NI, const int32_t* rtok,
                          const int32_t* ctok, const int32_t* img_rows, int Q, float* drow_emb,
                          float* dcol_emb, float* dreadout_pe, mmt_stream_t stream);
+/* The image row / column position-embedding gradients alone (drow_emb = dcol_emb = NULL above):
+ * d(row_emb)[t] += dx0[b, img_rows[j]] over the image tokens (b, j) whose row token (rtok, from
+ * mmt_patch_positions) is t, likewise columns. A patch row's tokens lie in one window of the
+ * table (patch_positions' q(ri P) .. q((ri + 1) P)), so a workgroup owns one window and keeps a
+ * register accumulator per window token: no LDS atomics (the form above: 268 -> ~40 us per step
+ * at OCTO-small B = 256). I images of Himg x Himg pixels, patch P, table Q rows per axis, dx0
+ * fp32 (B, L, D), tables fp32 (Q, D) accumulated. */
+int mmt_patch_embed_grad(int B, int L, int D, int I, int Himg, int P, int Q,
+                         const int32_t* img_rows, const void* dx0, const int32_t* rtok,
+                         const int32_t* ctok, float* drow_emb, float* dcol_emb,
+                         mmt_stream_t stream);
 /* AddPositionEmbedding standalone (tokenizers/readout/readout.py:18-33; also attention.py:71-85):
  * out (B, L, D) fp32 = x + pe[None] (x may alias out). Backward: dx = dout; d(pe) = mmt_colsum of
  * dout viewed as (B, L*D). The training step fuses this add into mmt_seq_assemble_fwd. */

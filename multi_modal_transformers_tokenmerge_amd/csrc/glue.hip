@@ -144,6 +144,77 @@ __global__ __launch_bounds__(256) void embed_grad_kernel(int B, int L, int D, in
   }
 }
 
+// Position-embedding gradients by window (mmt_patch_embed_grad). A patch in patch-row ri draws its
+// row token from the window [q(ri P), q((ri + 1) P)) of patch_positions_kernel (likewise columns),
+// so the image tokens of one patch row touch only that window's few table rows. One workgroup =
+// one window x 64 columns x a slice of the batch: each thread keeps a register accumulator per
+// window token (select + add per row, no atomics), the 32 row groups meet by shuffles and in LDS,
+// and the workgroup adds its WMAX x 64 partial table with one global atomic per entry.
+template <int WMAX>
+__global__ __launch_bounds__(256) void embed_grad_win_kernel(
+    int B, int L, int D, int I, int PPD, int Himg, int P, int Q, int splits,
+    const int32_t* __restrict__ img_rows, const float* __restrict__ dx0,
+    const int32_t* __restrict__ rtok, const int32_t* __restrict__ ctok, float* __restrict__ drow,
+    float* __restrict__ dcol) {
+  __shared__ float part[4][WMAX][EMB_COLS];
+  const int w = blockIdx.x, c0 = blockIdx.y * EMB_COLS;
+  const int z = blockIdx.z % 2, sp = blockIdx.z / 2;  // table (0 rows, 1 columns), batch slice
+  const int NP = PPD * PPD, NI = I * NP, RPS = I * PPD;  // image tokens per sample in the window
+  auto q = [&](int v) { return (int)floorf(((float)v / (float)Himg) * (float)(Q - 1)); };
+  const int ws = q(w * P), wn = max(1, q((w + 1) * P) - ws);
+  const int bper = (B + splits - 1) / splits, b0 = sp * bper, b1 = min(B, b0 + bper);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  const int col = c0 + cv * 8;
+  const int32_t* tok = z == 0 ? rtok : ctok;
+  float acc[WMAX][8];
+#pragma unroll
+  for (int t = 0; t < WMAX; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[t][e] = 0.f;
+  if (col < D && b0 < b1) {
+    const int nrows = (b1 - b0) * RPS;
+    for (int r = rg; r < nrows; r += 32) {
+      const int b = b0 + r / RPS, rem = r % RPS, i = rem / PPD, k = rem % PPD;
+      const int p = z == 0 ? k * PPD + w : w * PPD + k;  // patch_positions_kernel: ri = p % PPD
+      const int j = i * NP + p;
+      const int t = tok[(int64_t)b * NI + j] - ws;
+      const float* gp = dx0 + ((int64_t)b * L + img_rows[j]) * D + col;
+      const float4 a = *reinterpret_cast<const float4*>(gp), c = *reinterpret_cast<const float4*>(gp + 4);
+      const float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+      for (int u = 0; u < WMAX; ++u)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[u][e] += t == u ? v[e] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < WMAX; ++u)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = acc[u][e];
+      x += __shfl_xor(x, 8, 64);
+      x += __shfl_xor(x, 16, 64);
+      x += __shfl_xor(x, 32, 64);
+      acc[u][e] = x;
+    }
+  if (lane < 8)
+#pragma unroll
+    for (int u = 0; u < WMAX; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part[wave][u][cv * 8 + e] = acc[u][e];
+  __syncthreads();
+  float* table = z == 0 ? drow : dcol;
+  for (int i = threadIdx.x; i < WMAX * EMB_COLS; i += blockDim.x) {
+    const int u = i / EMB_COLS, cc = c0 + i % EMB_COLS;
+    if (u < wn && cc < D) {
+      const float val = part[0][u][i % EMB_COLS] + part[1][u][i % EMB_COLS] +
+                        part[2][u][i % EMB_COLS] + part[3][u][i % EMB_COLS];
+      if (val != 0.f) atomicAdd(table + (int64_t)(ws + u) * D + cc, val);
+    }
+  }
+}
+
 // e[b, :] = mean over the listed rows of x[b] ; written as bf16 into out (row stride ld_out)
 __global__ void rows_mean_fwd_kernel(const float* __restrict__ x, int64_t xs_b, int64_t xs_t,
                                      int D, const int32_t* __restrict__ rows, int nrows,
@@ -477,8 +548,11 @@ extern "C" int mmt_seq_assemble_bwd(int B, int L, int D, const int32_t* row_src,
                                     float* drow_emb, float* dcol_emb, float* dreadout_pe,
                                     mmt_stream_t stream) {
   MMT_CHECK_ARG(row_src && dx0 && D % 8 == 0 && B > 0 && L > 0, "mmt_seq_assemble_bwd: args");
-  MMT_CHECK_ARG(NI == 0 || (img_rows && rtok && ctok && drow_emb && dcol_emb && Q > 0 &&
-                            2 * Q * EMB_COLS * 4 <= 160 * 1024),
+  // drow_emb = dcol_emb = NULL: the image tokens' gradients only (the position-embedding
+  // gradients then come from mmt_patch_embed_grad)
+  const bool emb = drow_emb || dcol_emb;
+  MMT_CHECK_ARG(NI == 0 || !emb || (img_rows && rtok && ctok && drow_emb && dcol_emb && Q > 0 &&
+                                    2 * Q * EMB_COLS * 4 <= 160 * 1024),
                 "mmt_seq_assemble_bwd: image embedding arguments");
   const int64_t n = (int64_t)B * L * (D / 8);
   hipStream_t s = as_stream(stream);
@@ -486,7 +560,7 @@ extern "C" int mmt_seq_assemble_bwd(int B, int L, int D, const int32_t* row_src,
                      row_src, (const float*)dx0, (bf16_t*)dtext, T, (bf16_t*)dimg, NI, rtok, ctok,
                      drow_emb, dcol_emb, dreadout_pe);
   MMT_CHECK_LAUNCH("mmt_seq_assemble_bwd");
-  if (NI > 0) {
+  if (NI > 0 && emb) {
     const size_t sh = sizeof(float) * 2 * Q * EMB_COLS;
     static const bool attr_ = (hipFuncSetAttribute((const void*)embed_grad_kernel,
                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -497,6 +571,44 @@ extern "C" int mmt_seq_assemble_bwd(int B, int L, int D, const int32_t* row_src,
                        dcol_emb);
     MMT_CHECK_LAUNCH("mmt_seq_assemble_bwd(embedding grads)");
   }
+  return MMT_OK;
+}
+
+extern "C" int mmt_patch_embed_grad(int B, int L, int D, int I, int Himg, int P, int Q,
+                                    const int32_t* img_rows, const void* dx0, const int32_t* rtok,
+                                    const int32_t* ctok, float* drow_emb, float* dcol_emb,
+                                    mmt_stream_t stream) {
+  MMT_CHECK_ARG(img_rows && dx0 && rtok && ctok && drow_emb && dcol_emb && B > 0 && L > 0 &&
+                    D > 0 && D % 8 == 0 && I > 0 && P > 0 && Himg >= P && Himg % P == 0 && Q > 1,
+                "mmt_patch_embed_grad: args");
+  const int PPD = Himg / P;
+  int wmax = 1;  // widest token window (host float arithmetic = patch_positions_kernel's)
+  for (int w = 0; w < PPD; ++w) {
+    auto q = [&](int v) { return (int)floorf(((float)v / (float)Himg) * (float)(Q - 1)); };
+    wmax = std::max(wmax, q((w + 1) * P) - q(w * P));
+  }
+  hipStream_t s = as_stream(stream);
+  const int chunks = (D + EMB_COLS - 1) / EMB_COLS;
+  const int splits = std::max(1, std::min(B, 1024 / (PPD * chunks * 2)));
+  const dim3 grid(PPD, chunks, 2 * splits);
+#define EGW(WM)                                                                                   \
+  hipLaunchKernelGGL(embed_grad_win_kernel<WM>, grid, dim3(256), 0, s, B, L, D, I, PPD, Himg, P, \
+                     Q, splits, img_rows, (const float*)dx0, rtok, ctok, drow_emb, dcol_emb)
+  if (wmax <= 8) EGW(8);
+  else if (wmax <= 16) EGW(16);
+  else {  // wide windows: the LDS-atomic table kernel
+    const int NI = I * PPD * PPD;
+    MMT_CHECK_ARG(2 * Q * EMB_COLS * 4 <= 160 * 1024, "mmt_patch_embed_grad: Q too large");
+    static const bool attr_ = (hipFuncSetAttribute((const void*)embed_grad_kernel,
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   160 * 1024), true);
+    (void)attr_;
+    hipLaunchKernelGGL(embed_grad_kernel, dim3(chunks, EMB_SPLIT), dim3(256),
+                       sizeof(float) * 2 * Q * EMB_COLS, s, B, L, D, NI, Q, img_rows,
+                       (const float*)dx0, rtok, ctok, drow_emb, dcol_emb);
+  }
+#undef EGW
+  MMT_CHECK_LAUNCH("mmt_patch_embed_grad");
   return MMT_OK;
 }
 

@@ -358,10 +358,17 @@ class Octo:
         dimg = torch.empty((B, NI, D), dtype=torch.bfloat16, device=dx0.device)
         dtxt = torch.empty((B, T, D), dtype=torch.bfloat16, device=dx0.device) if self.text_proj else None
         it = self.image_tokenizer
+        # token gradients (and the readout embedding's); the image row / column position
+        # embedding gradients by token window (mmt_patch_embed_grad)
         _C.call("mmt_seq_assemble_bwd", B, self.L0, D, _C.ptr(self.row_src), _C.ptr(dx0),
                 _C.ptr(dtxt), T, _C.ptr(dimg), NI, _C.ptr(st["rt"]), _C.ptr(st["ct"]),
-                _C.ptr(self.img_rows), it.row_emb.grad.shape[0], _C.ptr(it.row_emb.grad), _C.ptr(it.col_emb.grad), _C.ptr(self.readout_pe.grad),
+                _C.ptr(self.img_rows), it.Q, None, None, _C.ptr(self.readout_pe.grad),
                 _C.stream_ptr())
+        if NI:
+            _C.call("mmt_patch_embed_grad", B, self.L0, D, self.n_images, self.cfg.image_size[0],
+                    self.cfg.patch_size, it.Q, _C.ptr(self.img_rows), _C.ptr(dx0),
+                    _C.ptr(st["rt"]), _C.ptr(st["ct"]), _C.ptr(it.row_emb.grad),
+                    _C.ptr(it.col_emb.grad), _C.stream_ptr())
         K.colsum(dx0.view(B, self.L0 * D), self.pos_embed.grad.view(-1))
         it.backward(dimg, st["img_sv"])
         if self.text_proj is not None:

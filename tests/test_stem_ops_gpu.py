@@ -131,3 +131,39 @@ def test_same_conv_im2col_col2im(dev, npatch, H, C):
     lhs = float((cols.float().cpu().double() * c.double()).sum())
     rhs = float((x.float().reshape(-1, C).double() * dx.cpu().double()).sum())
     assert abs(lhs - rhs) <= 1e-6 * max(1.0, abs(lhs)), (lhs, rhs)
+
+
+@pytest.mark.parametrize("B,I,H,P,Q,D", [(64, 1, 256, 16, 128, 384), (5, 2, 256, 16, 128, 768),
+                                         (3, 1, 128, 16, 256, 192), (4, 1, 64, 8, 256, 64)])
+def test_patch_embed_grad(dev, B, I, H, P, Q, D):
+    """Image row / column position-embedding gradients by token window (mmt_patch_embed_grad;
+    windows of 8 and 16 tokens and the wide-window fallback at 32) against a float64 index_add
+    over the training-mode tokens, and against the LDS-histogram form of mmt_seq_assemble_bwd."""
+    rng = torch.tensor([11, 3], dtype=torch.int32, device=dev)
+    rt, ct = K.patch_positions(B, I, H, P, Q, True, rng)
+    NP = (H // P) ** 2
+    NI = I * NP
+    L = NI + 7
+    g = torch.Generator().manual_seed(B + D)
+    img_rows = torch.randperm(L, generator=g)[:NI].to(torch.int32).to(dev)
+    dx0 = torch.randn((B, L, D), generator=g).to(dev)
+    drow = torch.zeros((Q, D), device=dev)
+    dcol = torch.zeros((Q, D), device=dev)
+    _C.call("mmt_patch_embed_grad", B, L, D, I, H, P, Q, _C.ptr(img_rows), _C.ptr(dx0), _C.ptr(rt),
+            _C.ptr(ct), _C.ptr(drow), _C.ptr(dcol), _C.stream_ptr())
+    rows = dx0[:, img_rows.long()].double().reshape(B * NI, D)
+    want_r = torch.zeros((Q, D), dtype=torch.float64, device=dev).index_add_(0, rt.reshape(-1).long(), rows)
+    want_c = torch.zeros((Q, D), dtype=torch.float64, device=dev).index_add_(0, ct.reshape(-1).long(), rows)
+    for got, want in ((drow, want_r), (dcol, want_c)):
+        torch.testing.assert_close(got.double(), want, rtol=1e-5, atol=1e-4)
+    # the LDS-histogram form (seq_assemble_bwd with tables) agrees
+    row_src = torch.zeros(L, dtype=torch.int32)
+    row_src[img_rows.cpu().long()] = (1 << 24) | torch.arange(NI, dtype=torch.int32)
+    row_src = row_src.to(dev)
+    dimg = torch.empty((B, NI, D), dtype=torch.bfloat16, device=dev)
+    hr, hc, pe = torch.zeros((Q, D), device=dev), torch.zeros((Q, D), device=dev), torch.zeros((1, D), device=dev)
+    _C.call("mmt_seq_assemble_bwd", B, L, D, _C.ptr(row_src), _C.ptr(dx0), None, 0, _C.ptr(dimg),
+            NI, _C.ptr(rt), _C.ptr(ct), _C.ptr(img_rows), Q, _C.ptr(hr), _C.ptr(hc), _C.ptr(pe),
+            _C.stream_ptr())
+    torch.testing.assert_close(hr, drow, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(hc, dcol, rtol=1e-5, atol=1e-4)
