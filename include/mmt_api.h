@@ -280,6 +280,13 @@ int mmt_patch_im2col(const void* img, int in_dtype, int B, int I, int Himg, int 
 /* max_pool over the `win` conv outputs of each patch (3x3 s1 VALID on the 3x3 map, :159) with
  * first-max argmax for the backward (fp32 conv [npatch][win][C] -> fp32 pooled [npatch][C]);
  * the backward scatters fp32 dpooled into the bf16 conv-output gradient G [npatch][win][C]. */
+/* The stem's input conv and pool fused (image_tokenizer.py:35-71,140-162 at its gato_resnet
+ * configuration): for every 16x16 patch of uint8 RGB images (B, I, H, H, 3), normalised as
+ * 2 * (x / 255) - 1, the 12x12 stride-2 VALID conv with w (64, 432) bf16 [out][(ky, kx, c)] plus
+ * bias, then the max over its 3x3 map: pooled (B*I*NP, 64) fp32 and the first-maximum position
+ * argmax (B*I*NP, 64) uint8 (as mmt_maxpool_patch), without the im2col matrix. */
+int mmt_stem_conv_pool(const void* img, int B, int I, int Himg, const void* w, const float* bias,
+                       float* pooled, uint8_t* argmax, mmt_stream_t stream);
 int mmt_maxpool_patch(const void* conv, int64_t npatch, int win, int C, void* pooled,
                       uint8_t* argmax, mmt_stream_t stream);
 int mmt_maxpool_patch_bwd(const void* dpooled, const uint8_t* argmax, int64_t npatch, int win,

@@ -61,6 +61,7 @@ SIGNATURES: dict[str, list] = {
     "mmt_seq_assemble_fwd": [I, I, I, P, P, I, P, I, P, P, P, P, P, P, P, P],
     "mmt_seq_assemble_bwd": [I, I, I, P, P, P, I, P, I, P, P, P, I, P, P, P, P],
     "mmt_patch_embed_grad": [I, I, I, I, I, I, I, P, P, P, P, P, P, P],
+    "mmt_stem_conv_pool": [P, I, I, I, P, P, P, P, P],
     "mmt_add_position_embedding": [P, P, P, I, I, I, P],
     "mmt_rows_mean_fwd": [P, L, L, I, I, P, I, P, L, P],
     "mmt_rows_mean_bwd": [P, L, I, I, I, P, I, P, P],

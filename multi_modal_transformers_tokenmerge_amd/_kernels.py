@@ -563,6 +563,27 @@ def groupnorm_gelu_bwd(dy, x, groups, gamma, beta, mean, rstd, dgamma, dbeta, dx
     return dx
 
 
+def stem_conv_pool(images: torch.Tensor, w: torch.Tensor, bias: torch.Tensor):
+    """images (B, I, H, H, 3) uint8, w (64, 432) bf16 [out][(ky, kx, c)], bias fp32 (64,) ->
+    (pooled (B*I*NP, 64) fp32, argmax (B*I*NP, 64) uint8): 12x12 s2 conv of each normalised
+    16x16 patch + bias, max over its 3x3 map (first maximum)."""
+    _dev(images, w, bias)
+    if images.dtype != torch.uint8 or images.dim() != 5 or images.shape[-1] != 3 or \
+            images.shape[2] != images.shape[3] or images.shape[2] % 16 or not images.is_contiguous():
+        raise ValueError("stem_conv_pool takes contiguous uint8 (B, I, H, H, 3) images, H % 16 == 0")
+    if w.dtype != torch.bfloat16 or tuple(w.shape) != (64, 432) or not w.is_contiguous():
+        raise ValueError("stem_conv_pool weight must be contiguous bf16 (64, 432)")
+    if bias.dtype != torch.float32 or bias.numel() != 64:
+        raise ValueError("stem_conv_pool bias must be fp32 (64,)")
+    B, I, H = images.shape[:3]
+    n = B * I * (H // 16) ** 2
+    pooled = torch.empty((n, 64), dtype=torch.float32, device=images.device)
+    arg = torch.empty((n, 64), dtype=torch.uint8, device=images.device)
+    _C.call("mmt_stem_conv_pool", ptr(images), B, I, H, ptr(w), ptr(bias), ptr(pooled), ptr(arg),
+            _C.stream_ptr())
+    return pooled, arg
+
+
 def patch_positions(B: int, I: int, H: int, patch: int, Q: int, train: bool, rng=None, site: int = 0,
                     sample_offset: int = 0, device=None):
     npatch = (H // patch) ** 2

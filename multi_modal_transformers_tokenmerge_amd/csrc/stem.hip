@@ -9,6 +9,8 @@
 // (C / G) channels of a sample (flax GroupNorm reduces every non-batch axis).
 #include <math.h>
 
+#include <algorithm>
+
 #include "common.h"
 
 using namespace mmt;
@@ -132,6 +134,100 @@ __global__ __launch_bounds__(256) void patch_im2col_lds_kernel(
       w[q] = h2[0] | (h2[1] << 16);
     }
     *reinterpret_cast<uint4*>(obase + (int64_t)r * K + k0) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// ---------------------------------------------------------------- fused stem conv + max-pool
+// The 12x12 stride-2 VALID conv of the 64-channel stem on 16x16 RGB uint8 patches, then the 3x3
+// max-pool over its 3x3 map, without the im2col matrix: a tile is 16 consecutive patches of one
+// patch row (12 KB of the image), normalised once into LDS as bf16 (patch-local rows of 56
+// elements, 48 used; patch stride 902 elements = 3 banks mod 64, so the 16 patches x 4 k-groups
+// of an A-fragment read hit at most 2 lanes per bank). K = 432 = 12 ky x 36 (kx, c) is padded to
+// 12 x 40 (weights zero in the pad) so an 8-element k-chunk never crosses a kernel row. Wave w
+// owns channels 16w .. 16w+15 with its weight fragments in registers for the whole launch; rows of
+// the 16x16x32 MFMA are the 16 patches, one accumulator per conv position, so the max-pool is a
+// register max over the 9 accumulators (first maximum, as maxpool_patch_kernel).
+constexpr int SCP_RB = 56, SCP_PS = 902, SCP_KS = 15;  // row / patch stride (elements), k-steps
+__global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
+    const uint8_t* __restrict__ img, int64_t s_img, int Himg, int64_t n_tiles,
+    const bf16_t* __restrict__ w, const float* __restrict__ bias, float* __restrict__ pooled,
+    uint8_t* __restrict__ arg) {
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  typedef float floatx4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) bf16_t pix[16 * SCP_PS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l15 = lane & 15, lg = lane >> 4;
+  const int PPD = Himg / 16, G16 = (PPD + 15) / 16, NP = PPD * PPD;
+  for (int i = threadIdx.x; i < 16 * SCP_PS; i += 256) pix[i] = 0;  // pads stay zero
+  // weight fragments: column n = 16 wave + l15, k' = 32 ks + 8 lg + j -> (ky, e) = (k' / 40, k' % 40)
+  bf16x8 bf[SCP_KS];
+  const int n = 16 * wave + l15;
+#pragma unroll
+  for (int ks = 0; ks < SCP_KS; ++ks) {
+    const int kc = 32 * ks + 8 * lg, ky = kc / 40, e0 = kc % 40;
+    short v8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v8[j] = e0 + j < 36 ? (short)w[n * 432 + ky * 36 + e0 + j] : (short)0;
+    bf[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<short __attribute__((ext_vector_type(8)))*>(v8));
+  }
+  const float bn = bias[n];
+  // A-fragment word offsets of this lane (patch l15, k-group lg) per k-step, without the position
+  int aoff[SCP_KS];
+#pragma unroll
+  for (int ks = 0; ks < SCP_KS; ++ks) {
+    const int kc = 32 * ks + 8 * lg, ky = kc / 40, e0 = kc % 40;
+    aoff[ks] = l15 * SCP_PS + ky * SCP_RB + e0;
+  }
+  for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    const int64_t bi = t / (PPD * G16);
+    const int rem = (int)(t - bi * PPD * G16), py = rem / G16, px0 = (rem - py * G16) * 16;
+    const int np = min(16, PPD - px0);
+    __syncthreads();  // the previous tile's fragment reads are done
+    // 16 pixel rows x np*48 bytes as dwords, normalised (image_tokenizer.py:67-68 order)
+    const int wpr = np * 12;  // dwords per pixel row of the tile
+    const uint8_t* src = img + bi * s_img + ((int64_t)py * 16 * Himg + px0 * 16) * 3;
+    for (int i = threadIdx.x; i < 16 * wpr; i += 256) {
+      const int y = i / wpr, xw = i - y * wpr;
+      const uint32_t u = *reinterpret_cast<const uint32_t*>(src + (int64_t)y * Himg * 3 + xw * 4);
+      const int byte0 = xw * 4, pl = byte0 / 48, off = byte0 - pl * 48;  // 48 = 16 px x 3
+      bf16_t* d = pix + pl * SCP_PS + y * SCP_RB + off;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q] = f2bf(normalize_px((float)((u >> (8 * q)) & 0xffu), 1.f));
+    }
+    __syncthreads();
+    floatx4 acc[9];
+#pragma unroll
+    for (int pos = 0; pos < 9; ++pos) acc[pos] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < SCP_KS; ++ks)
+#pragma unroll
+      for (int pos = 0; pos < 9; ++pos) {
+        const int oy = pos / 3, ox = pos % 3;
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(pix + aoff[ks] + oy * 2 * SCP_RB + ox * 6);
+        const uint32_t a4[4] = {q[0], q[1], q[2], q[3]};
+        const bf16x8 af = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(a4));
+        acc[pos] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[ks], acc[pos], 0, 0, 0);
+      }
+    // lane holds patches 4 lg + r, channel n: conv + bias, max over the 9 positions
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int pl = 4 * lg + r;
+      float best = acc[0][r] + bn;
+      int bpos = 0;
+#pragma unroll
+      for (int pos = 1; pos < 9; ++pos) {
+        const float v = acc[pos][r] + bn;
+        if (v > best) {
+          best = v;
+          bpos = pos;
+        }
+      }
+      if (pl < np) {
+        const int64_t pimg = bi * NP + (int64_t)py * PPD + px0 + pl;
+        pooled[pimg * 64 + n] = best;
+        arg[pimg * 64 + n] = (uint8_t)bpos;
+      }
+    }
   }
 }
 
@@ -668,6 +764,21 @@ extern "C" int mmt_patch_im2col(const void* img, int in_dtype, int B, int I, int
   else
     MMT_CHECK_ARG(false, "mmt_patch_im2col: dtype must be fp32 (0) or uint8 (2)");
   MMT_CHECK_LAUNCH("mmt_patch_im2col");
+  return MMT_OK;
+}
+
+extern "C" int mmt_stem_conv_pool(const void* img, int B, int I, int Himg, const void* w,
+                                  const float* bias, float* pooled, uint8_t* argmax,
+                                  mmt_stream_t stream) {
+  MMT_CHECK_ARG(img && w && bias && pooled && argmax && B > 0 && I > 0 && Himg >= 16 &&
+                    Himg % 16 == 0, "mmt_stem_conv_pool: args");
+  const int PPD = Himg / 16;
+  const int64_t n_tiles = (int64_t)B * I * PPD * ((PPD + 15) / 16);
+  const int grid = (int)std::min<int64_t>(n_tiles, 2 * 256);
+  hipLaunchKernelGGL(stem_conv_pool_kernel, dim3(grid), dim3(256), 0, as_stream(stream),
+                     (const uint8_t*)img, (int64_t)Himg * Himg * 3, Himg, n_tiles,
+                     (const bf16_t*)w, bias, pooled, argmax);
+  MMT_CHECK_LAUNCH("mmt_stem_conv_pool");
   return MMT_OK;
 }
 

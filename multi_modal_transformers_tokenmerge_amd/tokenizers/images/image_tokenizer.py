@@ -88,14 +88,24 @@ class ResNetV2Block:
         self.out = Dense(store, f"{name}/Dense_0", flat, embedding_dim,
                          kernel_init=he_normal((flat, embedding_dim)))
 
-    def forward(self, A: torch.Tensor, B: int, R: int):
-        """A: im2col rows (B*R*win, K_in). Returns tokens (B*R, D) bf16 and the saved state."""
+    def fused_ok(self, images: torch.Tensor, patch_size: int, normalize: bool) -> bool:
+        """The 64-channel 12x12 s2 conv + 3x3 pool on 16x16 uint8 RGB patches runs as one kernel
+        (csrc/stem.hip stem_conv_pool_kernel) without an im2col matrix."""
+        return (images.dtype == torch.uint8 and images.shape[-1] == 3 and patch_size == 16 and
+                normalize and (self.kh, self.kw, self.stride, self.kp, self.C) == (12, 12, 2, 3, 64))
+
+    def forward(self, A, B: int, R: int, images=None):
+        """A: im2col rows (B*R*win, K_in), or None with `images` (B, I, H, W, 3) uint8 for the
+        fused conv + pool (fused_ok). Returns tokens (B*R, D) bf16 and the saved state."""
         if self.general:
             return self._forward_general(A, B, R)
         # pre-normalisation tensors are fp32 (GroupNorm spans all patches of a sample: same
         # conditioning argument as the sequence LayerNorm, csrc/norm.hip)
-        conv = self.conv.fwd(A, out_mode=K.OUT_F32)               # (B*R*win, C)
-        pooled, arg = K.maxpool_patch(conv, self.win)             # (B*R, C) fp32
+        if A is None:
+            pooled, arg = K.stem_conv_pool(images, self.conv.w.bf16, self.conv.b.data)
+        else:
+            conv = self.conv.fwd(A, out_mode=K.OUT_F32)           # (B*R*win, C)
+            pooled, arg = K.maxpool_patch(conv, self.win)         # (B*R, C) fp32
         hs, zs, stats = [], [], []
         z = pooled
         for i in range(self.num_blocks):
@@ -109,7 +119,8 @@ class ResNetV2Block:
             z = zn
         r16 = K.cast_f32_bf16(z, torch.empty(z.shape, dtype=torch.bfloat16, device=z.device))
         tok = self.out.fwd(r16)                                   # (B*R, D)
-        return tok, dict(A=A, arg=arg, pooled=pooled, hs=hs, zs=zs, stats=stats, r=r16, B=B, R=R)
+        return tok, dict(A=A, images=images, arg=arg, pooled=pooled, hs=hs, zs=zs, stats=stats,
+                         r=r16, B=B, R=R)
 
     def backward(self, dtok: torch.Tensor, sv: dict):
         if self.general:
@@ -131,7 +142,10 @@ class ResNetV2Block:
                                           rs, g.grad, b.grad).view(B * R, self.C)
         G = K.maxpool_patch_bwd(dpooled, sv["arg"], self.win)    # (B*R*win, C)
         K.colsum(dpooled, self.conv.b.grad)                      # bias added before the max
-        self.conv.bwd(G, sv["A"], need_dx=False, bias_grad_done=True)
+        A = sv["A"]
+        if A is None:  # fused forward: the im2col rows are built here, for the weight gradient only
+            A = K.patch_im2col(sv["images"], 16, self.kh, self.kw, self.stride, True)
+        self.conv.bwd(G, A, need_dx=False, bias_grad_done=True)
 
 
     # ---------------------------------------------------------------- general maps (patch 56)
@@ -219,9 +233,12 @@ class ImageTokenizer:
         self.check(images)
         B, I = images.shape[:2]
         rs = self.resnet
-        A = K.patch_im2col(images.contiguous(), self.patch_size, rs.kh, rs.kw, rs.stride,
-                           self.normalize)
-        tok, sv = rs.forward(A, B, I * self.num_patches)
+        images = images.contiguous()
+        if not rs.general and rs.fused_ok(images, self.patch_size, self.normalize):
+            tok, sv = rs.forward(None, B, I * self.num_patches, images=images)
+        else:
+            A = K.patch_im2col(images, self.patch_size, rs.kh, rs.kw, rs.stride, self.normalize)
+            tok, sv = rs.forward(A, B, I * self.num_patches)
         if positions is None:
             positions = K.patch_positions(B, I, self.image_size[0], self.patch_size, self.Q, train,
                                           rng=rng, site=0, sample_offset=sample_offset,

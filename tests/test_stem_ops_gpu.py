@@ -167,3 +167,26 @@ def test_patch_embed_grad(dev, B, I, H, P, Q, D):
             _C.stream_ptr())
     torch.testing.assert_close(hr, drow, rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(hc, dcol, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("B,I,H", [(3, 1, 256), (2, 2, 64), (1, 1, 512), (2, 1, 48)])
+def test_stem_conv_pool_fused(dev, B, I, H):
+    """The fused 12x12 s2 conv + 3x3 pool on uint8 patches against the im2col + GEMM +
+    maxpool_patch path on the same bf16 weights: pooled within fp32 summation-order noise, argmax
+    equal wherever the top two positions are not a near-tie."""
+    g = torch.Generator().manual_seed(B * H + I)
+    img = torch.randint(0, 256, (B, I, H, H, 3), generator=g, dtype=torch.uint8).to(dev)
+    w = (torch.randn((64, 432), generator=g) * 0.05).bfloat16().to(dev)
+    bias = (torch.randn(64, generator=g) * 0.1).to(dev)
+    pooled, arg = K.stem_conv_pool(img, w, bias)
+    A = K.patch_im2col(img, 16, 12, 12, 2, True)
+    conv = K.gemm(A, w, False, True, out_mode=K.OUT_F32, bias=bias)
+    ref_p, ref_a = K.maxpool_patch(conv, 9)
+    torch.testing.assert_close(pooled, ref_p, rtol=1e-5, atol=1e-5)
+    c = conv.view(-1, 9, 64)
+    top2 = c.topk(2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 1e-4
+    assert bool((arg[clear] == ref_a[clear]).all())
+    # exact fp64 reference of the conv on the same bf16 operands
+    want = (A.double() @ w.double().t() + bias.double()).view(-1, 9, 64).amax(1)
+    torch.testing.assert_close(pooled.double(), want, rtol=1e-5, atol=1e-5)
