@@ -287,6 +287,15 @@ int mmt_patch_im2col(const void* img, int in_dtype, int B, int I, int Himg, int 
  * argmax (B*I*NP, 64) uint8 (as mmt_maxpool_patch), without the im2col matrix. */
 int mmt_stem_conv_pool(const void* img, int B, int I, int Himg, const void* w, const float* bias,
                        float* pooled, uint8_t* argmax, mmt_stream_t stream);
+/* Its weight gradient without im2col: dw (64, 432) += sum over patches and conv positions of
+ * G^T A, G the max-pool backward of dpooled (B*I*NP, 64) fp32 at argmax (bf16-rounded, as
+ * mmt_maxpool_patch_bwd), A the normalised patch pixels: each of mmt_stem_conv_wgrad_slabs(B, I,
+ * Himg) workgroups writes its partial (64, 432) to slab row i (caller-owned fp32), which the
+ * caller sums into dw (mmt_colsum). */
+int mmt_stem_conv_wgrad_slabs(int B, int I, int Himg);
+int mmt_stem_conv_wgrad(const void* img, int B, int I, int Himg, const float* dpooled,
+                        const uint8_t* argmax, float* slab, int64_t slab_elems,
+                        mmt_stream_t stream);
 int mmt_maxpool_patch(const void* conv, int64_t npatch, int win, int C, void* pooled,
                       uint8_t* argmax, mmt_stream_t stream);
 int mmt_maxpool_patch_bwd(const void* dpooled, const uint8_t* argmax, int64_t npatch, int win,

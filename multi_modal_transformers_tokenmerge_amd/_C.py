@@ -62,6 +62,8 @@ SIGNATURES: dict[str, list] = {
     "mmt_seq_assemble_bwd": [I, I, I, P, P, P, I, P, I, P, P, P, I, P, P, P, P],
     "mmt_patch_embed_grad": [I, I, I, I, I, I, I, P, P, P, P, P, P, P],
     "mmt_stem_conv_pool": [P, I, I, I, P, P, P, P, P],
+    "mmt_stem_conv_wgrad_slabs": [I, I, I],
+    "mmt_stem_conv_wgrad": [P, I, I, I, P, P, P, L, P],
     "mmt_add_position_embedding": [P, P, P, I, I, I, P],
     "mmt_rows_mean_fwd": [P, L, L, I, I, P, I, P, L, P],
     "mmt_rows_mean_bwd": [P, L, I, I, I, P, I, P, P],
@@ -81,7 +83,8 @@ SIGNATURES: dict[str, list] = {
 }
 _VOID = {"mmt_tome_set_match_path", "mmt_gemm_set_variant"}
 _RESTYPE = {"mmt_workspace_size": L,      # returns a byte count (negative: error)
-            "mmt_gemm_colsum_rows": I}    # returns a row count
+            "mmt_gemm_colsum_rows": I,    # returns a row count
+            "mmt_stem_conv_wgrad_slabs": I}
 
 
 class MMTError(RuntimeError):

@@ -584,6 +584,27 @@ def stem_conv_pool(images: torch.Tensor, w: torch.Tensor, bias: torch.Tensor):
     return pooled, arg
 
 
+def stem_conv_wgrad(images: torch.Tensor, dpooled: torch.Tensor, arg: torch.Tensor,
+                    wgrad: torch.Tensor):
+    """wgrad (64, 432) fp32 += the stem conv weight gradient from the pooled gradient (fp32
+    (B*I*NP, 64)) and the forward's argmax, straight from the uint8 images (no im2col)."""
+    _dev(images, dpooled, arg, wgrad)
+    B, I, H = images.shape[:3]
+    n = B * I * (H // 16) ** 2
+    if tuple(dpooled.shape) != (n, 64) or dpooled.dtype != torch.float32 or not dpooled.is_contiguous():
+        raise ValueError("dpooled must be contiguous fp32 (B*I*NP, 64)")
+    if tuple(arg.shape) != (n, 64) or arg.dtype != torch.uint8 or not arg.is_contiguous():
+        raise ValueError("argmax must be contiguous uint8 (B*I*NP, 64)")
+    if tuple(wgrad.shape) != (64, 432) or wgrad.dtype != torch.float32 or not wgrad.is_contiguous():
+        raise ValueError("wgrad must be contiguous fp32 (64, 432)")
+    rows = _C.call("mmt_stem_conv_wgrad_slabs", B, I, H)
+    slab = torch.empty((rows, 64 * 432), dtype=torch.float32, device=images.device)
+    _C.call("mmt_stem_conv_wgrad", ptr(images), B, I, H, ptr(dpooled), ptr(arg), ptr(slab),
+            slab.numel(), _C.stream_ptr())
+    colsum(slab, wgrad.view(-1))
+    return wgrad
+
+
 def patch_positions(B: int, I: int, H: int, patch: int, Q: int, train: bool, rng=None, site: int = 0,
                     sample_offset: int = 0, device=None):
     npatch = (H // patch) ** 2

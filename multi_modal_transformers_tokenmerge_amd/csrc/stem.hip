@@ -231,6 +231,102 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
   }
 }
 
+// Weight gradient of the same conv without im2col: dW[n][k] = sum over patches p and positions
+// s of G[p, s, n] A[p, s, k], G the max-pool backward (dpooled[p, n] at s = argmax[p, n], else 0,
+// rounded to bf16 as maxpool_patch_bwd stores it). A tile = 16 patches of a patch row: the pixels
+// normalised into LDS patch-minor ([y][x*3 + c][patch], so 8 patches of one k are one 16-B read)
+// and G per position ([s][n][patch]); per position one 32x32x16 MFMA per (32 channels, 32 k)
+// block with the 16 patches as the reduction. Wave w owns the k-blocks w, w + 4, ... of the
+// 12 x 40 padded K; each workgroup writes its partial (64, 432) to a slab row.
+constexpr int SCW_XE = 56;  // padded elements per pixel row (48 used)
+__global__ __launch_bounds__(256, 2) void stem_conv_wgrad_kernel(
+    const uint8_t* __restrict__ img, int64_t s_img, int Himg, int64_t n_tiles,
+    const float* __restrict__ dpooled, const uint8_t* __restrict__ arg, float* __restrict__ slab) {
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  typedef float floatx16 __attribute__((ext_vector_type(16)));
+  __shared__ __attribute__((aligned(16))) bf16_t pixT[16 * SCW_XE * 16];  // [y][xe][patch]
+  __shared__ __attribute__((aligned(16))) bf16_t gt[9 * 64 * 16];         // [s][n][patch]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l31 = lane & 31, lh = lane >> 5;
+  const int PPD = Himg / 16, G16 = (PPD + 15) / 16, NP = PPD * PPD;
+  for (int i = threadIdx.x; i < 16 * SCW_XE * 16; i += 256) pixT[i] = 0;  // pads stay zero
+  floatx16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][nb][r] = 0.f;
+  // this lane's k' column of each of its k-blocks: (ky, e) of k' = 32 kb + l31
+  int kyo[4], eo[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int kp = 32 * (wave + 4 * i) + l31;
+    kyo[i] = kp / 40;
+    eo[i] = kp % 40;
+  }
+  for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    const int64_t bi = t / (PPD * G16);
+    const int rem = (int)(t - bi * PPD * G16), py = rem / G16, px0 = (rem - py * G16) * 16;
+    const int np = min(16, PPD - px0);
+    const int64_t pbase = bi * NP + (int64_t)py * PPD + px0;
+    __syncthreads();
+    const int wpr = np * 12;
+    const uint8_t* src = img + bi * s_img + ((int64_t)py * 16 * Himg + px0 * 16) * 3;
+    for (int i = threadIdx.x; i < 16 * wpr; i += 256) {
+      const int y = i / wpr, xw = i - y * wpr;
+      const uint32_t u = *reinterpret_cast<const uint32_t*>(src + (int64_t)y * Himg * 3 + xw * 4);
+      const int byte0 = xw * 4, pl = byte0 / 48, off = byte0 - pl * 48;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        pixT[(y * SCW_XE + off + q) * 16 + pl] = f2bf(normalize_px((float)((u >> (8 * q)) & 0xffu), 1.f));
+    }
+    for (int i = threadIdx.x; i < 16 * 64; i += 256) {
+      const int pl = i / 64, n = i - pl * 64;
+      float d = 0.f;
+      int a = -1;
+      if (pl < np) {
+        d = dpooled[(pbase + pl) * 64 + n];
+        a = arg[(pbase + pl) * 64 + n];
+      }
+      const bf16_t db = f2bf(d);
+#pragma unroll
+      for (int s = 0; s < 9; ++s) gt[(s * 64 + n) * 16 + pl] = s == a ? db : (bf16_t)0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      const int oy = s / 3, ox = s % 3;
+      bf16x8 af[2];
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+        af[nb] = *reinterpret_cast<const bf16x8*>(gt + (s * 64 + 32 * nb + l31) * 16 + 8 * lh);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (wave + 4 * i >= 15) continue;  // wave-uniform
+        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(
+            pixT + ((oy * 2 + kyo[i]) * SCW_XE + ox * 6 + eo[i]) * 16 + 8 * lh);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          acc[i][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[nb], bfr, acc[i][nb], 0, 0, 0);
+      }
+    }
+  }
+  float* out = slab + (int64_t)blockIdx.x * 64 * 432;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (wave + 4 * i >= 15 || eo[i] >= 36) continue;
+    const int k = kyo[i] * 36 + eo[i];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = 32 * nb + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        out[n * 432 + k] = acc[i][nb][r];
+      }
+  }
+}
+
 // max over the `win` conv positions of each patch (3x3 window on a 3x3 map -> 1x1), per channel.
 __global__ void maxpool_patch_kernel(const float* __restrict__ conv, int64_t npatch, int win,
                                      int C, float* __restrict__ pooled, uint8_t* __restrict__ arg) {
@@ -779,6 +875,27 @@ extern "C" int mmt_stem_conv_pool(const void* img, int B, int I, int Himg, const
                      (const uint8_t*)img, (int64_t)Himg * Himg * 3, Himg, n_tiles,
                      (const bf16_t*)w, bias, pooled, argmax);
   MMT_CHECK_LAUNCH("mmt_stem_conv_pool");
+  return MMT_OK;
+}
+
+extern "C" int mmt_stem_conv_wgrad_slabs(int B, int I, int Himg) {
+  if (B <= 0 || I <= 0 || Himg < 16 || Himg % 16) return 0;
+  const int PPD = Himg / 16;
+  return (int)std::min<int64_t>((int64_t)B * I * PPD * ((PPD + 15) / 16), 256);
+}
+
+extern "C" int mmt_stem_conv_wgrad(const void* img, int B, int I, int Himg, const float* dpooled,
+                                   const uint8_t* argmax, float* slab, int64_t slab_elems,
+                                   mmt_stream_t stream) {
+  const int grid = mmt_stem_conv_wgrad_slabs(B, I, Himg);
+  MMT_CHECK_ARG(img && dpooled && argmax && slab && grid > 0 && slab_elems >= (int64_t)grid * 64 * 432,
+                "mmt_stem_conv_wgrad: args (slab of mmt_stem_conv_wgrad_slabs x 64 x 432 floats)");
+  const int PPD = Himg / 16;
+  const int64_t n_tiles = (int64_t)B * I * PPD * ((PPD + 15) / 16);
+  hipLaunchKernelGGL(stem_conv_wgrad_kernel, dim3(grid), dim3(256), 0, as_stream(stream),
+                     (const uint8_t*)img, (int64_t)Himg * Himg * 3, Himg, n_tiles, dpooled, argmax,
+                     slab);
+  MMT_CHECK_LAUNCH("mmt_stem_conv_wgrad");
   return MMT_OK;
 }
 

@@ -140,12 +140,12 @@ class ResNetV2Block:
             else:
                 dz = K.groupnorm_gelu_bwd(dh.view(B, R, self.C), zin, self.G, g.data, b.data, mu,
                                           rs, g.grad, b.grad).view(B * R, self.C)
-        G = K.maxpool_patch_bwd(dpooled, sv["arg"], self.win)    # (B*R*win, C)
         K.colsum(dpooled, self.conv.b.grad)                      # bias added before the max
-        A = sv["A"]
-        if A is None:  # fused forward: the im2col rows are built here, for the weight gradient only
-            A = K.patch_im2col(sv["images"], 16, self.kh, self.kw, self.stride, True)
-        self.conv.bwd(G, A, need_dx=False, bias_grad_done=True)
+        if sv["A"] is None:  # fused forward: the weight gradient straight from the images
+            K.stem_conv_wgrad(sv["images"], dpooled, sv["arg"], self.conv.w.grad)
+            return
+        G = K.maxpool_patch_bwd(dpooled, sv["arg"], self.win)    # (B*R*win, C)
+        self.conv.bwd(G, sv["A"], need_dx=False, bias_grad_done=True)
 
 
     # ---------------------------------------------------------------- general maps (patch 56)

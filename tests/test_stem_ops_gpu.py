@@ -190,3 +190,24 @@ def test_stem_conv_pool_fused(dev, B, I, H):
     # exact fp64 reference of the conv on the same bf16 operands
     want = (A.double() @ w.double().t() + bias.double()).view(-1, 9, 64).amax(1)
     torch.testing.assert_close(pooled.double(), want, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("B,I,H", [(3, 1, 256), (2, 2, 64), (1, 1, 512), (2, 1, 48)])
+def test_stem_conv_wgrad_implicit(dev, B, I, H):
+    """Weight gradient of the fused stem conv from the pooled gradient and argmax, straight from the
+    images, against G^T . im2col in float64 (G = maxpool_patch_bwd, bf16), accumulated into an
+    existing gradient."""
+    g = torch.Generator().manual_seed(7 * B + H)
+    img = torch.randint(0, 256, (B, I, H, H, 3), generator=g, dtype=torch.uint8).to(dev)
+    w = (torch.randn((64, 432), generator=g) * 0.05).bfloat16().to(dev)
+    bias = (torch.randn(64, generator=g) * 0.1).to(dev)
+    _, arg = K.stem_conv_pool(img, w, bias)
+    n = arg.shape[0]
+    dpooled = torch.randn((n, 64), generator=g).to(dev)
+    base = torch.randn((64, 432), generator=g).to(dev)
+    wg = base.clone()
+    K.stem_conv_wgrad(img, dpooled, arg, wg)
+    G = K.maxpool_patch_bwd(dpooled, arg, 9)
+    A = K.patch_im2col(img, 16, 12, 12, 2, True)
+    want = base.double() + G.double().t() @ A.double()
+    torch.testing.assert_close(wg.double(), want, rtol=1e-4, atol=1e-3)
