@@ -148,6 +148,7 @@ __global__ __launch_bounds__(256) void patch_im2col_lds_kernel(
 // the 16x16x32 MFMA are the 16 patches, one accumulator per conv position, so the max-pool is a
 // register max over the 9 accumulators (first maximum, as maxpool_patch_kernel).
 constexpr int SCP_RB = 56, SCP_PS = 902, SCP_KS = 15;  // row / patch stride (elements), k-steps
+constexpr int STEM_PXW = 12;  // pixel dwords per thread per tile (16 rows x 16 patches x 48 B / 256)
 __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
     const uint8_t* __restrict__ img, int64_t s_img, int Himg, int64_t n_tiles,
     const bf16_t* __restrict__ w, const float* __restrict__ bias, float* __restrict__ pooled,
@@ -155,10 +156,12 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
   typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
   typedef float floatx4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) bf16_t pix[16 * SCP_PS];
+  __shared__ bf16_t lut[256];  // bf16(2 * (x / 255) - 1) per byte value
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l15 = lane & 15, lg = lane >> 4;
   const int PPD = Himg / 16, G16 = (PPD + 15) / 16, NP = PPD * PPD;
   for (int i = threadIdx.x; i < 16 * SCP_PS; i += 256) pix[i] = 0;  // pads stay zero
+  lut[threadIdx.x] = f2bf(normalize_px((float)threadIdx.x, 1.f));
   // weight fragments: column n = 16 wave + l15, k' = 32 ks + 8 lg + j -> (ky, e) = (k' / 40, k' % 40)
   bf16x8 bf[SCP_KS];
   const int n = 16 * wave + l15;
@@ -178,36 +181,65 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
     const int kc = 32 * ks + 8 * lg, ky = kc / 40, e0 = kc % 40;
     aoff[ks] = l15 * SCP_PS + ky * SCP_RB + e0;
   }
+  // The tile's 16 pixel rows x np*48 bytes as dwords (12 per thread), loaded into registers one
+  // tile ahead so the global latency hides under the previous tile's MFMAs.
+  uint32_t px[STEM_PXW];
+  auto fetch = [&](int64_t t) {
+    const int64_t bi = t / (PPD * G16);
+    const int rem = (int)(t - bi * PPD * G16), py = rem / G16, px0 = (rem - py * G16) * 16;
+    const int wpr = min(16, PPD - px0) * 12;
+    const uint8_t* src = img + bi * s_img + ((int64_t)py * 16 * Himg + px0 * 16) * 3;
+#pragma unroll
+    for (int j = 0; j < STEM_PXW; ++j) {
+      const int i = min((int)threadIdx.x + 256 * j, 16 * wpr - 1), y = i / wpr, xw = i - y * wpr;
+      px[j] = *reinterpret_cast<const uint32_t*>(src + (int64_t)y * Himg * 3 + xw * 4);
+    }
+  };
+  if (blockIdx.x < n_tiles) fetch(blockIdx.x);
   for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
     const int64_t bi = t / (PPD * G16);
     const int rem = (int)(t - bi * PPD * G16), py = rem / G16, px0 = (rem - py * G16) * 16;
     const int np = min(16, PPD - px0);
     __syncthreads();  // the previous tile's fragment reads are done
-    // 16 pixel rows x np*48 bytes as dwords, normalised (image_tokenizer.py:67-68 order)
-    const int wpr = np * 12;  // dwords per pixel row of the tile
-    const uint8_t* src = img + bi * s_img + ((int64_t)py * 16 * Himg + px0 * 16) * 3;
-    for (int i = threadIdx.x; i < 16 * wpr; i += 256) {
-      const int y = i / wpr, xw = i - y * wpr;
-      const uint32_t u = *reinterpret_cast<const uint32_t*>(src + (int64_t)y * Himg * 3 + xw * 4);
-      const int byte0 = xw * 4, pl = byte0 / 48, off = byte0 - pl * 48;  // 48 = 16 px x 3
-      bf16_t* d = pix + pl * SCP_PS + y * SCP_RB + off;
+    {  // normalise (image_tokenizer.py:67-68 order) into the patch-local LDS rows
+      const int wpr = np * 12;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) d[q] = f2bf(normalize_px((float)((u >> (8 * q)) & 0xffu), 1.f));
+      for (int j = 0; j < STEM_PXW; ++j) {
+        const int i = threadIdx.x + 256 * j;
+        if (i >= 16 * wpr) break;
+        const int y = i / wpr, xw = i - y * wpr;
+        const int byte0 = xw * 4, pl = byte0 / 48, off = byte0 - pl * 48;  // 48 = 16 px x 3
+        bf16_t* d = pix + pl * SCP_PS + y * SCP_RB + off;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = lut[(px[j] >> (8 * q)) & 0xffu];
+      }
     }
     __syncthreads();
+    if (t + gridDim.x < n_tiles) fetch(t + gridDim.x);
     floatx4 acc[9];
 #pragma unroll
     for (int pos = 0; pos < 9; ++pos) acc[pos] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // A fragments of k-step ks + 1 (all 9 positions) are read while the MFMAs of ks run
+    auto afrag = [&](int ks, int pos) {
+      const int oy = pos / 3, ox = pos % 3;
+      const uint32_t* q = reinterpret_cast<const uint32_t*>(pix + aoff[ks] + oy * 2 * SCP_RB + ox * 6);
+      const uint32_t a4[4] = {q[0], q[1], q[2], q[3]};
+      return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(a4));
+    };
+    bf16x8 acur[9], anxt[9];
 #pragma unroll
-    for (int ks = 0; ks < SCP_KS; ++ks)
+    for (int pos = 0; pos < 9; ++pos) acur[pos] = afrag(0, pos);
 #pragma unroll
-      for (int pos = 0; pos < 9; ++pos) {
-        const int oy = pos / 3, ox = pos % 3;
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(pix + aoff[ks] + oy * 2 * SCP_RB + ox * 6);
-        const uint32_t a4[4] = {q[0], q[1], q[2], q[3]};
-        const bf16x8 af = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(a4));
-        acc[pos] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[ks], acc[pos], 0, 0, 0);
-      }
+    for (int ks = 0; ks < SCP_KS; ++ks) {
+      if (ks + 1 < SCP_KS)
+#pragma unroll
+        for (int pos = 0; pos < 9; ++pos) anxt[pos] = afrag(ks + 1, pos);
+#pragma unroll
+      for (int pos = 0; pos < 9; ++pos)
+        acc[pos] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(acur[pos], bf[ks], acc[pos], 0, 0, 0);
+#pragma unroll
+      for (int pos = 0; pos < 9; ++pos) acur[pos] = anxt[pos];
+    }
     // lane holds patches 4 lg + r, channel n: conv + bias, max over the 9 positions
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -246,10 +278,12 @@ __global__ __launch_bounds__(256, 2) void stem_conv_wgrad_kernel(
   typedef float floatx16 __attribute__((ext_vector_type(16)));
   __shared__ __attribute__((aligned(16))) bf16_t pixT[16 * SCW_XE * 16];  // [y][xe][patch]
   __shared__ __attribute__((aligned(16))) bf16_t gt[9 * 64 * 16];         // [s][n][patch]
+  __shared__ bf16_t lut[256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l31 = lane & 31, lh = lane >> 5;
   const int PPD = Himg / 16, G16 = (PPD + 15) / 16, NP = PPD * PPD;
   for (int i = threadIdx.x; i < 16 * SCW_XE * 16; i += 256) pixT[i] = 0;  // pads stay zero
+  lut[threadIdx.x] = f2bf(normalize_px((float)threadIdx.x, 1.f));
   floatx16 acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -265,35 +299,58 @@ __global__ __launch_bounds__(256, 2) void stem_conv_wgrad_kernel(
     kyo[i] = kp / 40;
     eo[i] = kp % 40;
   }
+  // pixels (12 dwords per thread) and the pooled gradient / argmax of the tile (4 (patch,
+  // channel) pairs per thread) loaded into registers one tile ahead
+  uint32_t px[STEM_PXW];
+  float dq[4];
+  int aq[4];
+  auto fetch = [&](int64_t t) {
+    const int64_t bi = t / (PPD * G16);
+    const int rem = (int)(t - bi * PPD * G16), py = rem / G16, px0 = (rem - py * G16) * 16;
+    const int np = min(16, PPD - px0), wpr = np * 12;
+    const int64_t pbase = bi * NP + (int64_t)py * PPD + px0;
+    const uint8_t* src = img + bi * s_img + ((int64_t)py * 16 * Himg + px0 * 16) * 3;
+#pragma unroll
+    for (int j = 0; j < STEM_PXW; ++j) {
+      const int i = min((int)threadIdx.x + 256 * j, 16 * wpr - 1), y = i / wpr, xw = i - y * wpr;
+      px[j] = *reinterpret_cast<const uint32_t*>(src + (int64_t)y * Himg * 3 + xw * 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = threadIdx.x + 256 * j, pl = i / 64, n = i - pl * 64;
+      const int64_t e = (pbase + min(pl, np - 1)) * 64 + n;
+      dq[j] = pl < np ? dpooled[e] : 0.f;
+      aq[j] = pl < np ? (int)arg[e] : -1;
+    }
+  };
+  if (blockIdx.x < n_tiles) fetch(blockIdx.x);
   for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
     const int64_t bi = t / (PPD * G16);
     const int rem = (int)(t - bi * PPD * G16), py = rem / G16, px0 = (rem - py * G16) * 16;
     const int np = min(16, PPD - px0);
-    const int64_t pbase = bi * NP + (int64_t)py * PPD + px0;
     __syncthreads();
-    const int wpr = np * 12;
-    const uint8_t* src = img + bi * s_img + ((int64_t)py * 16 * Himg + px0 * 16) * 3;
-    for (int i = threadIdx.x; i < 16 * wpr; i += 256) {
-      const int y = i / wpr, xw = i - y * wpr;
-      const uint32_t u = *reinterpret_cast<const uint32_t*>(src + (int64_t)y * Himg * 3 + xw * 4);
-      const int byte0 = xw * 4, pl = byte0 / 48, off = byte0 - pl * 48;
+    {
+      const int wpr = np * 12;
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        pixT[(y * SCW_XE + off + q) * 16 + pl] = f2bf(normalize_px((float)((u >> (8 * q)) & 0xffu), 1.f));
-    }
-    for (int i = threadIdx.x; i < 16 * 64; i += 256) {
-      const int pl = i / 64, n = i - pl * 64;
-      float d = 0.f;
-      int a = -1;
-      if (pl < np) {
-        d = dpooled[(pbase + pl) * 64 + n];
-        a = arg[(pbase + pl) * 64 + n];
+      for (int j = 0; j < STEM_PXW; ++j) {
+        const int i = threadIdx.x + 256 * j;
+        if (i >= 16 * wpr) break;
+        const int y = i / wpr, xw = i - y * wpr;
+        const int byte0 = xw * 4, pl = byte0 / 48, off = byte0 - pl * 48;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          pixT[(y * SCW_XE + off + q) * 16 + pl] = lut[(px[j] >> (8 * q)) & 0xffu];
       }
-      const bf16_t db = f2bf(d);
 #pragma unroll
-      for (int s = 0; s < 9; ++s) gt[(s * 64 + n) * 16 + pl] = s == a ? db : (bf16_t)0;
+      for (int j = 0; j < 4; ++j) {
+        const int i = threadIdx.x + 256 * j, pl = i / 64, n = i - pl * 64;
+        const bf16_t db = f2bf(dq[j]);
+#pragma unroll
+        for (int s = 0; s < 9; ++s) gt[(s * 64 + n) * 16 + pl] = s == aq[j] ? db : (bf16_t)0;
+      }
     }
     __syncthreads();
+    if (t + gridDim.x < n_tiles) fetch(t + gridDim.x);
 #pragma unroll
     for (int s = 0; s < 9; ++s) {
       const int oy = s / 3, ox = s % 3;
