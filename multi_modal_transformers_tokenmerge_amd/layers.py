@@ -9,6 +9,7 @@ sums for biases) and returns the input gradient.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -16,6 +17,38 @@ from . import _kernels as K
 from .params import ParamStore, const, he_normal, normal
 
 DROP_ATTN, DROP_ATTN_OUT, DROP_MLP_HIDDEN, DROP_MLP_OUT = 0, 1, 2, 3  # dropout "sites" per layer
+
+
+class wgrad_overlap:
+    """Within this context every Dense.bwd issues its weight-gradient GEMM (and bias column sum)
+    on a second HIP stream, forked from the main stream at the call, so the MFMA-bound dW
+    products run beside the latency- and memory-bound kernels of the backward's critical path
+    (attention backward, LayerNorm backward, ToMe unmerge). The operands stay referenced until
+    the join on exit (main waits for the stream), so the allocator cannot hand their memory to
+    the main stream early; the join also precedes any all-reduce of the gradients. Works the
+    same under HIP-graph capture (fork / join by events)."""
+    _streams: dict = {}
+    active = None  # (stream, keep-alive list)
+
+    def __init__(self, device):
+        key = torch.device(device).index
+        if key not in wgrad_overlap._streams:
+            wgrad_overlap._streams[key] = torch.cuda.Stream(device=device)
+        self.stream = wgrad_overlap._streams[key]
+
+    enabled = os.environ.get("MMT_WGRAD_OVERLAP", "1") != "0"  # benchmarking knob
+
+    def __enter__(self):
+        if wgrad_overlap.enabled:
+            wgrad_overlap.active = (self.stream, [])
+        return self
+
+    def __exit__(self, *exc):
+        if wgrad_overlap.active is not None:
+            torch.cuda.current_stream().wait_stream(self.stream)
+            wgrad_overlap.active[1].clear()
+            wgrad_overlap.active = None
+        return False
 
 
 def split_k_for(n_out: int, k_out: int, m_red: int) -> int:
@@ -56,10 +89,20 @@ class Dense:
         producing dy wrote in its epilogue (gemm colsum=); the bias gradient then sums the slab
         instead of re-reading dy."""
         M = dy2d.shape[0]
-        K.gemm(dy2d, x2d, trans_a=True, out=self.w.grad, out_mode=K.OUT_F32_ACCUM,
-               split_k=split_k_for(self.out_f, self.in_f, M))
-        if self.b is not None and not bias_grad_done:
-            K.colsum(dy_colsum if dy_colsum is not None else dy2d, self.b.grad)
+
+        def wgrad():
+            K.gemm(dy2d, x2d, trans_a=True, out=self.w.grad, out_mode=K.OUT_F32_ACCUM,
+                   split_k=split_k_for(self.out_f, self.in_f, M))
+            if self.b is not None and not bias_grad_done:
+                K.colsum(dy_colsum if dy_colsum is not None else dy2d, self.b.grad)
+        if wgrad_overlap.active is not None:
+            side, keep = wgrad_overlap.active
+            side.wait_stream(torch.cuda.current_stream())
+            keep.extend((dy2d, x2d, dy_colsum))
+            with torch.cuda.stream(side):
+                wgrad()
+        else:
+            wgrad()
         if need_dx:
             # dX = dY . W as an NT product on the transposed shadow W^T (in, out)
             return K.gemm(dy2d, self.w.bf16_t, trans_b=True, out=dx_out, **dx_epi)

@@ -28,7 +28,7 @@ from ...action_heads.categorical import CategoricalActionHead
 from ...action_heads.continuous import ContinuousActionHead
 from ...action_heads.diffusion import DiffusionActionHead
 from ...attention_blocks.attention import LayerCtx, StackedEncoder1DBlock
-from ...layers import Dense
+from ...layers import Dense, wgrad_overlap
 from ...params import ParamStore, he_normal, normal
 from ...tokenizers.images.image_tokenizer import ImageTokenizer
 from ...tokenizers.readout.readout import AddPositionEmbedding
@@ -317,14 +317,16 @@ class Octo:
         """Stage `stage` of a backward split into n_stages block ranges (the heads run in stage
         0, the stem / embeddings in the last): backward(st) == all stages in order."""
         b = self._stage_bounds(n_stages)
-        if stage == 0:
-            st["_dx"] = self._backward_head(st)
-        dx = self.stack.backward(st["_dx"], st["stack_sv"], st["ctxs"], lo=b[stage + 1], hi=b[stage])
-        if stage == n_stages - 1:
-            self._backward_tokens(st, dx)
-            st.pop("_dx", None)
-        else:
-            st["_dx"] = dx
+        with wgrad_overlap(self.device):  # dW products beside the critical path; joined here
+            if stage == 0:
+                st["_dx"] = self._backward_head(st)
+            dx = self.stack.backward(st["_dx"], st["stack_sv"], st["ctxs"], lo=b[stage + 1],
+                                     hi=b[stage])
+            if stage == n_stages - 1:
+                self._backward_tokens(st, dx)
+                st.pop("_dx", None)
+            else:
+                st["_dx"] = dx
 
     def backward(self, st: Dict):
         """Reverse schedule of compute_diffusion_denoise_loss / compute_l2_loss / compute_ce_loss;
