@@ -90,6 +90,17 @@ void mmt_tome_set_match_path(int use_mfma);
  * none either: argmax/argsort):  g_in[row] = g_out[pos(row)] * size_in[row] / size_out[pos(row)]
  * for set rows, plain copy for the others.  pos_map comes from the forward. size_in and size_out
  * may both be NULL: the bare merge(x, "sum") closure, whose Jacobian is a 0/1 gather. */
+/* mmt_tome_merge_wavg_fwd fused with the sequence-axis LayerNorm forward that follows it in the
+ * block (attention.py:66; mmt_seqnorm_fwd semantics): fp32 x, merged rows x_out (bit-identical to
+ * the unfused merge), size_out / pos_map as there, y = LN(x_out) bf16 with mean / rstd (B, D)
+ * (bit-identical to mmt_seqnorm_fwd on x_out). L - r <= 512, D % 8 == 0. */
+int mmt_tome_merge_seqnorm_fwd(const float* x, int n, int L, int D, int64_t x_s_n, int64_t x_s_t,
+                               int set_start, int t, int r, int flags, const float* size_in,
+                               const int32_t* unm_idx, const int32_t* src_idx,
+                               const int32_t* dst_idx, float* x_out, int64_t o_s_n, int64_t o_s_t,
+                               float* size_out, int32_t* pos_map, const float* gamma,
+                               const float* beta, float eps, void* y, int64_t y_s_n, int64_t y_s_t,
+                               float* mean, float* rstd, mmt_stream_t stream);
 int mmt_tome_merge_wavg_bwd(const void* g_out, int dtype, int n, int L, int D, int64_t go_s_n,
                             int64_t go_s_t, int set_start, int t, int r, const float* size_in,
                             const float* size_out, const int32_t* pos_map, void* g_in,

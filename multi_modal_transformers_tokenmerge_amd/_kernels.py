@@ -90,6 +90,36 @@ def tome_merge_fwd(x: torch.Tensor, set_start: int, t: int, r: int, unm, src, ds
     return out, size_out, pos_map
 
 
+def tome_merge_seqnorm_fwd(x: torch.Tensor, set_start: int, t: int, r: int, unm, src, dst,
+                           gamma: torch.Tensor, beta: torch.Tensor, eps: float,
+                           size_in: torch.Tensor | None = None, flags: int = 0):
+    """tome_merge_fwd (fp32 x) followed by seqnorm_fwd in one launch: returns (x_out, size_out,
+    pos_map, y bf16, mean, rstd), each bit-identical to the two-launch form."""
+    _dev(x, size_in, unm, src, dst, gamma, beta)
+    n, L, D = x.shape
+    if x.dtype != torch.float32 or x.stride(2) != 1:
+        raise ValueError("tome_merge_seqnorm_fwd takes an fp32 (n, L, D) sequence, unit stride along D")
+    if not (0 <= set_start and set_start + t <= L) or L - r > 512:
+        raise ValueError("token set out of range or sequence too long for the fused form")
+    for a, shape in ((unm, (n, (t + 1) // 2 - r)), (src, (n, r)), (dst, (n, r))):
+        if tuple(a.shape) != shape or a.dtype != torch.int32 or not a.is_contiguous():
+            raise ValueError(f"index tensor must be contiguous int32 {shape}")
+    if size_in is not None and (tuple(size_in.shape) != (n, t) or size_in.dtype != torch.float32
+                                or not size_in.is_contiguous()):
+        raise ValueError("size_in must be contiguous fp32 (n, t)")
+    out = torch.empty((n, L - r, D), dtype=torch.float32, device=x.device)
+    size_out = torch.empty((n, t - r), dtype=torch.float32, device=x.device)
+    pos_map = torch.empty((n, t), dtype=torch.int32, device=x.device)
+    y = torch.empty((n, L - r, D), dtype=torch.bfloat16, device=x.device)
+    mean = torch.empty((n, D), dtype=torch.float32, device=x.device)
+    rstd = torch.empty((n, D), dtype=torch.float32, device=x.device)
+    _C.call("mmt_tome_merge_seqnorm_fwd", ptr(x), n, L, D, x.stride(0), x.stride(1), set_start, t,
+            r, flags, ptr(size_in), ptr(unm), ptr(src), ptr(dst), ptr(out), out.stride(0),
+            out.stride(1), ptr(size_out), ptr(pos_map), ptr(gamma), ptr(beta), eps, ptr(y),
+            y.stride(0), y.stride(1), ptr(mean), ptr(rstd), _C.stream_ptr())
+    return out, size_out, pos_map, y, mean, rstd
+
+
 def tome_merge_bwd(g_out: torch.Tensor, set_start: int, t: int, r: int, pos_map: torch.Tensor,
                    size_in: torch.Tensor | None, size_out: torch.Tensor | None,
                    out: torch.Tensor | None = None):

@@ -146,15 +146,23 @@ class Encoder1DBlock:
         x1 = x1.view(B, Lo, D)
         tome = None
         new_size = size
+        ln1_done = None
         if ctx.r > 0:
             main.wait_stream(side)
             unm, src, dst = tome_idx
-            x1, new_size, pos = K.tome_merge_fwd(x1, s0, t, ctx.r, unm, src, dst, size_in=size)
+            if x1.dtype == torch.float32 and Lo - ctx.r <= 512:
+                # merge + LayerNorm_1 in one pass over the fp32 sequence (bit-identical outputs)
+                x1, new_size, pos, y1, mu1, rs1 = K.tome_merge_seqnorm_fwd(
+                    x1, s0, t, ctx.r, unm, src, dst, self.ln1.scale.data, self.ln1.bias.data,
+                    self.ln1.eps, size_in=size)
+                ln1_done = (y1, mu1, rs1)
+            else:
+                x1, new_size, pos = K.tome_merge_fwd(x1, s0, t, ctx.r, unm, src, dst, size_in=size)
             tome = (s0, t, ctx.r, pos, size, new_size, unm, src, dst)
         elif bits_ready is not None:
             main.wait_stream(side)
         L2 = x1.shape[1]
-        y1, mu1, rs1 = self.ln1.fwd(x1)
+        y1, mu1, rs1 = ln1_done if ln1_done is not None else self.ln1.fwd(x1)
         h = self.mlp.dense.fwd(y1.view(B * L2, D), act=K.ACT_RELU, **drop(DROP_MLP_HIDDEN, L2))
         x2 = self.mlp.dense_out.fwd(h, residual=x1.view(B * L2, D), out_mode=K.OUT_F32,
                                     **drop(DROP_MLP_OUT, L2))

@@ -826,6 +826,212 @@ static int check_vec(int dtype, int D, int64_t a, int64_t b, int64_t c2, int64_t
   return D % V == 0 && a % V == 0 && b % V == 0 && c2 % V == 0 && d % V == 0;
 }
 
+// ToMe merge fused with the following sequence-axis LayerNorm forward (attention.py:66 after
+// tome_attention.py:249-256): one workgroup = one sample x 64 columns. The output rows' sources
+// are resolved once per workgroup (as phase 1 of tome_merge_fwd_kernel, for all Lout rows);
+// pass 1 merges its columns with the merge kernel's exact arithmetic (this file is compiled
+// without FMA contraction: bit-identical merged rows), stores them and accumulates the LN sums;
+// pass 2 re-reads the just-written rows and writes y (bf16). Saves the LN's separate read of the
+// merged sequence and a launch. fp32 residual stream, Lout <= kFusedRows.
+constexpr int kFusedRows = 512, kFRG = 32;
+__global__ __launch_bounds__(256) void tome_merge_seqnorm_fwd_kernel(
+    const float* __restrict__ x, int L, int D, int64_t xs_n, int64_t xs_t, int set_start, int t,
+    int r, int flags, const float* __restrict__ size_in, const int32_t* __restrict__ unm_g,
+    const int32_t* __restrict__ src_g, const int32_t* __restrict__ dst_g, float* __restrict__ out,
+    int64_t os_n, int64_t os_t, float* __restrict__ size_out, int32_t* __restrict__ pos_map,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+    bf16_t* __restrict__ y, int64_t ys_n, int64_t ys_t, float* __restrict__ mean_out,
+    float* __restrict__ rstd_out) {
+  __shared__ int32_t s_unm[1024];
+  __shared__ int32_t s_src[512];
+  __shared__ int32_t s_dst[512];
+  __shared__ int32_t m_prim[kFusedRows], m_cnt[kFusedRows], m_j[kFusedRows];
+  __shared__ float m_sp[kFusedRows], m_S[kFusedRows];
+  __shared__ int32_t m_list[kFusedRows][kMergeSeg];
+  __shared__ float m_ss[kFusedRows][kMergeSeg];
+  __shared__ float red[2 * kFRG * 64];
+  __shared__ float s_mul[64], s_add[64];
+  const int n = blockIdx.x, c0 = blockIdx.y * 64;
+  const int ta = (t + 1) / 2, nu = ta - r;
+  const bool dis = flags & MMT_TOME_DISTILL_TOKEN;
+  const bool plain = flags & MMT_TOME_PLAIN_SUM;
+  const bool scatter = !(flags & MMT_TOME_NO_SCATTER);
+  const bool lead = blockIdx.y == 0;  // writes the sizes and the position map
+  for (int k = threadIdx.x; k < nu; k += blockDim.x) s_unm[k] = unm_g[(int64_t)n * nu + k];
+  for (int k = threadIdx.x; k < r; k += blockDim.x) {
+    s_src[k] = src_g[(int64_t)n * r + k];
+    s_dst[k] = dst_g[(int64_t)n * r + k];
+  }
+  __syncthreads();
+  const float* sb = size_in ? size_in + (int64_t)n * t : nullptr;
+  const int Lout = L - r;
+  for (int o = threadIdx.x; o < Lout; o += blockDim.x) {  // phase 1 (tome_merge_fwd_kernel)
+    if (o < set_start || o >= set_start + t - r) {
+      m_prim[o] = o < set_start ? o : o + r;
+      m_j[o] = -2;
+      m_cnt[o] = 0;
+    } else {
+      const int q = o - set_start;
+      int tok, j;
+      merged_row_source(q, ta, r, dis, s_unm, &tok, &j);
+      m_prim[o] = set_start + tok;
+      m_sp[o] = (sb && !plain) ? sb[tok] : 1.f;
+      float S = sb ? sb[tok] : 1.f;
+      int cnt = 0;
+      if (j >= 0 && scatter) {
+        for (int i = 0; i < r; ++i) {
+          if (s_dst[i] != j) continue;
+          const int st = 2 * s_src[i];
+          S = S + (sb ? sb[st] : 1.f);
+          if (cnt < kMergeSeg) {
+            m_list[o][cnt] = set_start + st;
+            m_ss[o][cnt] = (sb && !plain) ? sb[st] : 1.f;
+          }
+          ++cnt;
+        }
+      }
+      m_j[o] = (j >= 0 && scatter) ? j : -1;
+      m_cnt[o] = cnt;
+      m_S[o] = S;
+      if (lead && size_out) size_out[(int64_t)n * (t - r) + q] = S;
+      if (lead && pos_map) {
+        int32_t* pm = pos_map + (int64_t)n * t;
+        pm[tok] = q;
+        if (j >= 0 && scatter)
+          for (int i = 0; i < r; ++i)
+            if (s_dst[i] == j) pm[2 * s_src[i]] = q;
+      }
+    }
+  }
+  __syncthreads();
+  // pass 1: 8 column vectors x 32 row groups, 8 columns per thread (as seqnorm_fwd_kernel)
+  const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  const int col = c0 + cv * 8;
+  const bool cok = col < D;
+  const float* xb = x + (int64_t)n * xs_n + col;
+  float* ob = out + (int64_t)n * os_n + col;
+  float part[2][8] = {};
+  if (cok)
+    for (int o = rg; o < Lout; o += kFRG) {
+      float v[8];
+      Vec<float>::load(xb + (int64_t)m_prim[o] * xs_t, v);
+      Vec<float>::load(xb + (int64_t)m_prim[o] * xs_t + 4, v + 4);
+      const int jr = m_j[o];
+      if (jr != -2) {
+        const float sp = m_sp[o];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = v[e] * sp;
+        const int cnt = m_cnt[o];
+        if (cnt <= kMergeSeg) {
+          for (int k = 0; k < cnt; ++k) {
+            float w[8];
+            Vec<float>::load(xb + (int64_t)m_list[o][k] * xs_t, w);
+            Vec<float>::load(xb + (int64_t)m_list[o][k] * xs_t + 4, w + 4);
+            const float ss = m_ss[o][k];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = v[e] + w[e] * ss;
+          }
+        } else {
+          for (int i = 0; i < r; ++i) {
+            if (s_dst[i] != jr) continue;
+            const int st = 2 * s_src[i];
+            const float ss = (sb && !plain) ? sb[st] : 1.f;
+            float w[8];
+            Vec<float>::load(xb + (int64_t)(set_start + st) * xs_t, w);
+            Vec<float>::load(xb + (int64_t)(set_start + st) * xs_t + 4, w + 4);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = v[e] + w[e] * ss;
+          }
+        }
+        if (!plain) {
+          const float S = m_S[o];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = __fdiv_rn(v[e], S);
+        }
+      }
+      Vec<float>::store(ob + (int64_t)o * os_t, v);
+      Vec<float>::store(ob + (int64_t)o * os_t + 4, v + 4);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        part[0][e] += v[e];
+        part[1][e] = __builtin_fmaf(v[e], v[e], part[1][e]);
+      }
+    }
+#pragma unroll
+  for (int vv = 0; vv < 2; ++vv)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[(vv * kFRG + rg) * 64 + cv * 8 + e] = part[vv][e];
+  __syncthreads();
+  if (threadIdx.x < 64 && c0 + threadIdx.x < D) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int g = 0; g < kFRG; ++g) {
+      s1 += red[g * 64 + threadIdx.x];
+      s2 += red[(kFRG + g) * 64 + threadIdx.x];
+    }
+    const int c = c0 + threadIdx.x;
+    // the arithmetic of seqnorm_fwd_kernel as compiled there (norm.hip contracts to these fmas):
+    // bit-identical statistics and outputs to merge followed by mmt_seqnorm_fwd
+    const float mu = s1 / Lout;
+    const float var = fmaxf(0.f, __builtin_fmaf(-mu, mu, s2 / Lout));
+    const float rs = rsqrtf(var + eps);
+    const float mul = rs * gamma[c];
+    s_mul[threadIdx.x] = mul;
+    s_add[threadIdx.x] = __builtin_fmaf(-mu, mul, beta[c]);
+    mean_out[(int64_t)n * D + c] = mu;
+    rstd_out[(int64_t)n * D + c] = rs;
+  }
+  __syncthreads();
+  if (!cok) return;
+  float mul[8], add[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mul[e] = s_mul[cv * 8 + e];
+    add[e] = s_add[cv * 8 + e];
+  }
+  bf16_t* yb = y + (int64_t)n * ys_n + col;
+  for (int o = rg; o < Lout; o += kFRG) {
+    float f[8];
+    Vec<float>::load(ob + (int64_t)o * os_t, f);
+    Vec<float>::load(ob + (int64_t)o * os_t + 4, f + 4);
+    uint32_t wds[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float a = __builtin_fmaf(f[2 * q], mul[2 * q], add[2 * q]);
+      const float b = __builtin_fmaf(f[2 * q + 1], mul[2 * q + 1], add[2 * q + 1]);
+      wds[q] = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+    }
+    *reinterpret_cast<uint4*>(yb + (int64_t)o * ys_t) = make_uint4(wds[0], wds[1], wds[2], wds[3]);
+  }
+}
+
+extern "C" int mmt_tome_merge_seqnorm_fwd(const float* x, int n, int L, int D, int64_t x_s_n,
+                                          int64_t x_s_t, int set_start, int t, int r, int flags,
+                                          const float* size_in, const int32_t* unm_idx,
+                                          const int32_t* src_idx, const int32_t* dst_idx,
+                                          float* x_out, int64_t o_s_n, int64_t o_s_t,
+                                          float* size_out, int32_t* pos_map, const float* gamma,
+                                          const float* beta, float eps, void* y, int64_t y_s_n,
+                                          int64_t y_s_t, float* mean, float* rstd,
+                                          mmt_stream_t stream) {
+  MMT_CHECK_ARG(x && x_out && unm_idx && src_idx && dst_idx && gamma && beta && y && mean && rstd,
+                "mmt_tome_merge_seqnorm_fwd: null pointer");
+  MMT_CHECK_ARG(n > 0 && L > 0 && D > 0 && D % 8 == 0 && t >= 2 && set_start >= 0 &&
+                    set_start + t <= L && L - r <= kFusedRows,
+                "mmt_tome_merge_seqnorm_fwd: bad shape (L - r <= %d)", kFusedRows);
+  MMT_CHECK_ARG(r > 0 && r <= t / 2 && (t + 1) / 2 - r <= 1024 && r <= 512,
+                "mmt_tome_merge_seqnorm_fwd: bad r=%d for t=%d", r, t);
+  MMT_CHECK_ARG(x_s_t % 8 == 0 && x_s_n % 8 == 0 && o_s_t % 8 == 0 && o_s_n % 8 == 0 &&
+                    y_s_t % 8 == 0 && y_s_n % 8 == 0,
+                "mmt_tome_merge_seqnorm_fwd: strides must be multiples of 8");
+  dim3 grid(n, (D + 63) / 64);
+  hipLaunchKernelGGL(tome_merge_seqnorm_fwd_kernel, grid, dim3(256), 0, as_stream(stream), x, L, D,
+                     x_s_n, x_s_t, set_start, t, r, flags, size_in, unm_idx, src_idx, dst_idx,
+                     x_out, o_s_n, o_s_t, size_out, pos_map, gamma, beta, eps, (bf16_t*)y, y_s_n,
+                     y_s_t, mean, rstd);
+  MMT_CHECK_LAUNCH("mmt_tome_merge_seqnorm_fwd");
+  return MMT_OK;
+}
+
 extern "C" int mmt_tome_merge_wavg_fwd(const void* x, int dtype, int n, int L, int D, int64_t x_s_n,
                                        int64_t x_s_t, int set_start, int t, int r, int flags,
                                        const float* size_in, const int32_t* unm_idx,

@@ -142,3 +142,25 @@ def test_reference_api_merge_wavg_autograd(dev):
     np.testing.assert_allclose(x.grad.cpu().numpy(), xc.grad.numpy(), rtol=1e-5, atol=1e-6)
     # r = 0: reference returns the do_nothing pair
     assert bipartite_soft_matching(metric[:, :1], 3) == (do_nothing, do_nothing)
+
+
+@pytest.mark.parametrize("n,L,D,s0,t,r,sized", [(3, 292, 384, 32, 256, 16, False),
+                                                (2, 276, 384, 32, 240, 16, True),
+                                                (2, 40, 64, 4, 33, 16, True)])
+def test_merge_seqnorm_fused_bit_exact(dev, n, L, D, s0, t, r, sized):
+    """The fused ToMe merge + sequence LayerNorm forward equals the merge kernel followed by
+    mmt_seqnorm_fwd bit for bit: merged rows, sizes, position map, y, mean and rstd."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    g = torch.Generator().manual_seed(n * L + t)
+    x = (torch.randn((n, L, D), generator=g) * 3 + 1).to(dev)
+    metric = torch.randn((n, t, 64), generator=g).bfloat16().to(dev)
+    unm, src, dst = K.tome_match(metric, r)
+    size = (torch.rand((n, t), generator=g) * 3 + 1).to(dev) if sized else None
+    gamma = torch.randn(D, generator=g).to(dev)
+    beta = torch.randn(D, generator=g).to(dev)
+    a_x, a_s, a_p = K.tome_merge_fwd(x, s0, t, r, unm, src, dst, size_in=size)
+    a_y, a_m, a_r = K.seqnorm_fwd(a_x, gamma, beta, 1e-6)
+    b_x, b_s, b_p, b_y, b_m, b_r = K.tome_merge_seqnorm_fwd(x, s0, t, r, unm, src, dst, gamma,
+                                                            beta, 1e-6, size_in=size)
+    for a, b in ((a_x, b_x), (a_s, b_s), (a_p, b_p), (a_y, b_y), (a_m, b_m), (a_r, b_r)):
+        assert torch.equal(a, b)
