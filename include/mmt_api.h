@@ -90,6 +90,20 @@ void mmt_tome_set_match_path(int use_mfma);
  * none either: argmax/argsort):  g_in[row] = g_out[pos(row)] * size_in[row] / size_out[pos(row)]
  * for set rows, plain copy for the others.  pos_map comes from the forward. size_in and size_out
  * may both be NULL: the bare merge(x, "sum") closure, whose Jacobian is a 0/1 gather. */
+/* The backward of the same pair plus the attention-output dropout, fused: mmt_seqnorm_bwd over the
+ * merged sequence (dy bf16, x and addend fp32, L2 = L - r rows), then mmt_tome_merge_wavg_bwd
+ * (pos_map, size_in, size_out) into g_in (B, L, D) fp32, then mmt_dropout_bwd (layer, site,
+ * keep_prob, row_offset; rng NULL = no dropout) of g_in into z bf16 with its column sums added
+ * to bias_grad. The merged gradient stays in LDS. L <= 512, L2 * 256 B <= 96 KB. */
+int mmt_ln_unmerge_dropout_bwd(const void* dy, int64_t ds_b, int64_t ds_t, const float* x,
+                               int64_t xs_b, int64_t xs_t, int B, int L2, int D, const float* mean,
+                               const float* rstd, const float* gamma, const float* addend,
+                               int64_t as_b, int64_t as_t, float* dgamma, float* dbeta, int L,
+                               int set_start, int t, int r, const float* size_in,
+                               const float* size_out, const int32_t* pos_map, float* g_in,
+                               int64_t gs_b, int64_t gs_t, const uint32_t* rng, uint32_t layer,
+                               uint32_t site, float keep_prob, int64_t row_offset, void* z,
+                               int64_t zs_b, int64_t zs_t, float* bias_grad, mmt_stream_t stream);
 /* mmt_tome_merge_wavg_fwd fused with the sequence-axis LayerNorm forward that follows it in the
  * block (attention.py:66; mmt_seqnorm_fwd semantics): fp32 x, merged rows x_out (bit-identical to
  * the unfused merge), size_out / pos_map as there, y = LN(x_out) bf16 with mean / rstd (B, D)

@@ -464,6 +464,28 @@ def colsum(x2d: torch.Tensor, out: torch.Tensor):
     return out
 
 
+def ln_unmerge_dropout_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, addend, tome, rng, layer: int,
+                           site: int, keep_prob: float, row_offset: int, bias_grad=None):
+    """seqnorm_bwd (merged layout: dy bf16, x / addend fp32) -> tome_merge_bwd -> dropout_bwd in one
+    launch: returns (g_in fp32 (B, L, D), z bf16 (B, L, D)); dgamma / dbeta / bias_grad accumulated.
+    tome = (set_start, t, r, pos_map, size_in, size_out)."""
+    _dev(dy, x, mean, rstd, gamma, dgamma, dbeta, addend, rng, bias_grad)
+    B, L2, D = x.shape
+    s0, t, r, pos, size_in, size_out = tome
+    L = L2 + r
+    if x.dtype != torch.float32 or dy.dtype != torch.bfloat16 or (addend is not None and addend.dtype != torch.float32):
+        raise TypeError("ln_unmerge_dropout_bwd takes bf16 dy and fp32 x / addend")
+    g_in = torch.empty((B, L, D), dtype=torch.float32, device=x.device)
+    z = torch.empty((B, L, D), dtype=torch.bfloat16, device=x.device)
+    a_sb, a_st = (addend.stride(0), addend.stride(1)) if addend is not None else (0, 0)
+    _C.call("mmt_ln_unmerge_dropout_bwd", ptr(dy), dy.stride(0), dy.stride(1), ptr(x), x.stride(0),
+            x.stride(1), B, L2, D, ptr(mean), ptr(rstd), ptr(gamma), ptr(addend), a_sb, a_st,
+            ptr(dgamma), ptr(dbeta), L, s0, t, r, ptr(size_in), ptr(size_out), ptr(pos), ptr(g_in),
+            g_in.stride(0), g_in.stride(1), ptr(rng), layer, site, keep_prob, row_offset, ptr(z),
+            z.stride(0), z.stride(1), ptr(bias_grad), _C.stream_ptr())
+    return g_in, z
+
+
 def dropout_bwd(dy2d: torch.Tensor, rng, layer: int, site: int, keep_prob: float,
                 row_offset: int = 0, out: torch.Tensor | None = None, colsum_out=None):
     """dz (bf16) = dy * keep / keep_prob; rng None: plain cast. colsum_out += column sums."""

@@ -192,14 +192,23 @@ class Encoder1DBlock:
                                      gate_scale=(1.0 / kp) if dropping else 1.0, colsum=cs)
         # dX of the LN-fed Dense in bf16 (the LN backward accumulates in fp32): halves its traffic
         dy1 = self.mlp.dense.bwd(dz1, sv["y1"].view(B * L2, D), dy_colsum=cs)
-        dx1 = self.ln1.bwd(dy1.view(B, L2, D), sv["x1"], sv["mu1"], sv["rs1"], addend=dx2)
-        if sv["tome"] is not None:
-            s0, t, r, pos, size_in, size_out = sv["tome"][:6]
-            dx1 = K.tome_merge_bwd(dx1, s0, t, r, pos, size_in, size_out)
         Lo = sv["o_in"].shape[1]
-        dx1f = dx1.reshape(B * Lo, D)
-        dzo = K.dropout_bwd(dx1f, rng, ctx.layer, DROP_ATTN_OUT, kp, row_offset=ctx.sample_offset * Lo,
-                            colsum_out=self.out.b.grad)
+        if sv["tome"] is not None and Lo <= 512 and sv["x1"].dtype == torch.float32:
+            # LayerNorm_1 backward + unmerge + attention-output dropout backward in one pass (the
+            # merged-layout gradient never reaches HBM)
+            dx1, dzo = K.ln_unmerge_dropout_bwd(
+                dy1.view(B, L2, D), sv["x1"], sv["mu1"], sv["rs1"], self.ln1.scale.data,
+                self.ln1.scale.grad, self.ln1.bias.grad, dx2, sv["tome"][:6], rng, ctx.layer,
+                DROP_ATTN_OUT, kp, ctx.sample_offset * Lo, bias_grad=self.out.b.grad)
+            dzo = dzo.view(B * Lo, D)
+        else:
+            dx1 = self.ln1.bwd(dy1.view(B, L2, D), sv["x1"], sv["mu1"], sv["rs1"], addend=dx2)
+            if sv["tome"] is not None:
+                s0, t, r, pos, size_in, size_out = sv["tome"][:6]
+                dx1 = K.tome_merge_bwd(dx1, s0, t, r, pos, size_in, size_out)
+            dx1f = dx1.reshape(B * Lo, D)
+            dzo = K.dropout_bwd(dx1f, rng, ctx.layer, DROP_ATTN_OUT, kp,
+                                row_offset=ctx.sample_offset * Lo, colsum_out=self.out.b.grad)
         do = self.out.bwd(dzo, sv["o_in"].reshape(B * Lo, D), bias_grad_done=True)
         if sv["prune"] is not None:  # the top-k indices carry no gradient (lax.top_k indices)
             pidx = sv["prune"][0]

@@ -12,6 +12,8 @@
 // this architecture is large next to the per-token deviations (attention outputs are averages
 // over the sequence). The residual stream x and its gradient are therefore fp32 (x_dtype /
 // res_dtype = MMT_F32 on the training path); y is emitted in bf16 for the MFMA GEMMs.
+#include <algorithm>
+
 #include "common.h"
 
 using namespace mmt;
@@ -188,6 +190,135 @@ __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
   }
 }
 
+// LayerNorm_1 backward + ToMe unmerge + the attention-output dropout backward of one block, fused
+// (attention_blocks/attention.py backward: ln1.bwd -> tome_merge_bwd -> dropout_bwd(site 1)).
+// One workgroup = one sample x 64 columns: pass 1 as seqnorm_bwd_kernel (x1, dy1 of the merged
+// sequence; dgamma / dbeta), pass 2 computes the merged-layout input gradient (+ addend) into an
+// LDS panel instead of HBM, pass 3 walks the L unmerged rows: g_in = (g[orow] * s) / S (the merge
+// backward's arithmetic) or a copy, stored fp32, then z = keep ? g_in / keep_prob : 0 stored bf16
+// with its column sums (the out-projection bias gradient). Same expressions as the three kernels
+// (this file's compilation): bit-identical g_in, z and LN gradients; the column-sum atomics
+// differ in order only.
+constexpr int kUnmergeMax = 512;  // unmerged rows per sample of the fused form
+__global__ __launch_bounds__(NT) void ln_unmerge_dropout_bwd_kernel(
+    const bf16_t* __restrict__ dy, int64_t ds_b, int64_t ds_t, const float* __restrict__ x,
+    int64_t xs_b, int64_t xs_t, int L2, int D, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ gamma, const float* addend,
+    int64_t as_b, int64_t as_t, float* __restrict__ dgamma, float* __restrict__ dbeta, int L,
+    int set_start, int t, int r, const float* __restrict__ size_in,
+    const float* __restrict__ size_out, const int32_t* __restrict__ pos_map,
+    float* __restrict__ g_in, int64_t gs_b, int64_t gs_t, const uint32_t* __restrict__ rng,
+    uint32_t layer, uint32_t site, uint32_t thresh, float scale, int64_t row_offset,
+    bf16_t* __restrict__ z, int64_t zs_b, int64_t zs_t, float* __restrict__ bias_grad) {
+  extern __shared__ __attribute__((aligned(16))) float dyn_f[];  // [max(L2*64, 4*RG*CW)]
+  __shared__ int32_t u_orow[kUnmergeMax];
+  __shared__ float u_s[kUnmergeMax], u_S[kUnmergeMax];
+  float* red = dyn_f;
+  float* panel = dyn_f;  // reused after the reduction: merged-layout gradient [L2][64]
+  const int b = blockIdx.x, c0 = blockIdx.y * CW;
+  const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  const int col = c0 + cv * 8;
+  const bool cok = col < D;
+  for (int row = threadIdx.x; row < L; row += NT) {  // merge-backward row sources
+    if (row < set_start || row >= set_start + t) {
+      u_orow[row] = row < set_start ? row : row - r;
+      u_s[row] = -1.f;  // copy
+    } else {
+      const int tok = row - set_start;
+      const int q = pos_map[(int64_t)b * t + tok];
+      u_orow[row] = set_start + q;
+      u_s[row] = size_in ? size_in[(int64_t)b * t + tok] : 1.f;
+      u_S[row] = size_out ? size_out[(int64_t)b * (t - r) + q] : 1.f;
+    }
+  }
+  float mu[8], rs[8], ga[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mu[e] = cok ? mean[(int64_t)b * D + col + e] : 0.f;
+    rs[e] = cok ? rstd[(int64_t)b * D + col + e] : 0.f;
+    ga[e] = cok ? gamma[col + e] : 0.f;
+  }
+  const float* xb = x + (int64_t)b * xs_b + col;
+  const bf16_t* db = dy + (int64_t)b * ds_b + col;
+  float part[4][8] = {};  // pass 1 (seqnorm_bwd_kernel)
+  if (cok)
+    for (int l = rg; l < L2; l += RG) {
+      float fx[8], fd[8];
+      load8(xb + (int64_t)l * xs_t, fx);
+      load8(db + (int64_t)l * ds_t, fd);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xh = (fx[e] - mu[e]) * rs[e];
+        const float g = fd[e] * ga[e];
+        part[0][e] += g;
+        part[1][e] += g * xh;
+        part[2][e] += fd[e] * xh;
+        part[3][e] += fd[e];
+      }
+    }
+  reduce_rows<4>(part, red);
+  if (threadIdx.x < CW && c0 + threadIdx.x < D) {
+    atomicAdd(dgamma + c0 + threadIdx.x, red[2 * RG * CW + threadIdx.x]);
+    atomicAdd(dbeta + c0 + threadIdx.x, red[3 * RG * CW + threadIdx.x]);
+  }
+  float mg[8], mgx[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mg[e] = red[cv * 8 + e] / L2;
+    mgx[e] = red[RG * CW + cv * 8 + e] / L2;
+  }
+  __syncthreads();  // red is read; the panel reuses it
+  const float* ab = addend ? addend + (int64_t)b * as_b + col : nullptr;
+  if (cok)
+    for (int l = rg; l < L2; l += RG) {  // pass 2: merged-layout input gradient into LDS
+      float fx[8], fd[8], fa[8];
+      load8(xb + (int64_t)l * xs_t, fx);
+      load8(db + (int64_t)l * ds_t, fd);
+      if (ab) load8(ab + (int64_t)l * as_t, fa);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xh = (fx[e] - mu[e]) * rs[e];
+        const float g = fd[e] * ga[e];
+        fx[e] = rs[e] * (g - mg[e] - xh * mgx[e]) + (ab ? fa[e] : 0.f);
+      }
+      store8(panel + l * CW + cv * 8, fx);
+    }
+  __syncthreads();
+  // pass 3: unmerge (tome_merge_bwd_kernel), dropout backward (colsum_kernel), column sums
+  const uint32_t key = rng ? stream_key(rng[0], rng[1], layer, site) : 0u;
+  float cs[8] = {};
+  if (cok)
+    for (int row = rg; row < L; row += RG) {
+      float f[8];
+      load8(panel + u_orow[row] * CW + cv * 8, f);
+      const float sv = u_s[row];
+      if (sv >= 0.f) {
+        const float S = u_S[row];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = (f[e] * sv) / S;
+      }
+      store8(g_in + (int64_t)b * gs_b + (int64_t)row * gs_t + col, f);
+      if (rng) {
+        const int64_t m = (int64_t)b * L + row;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t ctr = (uint32_t)((row_offset + m) * (int64_t)D + col + e);
+          f[e] = keep_elem(key, ctr, thresh) ? f[e] * scale : 0.f;
+        }
+      }
+      store8(z + (int64_t)b * zs_b + (int64_t)row * zs_t + col, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs[e] += f[e];
+    }
+  __syncthreads();  // the panel is read; reduce the column sums in its place
+  float part1[1][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part1[0][e] = cs[e];
+  reduce_rows<1>(part1, red);
+  if (bias_grad && threadIdx.x < CW && c0 + threadIdx.x < D)
+    atomicAdd(bias_grad + c0 + threadIdx.x, red[threadIdx.x]);
+}
+
 // out[n] += sum_m x[m][n]  and, with z != NULL, z = x * keep / keep_prob (keep = 1 when rng is
 // NULL: a cast to bf16) written first — the dropout backward of a GEMM-epilogue dropout, whose
 // column sum is the bias gradient.
@@ -315,5 +446,37 @@ extern "C" int mmt_dropout_bwd(const void* dy, int dtype, int64_t ldy, int M, in
                        (const bf16_t*)dy, ldy, M, N, colsum, rng, layer, site, th, sc, row_offset,
                        (bf16_t*)dz, ldz);
   MMT_CHECK_LAUNCH("mmt_dropout_bwd");
+  return MMT_OK;
+}
+
+extern "C" int mmt_ln_unmerge_dropout_bwd(
+    const void* dy, int64_t ds_b, int64_t ds_t, const float* x, int64_t xs_b, int64_t xs_t, int B,
+    int L2, int D, const float* mean, const float* rstd, const float* gamma, const float* addend,
+    int64_t as_b, int64_t as_t, float* dgamma, float* dbeta, int L, int set_start, int t, int r,
+    const float* size_in, const float* size_out, const int32_t* pos_map, float* g_in, int64_t gs_b,
+    int64_t gs_t, const uint32_t* rng, uint32_t layer, uint32_t site, float keep_prob,
+    int64_t row_offset, void* z, int64_t zs_b, int64_t zs_t, float* bias_grad, mmt_stream_t stream) {
+  MMT_CHECK_ARG(dy && x && mean && rstd && gamma && dgamma && dbeta && pos_map && g_in && z,
+                "mmt_ln_unmerge_dropout_bwd: null pointer");
+  MMT_CHECK_ARG(B > 0 && L2 > 0 && D > 0 && D % 8 == 0 && L == L2 + r && r > 0 && t >= 2 &&
+                    set_start >= 0 && set_start + t <= L && L <= kUnmergeMax &&
+                    L2 * CW * 4 <= 96 * 1024,
+                "mmt_ln_unmerge_dropout_bwd: bad shape (L <= %d)", kUnmergeMax);
+  MMT_CHECK_ARG(ds_t % 8 == 0 && xs_t % 8 == 0 && gs_t % 8 == 0 && zs_t % 8 == 0 &&
+                    (!addend || as_t % 8 == 0),
+                "mmt_ln_unmerge_dropout_bwd: strides must be multiples of 8");
+  MMT_CHECK_ARG(!rng || (keep_prob > 0.f && keep_prob <= 1.f), "mmt_ln_unmerge_dropout_bwd: keep_prob");
+  const size_t dyn = sizeof(float) * (size_t)std::max(L2 * CW, 4 * RG * CW);
+  static const bool attr_ = (hipFuncSetAttribute((const void*)ln_unmerge_dropout_bwd_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 96 * 1024), true);
+  (void)attr_;
+  dim3 grid(B, (D + CW - 1) / CW);
+  hipLaunchKernelGGL(ln_unmerge_dropout_bwd_kernel, grid, dim3(NT), dyn, as_stream(stream),
+                     (const bf16_t*)dy, ds_b, ds_t, x, xs_b, xs_t, L2, D, mean, rstd, gamma, addend,
+                     as_b, as_t, dgamma, dbeta, L, set_start, t, r, size_in, size_out, pos_map,
+                     g_in, gs_b, gs_t, rng, layer, site, rng ? keep_threshold16(keep_prob) : 0u,
+                     rng ? 1.f / keep_prob : 1.f, row_offset, (bf16_t*)z, zs_b, zs_t, bias_grad);
+  MMT_CHECK_LAUNCH("mmt_ln_unmerge_dropout_bwd");
   return MMT_OK;
 }

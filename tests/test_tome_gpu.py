@@ -164,3 +164,36 @@ def test_merge_seqnorm_fused_bit_exact(dev, n, L, D, s0, t, r, sized):
                                                             beta, 1e-6, size_in=size)
     for a, b in ((a_x, b_x), (a_s, b_s), (a_p, b_p), (a_y, b_y), (a_m, b_m), (a_r, b_r)):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n,L,D,s0,t,r,drop", [(3, 292, 384, 32, 256, 16, True),
+                                               (2, 276, 384, 32, 240, 16, False),
+                                               (2, 40, 64, 4, 33, 16, True)])
+def test_ln_unmerge_dropout_bwd_fused(dev, n, L, D, s0, t, r, drop):
+    """LayerNorm backward + ToMe unmerge + dropout backward in one launch against the three
+    kernels in sequence: the unmerged gradient and the dropout output bit for bit, the LayerNorm
+    parameter gradients and the bias column sums to fp32 atomic-order rounding."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    g = torch.Generator().manual_seed(n * L + r)
+    metric = torch.randn((n, t, 64), generator=g).bfloat16().to(dev)
+    unm, src, dst = K.tome_match(metric, r)
+    size = (torch.rand((n, t), generator=g) * 3 + 1).to(dev)
+    x = (torch.randn((n, L, D), generator=g) * 2).to(dev)
+    gamma, beta = torch.randn(D, generator=g).to(dev), torch.randn(D, generator=g).to(dev)
+    x1, size_out, pos, _, mu, rs = K.tome_merge_seqnorm_fwd(x, s0, t, r, unm, src, dst, gamma, beta,
+                                                            1e-6, size_in=size)
+    L2 = L - r
+    dy = torch.randn((n, L2, D), generator=g).bfloat16().to(dev)
+    addend = torch.randn((n, L2, D), generator=g).to(dev)
+    rng = torch.tensor([5, 9], dtype=torch.int32, device=dev) if drop else None
+    grads = [torch.zeros(D, device=dev) for _ in range(6)]
+    dx = K.seqnorm_bwd(dy, x1, mu, rs, gamma, grads[0], grads[1], addend=addend)
+    a_g = K.tome_merge_bwd(dx, s0, t, r, pos, size, size_out)
+    a_z = K.dropout_bwd(a_g.reshape(n * L, D), rng, 3, 1, 0.9, row_offset=7 * L, colsum_out=grads[2])
+    b_g, b_z = K.ln_unmerge_dropout_bwd(dy, x1, mu, rs, gamma, grads[3], grads[4], addend,
+                                        (s0, t, r, pos, size, size_out), rng, 3, 1, 0.9, 7 * L,
+                                        bias_grad=grads[5])
+    assert torch.equal(a_g, b_g)
+    assert torch.equal(a_z.view(n, L, D), b_z)
+    for i in range(3):
+        torch.testing.assert_close(grads[i + 3], grads[i], rtol=1e-5, atol=1e-4)
