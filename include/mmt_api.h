@@ -281,6 +281,17 @@ int mmt_seqnorm_bwd(const void* dy, int dy_dtype, int64_t ds_b, int64_t ds_t, co
                     const float* gamma, const void* addend, int64_t as_b, int64_t as_t, void* dx,
                     int64_t dxs_b, int64_t dxs_t, float* dgamma, float* dbeta,
                     mmt_stream_t stream);
+/* mmt_seqnorm_bwd (bf16 dy, fp32 x / addend / dx) that also applies the dropout backward of the
+ * PREVIOUS block's MLP output (layer, site, keep_prob, row_offset; rng NULL = a plain cast) to
+ * the dx it writes: z (B, L, D) bf16 = keep ? dx / keep_prob : 0, colsum += its column sums (as
+ * mmt_dropout_bwd), without reading dx back. */
+int mmt_seqnorm_dropout_bwd(const void* dy, int64_t ds_b, int64_t ds_t, const float* x,
+                            int64_t xs_b, int64_t xs_t, int B, int L, int D, const float* mean,
+                            const float* rstd, const float* gamma, const float* addend,
+                            int64_t as_b, int64_t as_t, float* dx, int64_t dxs_b, int64_t dxs_t,
+                            float* dgamma, float* dbeta, const uint32_t* rng, uint32_t layer,
+                            uint32_t site, float keep_prob, int64_t row_offset, void* z,
+                            int64_t zs_b, int64_t zs_t, float* colsum, mmt_stream_t stream);
 
 /* ------------------------------------------------------------------ reductions / dropout
  * out[n] += sum_m x[m][n] (bf16 x, fp32 out): Dense bias gradients. */

@@ -32,6 +32,8 @@ SIGNATURES: dict[str, list] = {
     "mmt_tome_match": [P, I, I, I, I, I, L, L, L, I, I, P, P, P, P, P, L, P],
     "mmt_tome_merge_wavg_fwd": [P, I, I, I, I, L, L, I, I, I, I, P, P, P, P, P, L, L, P, P, P],
     "mmt_tome_merge_wavg_bwd": [P, I, I, I, I, L, L, I, I, I, P, P, P, P, L, L, P],
+    "mmt_seqnorm_dropout_bwd": [P, L, L, P, L, L, I, I, I, P, P, P, P, L, L, P, L, L, P, P, P, U32,
+                                U32, F, L, P, L, L, P, P],
     "mmt_ln_unmerge_dropout_bwd": [P, L, L, P, L, L, I, I, I, P, P, P, P, L, L, P, P, I, I, I, I, P,
                                    P, P, P, L, L, P, U32, U32, F, L, P, L, L, P, P],
     "mmt_tome_merge_seqnorm_fwd": [P, I, I, I, L, L, I, I, I, I, P, P, P, P, P, L, L, P, P, P, P, F,

@@ -464,6 +464,24 @@ def colsum(x2d: torch.Tensor, out: torch.Tensor):
     return out
 
 
+def seqnorm_dropout_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, addend, rng, layer: int,
+                        site: int, keep_prob: float, row_offset: int, colsum=None):
+    """seqnorm_bwd (bf16 dy, fp32 x / addend) returning (dx fp32, z bf16), z = the previous
+    block's dropout backward of dx (dropout_bwd semantics, colsum += its column sums)."""
+    _dev(dy, x, mean, rstd, gamma, dgamma, dbeta, addend, rng, colsum)
+    B, L, D = x.shape
+    if x.dtype != torch.float32 or dy.dtype != torch.bfloat16 or (addend is not None and addend.dtype != torch.float32):
+        raise TypeError("seqnorm_dropout_bwd takes bf16 dy and fp32 x / addend")
+    dx = torch.empty((B, L, D), dtype=torch.float32, device=x.device)
+    z = torch.empty((B, L, D), dtype=torch.bfloat16, device=x.device)
+    a_sb, a_st = (addend.stride(0), addend.stride(1)) if addend is not None else (0, 0)
+    _C.call("mmt_seqnorm_dropout_bwd", ptr(dy), dy.stride(0), dy.stride(1), ptr(x), x.stride(0),
+            x.stride(1), B, L, D, ptr(mean), ptr(rstd), ptr(gamma), ptr(addend), a_sb, a_st, ptr(dx),
+            dx.stride(0), dx.stride(1), ptr(dgamma), ptr(dbeta), ptr(rng), layer, site, keep_prob,
+            row_offset, ptr(z), z.stride(0), z.stride(1), ptr(colsum), _C.stream_ptr())
+    return dx, z
+
+
 def ln_unmerge_dropout_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, addend, tome, rng, layer: int,
                            site: int, keep_prob: float, row_offset: int, bias_grad=None):
     """seqnorm_bwd (merged layout: dy bf16, x / addend fp32) -> tome_merge_bwd -> dropout_bwd in one

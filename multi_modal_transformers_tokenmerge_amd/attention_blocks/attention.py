@@ -171,7 +171,11 @@ class Encoder1DBlock:
         return x2.view(B, L2, D), saved, new_size
 
     # ----------------------------------------------------------------------------- backward
-    def backward(self, dx2: torch.Tensor, sv: dict, ctx: LayerCtx) -> torch.Tensor:
+    def backward(self, dx2: torch.Tensor, sv: dict, ctx: LayerCtx, dz2=None, prev=None):
+        """Returns (dx, dz_prev). dz2: this block's MLP-output dropout backward of dx2, already
+        produced by the next block's LayerNorm_0 backward (with this block's Dense_1 bias
+        gradient), or None; prev = (block, saved, ctx) of the block before this one, whose
+        dropout backward this block's LayerNorm_0 backward then produces (dz_prev)."""
         B, L2, D = dx2.shape
         L = sv["x"].shape[1]
         kp, kpa, train = sv["kp"], sv["kpa"], ctx.train
@@ -180,8 +184,10 @@ class Encoder1DBlock:
         rng = ctx.rng if dropping else None
         # MLP out: x2 = x1 + drop3(h W2^T + b2); dropout backward = mask/scale + cast to bf16,
         # fused with the bias gradient (column sum)
-        dz2 = K.dropout_bwd(dx2f, rng, ctx.layer, DROP_MLP_OUT, kp, row_offset=ctx.sample_offset * L2,
-                            colsum_out=self.mlp.dense_out.b.grad)
+        if dz2 is None:
+            dz2 = K.dropout_bwd(dx2f, rng, ctx.layer, DROP_MLP_OUT, kp,
+                                row_offset=ctx.sample_offset * L2,
+                                colsum_out=self.mlp.dense_out.b.grad)
         # dh gated by (h > 0): relu + hidden-dropout backward fused into the dX GEMM epilogue,
         # which also writes per-256-row column sums of dz1 (Dense_0's bias gradient) where the
         # launch supports it
@@ -218,7 +224,16 @@ class Encoder1DBlock:
         dqkv = K.attn_bwd(sv["qkv"], sv["o"], do.view(B, L, D), sv["lse"], self.H, self.scale,
                           ctx.table, sv["bits"], kpa, bias_grad=self.qkv.b.grad)
         dy0 = self.qkv.bwd(dqkv.view(B * L, 3 * D), sv["y0"].view(B * L, D), bias_grad_done=True)
-        return self.ln0.bwd(dy0.view(B, L, D), sv["x"], sv["mu0"], sv["rs0"], addend=dx1)
+        if prev is not None and sv["x"].dtype == torch.float32 and dy0.dtype == torch.bfloat16:
+            pblk, psv, pctx = prev
+            pkp = psv["kp"]
+            prng = pctx.rng if (pctx.train and pkp < 1.0) else None
+            dx, dzp = K.seqnorm_dropout_bwd(
+                dy0.view(B, L, D), sv["x"], sv["mu0"], sv["rs0"], self.ln0.scale.data,
+                self.ln0.scale.grad, self.ln0.bias.grad, dx1, prng, pctx.layer, DROP_MLP_OUT, pkp,
+                pctx.sample_offset * L, colsum=pblk.mlp.dense_out.b.grad)
+            return dx, dzp.view(B * L, D)
+        return self.ln0.bwd(dy0.view(B, L, D), sv["x"], sv["mu0"], sv["rs0"], addend=dx1), None
 
 
 class StackedEncoder1DBlock:
@@ -244,6 +259,9 @@ class StackedEncoder1DBlock:
         """Backward through blocks hi-1 .. lo (all by default); a staged backward (gradient
         all-reduce overlapped with the remaining blocks) calls it in several ranges."""
         hi = len(self.blocks) if hi is None else hi
+        dz = None
         for i in range(hi - 1, lo - 1, -1):
-            dx = self.blocks[i].backward(dx, saved[i], ctxs[i])
+            # block i's LayerNorm_0 backward also does block i-1's MLP-output dropout backward
+            prev = (self.blocks[i - 1], saved[i - 1], ctxs[i - 1]) if i - 1 >= lo else None
+            dx, dz = self.blocks[i].backward(dx, saved[i], ctxs[i], dz2=dz, prev=prev)
         return dx

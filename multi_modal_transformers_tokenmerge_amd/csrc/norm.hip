@@ -124,13 +124,26 @@ __global__ __launch_bounds__(NT) void seqnorm_fwd_kernel(
 // dx = rstd * (g - mean_L(g) - xhat * mean_L(g * xhat)),  g = dy * gamma  (+ optional addend)
 // dgamma += sum_{b,l} dy * xhat ; dbeta += sum_{b,l} dy   (fp32 atomics, one per column per block)
 // x, addend and dx share the residual dtype TX; dy has its own (TDY).
-template <typename TDY, typename TX>
+// DZ: also the dropout backward of the block BEFORE this LayerNorm's block (its MLP-output
+// dropout, site 3, applied to this dx: z = keep ? dx / keep_prob : 0 in bf16, the colsum_kernel
+// arithmetic) with its column sums (that block's Dense_1 bias gradient), so the block-input
+// gradient is not read again by a separate dropout pass.
+struct DropZ {
+  const uint32_t* rng;
+  uint32_t layer, site, thresh;
+  float scale;
+  int64_t row_offset;
+  bf16_t* z;
+  int64_t zs_b, zs_t;
+  float* colsum;
+};
+template <typename TDY, typename TX, bool DZ = false>
 __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
     const TDY* __restrict__ dy, int64_t ds_b, int64_t ds_t, const TX* __restrict__ x,
     int64_t xs_b, int64_t xs_t, int L, int D, const float* __restrict__ mean,
     const float* __restrict__ rstd, const float* __restrict__ gamma, const TX* addend,
     int64_t as_b, int64_t as_t, TX* dx, int64_t dxs_b, int64_t dxs_t,
-    float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    float* __restrict__ dgamma, float* __restrict__ dbeta, DropZ dz = DropZ{}) {
   __shared__ float red[4 * RG * CW];
   const int b = blockIdx.x, c0 = blockIdx.y * CW;
   const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;
@@ -166,7 +179,7 @@ __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
     atomicAdd(dgamma + c0 + threadIdx.x, red[2 * RG * CW + threadIdx.x]);
     atomicAdd(dbeta + c0 + threadIdx.x, red[3 * RG * CW + threadIdx.x]);
   }
-  if (!cok) return;
+  // (threads past D skip the loop but stay for the DZ reduction's barriers)
   float mg[8], mgx[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -175,7 +188,9 @@ __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
   }
   TX* dxb = dx + (int64_t)b * dxs_b + col;
   const TX* ab = addend ? addend + (int64_t)b * as_b + col : nullptr;
-  for (int l = rg; l < L; l += RG) {
+  [[maybe_unused]] float cs[8] = {};
+  [[maybe_unused]] const uint32_t key = DZ && dz.rng ? stream_key(dz.rng[0], dz.rng[1], dz.layer, dz.site) : 0u;
+  for (int l = rg; cok && l < L; l += RG) {
     float fx[8], fd[8], fa[8];
     load8(xb + (int64_t)l * xs_t, fx);
     load8(db + (int64_t)l * ds_t, fd);
@@ -187,6 +202,31 @@ __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
       fx[e] = rs[e] * (g - mg[e] - xh * mgx[e]) + (ab ? fa[e] : 0.f);
     }
     store8(dxb + (int64_t)l * dxs_t, fx);
+    if constexpr (DZ) {
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = fx[e];  // the stored (TX) value
+      if (dz.rng) {
+        const int64_t m = (int64_t)b * L + l;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t ctr = (uint32_t)((dz.row_offset + m) * (int64_t)D + col + e);
+          f[e] = keep_elem(key, ctr, dz.thresh) ? f[e] * dz.scale : 0.f;
+        }
+      }
+      store8(dz.z + (int64_t)b * dz.zs_b + (int64_t)l * dz.zs_t + col, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs[e] += f[e];
+    }
+  }
+  if constexpr (DZ) {
+    float p1[1][8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) p1[0][e] = cs[e];
+    __syncthreads();  // every thread has read mg / mgx out of red
+    reduce_rows<1>(p1, red);
+    if (dz.colsum && threadIdx.x < CW && c0 + threadIdx.x < D)
+      atomicAdd(dz.colsum + c0 + threadIdx.x, red[threadIdx.x]);
   }
 }
 
@@ -478,5 +518,29 @@ extern "C" int mmt_ln_unmerge_dropout_bwd(
                      g_in, gs_b, gs_t, rng, layer, site, rng ? keep_threshold16(keep_prob) : 0u,
                      rng ? 1.f / keep_prob : 1.f, row_offset, (bf16_t*)z, zs_b, zs_t, bias_grad);
   MMT_CHECK_LAUNCH("mmt_ln_unmerge_dropout_bwd");
+  return MMT_OK;
+}
+
+extern "C" int mmt_seqnorm_dropout_bwd(const void* dy, int64_t ds_b, int64_t ds_t, const float* x,
+                                       int64_t xs_b, int64_t xs_t, int B, int L, int D,
+                                       const float* mean, const float* rstd, const float* gamma,
+                                       const float* addend, int64_t as_b, int64_t as_t, float* dx,
+                                       int64_t dxs_b, int64_t dxs_t, float* dgamma, float* dbeta,
+                                       const uint32_t* rng, uint32_t layer, uint32_t site,
+                                       float keep_prob, int64_t row_offset, void* z, int64_t zs_b,
+                                       int64_t zs_t, float* colsum, mmt_stream_t stream) {
+  MMT_CHECK_ARG(dy && x && mean && rstd && gamma && dx && dgamma && dbeta && z,
+                "mmt_seqnorm_dropout_bwd: null pointer");
+  MMT_CHECK_ARG(B > 0 && L > 0 && D > 0 && D % 8 == 0 && ds_t % 8 == 0 && xs_t % 8 == 0 &&
+                    dxs_t % 8 == 0 && zs_t % 8 == 0 && (!addend || as_t % 8 == 0),
+                "mmt_seqnorm_dropout_bwd: D and strides must be multiples of 8");
+  MMT_CHECK_ARG(!rng || (keep_prob > 0.f && keep_prob <= 1.f), "mmt_seqnorm_dropout_bwd: keep_prob");
+  DropZ dz{rng, layer, site, rng ? keep_threshold16(keep_prob) : 0u, rng ? 1.f / keep_prob : 1.f,
+           row_offset, (bf16_t*)z, zs_b, zs_t, colsum};
+  dim3 grid(B, (D + CW - 1) / CW);
+  hipLaunchKernelGGL((seqnorm_bwd_kernel<bf16_t, float, true>), grid, dim3(NT), 0,
+                     as_stream(stream), (const bf16_t*)dy, ds_b, ds_t, x, xs_b, xs_t, L, D, mean,
+                     rstd, gamma, addend, as_b, as_t, dx, dxs_b, dxs_t, dgamma, dbeta, dz);
+  MMT_CHECK_LAUNCH("mmt_seqnorm_dropout_bwd");
   return MMT_OK;
 }

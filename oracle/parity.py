@@ -231,7 +231,7 @@ def hip_blockwise(cfg, B, seed=0):
     douts, dins = [None] * nb, [None] * nb
     for i in reversed(range(nb)):
         douts[i] = g.cpu()
-        g = model.stack.blocks[i].backward(g, svs[i], ctxs[i])
+        g, _ = model.stack.blocks[i].backward(g, svs[i], ctxs[i])
         dins[i] = g.cpu()
     model._backward_tokens(st, g)
     torch.cuda.synchronize()

@@ -264,3 +264,28 @@ def test_colsum_and_dropout_bwd(dev):
     ref = torch.where(keep, x.float() / 0.9, torch.zeros_like(x.float()))
     assert (dz.float() - ref).abs().max().item() <= 2 ** -7 * ref.abs().max().item()
     torch.testing.assert_close(cs, ref.sum(0), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("B,L,D,drop", [(4, 292, 384, True), (2, 276, 384, False),
+                                         (2, 1064, 768, True), (3, 20, 192, True)])
+def test_seqnorm_dropout_bwd_fused(dev, B, L, D, drop):
+    """LayerNorm_0 backward fused with the previous block's MLP-output dropout backward, against
+    seqnorm_bwd then dropout_bwd: dx and the dropout output bit for bit, the LayerNorm parameter
+    gradients and the bias column sums to fp32 atomic-order rounding."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    g = torch.Generator().manual_seed(B * L + D)
+    x = (torch.randn((B, L, D), generator=g) * 2 + 0.5).to(dev)
+    gamma, beta = torch.randn(D, generator=g).to(dev), torch.randn(D, generator=g).to(dev)
+    _, mean, rstd = K.seqnorm_fwd(x, gamma, beta, 1e-6)
+    dy = torch.randn((B, L, D), generator=g).bfloat16().to(dev)
+    add = torch.randn((B, L, D), generator=g).to(dev)
+    rng = torch.tensor([5, 9], dtype=torch.int32, device=dev) if drop else None
+    grads = [torch.zeros(D, device=dev) for _ in range(6)]
+    a_x = K.seqnorm_bwd(dy, x, mean, rstd, gamma, grads[0], grads[1], addend=add)
+    a_z = K.dropout_bwd(a_x.reshape(B * L, D), rng, 4, 3, 0.9, row_offset=5 * L, colsum_out=grads[2])
+    b_x, b_z = K.seqnorm_dropout_bwd(dy, x, mean, rstd, gamma, grads[3], grads[4], add, rng, 4, 3,
+                                     0.9, 5 * L, colsum=grads[5])
+    assert torch.equal(a_x, b_x)
+    assert torch.equal(a_z.view(B, L, D), b_z)
+    for i in range(3):
+        torch.testing.assert_close(grads[i + 3], grads[i], rtol=1e-5, atol=1e-4)
