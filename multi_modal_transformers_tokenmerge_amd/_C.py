@@ -104,7 +104,9 @@ def lib():
             raise ImportError(f"{_LIB_PATH} is missing: build it with "
                               "`python -m multi_modal_transformers_tokenmerge_amd.csrc.build` "
                               "(no CPU fallback exists by design)")
-        h = ctypes.CDLL(str(_LIB_PATH))
+        import os
+        # benchmarking knob: A/B a second build of the same C ABI (never set on the product path)
+        h = ctypes.CDLL(os.environ.get("MMT_LIB_AB") or str(_LIB_PATH))
         h.mmt_last_error.restype = ctypes.c_char_p
         h.mmt_last_error.argtypes = []
         for name, args in SIGNATURES.items():
@@ -112,7 +114,6 @@ def lib():
             fn.argtypes = args
             fn.restype = None if name in _VOID else _RESTYPE.get(name, I)
         _lib = h
-        import os
         if os.environ.get("MMT_GEMM_VARIANT"):  # benchmarking knob (include/mmt_api.h)
             h.mmt_gemm_set_variant(int(os.environ["MMT_GEMM_VARIANT"]))
     return _lib

@@ -584,8 +584,37 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_glds_nt_kernel(
   float* Ct = reinterpret_cast<float*>(smem);
   const int c8 = (threadIdx.x & 15) * 8;
   const int gc = w.n0 + c8;
+  // Every global operand of the epilogue (bias, gate, residual, the old C of C += ...) is loaded
+  // before the first store of its half: one in-order vmcnt retires loads and stores together, so
+  // a load issued behind stores waits for all of them. alpha, bias, relu, gate and the residual
+  // are applied here, dropout through epilogue_w with the rest of epi: epilogue_w's order.
+  constexpr int RPT = 64 / (NTHREADS / 16);  // rows per thread per half
+  const int gcl = min(gc, N - 8);            // clamped: unpredicated loads keep vmcnt exact
+  float bias_r[8];
+  if (epi.bias) ldw<8>(epi.bias + gcl, bias_r);
+  Epi rest = epi;
+  rest.alpha = 1.f;
+  rest.bias = nullptr;
+  rest.act = MMT_ACT_NONE;
+  rest.gate = nullptr;
+  rest.residual = nullptr;
+  const bool old_c = OUT == 1 && epi.beta != 0.f;
 #pragma unroll 1
   for (int hf = 0; hf < 2; ++hf) {
+    float res_r[RPT][8], c_r[RPT][8];
+    uint4 gate_r[RPT];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int gr = min(w.m0 + hf * 64 + (threadIdx.x >> 4) + i * (NTHREADS / 16), M - 1);
+      if (epi.residual) {
+        const int64_t ro = (int64_t)gr * epi.ld_res + gcl;
+        if (epi.res_f32) ldw<8>(reinterpret_cast<const float*>(epi.residual) + ro, res_r[i]);
+        else ldw<8>(reinterpret_cast<const bf16_t*>(epi.residual) + ro, res_r[i]);
+      }
+      if (epi.gate)
+        gate_r[i] = *reinterpret_cast<const uint4*>(epi.gate + (int64_t)gr * epi.ld_gate + gcl);
+      if (old_c) ldw<8>(reinterpret_cast<const float*>(Cv) + w.bz * sC + (int64_t)gr * ldc + gcl, c_r[i]);
+    }
     __syncthreads();
     if (wm == hf) {
 #pragma unroll
@@ -601,14 +630,38 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_glds_nt_kernel(
     }
     __syncthreads();
     if (gc >= N) continue;
-#pragma unroll 2
-    for (int r = threadIdx.x >> 4; r < 64; r += NTHREADS / 16) {
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int r = (threadIdx.x >> 4) + i * (NTHREADS / 16);
       const int gr = w.m0 + hf * 64 + r;
       if (gr >= M) break;
       float v[8];
       ldw<8>(Ct + r * CTS + c8, v);
-      epilogue_w<8>(epi, key, N, gr, gc, v);
-      store_w<OUT, 8>(Cv, w.bz * sC + (int64_t)gr * ldc + gc, epi.beta, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= epi.alpha;
+      if (epi.bias)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bias_r[e];
+      if (epi.act == MMT_ACT_RELU)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      if (epi.gate) {
+        const uint32_t gw[4] = {gate_r[i].x, gate_r[i].y, gate_r[i].z, gate_r[i].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float g0 = __uint_as_float(gw[q] << 16), g1 = __uint_as_float(gw[q] & 0xffff0000u);
+          v[2 * q] *= (g0 > 0.f) ? epi.gate_scale : 0.f;
+          v[2 * q + 1] *= (g1 > 0.f) ? epi.gate_scale : 0.f;
+        }
+      }
+      epilogue_w<8>(rest, key, N, gr, gc, v);
+      if (epi.residual)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += res_r[i][e];
+      if (old_c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += epi.beta * c_r[i][e];
+      store_w<OUT, 8>(Cv, w.bz * sC + (int64_t)gr * ldc + gc, 0.f, v);
     }
   }
 }
@@ -777,6 +830,7 @@ __global__ __launch_bounds__(NT2, 1) void gemm_big_kernel(
 // Requires K % 64 == 0 and N % BN == 0 (checked by mmt_gemm); rows past M are clamped on load
 // and not stored.
 constexpr int NT3 = 512;
+constexpr int NT_BIAS_LDS = 3072;  // floats of bias held in LDS (every step shape: N <= 3072)
 #ifndef NT_SH256  // stashed output chunks of the bf16 256-wide tile (0: all stored by the epilogue;
 #define NT_SH256 0  // measured: 4 and 8 slower at M = 70656, K = 384 and 1536)
 #endif
@@ -812,8 +866,15 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
   static_assert(SH % SPS == 0 && SH <= E && EI % 2 == 0, "stash chunks");
   static_assert(NS == 2 || (NS == 3 && STASH && EI == 0), "3 stages only with the full stash");
   static_assert(!CS || OUT == 0, "column sums of bf16 outputs only");
-  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
-  __shared__ float s_cs[CS ? 4 : 1][CS ? BN : 1];  // per-wave-row column sums (CS)
+  // ONE LDS object: the operand stages, then the bias vector (the host sends N > NT_BIAS_LDS with
+  // a bias elsewhere; staged once per launch — an epilogue global load issued behind the previous
+  // chunks' stores waits for all of them on the one in-order vmcnt), then the CS column sums.
+  // Separate __shared__ arrays make the compiler put a vmcnt(0) in front of every ds_read that
+  // follows a buffer_load ... lds (it cannot tell the objects apart), serialising the K-loop.
+  constexpr int CS_FLOATS = CS ? 4 * BN : 0;
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + 4 * (NT_BIAS_LDS + CS_FLOATS)];
+  float* const s_bias = reinterpret_cast<float*>(smem + NS * STAGE);
+  float (*const s_cs)[BN] = reinterpret_cast<float (*)[BN]>(s_bias + NT_BIAS_LDS);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -837,6 +898,14 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
   const int S = n_mine * nk;
   uint32_t key = 0;
   if (epi.rng) key = stream_key(epi.rng[0], epi.rng[1], epi.drop_layer, epi.drop_site);
+  // The epilogue applies alpha, bias (from LDS), relu and the gate (its loads issued one fragment
+  // row ahead, before the previous row's stores) itself; dropout and residual go through
+  // epilogue_w with the rest of epi. Same arithmetic, same order as epilogue_w.
+  Epi rest = epi;
+  rest.alpha = 1.f;
+  rest.bias = nullptr;
+  rest.act = MMT_ACT_NONE;
+  rest.gate = nullptr;
 
   auto fA = [](int r) { return r & 6; };
   auto fB = [](int r) { return (r & 2) | (((r >> 3) & 1) << 2); };
@@ -973,16 +1042,50 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
       srow = tm * 256 + wm * 64 + l15;
       sgc = gc0;
     }
+    // gate rows, double-buffered one fragment row ahead (rows clamped into range: an unpredicated
+    // load keeps the compiler's vmcnt counting exact)
+    uint4 gq[2][Q / 8];
+    auto gate_load = [&](int mf, int buf) {
+      const int gr = min(tm * 256 + wm * 64 + mf * 16 + l15, M - 1);
+#pragma unroll
+      for (int c8 = 0; c8 < Q / 8; ++c8)
+        gq[buf][c8] = *reinterpret_cast<const uint4*>(epi.gate + (int64_t)gr * epi.ld_gate + gc0 + 32 * c8);
+    };
+    if (epi.gate) gate_load(0, 0);
 #pragma unroll
     for (int mf = 0; mf < 4; ++mf) {
       const int gr = tm * 256 + wm * 64 + mf * 16 + l15;
+      if (epi.gate && mf < 3) gate_load(mf + 1, (mf + 1) & 1);
       if (gr < M) {
 #pragma unroll
         for (int c8 = 0; c8 < Q / 8; ++c8) {
           float v[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = acc[mf][(8 * c8 + e) >> 2][e & 3];
-          epilogue_w<8>(epi, key, N, gr, gc0 + 32 * c8, v);
+          for (int e = 0; e < 8; ++e) v[e] = acc[mf][(8 * c8 + e) >> 2][e & 3] * epi.alpha;
+          const int gc = gc0 + 32 * c8;
+          if (epi.bias) {
+            float bb[8];
+            const float4 b0 = *reinterpret_cast<const float4*>(s_bias + gc);
+            const float4 b1 = *reinterpret_cast<const float4*>(s_bias + gc + 4);
+            bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
+            bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += bb[e];
+          }
+          if (epi.act == MMT_ACT_RELU)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+          if (epi.gate) {
+            const uint4 u = gq[mf & 1][c8];
+            const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float g0 = __uint_as_float(w[q] << 16), g1 = __uint_as_float(w[q] & 0xffff0000u);
+              v[2 * q] *= (g0 > 0.f) ? epi.gate_scale : 0.f;
+              v[2 * q + 1] *= (g1 > 0.f) ? epi.gate_scale : 0.f;
+            }
+          }
+          epilogue_w<8>(rest, key, N, gr, gc, v);
           if constexpr (CS)  // the values as stored (bf16)
 #pragma unroll
             for (int e = 0; e < 8; ++e) cs[8 * c8 + e] += __uint_as_float((uint32_t)f2bf(v[e]) << 16);
@@ -1042,6 +1145,9 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
 #pragma unroll
       for (int p = 0; p < G; ++p) piece(m0, n0, k0, q, p);
     }
+  // published by the loop's first barrier, long before the first epilogue
+  if (epi.bias)  // N <= NT_BIAS_LDS (nt_bn)
+    for (int i = threadIdx.x; i < N; i += NT3) s_bias[i] = epi.bias[i];
   // vmcnt(n) for the wave-uniform counts the loop can need
   auto wait_vm = [](int n) {
     if (n == SPS) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPS) : "memory");
@@ -1391,7 +1497,7 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     out_kind = 2;
   }
   // Persistent 256 x BN NT kernel (variant -1 auto, 5/6/7 force BN 256/192/128)
-  const int bn = nt_bn(M, N, K, transA, transB, batch, out_kind, final_kind);
+  const int bn = (epi.bias && N > NT_BIAS_LDS) ? 0 : nt_bn(M, N, K, transA, transB, batch, out_kind, final_kind);
   if (bn) {
     static const int g_nt_xcd_order = getenv("MMT_NT_ORDER") ? atoi(getenv("MMT_NT_ORDER")) : 1;
     const int n_cu = cu_count();
