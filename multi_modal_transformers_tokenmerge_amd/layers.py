@@ -95,18 +95,24 @@ class Dense:
                    split_k=split_k_for(self.out_f, self.in_f, M))
             if self.b is not None and not bias_grad_done:
                 K.colsum(dy_colsum if dy_colsum is not None else dy2d, self.b.grad)
-        if wgrad_overlap.active is not None:
-            side, keep = wgrad_overlap.active
-            side.wait_stream(torch.cuda.current_stream())
-            keep.extend((dy2d, x2d, dy_colsum))
-            with torch.cuda.stream(side):
-                wgrad()
-        else:
-            wgrad()
-        if need_dx:
+        def dgrad():
             # dX = dY . W as an NT product on the transposed shadow W^T (in, out)
-            return K.gemm(dy2d, self.w.bf16_t, trans_b=True, out=dx_out, **dx_epi)
-        return None
+            return K.gemm(dy2d, self.w.bf16_t, trans_b=True, out=dx_out, **dx_epi) if need_dx else None
+        if wgrad_overlap.active is None:
+            wgrad()
+            return dgrad()
+        side, keep = wgrad_overlap.active
+        keep.extend((dy2d, x2d, dy_colsum))
+        # fork point before dX, dX issued first: the graph's first child of the fork is the
+        # critical-path product, which keeps it on the main stream's hardware queue (issued after
+        # the fork, it was queued behind the dW GEMM and its split-K combine on one queue)
+        fork = torch.cuda.Event()
+        fork.record(torch.cuda.current_stream())
+        dx = dgrad()
+        side.wait_event(fork)
+        with torch.cuda.stream(side):
+            wgrad()
+        return dx
 
 
 class SeqLayerNorm:
