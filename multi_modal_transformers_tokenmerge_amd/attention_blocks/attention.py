@@ -111,13 +111,6 @@ class Encoder1DBlock:
         main = torch.cuda.current_stream()
         side = side_stream(x.device)
         bits = None
-        bits_ready = None
-        if train and kpa < 1:  # the (L, L) attention keep mask depends only on the RNG state
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                bits = K.dropout_bits(ctx.rng, ctx.layer, DROP_ATTN, L, L, kpa)
-                bits_ready = torch.cuda.Event()
-                bits_ready.record(side)
         y0, mu0, rs0 = self.ln0.fwd(x)
         qkv = self.qkv.fwd(y0.view(B * L, D)).view(B, L, 3 * D)
         tome_idx = None
@@ -127,8 +120,10 @@ class Encoder1DBlock:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 tome_idx = K.tome_match(metric, ctx.r)
-        if bits_ready is not None:
-            main.wait_event(bits_ready)
+        if train and kpa < 1:
+            # the (L, L) attention keep mask (RNG state only), on the main stream: a 7 us launch
+            # costs less than the cross-queue wait it took beside the QKV GEMM (~10 us idle)
+            bits = K.dropout_bits(ctx.rng, ctx.layer, DROP_ATTN, L, L, kpa)
         wsum = (torch.empty((B, H, L), dtype=torch.float32, device=x.device)
                 if ctx.prune is not None else None)
         o, lse = K.attn_fwd(qkv, H, self.scale, ctx.table, bits, kpa, wsum=wsum)
@@ -159,8 +154,6 @@ class Encoder1DBlock:
             else:
                 x1, new_size, pos = K.tome_merge_fwd(x1, s0, t, ctx.r, unm, src, dst, size_in=size)
             tome = (s0, t, ctx.r, pos, size, new_size, unm, src, dst)
-        elif bits_ready is not None:
-            main.wait_stream(side)
         L2 = x1.shape[1]
         y1, mu1, rs1 = ln1_done if ln1_done is not None else self.ln1.fwd(x1)
         h = self.mlp.dense.fwd(y1.view(B * L2, D), act=K.ACT_RELU, **drop(DROP_MLP_HIDDEN, L2))
