@@ -28,7 +28,7 @@ from typing import List, Optional
 import torch
 
 from .. import _kernels as K
-from ..layers import (DROP_ATTN, DROP_ATTN_OUT, DROP_MLP_HIDDEN, DROP_MLP_OUT, Dense,
+from ..layers import (DROP_ATTN, DROP_ATTN_OUT, DROP_MLP_HIDDEN, DROP_MLP_OUT, Dense, wgrad_overlap,
                       SeqLayerNorm)
 from ..params import ParamStore, he_normal, normal
 from ..tokenizers.token_sequencer import LayerSets
@@ -257,4 +257,5 @@ class StackedEncoder1DBlock:
             # block i's LayerNorm_0 backward also does block i-1's MLP-output dropout backward
             prev = (self.blocks[i - 1], saved[i - 1], ctxs[i - 1]) if i - 1 >= lo else None
             dx, dz = self.blocks[i].backward(dx, saved[i], ctxs[i], dz2=dz, prev=prev)
+            wgrad_overlap.block_done()
         return dx

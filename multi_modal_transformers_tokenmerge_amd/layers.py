@@ -43,7 +43,26 @@ class wgrad_overlap:
             wgrad_overlap.active = (self.stream, [])
         return self
 
+    lag = int(os.environ.get("MMT_WGRAD_LAG", "1"))  # blocks the dW stream may run behind
+    _marks: list = []
+
+    @staticmethod
+    def block_done():
+        """End of one block's backward: the main stream waits for the dW work of the block
+        `lag` blocks back. Without it the graph ran the whole backward's critical path first and
+        the side stream's dW products late (measured: the side queue idle for the first 6 ms of
+        the backward, then 2.5 ms of dW alone after the critical path)."""
+        a = wgrad_overlap.active
+        if a is None or wgrad_overlap.lag <= 0:
+            return
+        ev = torch.cuda.Event()
+        ev.record(a[0])
+        wgrad_overlap._marks.append(ev)
+        if len(wgrad_overlap._marks) > wgrad_overlap.lag:
+            torch.cuda.current_stream().wait_event(wgrad_overlap._marks.pop(0))
+
     def __exit__(self, *exc):
+        wgrad_overlap._marks.clear()
         if wgrad_overlap.active is not None:
             torch.cuda.current_stream().wait_stream(self.stream)
             wgrad_overlap.active[1].clear()
