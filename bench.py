@@ -6,8 +6,9 @@ metric, config[2] (the single-GPU line uses the same workload at N=1).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config NAME]
     torchrun --nproc-per-node N bench.py --gpus N ...          (one process per GPU, RCCL)
 
-Per-GPU batch 256 by default (measured 5.7k / 7.4k / 8.6k / 9.1k samples/s at B = 64 / 128 / 256 /
-512 on one MI355X: at B = 64 the launches are too small to fill 256 CUs; see DESIGN.md "Batch").
+Per-GPU batch 512 by default (round-2 sweep on one MI355X: 11.4k / 12.3k / 12.7k / 12.8k / 13.4k /
+13.6k / 13.8k samples/s at B = 192 / 256 / 320 / 384 / 512 / 768 / 1024; fixed per-step costs —
+cross-queue waits, small launches, AdamW — amortise; see DESIGN.md "Batch").
 One step = zero grads -> forward (frozen T5, image stem, 12 ToMe blocks, diffusion loss) ->
 backward -> [gradient all-reduce over RCCL] -> fused AdamW -> device step counter, on synthetic
 inputs resident in HBM (numpy default_rng(0) shapes of SURVEY §8d). The N=1 step is one HIP graph
@@ -223,18 +224,20 @@ def kernel_probes(model, B, reps=20):
     return out
 
 
-def probe_traffic():
+def probe_traffic(B: int):
     """HBM bytes per launch of each probe from the committed rocprofv3 PMC passes
     (profiles/*_probe_pmc.json, written by tools/pmc_traffic.py from a FETCH_SIZE and a WRITE_SIZE
     pass over `bench.py --probe-only`: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
-    MI355X_MICROARCH.md "HBM"); {} when none is committed."""
+    MI355X_MICROARCH.md "HBM"), the newest file measured at this per-GPU batch; {} when none is
+    committed."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_probe_pmc.json")))
-    if not files:
-        return {}
-    with open(files[-1]) as fh:
-        d = json.load(fh)
-    return {k: v["hbm_bytes_per_launch"] for k, v in d.get("probes", {}).items()}
+    found = {}
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_probe_pmc.json"))):
+        with open(f) as fh:
+            d = json.load(fh)
+        if d.get("batch", 256) == B:
+            found = {k: v["hbm_bytes_per_launch"] for k, v in d.get("probes", {}).items()}
+    return found
 
 
 def _cpu_model() -> str:
@@ -296,8 +299,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256,
-                    help="per-GPU batch (256: see DESIGN.md 'Batch'; 64 leaves the chip underfilled)")
+    ap.add_argument("--batch", type=int, default=512,
+                    help="per-GPU batch (512: see DESIGN.md 'Batch'; 64 leaves the chip underfilled)")
     ap.add_argument("--config", default="octo-small-tome16")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -322,7 +325,7 @@ def main():
     B = args.batch
     model = Octo(cfg, dev, seed=0)
     if args.probe_only:  # for rocprofv3 --pmc traffic passes (tools/pmc_traffic.py)
-        print(json.dumps(dict(probe_only=True, probes=kernel_probes(model, B))), flush=True)
+        print(json.dumps(dict(probe_only=True, batch=B, probes=kernel_probes(model, B))), flush=True)
         return
     if di.enabled:  # identical initial parameters on every rank (broadcast from rank 0)
         dist.broadcast(model.store.flat, 0)
@@ -360,7 +363,7 @@ def main():
         ms = elapsed / args.steps * 1e3
         value = N * B * args.steps / elapsed
         probes = [] if args.no_probes else kernel_probes(model, B)
-        traffic = probe_traffic()
+        traffic = probe_traffic(B)
         for pr in probes:
             pr["traffic"] = traffic.get(pr["name"])
         top = probes[0] if probes else dict(achieved=None, frac=None, traffic=None, kernel=PROBE_KERNEL,

@@ -31,6 +31,10 @@ def main():
         ("down f32 bias+drop+res", 384, 1536, dict(out=K.OUT_F32, bias="f32", rng=rng, keep_prob=0.9,
                                                    residual="f32")),
         ("dX384 bf16 plain", 384, 1536, {}),
+        ("oproj f32 bias+drop+res", 384, 384, dict(out=K.OUT_F32, bias="f32", rng=rng, keep_prob=0.9,
+                                                   residual="f32")),
+        ("dX384k384 bf16 plain", 384, 384, {}),
+        ("dX384k1152 bf16 plain", 384, 1152, {}),
     ]
     only = [a for a in sys.argv[1:] if not a.startswith("-")]
     for name, N, Kd, epi in cases:

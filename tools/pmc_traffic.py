@@ -46,7 +46,8 @@ def main():
     a = ap.parse_args()
     with open(a.probes) as fh:
         line = [ln for ln in fh if ln.startswith("{")][-1]
-    probes = json.loads(line)["probes"]
+    meta = json.loads(line)
+    probes = meta["probes"]
     res = {}
     for p in probes:
         fetch = per_dispatch(a.fetch_dir, "FETCH_SIZE", p["kernel"])
@@ -63,7 +64,7 @@ def main():
                               hbm_bytes_per_launch=round(hbm), algorithmic_bytes_per_launch=alg,
                               ratio_to_algorithmic=round(hbm / alg, 3) if alg else None)
     with open(a.out, "w") as fh:
-        json.dump(dict(probes=res), fh, indent=1)
+        json.dump(dict(batch=meta.get("batch", 256), probes=res), fh, indent=1)
     print(json.dumps(res))
 
 
