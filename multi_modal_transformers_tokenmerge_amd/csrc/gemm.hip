@@ -1217,6 +1217,155 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
   NT_CLK(1);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Weight-gradient (TN) split-K partial products with direct global->LDS loads: slab[z] =
+// A[k0:k1]^T . B[k0:k1] for A [K][M] (dY, rows = tokens) and B [K][N] (X), both MN-contiguous.
+// 256 x 192 output tile, 8 waves as 4 (M) x 2 (N) of 64 x 96 (2 x 3 MFMA 32x32x16 blocks, the
+// register-staged gemm_big_kernel's geometry), K-steps of 64 tokens, two LDS stages of unpadded
+// [64][256] + [64][192] bf16 images (56 KB each) filled by buffer_load ... lds (no VGPR staging,
+// no ds_write pass: the register-staged kernel spent 56 KB of ds_write per K-step on top of the
+// fragment reads). The 16-B chunk c of k-row r sits at c ^ 2(r & 3) (applied to each lane's SOURCE
+// address, the DMA destination is lane-linear): the transposed fragment reads
+// (ds_read_b64_tr_b16, 4 k-rows x 2 chunks per 16 lanes) hit 8 distinct 4-bank groups.
+// Columns past M / N read whatever lies there (only output rows / columns past M / N depend on
+// them, and those are not stored); rows past K read zeros (buffer range). One tile per workgroup,
+// so the K-loop carries no stores: the wait for a K-step's DMA is vmcnt(0) on nothing else.
+constexpr int TN_BM = 256, TN_BN = 192, TN_NT = 512;
+// buffer_load_dwordx4 ... lds as inline asm (same operation as dma16): issued through the
+// builtin, the compiler cannot tell the transposed fragment reads (ds_read_b64_tr_b16) from the
+// stage being filled and puts a vmcnt(0) behind every DMA (the next K-step's, meant to stay in
+// flight under these MFMAs). Completion is waited for explicitly (vmcnt(0) + s_barrier at the
+// top of each K-step). Raw buffer resource: stride 0, num_records = bytes (reads past it: 0).
+__device__ __forceinline__ void dma16_asm(const void* base, int64_t bytes, void* lds, int voffset) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  i32x4 r;
+  r[0] = (int)(uint32_t)b;
+  r[1] = (int)((uint32_t)(b >> 32) & 0xffffu);
+  r[2] = (int)min(bytes, (int64_t)0x7ffffff0);
+  r[3] = 0x00020000;
+  const uint32_t l = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)lds);
+  asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               :: "v"(voffset), "s"(r), "s"(l) : "m0", "memory");
+}
+__global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
+    int64_t ldb, float* __restrict__ slab, int split_k, int k_chunk, int tiles_n) {
+  constexpr int A_ROWB = TN_BM * 2, B_ROWB = TN_BN * 2;            // bytes per k-row
+  constexpr int A_BYTES = 64 * A_ROWB, B_BYTES = 64 * B_ROWB, STAGE = A_BYTES + B_BYTES;
+  constexpr int GA = A_BYTES / 1024 / 8, GB = B_BYTES / 1024 / 8;   // DMA pieces per wave (4 + 3)
+  constexpr int G = GA + GB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1, hl = lane >> 5;
+  const int tiles = ((M + TN_BM - 1) / TN_BM) * tiles_n;
+  const int wi = xcd_remap(blockIdx.x, gridDim.x);
+  const int z = wi / tiles, t = wi - z * tiles;
+  const int tm = t / tiles_n;
+  const int m0 = tm * TN_BM, n0 = (t - tm * tiles_n) * TN_BN;
+  const int kbeg = z * k_chunk, kend = min(K, kbeg + k_chunk);
+  const int nk = max(0, (kend - kbeg + 63) / 64);
+  auto sw = [](int r) { return 2 * (r & 3); };
+
+  // per-lane source offsets (bytes from the K-step's panel base) of this wave's DMA pieces
+  int voff[G];
+#pragma unroll
+  for (int p = 0; p < G; ++p) {
+    if (p < GA) {  // A piece j = wave * GA + p: k-rows 2j, 2j + 1 (32 chunks each)
+      const int j = wave * GA + p, row = 2 * j + (lane >> 5), c = (lane & 31) ^ sw(row);
+      voff[p] = row * (int)(lda * 2) + c * 16;
+    } else {       // B piece j: 1 KB of the [64][192] image (24 chunks per k-row)
+      const int j = wave * GB + (p - GA), e = j * 64 + lane, row = e / 24, c = (e % 24) ^ sw(row);
+      voff[p] = row * (int)(ldb * 2) + c * 16;
+    }
+  }
+  // buffer ranges end at row K (zeros past it); the panel base moves with the K-step
+  auto piece = [&](int kt, int st, int p) {
+    const int k0 = kbeg + kt * 64;
+    char* S0 = smem + st * STAGE;
+    if (p < GA)
+      dma16_asm(A + (int64_t)k0 * lda + m0, ((int64_t)(K - k0) * lda - m0) * 2,
+                S0 + (wave * GA + p) * 1024, voff[p]);
+    else
+      dma16_asm(B + (int64_t)k0 * ldb + n0, ((int64_t)(K - k0) * ldb - n0) * 2,
+                S0 + A_BYTES + (wave * GB + (p - GA)) * 1024, voff[p]);
+  };
+
+  floatx16 acc[2][3];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[a][b][q] = 0.f;
+
+  // fragment of rows rbase.. (M or N index) for k-slice ks: lane (i = lane & 15: k-row q = i >> 2,
+  // column group p4 = i & 3; g = lane >> 4; h = lane >> 5) reads 4 columns of k-rows k1 and k1 + 4
+  const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g16 = lane >> 4;
+  auto frag = [&](const char* S, int rowb, int rbase, int ks) {
+    const int col = rbase + 16 * (g16 & 1) + 4 * p4;
+    const int k1 = ks * 16 + 8 * hl + q4;
+    const int cofs = (col & 7) * 2;
+    const short4v v1 = tr_read(reinterpret_cast<const bf16_t*>(
+        S + k1 * rowb + ((((col >> 3) ^ sw(k1))) << 4) + cofs));
+    const short4v v2 = tr_read(reinterpret_cast<const bf16_t*>(
+        S + (k1 + 4) * rowb + ((((col >> 3) ^ sw(k1 + 4))) << 4) + cofs));
+    short __attribute__((ext_vector_type(8))) v = {v1[0], v1[1], v1[2], v1[3],
+                                                   v2[0], v2[1], v2[2], v2[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
+  if (nk > 0)
+#pragma unroll
+    for (int p = 0; p < G; ++p) piece(0, 0, p);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 1;
+    // this K-step's DMA is the only memory operation in flight
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    const bool nxt = kt + 1 < nk;
+    const char* As = smem + st * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bf16x8 af[2], bfr[3];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) af[a] = frag(As, A_ROWB, wm * 64 + a * 32, ks);
+#pragma unroll
+      for (int b = 0; b < 3; ++b) bfr[b] = frag(Bs, B_ROWB, wn * 96 + b * 32, ks);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b)  // operands swapped: the accumulator holds C^T
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+      // the next K-step's DMA into the other stage (free since this K-step's barrier), spread
+      // over the k-slices so the SIMD partner wave keeps issuing MFMAs
+      if (nxt) {
+        if (2 * ks < G) piece(kt + 1, st ^ 1, 2 * ks);
+        if (2 * ks + 1 < G) piece(kt + 1, st ^ 1, 2 * ks + 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // fp32 slab z: lane (m = lane & 31, h) of block (a, b) holds row m, columns 8g + 4h + {0..3}
+  float* out = slab + (int64_t)z * M * N;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int gr = m0 + wm * 64 + a * 32 + (lane & 31);
+    if (gr >= M) continue;
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int gc = n0 + wn * 96 + b * 32 + 8 * g + 4 * hl;
+        if (gc >= N) continue;
+        *reinterpret_cast<float4*>(out + (int64_t)gr * N + gc) =
+            make_float4(acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2],
+                        acc[a][b][4 * g + 3]);
+      }
+  }
+}
+
 // Split-K combine: v = sum_s slab[s][m][n] (fp32), then the GEMM epilogue, 8 columns per thread.
 template <int OUT>
 __global__ void splitk_epilogue_kernel(const float* __restrict__ ws, int split, int M, int N,
@@ -1561,6 +1710,15 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
                      (const bf16_t*)A, lda, sA, (const bf16_t*)B, ldb, sB, Cdst, ldd, sdd,        \
                      split_k, k_chunk, tiles_n, n_work, epi)
   if (pipe == 4 && !(!transA && transB && K % 8 == 0)) pipe = 1;  // glds path: NT only
+  // TN split-K slabs (every weight gradient of the step): the direct-to-LDS TN kernel
+  static const int g_tn_dma = getenv("MMT_TN_DMA") ? atoi(getenv("MMT_TN_DMA")) : 1;
+  if (pipe == 3 && out_kind == 2 && transA && !transB && batch == 1 && g_tn_dma) {
+    const int tn = (N + TN_BN - 1) / TN_BN;
+    const int work = ((M + TN_BM - 1) / TN_BM) * tn * split_k;
+    hipLaunchKernelGGL(gemm_tn_dma_kernel, dim3(work), dim3(TN_NT), 0, s, M, N, K,
+                       (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
+    MMT_CHECK_LAUNCH("mmt_gemm(tn dma)");
+  } else {
 #define GL(TA, TB, OUT)                          \
   do {                                           \
     if (pipe == 4) GLG(OUT);                     \
@@ -1579,6 +1737,7 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
   else if (!transA && !transB) GL_OUT(false, false);
   else if (transA && !transB) GL_OUT(true, false);
   else GL_OUT(true, true);
+  }
 #undef GL_OUT
 #undef GL
 #undef GL1

@@ -88,6 +88,21 @@ def test_gemm_gate_and_beta_and_atomic_splitk(dev):
     torch.testing.assert_close(dw, ref, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("M,N,K", [(1536, 384, 16384), (1152, 384, 9997), (384, 1536, 12288),
+                                   (640, 200, 30000), (384, 384, 20480)])
+def test_gemm_tn_splitk_weight_gradient(dev, M, N, K):
+    """The step's weight-gradient launches (TN, fp32 split-K slabs + combine, C += A^T B): the
+    direct-to-LDS TN kernel at full and partial M / N tiles and a partial last K-step."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    from multi_modal_transformers_tokenmerge_amd.layers import split_k_for
+    g = torch.Generator().manual_seed(M + N + K)
+    dy, x = _mk((K, M), dev, g), _mk((K, N), dev, g)
+    dw = torch.randn(M, N, generator=g).to(dev)
+    ref = dw + dy.float().t() @ x.float()
+    Kn.gemm(dy, x, trans_a=True, out=dw, out_mode=Kn.OUT_F32_ACCUM, split_k=split_k_for(M, N, K))
+    torch.testing.assert_close(dw, ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
+
+
 def test_gemm_rejects_bad_shapes(dev):
     from multi_modal_transformers_tokenmerge_amd import _kernels as Kn, _C
     a = torch.zeros((16, 12), dtype=torch.bfloat16, device=dev)
