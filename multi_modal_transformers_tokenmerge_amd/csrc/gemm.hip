@@ -544,18 +544,26 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_glds_nt_kernel(
     asm volatile("s_barrier" ::: "memory");
     const bf16_t* As = smem + st * STAGE;
     const bf16_t* Bs = As + OPE;
+    // fragments one k-slice ahead (slice ks + 1's reads in flight under slice ks's MFMAs)
+    bf16x8 af[2][2], bfr[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) af[0][a] = frag(As, wm * 64 + a * 32, 0);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) bfr[0][b] = frag(Bs, wn * 64 + b * 32, 0);
 #pragma unroll
     for (int ks = 0; ks < BKG / 16; ++ks) {
-      bf16x8 af[2], bfr[2];
+      const int cu = ks & 1;
+      if (ks + 1 < BKG / 16) {
 #pragma unroll
-      for (int a = 0; a < 2; ++a) af[a] = frag(As, wm * 64 + a * 32, ks);
+        for (int a = 0; a < 2; ++a) af[cu ^ 1][a] = frag(As, wm * 64 + a * 32, ks + 1);
 #pragma unroll
-      for (int b = 0; b < 2; ++b) bfr[b] = frag(Bs, wn * 64 + b * 32, ks);
+        for (int b = 0; b < 2; ++b) bfr[cu ^ 1][b] = frag(Bs, wn * 64 + b * 32, ks + 1);
+      }
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[cu][b], af[cu][a], acc[a][b], 0, 0, 0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // stage st free again
   }
@@ -1326,18 +1334,27 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
     const bool nxt = kt + 1 < nk;
     const char* As = smem + st * STAGE;
     const char* Bs = As + A_BYTES;
+    // fragments one k-slice ahead: slice ks + 1's reads are in flight under slice ks's MFMAs (every
+    // wave reaches this point together after the barrier, so the partner wave cannot cover them)
+    bf16x8 af[2][2], bfr[2][3];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) af[0][a] = frag(As, A_ROWB, wm * 64 + a * 32, 0);
+#pragma unroll
+    for (int b = 0; b < 3; ++b) bfr[0][b] = frag(Bs, B_ROWB, wn * 96 + b * 32, 0);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      bf16x8 af[2], bfr[3];
+      const int cu = ks & 1;
+      if (ks < 3) {
 #pragma unroll
-      for (int a = 0; a < 2; ++a) af[a] = frag(As, A_ROWB, wm * 64 + a * 32, ks);
+        for (int a = 0; a < 2; ++a) af[cu ^ 1][a] = frag(As, A_ROWB, wm * 64 + a * 32, ks + 1);
 #pragma unroll
-      for (int b = 0; b < 3; ++b) bfr[b] = frag(Bs, B_ROWB, wn * 96 + b * 32, ks);
+        for (int b = 0; b < 3; ++b) bfr[cu ^ 1][b] = frag(Bs, B_ROWB, wn * 96 + b * 32, ks + 1);
+      }
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 3; ++b)  // operands swapped: the accumulator holds C^T
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[cu][b], af[cu][a], acc[a][b], 0, 0, 0);
       // the next K-step's DMA into the other stage (free since this K-step's barrier), spread
       // over the k-slices so the SIMD partner wave keeps issuing MFMAs
       if (nxt) {
