@@ -174,7 +174,7 @@ def kernel_probes(model, B, reps=20):
         "mfma", 2.0 * M * D * Mh, f"M={M} N={D} K={Mh}, 2MNK", _gemm_bytes(M, D, Mh))
     # 3. MLP Dense_0 weight gradient dW += dz1^T . y1 (TN, split-K fp32 slabs + combine)
     wgrad = torch.zeros((Mh, D), dtype=torch.float32, device=dev)
-    add("mlp_dw", "gemm_big_kernel<true, false, 2>",
+    add("mlp_dw", "gemm_tn_dma_kernel",
         lambda: K.gemm(dz1, y1, trans_a=True, out=wgrad, out_mode=K.OUT_F32_ACCUM,
                        split_k=split_k_for(Mh, D, M)),
         "mfma", 2.0 * M * D * Mh,
@@ -366,18 +366,25 @@ def main():
         traffic = probe_traffic(B)
         for pr in probes:
             pr["traffic"] = traffic.get(pr["name"])
-        top = probes[0] if probes else dict(achieved=None, frac=None, traffic=None, kernel=PROBE_KERNEL,
-                                            avg_launch_us=None, flops_per_launch=None)
+        # headline: the dominant kernel of the step trace — the weight-gradient GEMM (TN, split-K
+        # slabs + combine; ≈ 23 % of kernel time, profiles/r02_b512_kernel_stats_step.csv), at
+        # the MLP Dense_0 dW shape; every other probe follows in `kernels`
+        top = next((p for p in probes if p["name"] == "mlp_dw"), None)
         sets0, _, _, r0, pr0 = model.layer_sets[0]
         M_ = B * (sum(pr0[1]) if pr0 else sets0.L - r0)
         N_, K_ = cfg.mlp_dim, cfg.token_embedding_dim
+        if top is None:
+            top = dict(achieved=None, frac=None, traffic=None, kernel="gemm_tn_dma_kernel",
+                       avg_launch_us=None, flops_per_launch=None)
         roof = dict(bound="mfma", achieved=top["achieved"], peak=MFMA_BF16_PEAK_TFLOPS,
                     unit="TFLOP/s", frac=top["frac"], traffic=top["traffic"],
-                    kernel=top["kernel"] + " (MLP Dense_0 fwd, bias+relu+dropout epilogue)",
-                    shape_MNK=[M_, N_, K_], avg_launch_us=top["avg_launch_us"],
+                    kernel=top["kernel"] + " + splitk_epilogue_kernel<1> (MLP Dense_0 weight "
+                    "gradient dW += dz1^T . y1: one mmt_gemm launch, split-K GEMM and its combine "
+                    "timed together)",
+                    shape_MNK=[N_, K_, M_], avg_launch_us=top["avg_launch_us"],
                     flops_per_launch=top["flops_per_launch"],
-                    algorithmic_bytes_per_launch=_gemm_bytes(M_, N_, K_, extra=4 * N_),
-                    kernels=probes[1:])
+                    algorithmic_bytes_per_launch=2 * (M_ * N_ + M_ * K_) + 8 * N_ * K_,
+                    kernels=[p for p in probes if p is not top])
         fps = algorithmic_flops_per_sample(model)
         cpu = None
         if N == 1 and not args.no_cpu_baseline:

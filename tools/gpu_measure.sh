@@ -12,4 +12,5 @@ timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/${TA
 python tools/pmc_traffic.py gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write --probes gpurun_out/${TAG}_probes.json --out gpurun_out/${TAG}_probe_pmc.json > gpurun_out/${TAG}_pmc3.log 2>&1 &&
 cp gpurun_out/${TAG}_probe_pmc.json profiles/ &&
 timeout -k 10 400 python bench.py > gpurun_out/${TAG}_bench.log 2>&1 &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_benchprof -o run --output-format csv -- python bench.py --no-cpu-baseline > gpurun_out/${TAG}_benchprof.log 2>&1 &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-probes > gpurun_out/${TAG}_prof.log 2>&1
