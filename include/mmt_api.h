@@ -189,6 +189,17 @@ typedef struct {
                                  (not accumulated) — the bias gradient of the next Dense backward
                                  (layers.py:59 colsum) without re-reading C; only where
                                  mmt_gemm_colsum_rows is nonzero, else mmt_gemm fails */
+  /* 1-bit form of the relu gate (the MLP hidden layer, attention.py:20-39 MLPBlock), both only
+   * where mmt_gemm_colsum_rows is nonzero (the 256-wide bf16 NT path), else mmt_gemm fails:
+   * relu_bits (out): [ceil(M/256)*256][N/32] words (16-B aligned), bit set iff the output is
+   *   > 0 (the stored bf16 value has the same sign); output (m, n) is bit 8 c + e of the word
+   *   at flat index (g * N/32 + w) * 4 + f, g = (m / 256) * 64 + ((m / 64) & 3) * 16 + (m & 15),
+   *   f = (m / 16) & 3, n = 256 (w / 8) + 128 ((w / 4) & 1) + 8 (w & 3) + 32 c + e (c < 4,
+   *   e < 8): one 16-B vector per lane of that path's epilogue (its 4 rows x 32 columns);
+   * gate_bits (in): the same layout, used in place of gate (v *= bit ? gate_scale : 0), so a
+   *   backward reads M*N/8 bytes instead of the bf16 gate's 2*M*N. NULL: unused. */
+  uint32_t* relu_bits;
+  const uint32_t* gate_bits;
 } mmt_epilogue_t;
 
 /* Tuning knob (benchmarks): 0 = 128x128 register-staged, double-buffered LDS; 1 = same, single

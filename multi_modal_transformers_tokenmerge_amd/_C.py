@@ -21,7 +21,7 @@ class Epilogue(ctypes.Structure):
     _fields_ = [("bias", P), ("act", I), ("rng", P), ("drop_layer", U32), ("drop_site", U32),
                 ("keep_prob", F), ("drop_row_offset", L), ("gate", P), ("ld_gate", L),
                 ("gate_scale", F), ("residual", P), ("ld_res", L), ("alpha", F), ("beta", F),
-                ("res_dtype", I), ("colsum", P)]
+                ("res_dtype", I), ("colsum", P), ("relu_bits", P), ("gate_bits", P)]
 
 
 # name -> argtypes (every entry point returns int status unless listed in _VOID)

@@ -141,9 +141,11 @@ ACT_NONE, ACT_RELU = 0, 1
 
 def _epi(bias=None, act=ACT_NONE, rng=None, drop_layer=0, drop_site=0, keep_prob=1.0,
          drop_row_offset=0, gate=None, gate_scale=1.0, residual=None, alpha=1.0, beta=0.0,
-         colsum=None):
+         colsum=None, relu_bits=None, gate_bits=None):
     e = _C.Epilogue()
     e.colsum = ptr(colsum)
+    e.relu_bits = ptr(relu_bits)
+    e.gate_bits = ptr(gate_bits)
     e.bias = ptr(bias)
     e.act = act
     e.rng = ptr(rng)
@@ -197,6 +199,15 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
     bias = epi.get("bias")
     if bias is not None and (bias.numel() != N or bias.dtype != torch.float32):
         raise ValueError("gemm bias must be fp32 [N]")
+    for name in ("relu_bits", "gate_bits"):
+        t = epi.get(name)
+        if t is not None:
+            if not gemm_bits_supported(M, N, K, trans_a, trans_b, out_mode, split_k):
+                raise ValueError(f"gemm {name}: this launch shape has no 1-bit gate path")
+            rows = -(-M // 256) * 256
+            if t.dtype != torch.int32 or tuple(t.shape) != (rows, N // 32) or not t.is_contiguous():
+                raise ValueError(f"gemm {name} must be contiguous int32 ({rows}, {N // 32})")
+            split_k = 1
     cs = epi.get("colsum")
     if cs is not None:
         rows = gemm_colsum_rows(M, N, K, trans_a, trans_b, out_mode, 1 if split_k is None else split_k)
@@ -213,6 +224,13 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
             b.stride(0), ptr(out), out_mode, out.stride(0), 1, 0, 0, 0, split_k,
             _C.ctypes.byref(e), ptr(ws), 0 if ws is None else ws.numel(), _C.stream_ptr())
     return out
+
+
+def gemm_bits_supported(M: int, N: int, K: int, trans_a: bool = False, trans_b: bool = True,
+                        out_mode: int = OUT_BF16, split_k: int | None = 1) -> bool:
+    """Whether gemm(..., relu_bits= / gate_bits=) works for this launch (the 256-wide bf16 NT
+    path, the same launches that can write epilogue column sums)."""
+    return gemm_colsum_rows(M, N, K, trans_a, trans_b, out_mode, 1 if split_k is None else split_k) > 0
 
 
 def gemm_colsum_rows(M: int, N: int, K: int, trans_a: bool = False, trans_b: bool = True,

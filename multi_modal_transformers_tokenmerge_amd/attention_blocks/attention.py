@@ -25,6 +25,8 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import List, Optional
 
+import os
+
 import torch
 
 from .. import _kernels as K
@@ -50,6 +52,9 @@ class LayerCtx:
 
 
 _SIDE = {}
+
+
+_RELU_BITS = os.environ.get("MMT_RELU_BITS", "1") != "0"  # benchmarking knob: bf16 gate instead
 
 
 def side_stream(device) -> torch.cuda.Stream:
@@ -156,11 +161,19 @@ class Encoder1DBlock:
             tome = (s0, t, ctx.r, pos, size, new_size, unm, src, dst)
         L2 = x1.shape[1]
         y1, mu1, rs1 = ln1_done if ln1_done is not None else self.ln1.fwd(x1)
-        h = self.mlp.dense.fwd(y1.view(B * L2, D), act=K.ACT_RELU, **drop(DROP_MLP_HIDDEN, L2))
+        # the relu gate of the backward as 1 bit per hidden unit where the launch supports it
+        # (the gated dX then reads M*Mh/8 bytes instead of h's 2*M*Mh)
+        Mh = self.mlp.dense.out_f
+        hbits = (torch.empty((-(-B * L2 // 256) * 256, Mh // 32), dtype=torch.int32, device=x.device)
+                 if train and not self.mlp.dense.fp8 and _RELU_BITS and K.gemm_bits_supported(B * L2, Mh, D)
+                 else None)
+        h = self.mlp.dense.fwd(y1.view(B * L2, D), act=K.ACT_RELU, relu_bits=hbits,
+                               **drop(DROP_MLP_HIDDEN, L2))
         x2 = self.mlp.dense_out.fwd(h, residual=x1.view(B * L2, D), out_mode=K.OUT_F32,
                                     **drop(DROP_MLP_OUT, L2))
         saved = dict(x=x, y0=y0, mu0=mu0, rs0=rs0, qkv=qkv, o=o, o_in=o_in, lse=lse, bits=bits,
-                     x1=x1, y1=y1, mu1=mu1, rs1=rs1, h=h, tome=tome, prune=prune, kp=kp, kpa=kpa)
+                     x1=x1, y1=y1, mu1=mu1, rs1=rs1, h=h, hbits=hbits, tome=tome, prune=prune,
+                     kp=kp, kpa=kpa)
         return x2.view(B, L2, D), saved, new_size
 
     # ----------------------------------------------------------------------------- backward
@@ -187,8 +200,9 @@ class Encoder1DBlock:
         Mh = self.mlp.dense.out_f
         rows = K.gemm_colsum_rows(B * L2, Mh, D)
         cs = torch.empty((rows, Mh), dtype=torch.float32, device=dz2.device) if rows else None
-        dz1 = self.mlp.dense_out.bwd(dz2, sv["h"], bias_grad_done=True, gate=sv["h"],
-                                     gate_scale=(1.0 / kp) if dropping else 1.0, colsum=cs)
+        gate = dict(gate_bits=sv["hbits"]) if sv.get("hbits") is not None else dict(gate=sv["h"])
+        dz1 = self.mlp.dense_out.bwd(dz2, sv["h"], bias_grad_done=True,
+                                     gate_scale=(1.0 / kp) if dropping else 1.0, colsum=cs, **gate)
         # dX of the LN-fed Dense in bf16 (the LN backward accumulates in fp32): halves its traffic
         dy1 = self.mlp.dense.bwd(dz1, sv["y1"].view(B * L2, D), dy_colsum=cs)
         Lo = sv["o_in"].shape[1]

@@ -105,6 +105,8 @@ struct Epi {
   int64_t ld_res;
   float alpha, beta;
   float* colsum;  // nt256 only: per-256-row-panel column sums of the stored (bf16) C, or null
+  uint32_t* relu_bits;         // nt256 BN 256 only: 1 bit per output, set iff stored bf16 > 0
+  const uint32_t* gate_bits;   // nt256 BN 256 only: the gate in that 1-bit form
 };
 
 // global -> registers for one 128 x 64 (K-contig) or 64 x 128 (MN-contig) operand tile.
@@ -855,7 +857,7 @@ __device__ __forceinline__ void dma16(const void* base, int64_t bytes, void* lds
 #endif
 }
 
-template <int BN, int OUT, int SHV, int NS, bool CS = false>
+template <int BN, int OUT, int SHV, int NS, bool CS = false, bool GBITS = false>
 __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
     int64_t ldb, void* __restrict__ Cv, int64_t ldc, int tiles_n, int n_tiles, int xcd_order,
@@ -914,6 +916,13 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
   rest.bias = nullptr;
   rest.act = MMT_ACT_NONE;
   rest.gate = nullptr;
+  rest.relu_bits = nullptr;
+  rest.gate_bits = nullptr;
+  constexpr bool BITS = BN == 256;  // the 1-bit gate layout is this tile's lane layout (Q = 32)
+  static_assert(!GBITS || BITS, "1-bit gate only on 256-wide tiles");
+  constexpr bool RBITS = BITS && !CS && !GBITS;  // relu_bits writer (a forward launch)
+  // GBITS: the gate comes as bits (gate_bits); otherwise as bf16 rows (gate) — one of the two
+  // compiled per instantiation (both at once spill registers in the column-sum variant)
 
   auto fA = [](int r) { return r & 6; };
   auto fB = [](int r) { return (r & 2) | (((r >> 3) & 1) << 2); };
@@ -1059,11 +1068,18 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
       for (int c8 = 0; c8 < Q / 8; ++c8)
         gq[buf][c8] = *reinterpret_cast<const uint4*>(epi.gate + (int64_t)gr * epi.ld_gate + gc0 + 32 * c8);
     };
-    if (epi.gate) gate_load(0, 0);
+    // 1-bit gate / relu words (include/mmt_api.h layout): this lane's 4 rows (mf) x 32 columns
+    // are one uint4 at [(tm * 64 + wm * 16 + l15)][tn * 8 + wn * 4 + lq]: one 16-B load / store
+    // per lane per tile, the 4 lq lanes of a row group writing 64 contiguous bytes
+    const int64_t bidx = (int64_t)(tm * 64 + wm * 16 + l15) * (N / 32) + (tn * 8 + wn * 4 + lq);
+    uint4 gbw = make_uint4(0u, 0u, 0u, 0u);
+    if (GBITS && epi.gate_bits) gbw = reinterpret_cast<const uint4*>(epi.gate_bits)[bidx];
+    uint32_t rbw[4] = {0u, 0u, 0u, 0u};  // relu_bits words of this lane's 4 rows
+    if (!GBITS && epi.gate) gate_load(0, 0);
 #pragma unroll
     for (int mf = 0; mf < 4; ++mf) {
       const int gr = tm * 256 + wm * 64 + mf * 16 + l15;
-      if (epi.gate && mf < 3) gate_load(mf + 1, (mf + 1) & 1);
+      if (!GBITS && epi.gate && mf < 3) gate_load(mf + 1, (mf + 1) & 1);
       if (gr < M) {
 #pragma unroll
         for (int c8 = 0; c8 < Q / 8; ++c8) {
@@ -1083,7 +1099,7 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
           if (epi.act == MMT_ACT_RELU)
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-          if (epi.gate) {
+          if (!GBITS && epi.gate) {
             const uint4 u = gq[mf & 1][c8];
             const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
@@ -1093,7 +1109,15 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
               v[2 * q + 1] *= (g1 > 0.f) ? epi.gate_scale : 0.f;
             }
           }
+          if (GBITS && epi.gate_bits) {
+            const uint32_t w = (mf == 0 ? gbw.x : mf == 1 ? gbw.y : mf == 2 ? gbw.z : gbw.w) >> (8 * c8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= ((w >> e) & 1u) ? epi.gate_scale : 0.f;
+          }
           epilogue_w<8>(rest, key, N, gr, gc, v);
+          if (RBITS && epi.relu_bits)  // stored bf16 > 0 <=> v > 0 (bf16 keeps fp32's exponent range)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) rbw[mf] |= (v[e] > 0.f ? 1u : 0u) << (8 * c8 + e);
           if constexpr (CS)  // the values as stored (bf16)
 #pragma unroll
             for (int e = 0; e < 8; ++e) cs[8 * c8 + e] += __uint_as_float((uint32_t)f2bf(v[e]) << 16);
@@ -1122,6 +1146,8 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
 #pragma unroll
       for (int nf = 0; nf < NF; ++nf) acc[mf][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
+    if (RBITS && epi.relu_bits)
+      reinterpret_cast<uint4*>(epi.relu_bits)[bidx] = make_uint4(rbw[0], rbw[1], rbw[2], rbw[3]);
     if constexpr (CS) {
       // sum over the 16 row lanes (l15) of each DPP row: xor 1, xor 2, half-row and row mirrors
 #pragma unroll
@@ -1642,6 +1668,11 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     epi.ld_res = e->ld_res;
     epi.alpha = e->alpha;
     epi.beta = e->beta;
+    epi.relu_bits = e->relu_bits;
+    epi.gate_bits = e->gate_bits;
+    MMT_CHECK_ARG(!(e->gate && e->gate_bits), "mmt_gemm: gate and gate_bits are exclusive");
+    MMT_CHECK_ARG(!(e->relu_bits && (e->gate_bits || e->colsum)),
+                  "mmt_gemm: relu_bits is a forward output (no gate_bits / colsum in that launch)");
     epi.colsum = e->colsum;
     MMT_CHECK_ARG((!e->gate || (e->ld_gate % 8 == 0 && (uintptr_t)e->gate % 16 == 0)) &&
                       (!e->residual || (e->ld_res % 8 == 0 && (uintptr_t)e->residual % 16 == 0)),
@@ -1664,6 +1695,8 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
   }
   // Persistent 256 x BN NT kernel (variant -1 auto, 5/6/7 force BN 256/192/128)
   const int bn = (epi.bias && N > NT_BIAS_LDS) ? 0 : nt_bn(M, N, K, transA, transB, batch, out_kind, final_kind);
+  MMT_CHECK_ARG(!(epi.relu_bits || epi.gate_bits) || (bn == 256 && final_kind == 0),
+                "mmt_gemm: relu_bits / gate_bits need the 256-wide bf16 nt path (mmt_gemm_colsum_rows)");
   if (bn) {
     static const int g_nt_xcd_order = getenv("MMT_NT_ORDER") ? atoi(getenv("MMT_NT_ORDER")) : 1;
     const int n_cu = cu_count();
@@ -1675,7 +1708,16 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
                      (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, tn, n_tiles, g_nt_xcd_order, epi)
       // the register stash fits 2 waves/SIMD for bf16 at BN <= 192 and fp32 at BN 128;
       // BN 128 has LDS for 3 stages (DMA two K-steps ahead)
-      if (epi.colsum) {
+      if (epi.gate_bits) {  // 256-wide bf16 (checked above)
+        if (epi.colsum)
+          hipLaunchKernelGGL((gemm_nt256_kernel<256, 0, NT_SH256, 2, true, true>), dim3(grid), dim3(NT3),
+                             0, s, M, N, K, (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, tn,
+                             n_tiles, g_nt_xcd_order, epi);
+        else
+          hipLaunchKernelGGL((gemm_nt256_kernel<256, 0, NT_SH256, 2, false, true>), dim3(grid), dim3(NT3),
+                             0, s, M, N, K, (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, tn,
+                             n_tiles, g_nt_xcd_order, epi);
+      } else if (epi.colsum) {
         MMT_CHECK_ARG(final_kind == 0 && bn == 256, "mmt_gemm: colsum needs the 256-wide bf16 nt path "
                       "(mmt_gemm_colsum_rows)");
         hipLaunchKernelGGL((gemm_nt256_kernel<256, 0, NT_SH256, 2, true>), dim3(grid), dim3(NT3), 0, s,
@@ -1815,6 +1857,11 @@ extern "C" int mmt_gemm_fp8(int M, int N, int K, const void* A, int64_t lda, con
     epi.ld_res = e->ld_res;
     epi.alpha = e->alpha;
     epi.beta = e->beta;
+    epi.relu_bits = e->relu_bits;
+    epi.gate_bits = e->gate_bits;
+    MMT_CHECK_ARG(!(e->gate && e->gate_bits), "mmt_gemm: gate and gate_bits are exclusive");
+    MMT_CHECK_ARG(!(e->relu_bits && (e->gate_bits || e->colsum)),
+                  "mmt_gemm: relu_bits is a forward output (no gate_bits / colsum in that launch)");
   }
   const int tiles_n = (N + F8_BN - 1) / F8_BN, n_work = ((M + F8_BM - 1) / F8_BM) * tiles_n;
   hipStream_t s = as_stream(stream);

@@ -124,3 +124,61 @@ def test_nt256_colsum_slab(dev, variant, M):
     assert Kn.gemm_colsum_rows(M, 384, K) == 0 and Kn.gemm_colsum_rows(M, N, K, out_mode=Kn.OUT_F32) == 0
     with pytest.raises(ValueError):
         Kn.gemm(a, w[:384], False, True, colsum=torch.zeros((rows, 384), device=dev))
+
+
+def _bits_to_mask(bits, M, N):
+    """Expand relu_bits / gate_bits (include/mmt_api.h layout) to an (M, N) bool mask."""
+    m = torch.arange(M, device=bits.device)
+    g = (m // 256) * 64 + ((m // 64) & 3) * 16 + (m & 15)
+    f = (m // 16) & 3
+    words = bits.view(-1, N // 32, 4)[g, :, f].to(torch.int64) & 0xFFFFFFFF  # (M, N/32)
+    wi = torch.arange(N // 32, device=bits.device)
+    c = torch.arange(4, device=bits.device)
+    e = torch.arange(8, device=bits.device)
+    col = ((256 * (wi // 8) + 128 * ((wi // 4) & 1) + 8 * (wi & 3))[:, None, None]
+           + 32 * c[None, :, None] + e[None, None, :])
+    bit = (8 * c[:, None] + e[None, :])[None, None]                 # (1, 1, 4, 8)
+    val = (words[:, :, None, None] >> bit) & 1                       # (M, N/32, 4, 8)
+    mask = torch.zeros((M, N), dtype=torch.bool, device=bits.device)
+    mask[:, col.reshape(-1)] = val.reshape(M, -1).bool()
+    return mask
+
+
+@pytest.mark.parametrize("M", [11264, 11000])
+def test_relu_bits_and_gate_bits(dev, M):
+    """MLP hidden layer in 1-bit form: the forward's relu_bits equal (stored h > 0) under the
+    documented layout, and the gated input gradient from gate_bits is bit-identical (values and
+    epilogue column sums) to the one gated by h itself."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    N, K = 1536, 384
+    assert Kn.gemm_bits_supported(M, N, K)
+    g = torch.Generator().manual_seed(M)
+    y, w1 = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    bias = (torch.randn(N, generator=g) * 0.5).to(dev)
+    rng = torch.tensor([11, 3], dtype=torch.int32, device=dev)
+    bits = torch.empty((-(-M // 256) * 256, N // 32), dtype=torch.int32, device=dev)
+    h = Kn.gemm(y, w1, False, True, bias=bias, act=Kn.ACT_RELU, rng=rng, drop_layer=1, drop_site=2,
+                keep_prob=0.9, relu_bits=bits)
+    h_ref = Kn.gemm(y, w1, False, True, bias=bias, act=Kn.ACT_RELU, rng=rng, drop_layer=1,
+                    drop_site=2, keep_prob=0.9)
+    assert torch.equal(h, h_ref)
+    torch.testing.assert_close(_bits_to_mask(bits, M, N), h.float() > 0, rtol=0, atol=0)
+    dz2, w2t = _mk((M, K), dev, g), _mk((N, K), dev, g)  # dX of a Dense with W2^T (N, K)
+    rows = Kn.gemm_colsum_rows(M, N, K)
+    cs_a = torch.empty((rows, N), device=dev)
+    cs_b = torch.empty((rows, N), device=dev)
+    d_a = Kn.gemm(dz2, w2t, False, True, gate=h, gate_scale=1 / 0.9, colsum=cs_a)
+    d_b = Kn.gemm(dz2, w2t, False, True, gate_bits=bits, gate_scale=1 / 0.9, colsum=cs_b)
+    assert torch.equal(d_a, d_b)
+    assert torch.equal(cs_a, cs_b)
+    d_c = Kn.gemm(dz2, w2t, False, True, gate_bits=bits, gate_scale=1 / 0.9)  # no column sums
+    assert torch.equal(d_a, d_c)
+
+
+def test_bits_rejected_off_the_256_path(dev):
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    M, N, K = 300, 1536, 384
+    assert not Kn.gemm_bits_supported(M, N, K)
+    a, w = torch.zeros((M, K), dtype=torch.bfloat16, device=dev), torch.zeros((N, K), dtype=torch.bfloat16, device=dev)
+    with pytest.raises(ValueError):
+        Kn.gemm(a, w, False, True, relu_bits=torch.empty((512, N // 32), dtype=torch.int32, device=dev))
