@@ -6,6 +6,8 @@ here computes on the CPU: a missing library raises (see _C.py).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _C
@@ -224,6 +226,28 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
             b.stride(0), ptr(out), out_mode, out.stride(0), 1, 0, 0, 0, split_k,
             _C.ctypes.byref(e), ptr(ws), 0 if ws is None else ws.numel(), _C.stream_ptr())
     return out
+
+
+_BLASLT = os.environ.get("MMT_BLASLT", "1") != "0"  # benchmarking knob: every product on libmmt_hip
+
+
+def library_gemm_ok(M: int, N: int, K: int) -> bool:
+    """Plain (epilogue-free) NT products that hipBLASLt runs faster than this library's kernels
+    (tools/gemm_bench.py --torch, B = 512 shapes): narrow outputs (N <= 768) over a long
+    reduction (K >= 1536) — the MLP input gradient 141,312 x 384 x 1536 (189 vs 238 us) and the
+    frozen T5's FF output 16,384 x 768 x 3072 (64 vs 92 us). Everything with a fused epilogue
+    beyond a residual, and every other shape, stays on libmmt_hip."""
+    return _BLASLT and N <= 768 and K >= 1536 and M >= 8192
+
+
+def library_gemm_nt(a: torch.Tensor, b: torch.Tensor, residual: torch.Tensor | None = None,
+                    out: torch.Tensor | None = None) -> torch.Tensor:
+    """bf16 a (M, K) . b (N, K)^T [+ residual (M, N) bf16] on hipBLASLt (torch.mm / addmm: fp32
+    accumulation, one bf16 rounding of the result — the same contract as gemm(..., OUT_BF16))."""
+    bt = b.t()
+    if residual is not None:
+        return torch.addmm(residual, a, bt, out=out) if out is not None else torch.addmm(residual, a, bt)
+    return torch.mm(a, bt, out=out) if out is not None else torch.mm(a, bt)
 
 
 def gemm_bits_supported(M: int, N: int, K: int, trans_a: bool = False, trans_b: bool = True,

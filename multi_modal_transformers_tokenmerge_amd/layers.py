@@ -115,8 +115,13 @@ class Dense:
             if self.b is not None and not bias_grad_done:
                 K.colsum(dy_colsum if dy_colsum is not None else dy2d, self.b.grad)
         def dgrad():
-            # dX = dY . W as an NT product on the transposed shadow W^T (in, out)
-            return K.gemm(dy2d, self.w.bf16_t, trans_b=True, out=dx_out, **dx_epi) if need_dx else None
+            # dX = dY . W as an NT product on the transposed shadow W^T (in, out); plain narrow
+            # long-K products on hipBLASLt (K.library_gemm_ok)
+            if not need_dx:
+                return None
+            if not dx_epi and K.library_gemm_ok(M, self.in_f, self.out_f):
+                return K.library_gemm_nt(dy2d, self.w.bf16_t, out=dx_out)
+            return K.gemm(dy2d, self.w.bf16_t, trans_b=True, out=dx_out, **dx_epi)
         if wgrad_overlap.active is None:
             wgrad()
             return dgrad()

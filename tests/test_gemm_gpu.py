@@ -146,3 +146,21 @@ def test_auto_split_small_m(dev):
     ref = a.float() @ w.float().t() + res.float()
     _close_bf16(o_auto, ref)
     _close_bf16(o_one, ref)
+
+
+@pytest.mark.parametrize("N,K,res", [(384, 1536, False), (768, 3072, True)])
+def test_library_gemm_plain_products(dev, N, K, res):
+    """The plain narrow long-K products routed to hipBLASLt (Dense input gradients, the frozen T5's
+    FF output + residual) agree with libmmt_hip's kernel on the same bf16 operands (fp32
+    accumulation either way: one bf16 rounding apart)."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    M = 8192
+    assert Kn.library_gemm_ok(M, N, K) == Kn._BLASLT
+    g = torch.Generator().manual_seed(N + K)
+    a, b = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    r = _mk((M, N), dev, g) if res else None
+    lib = Kn.library_gemm_nt(a, b, residual=r)
+    ours = Kn.gemm(a, b, False, True, residual=r)
+    ref = a.float() @ b.float().t() + (r.float() if res else 0.0)
+    _close_bf16(lib, ref)
+    _close_bf16(ours, ref)
