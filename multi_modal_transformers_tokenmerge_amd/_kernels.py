@@ -233,11 +233,13 @@ _BLASLT = os.environ.get("MMT_BLASLT", "1") != "0"  # benchmarking knob: every p
 
 def library_gemm_ok(M: int, N: int, K: int) -> bool:
     """Plain (epilogue-free) NT products that hipBLASLt runs faster than this library's kernels
-    (tools/gemm_bench.py --torch, B = 512 shapes): narrow outputs (N <= 768) over a long
-    reduction (K >= 1536) — the MLP input gradient 141,312 x 384 x 1536 (189 vs 238 us) and the
-    frozen T5's FF output 16,384 x 768 x 3072 (64 vs 92 us). Everything with a fused epilogue
-    beyond a residual, and every other shape, stays on libmmt_hip."""
-    return _BLASLT and N <= 768 and K >= 1536 and M >= 8192
+    (tools/blaslt_probe.py, B = 512 shapes, graph-timed): narrow outputs (N <= 768) over a long
+    reduction (K >= 1152) — the MLP input gradient 141,312 x 384 x 1536 (208 vs 241 us), the QKV
+    input gradient 149,504 x 384 x 1152 (156 vs 187 us) and the frozen T5's FF output + residual
+    16,384 x 768 x 3072 (80 vs 98 us). Shorter reductions (out-projection input gradient, T5
+    attention output) are faster here; everything with a fused epilogue beyond a residual stays
+    on libmmt_hip."""
+    return _BLASLT and N <= 768 and K >= 1152 and M >= 8192
 
 
 def library_gemm_nt(a: torch.Tensor, b: torch.Tensor, residual: torch.Tensor | None = None,
