@@ -164,3 +164,16 @@ def test_library_gemm_plain_products(dev, N, K, res):
     ref = a.float() @ b.float().t() + (r.float() if res else 0.0)
     _close_bf16(lib, ref)
     _close_bf16(ours, ref)
+
+
+def test_library_relu_product(dev):
+    """The frozen T5's FF input on hipBLASLt's relu epilogue equals libmmt_hip's relu product."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    M, N, K = 8192, 3072, 768
+    g = torch.Generator().manual_seed(5)
+    a, b = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    ref = torch.relu(a.float() @ b.float().t())
+    ours = Kn.gemm(a, b, False, True, act=Kn.ACT_RELU)
+    _close_bf16(ours, ref)
+    if Kn.library_relu_gemm_ok(M, N, K):
+        _close_bf16(Kn.library_relu_gemm_nt(a, b), ref)
