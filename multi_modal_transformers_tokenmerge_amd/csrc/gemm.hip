@@ -1258,9 +1258,9 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
 // register-staged gemm_big_kernel's geometry), K-steps of 64 tokens, two LDS stages of unpadded
 // [64][256] + [64][192] bf16 images (56 KB each) filled by buffer_load ... lds (no VGPR staging,
 // no ds_write pass: the register-staged kernel spent 56 KB of ds_write per K-step on top of the
-// fragment reads). The 16-B chunk c of k-row r sits at c ^ 2(r & 3) (applied to each lane's SOURCE
-// address, the DMA destination is lane-linear): the transposed fragment reads
-// (ds_read_b64_tr_b16, 4 k-rows x 2 chunks per 16 lanes) hit 8 distinct 4-bank groups.
+// fragment reads). The 16-B chunk c of k-row r sits at c ^ swA/swB(r) (applied to each lane's
+// SOURCE address, the DMA destination is lane-linear), so each 32-lane group of a transposed
+// fragment read (ds_read_b64_tr_b16: 4 k-rows x 64 B) covers the 64 banks once.
 // Columns past M / N read whatever lies there (only output rows / columns past M / N depend on
 // them, and those are not stored); rows past K read zeros (buffer range). One tile per workgroup,
 // so the K-loop carries no stores: the wait for a K-step's DMA is vmcnt(0) on nothing else.
@@ -1300,17 +1300,22 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
   const int m0 = tm * TN_BM, n0 = (t - tm * tiles_n) * TN_BN;
   const int kbeg = z * k_chunk, kend = min(K, kbeg + k_chunk);
   const int nk = max(0, (kend - kbeg + 63) / 64);
-  auto sw = [](int r) { return 2 * (r & 3); };
+  // chunk swizzles (16-B chunks of a k-row): A rows are 512 B (every row starts on bank 0), so
+  // the 4 k-rows of a transposed read take 4 disjoint 64-B slots: c ^ 4 (r & 3); B rows are
+  // 384 B (odd rows start half a bank window on), c ^ 2 (r & 3) keeps them apart (simulated for
+  // every fragment read; the A form 2 (r & 3) measured 29 % of LDS cycles in bank conflicts)
+  auto swA = [](int r) { return 4 * (r & 3); };
+  auto swB = [](int r) { return 2 * (r & 3); };
 
   // per-lane source offsets (bytes from the K-step's panel base) of this wave's DMA pieces
   int voff[G];
 #pragma unroll
   for (int p = 0; p < G; ++p) {
     if (p < GA) {  // A piece j = wave * GA + p: k-rows 2j, 2j + 1 (32 chunks each)
-      const int j = wave * GA + p, row = 2 * j + (lane >> 5), c = (lane & 31) ^ sw(row);
+      const int j = wave * GA + p, row = 2 * j + (lane >> 5), c = (lane & 31) ^ swA(row);
       voff[p] = row * (int)(lda * 2) + c * 16;
     } else {       // B piece j: 1 KB of the [64][192] image (24 chunks per k-row)
-      const int j = wave * GB + (p - GA), e = j * 64 + lane, row = e / 24, c = (e % 24) ^ sw(row);
+      const int j = wave * GB + (p - GA), e = j * 64 + lane, row = e / 24, c = (e % 24) ^ swB(row);
       voff[p] = row * (int)(ldb * 2) + c * 16;
     }
   }
@@ -1341,10 +1346,12 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
     const int col = rbase + 16 * (g16 & 1) + 4 * p4;
     const int k1 = ks * 16 + 8 * hl + q4;
     const int cofs = (col & 7) * 2;
+    const int s1 = rowb == A_ROWB ? swA(k1) : swB(k1);
+    const int s2 = rowb == A_ROWB ? swA(k1 + 4) : swB(k1 + 4);
     const short4v v1 = tr_read(reinterpret_cast<const bf16_t*>(
-        S + k1 * rowb + ((((col >> 3) ^ sw(k1))) << 4) + cofs));
+        S + k1 * rowb + ((((col >> 3) ^ s1)) << 4) + cofs));
     const short4v v2 = tr_read(reinterpret_cast<const bf16_t*>(
-        S + (k1 + 4) * rowb + ((((col >> 3) ^ sw(k1 + 4))) << 4) + cofs));
+        S + (k1 + 4) * rowb + ((((col >> 3) ^ s2)) << 4) + cofs));
     short __attribute__((ext_vector_type(8))) v = {v1[0], v1[1], v1[2], v1[3],
                                                    v2[0], v2[1], v2[2], v2[3]};
     return __builtin_bit_cast(bf16x8, v);
