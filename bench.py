@@ -124,8 +124,9 @@ def kernel_probes(model, B, reps=20):
     algorithmic work per launch (flops for MFMA-bound kernels, bytes for HBM-bound ones; DESIGN.md
     §3 states each figure). Covers the top of the step's trace: the nt256 GEMM (MLP up), the
     direct-to-LDS NT GEMM (MLP input gradient, N = 384, K = 1536), the split-K weight-gradient
-    GEMM (MLP Dense_0 dW), attention forward and backward (dQ + dK/dV), ToMe matching and merge
-    forward and the sequence-axis LayerNorm backward."""
+    GEMM (MLP Dense_0 dW), attention forward and backward (dQ + dK/dV), ToMe matching, the merge
+    forward alone and fused with LayerNorm_1 (the form the step runs), the fused LN_1 backward +
+    unmerge + dropout backward, and the sequence-axis LayerNorm forward and backward."""
     from multi_modal_transformers_tokenmerge_amd.layers import split_k_for
     cfg = model.cfg
     dev = model.device
@@ -195,7 +196,7 @@ def kernel_probes(model, B, reps=20):
     scale = Dh ** -0.5
     o, lse = K.attn_fwd(qkv, H, scale, table, bits, kpa)
     fwd_flops = 4.0 * L * L * Dh * H * B
-    add("attn_fwd", "attn_fwd_kernel",
+    add("attn_fwd", "attn_fwd_res_kernel" if K.attn_fwd_resident(L, Dh) else "attn_fwd_kernel",
         lambda: K.attn_fwd(qkv, H, scale, table, bits, kpa), "mfma", fwd_flops,
         f"B={B} L={L} H={H} Dh={Dh}: 4 L^2 Dh H B (dense count, masked tiles included)",
         B * L * (3 * D + D) * 2 + B * H * L * 4)
@@ -221,8 +222,36 @@ def kernel_probes(model, B, reps=20):
             lambda: K.tome_merge_fwd(x1, s0, t, r, unm, src, dst, size_in=None), "hbm",
             B * L * D * 4 + B * (L - r) * D * 4 + B * (t - r) * 4,
             "read the fp32 sequence, write the merged sequence and the token sizes")
-    # 7. sequence-axis LayerNorm backward (fp32 x, bf16 dy, fp32 addend and dx)
+        # 6b. what the step actually runs after the attention residual: the ToMe merge fused with
+        # LayerNorm_1's forward (one pass: merged fp32 sequence, sizes, pos_map, y bf16, stats)
+        gam = torch.ones(D, device=dev)
+        bet = torch.zeros(D, device=dev)
+        nidx = (t + 1) // 2 + r           # unm + src + dst indices read
+        add("tome_merge_seqnorm_fwd", "tome_merge_seqnorm_fwd_kernel",
+            lambda: K.tome_merge_seqnorm_fwd(x1, s0, t, r, unm, src, dst, gam, bet, 1e-6),
+            "hbm", B * L * D * 4 + B * (L - r) * D * (4 + 2) + B * (t - r) * 4 + B * t * 4
+            + 2 * B * D * 4 + B * nidx * 4,
+            "read the fp32 sequence; write the merged sequence (fp32), LN_1 output (bf16), sizes, "
+            "pos_map and the LN statistics (token_compression.py:90-129 + attention.py:66)")
+        # 6c. its backward: LayerNorm_1 backward + unmerge + attention-output dropout backward
+        xm, so, pos, _, mu1, rs1 = K.tome_merge_seqnorm_fwd(x1, s0, t, r, unm, src, dst, gam, bet, 1e-6)
+        L2 = L - r
+        dy1 = rnd(B, L2, D)
+        dx2 = rnd(B, L2, D, dt=torch.float32)
+        ggam, gbet, gb = (torch.zeros(D, device=dev) for _ in range(3))
+        if K.ln_unmerge_ok(L, L2):
+            add("ln_unmerge_dropout_bwd", "ln_unmerge_dropout_bwd_kernel",
+                lambda: K.ln_unmerge_dropout_bwd(dy1, xm, mu1, rs1, gam, ggam, gbet, dx2,
+                                                 (s0, t, r, pos, None, so), rng, 0, 1, 0.9, 0,
+                                                 bias_grad=gb),
+                "hbm", B * L2 * D * (2 + 4 + 4) + B * L * D * (4 + 2) + B * t * 4 + B * (t - r) * 4
+                + 2 * B * D * 4,
+                "read dy (bf16), x and the residual gradient (fp32); write the unmerged gradient "
+                "(fp32) and the dropout output (bf16)")
+    # 7. sequence-axis LayerNorm forward (fp32 residual stream -> bf16) and backward
     x = rnd(B, L1, D, dt=torch.float32)
+    add("seqnorm_fwd", "seqnorm_fwd_kernel", lambda: blk.ln1.fwd(x), "hbm",
+        B * L1 * D * (4 + 2) + 2 * B * D * 4, "read x (fp32); write y (bf16) and mean / rstd")
     _, mu, rs = blk.ln1.fwd(x)
     dy = rnd(B, L1, D)
     addend = rnd(B, L1, D, dt=torch.float32)

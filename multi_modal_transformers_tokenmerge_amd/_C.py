@@ -105,8 +105,18 @@ def lib():
                               "`python -m multi_modal_transformers_tokenmerge_amd.csrc.build` "
                               "(no CPU fallback exists by design)")
         import os
-        # benchmarking knob: A/B a second build of the same C ABI (never set on the product path)
-        h = ctypes.CDLL(os.environ.get("MMT_LIB_AB") or str(_LIB_PATH))
+        import sys
+        path = str(_LIB_PATH)
+        ab = os.environ.get("MMT_LIB_AB")
+        if ab:  # benchmarking knob: A/B a second build of the same C ABI from inside the build tree
+            p = Path(ab).resolve()
+            root = _LIB_PATH.resolve().parent.parent
+            if root not in p.parents or p.suffix != ".so":
+                raise ImportError(f"MMT_LIB_AB={ab!r}: only a .so inside {root} may replace "
+                                  f"{_LIB_PATH.name}")
+            print(f"[mmt] MMT_LIB_AB: loading {p} instead of {_LIB_PATH}", file=sys.stderr)
+            path = str(p)
+        h = ctypes.CDLL(path)
         h.mmt_last_error.restype = ctypes.c_char_p
         h.mmt_last_error.argtypes = []
         for name, args in SIGNATURES.items():

@@ -435,6 +435,13 @@ def _check_attn_bits(bits: torch.Tensor, L: int):
                          f"contiguous int32 {want}, got {tuple(bits.shape)}")
 
 
+def attn_fwd_resident(L: int, Dh: int, bias: bool = False) -> bool:
+    """Whether mmt_attn_fwd takes the K/V-resident kernel (attn_fwd_res_kernel: Dh 64,
+    32 < L <= 320, no additive bias; MMT_ATTN_RES=0 disables it) — csrc/attention.hip."""
+    import os
+    return os.environ.get("MMT_ATTN_RES", "1") != "0" and Dh == 64 and not bias and 32 < L <= 320
+
+
 def attn_fwd(qkv: torch.Tensor, H: int, scale: float, table: SetTable | None = None,
              drop_bits: torch.Tensor | None = None, keep_prob: float = 1.0,
              bias: torch.Tensor | None = None, out: torch.Tensor | None = None,
@@ -543,6 +550,17 @@ def seqnorm_dropout_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, addend, rng, la
             dx.stride(0), dx.stride(1), ptr(dgamma), ptr(dbeta), ptr(rng), layer, site, keep_prob,
             row_offset, ptr(z), z.stride(0), z.stride(1), ptr(colsum), _C.stream_ptr())
     return dx, z
+
+
+UNMERGE_MAX_L = 512          # csrc/norm.hip kUnmergeMax: unmerged rows per sample
+UNMERGE_MAX_L2 = 96 * 1024 // (64 * 4)   # the merged (L2, 64-column) fp32 panel in <= 96 KB LDS
+
+
+def ln_unmerge_ok(L: int, L2: int) -> bool:
+    """The shapes mmt_ln_unmerge_dropout_bwd accepts (its C-side check, csrc/norm.hip): at most
+    512 unmerged rows AND a merged panel of at most 384 rows; otherwise the caller takes the
+    three-kernel path (seqnorm_bwd -> tome_merge_bwd -> dropout_bwd)."""
+    return L <= UNMERGE_MAX_L and L2 <= UNMERGE_MAX_L2
 
 
 def ln_unmerge_dropout_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, addend, tome, rng, layer: int,

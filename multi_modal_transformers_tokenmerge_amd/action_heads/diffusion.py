@@ -18,7 +18,13 @@ import torch
 
 from .. import _C, _kernels as K
 from ..layers import Dense
-from ..params import ParamStore, he_normal
+from ..module_api import Bindable, init_from_spec, sget, spec
+from ..params import ParamStore
+
+_REF = "multi_modal_transformers."
+_REF_MLP = _REF + "attention_blocks.attention.MLPBlock"
+_REF_DENOISE = _REF + "action_heads.diffusion.OctoDenoise"
+_REF_FOURIER = _REF + "action_heads.diffusion.FourierFeatures"
 
 
 def cosine_beta_schedule(timesteps: int, s: float = 0.008) -> np.ndarray:
@@ -38,29 +44,121 @@ def alpha_hats_of(betas: np.ndarray) -> np.ndarray:
                     dtype=np.float32)
 
 
-class DiffusionActionHead:
-    def __init__(self, store: ParamStore, name: str, embedding_dim: int, action_dim: int = 8,
-                 diffusion_steps: int = 32, time_dim: int | None = None, hidden: int | None = None):
-        D = embedding_dim
-        self.D, self.A, self.steps = D, action_dim, diffusion_steps
-        self.F = (time_dim or D) // 2
-        T = 2 * self.F
-        self.time_dim = T
-        self.hidden = hidden or D
-        p = f"{name}/OctoDenoise_0"
-        self.fourier = store.add(f"{p}/FourierFeatures_0/fourier_kernel", (self.F, 1),
-                                 he_normal((self.F, 1)))
-        self.t1 = Dense(store, f"{p}/FourierFeatures_0/MLPBlock_0/Dense_0", T, T)
-        self.t2 = Dense(store, f"{p}/FourierFeatures_0/MLPBlock_0/Dense_1", T, T)
-        self.cat_dim = action_dim + T + D
-        self.d1 = Dense(store, f"{p}/MLPBlock_0/Dense_0", self.cat_dim, self.hidden)
-        self.d2 = Dense(store, f"{p}/MLPBlock_0/Dense_1", self.hidden, action_dim)
-        betas = cosine_beta_schedule(diffusion_steps)
+class DiffusionActionHead(Bindable):
+    """Reference :68-209: ``DiffusionActionHead(diffusion_steps, attention_pooling,
+    denoising_model, rng_collection="diffusion")`` with the model_configs/action_heads/diffusion.yaml
+    nodes: ``denoising_model`` = OctoDenoise(time_encoder = FourierFeatures(output_dim, kernel_init,
+    mlp_block), num_blocks, mlp_block) (:30-65). ``attention_pooling`` is accepted and unused, as in
+    the reference (the pooling call is commented out, :99-102: the readouts are averaged).
+    ``denoise_loss(readouts, actions)``, ``predict_denoise_term(readouts, time, noisy_actions)`` and
+    ``predict_action(readouts)`` take the readout tokens (B, n, D) like the reference; the Octo
+    training path feeds the readout MEAN straight from the backbone's fused rows-mean kernel
+    (``loss_forward`` / ``*_mean``)."""
+
+    def __init__(self, diffusion_steps: int = 32, attention_pooling=None, denoising_model=None,
+                 rng_collection: str = "diffusion"):
+        self.steps = int(diffusion_steps)
+        self.rng_collection = rng_collection
+        self.attention_pooling = attention_pooling
+        dm = spec(denoising_model)
+        te = spec(sget(dm, "time_encoder"))
+        if int(sget(dm, "num_blocks", 1)) != 1:
+            raise NotImplementedError("OctoDenoise num_blocks != 1 (the reference configs use 1)")
+        mlp = spec(sget(dm, "mlp_block"))
+        self.time_dim_cfg = sget(te, "output_dim")
+        self.fourier_init = sget(te, "kernel_init")
+        tm = spec(sget(te, "mlp_block"))
+        self.time_mlp_cfg = (sget(getattr(tm, "dense_spec", None), "features"),
+                             sget(getattr(tm, "dense_out_spec", None), "features"))
+        self.hidden_cfg = sget(getattr(mlp, "dense_spec", None), "features")
+        self.A = int(sget(getattr(mlp, "dense_out_spec", None), "features", 8))
+        betas = cosine_beta_schedule(self.steps)
         self.betas_np = betas
         self.alpha_hats_np = alpha_hats_of(betas)
         self._dev_consts = {}
+
+    @classmethod
+    def create(cls, store: ParamStore, name: str, embedding_dim: int, action_dim: int = 8,
+               diffusion_steps: int = 32, time_dim: int | None = None,
+               hidden: int | None = None) -> "DiffusionActionHead":
+        """The head from its dimensions, declared in ``store`` (the Octo model's path)."""
+        D = embedding_dim
+        T = time_dim or D
+
+        def mlp(h, o):
+            return {"_target_": _REF_MLP, "dense": {"_target_": "flax.linen.Dense", "features": h},
+                    "dense_out": {"_target_": "flax.linen.Dense", "features": o}}
+        dm = {"_target_": _REF_DENOISE, "num_blocks": 1,
+              "time_encoder": {"_target_": _REF_FOURIER, "output_dim": T, "mlp_block": mlp(T, T)},
+              "mlp_block": mlp(hidden or D, action_dim)}
+        return cls(diffusion_steps, None, dm).bind(store, name, D)
+
+    def _declare(self, store: ParamStore, name: str, embedding_dim: int):
+        D = embedding_dim
+        self.D = D
+        T0 = int(self.time_dim_cfg or D)
+        self.F = T0 // 2
+        T = 2 * self.F
+        t_h, t_o = self.time_mlp_cfg
+        if (t_h is not None and int(t_h) != T) or (t_o is not None and int(t_o) != T):
+            raise NotImplementedError("FourierFeatures' MLPBlock must keep the output_dim width")
+        self.time_dim = T
+        self.hidden = int(self.hidden_cfg or D)
+        p = f"{name}/OctoDenoise_0"
+        self.fourier = store.add(f"{p}/FourierFeatures_0/fourier_kernel", (self.F, 1),
+                                 init_from_spec(self.fourier_init, (self.F, 1)))
+        self.t1 = Dense(store, f"{p}/FourierFeatures_0/MLPBlock_0/Dense_0", T, T)
+        self.t2 = Dense(store, f"{p}/FourierFeatures_0/MLPBlock_0/Dense_1", T, T)
+        self.cat_dim = self.A + T + D
+        self.d1 = Dense(store, f"{p}/MLPBlock_0/Dense_0", self.cat_dim, self.hidden)
+        self.d2 = Dense(store, f"{p}/MLPBlock_0/Dense_1", self.hidden, self.A)
         if self.cat_dim % 8:
             raise ValueError("action_dim + time_dim + D must be a multiple of 8 (16-B rows)")
+
+    # ------------------------------------------------------------- reference-signature methods
+    def _mean_into(self, readouts: torch.Tensor, out: torch.Tensor):
+        """mean over the readout axis (:102) of (B, n, D) readouts into a (B, D) bf16 view."""
+        if readouts.dim() != 3 or readouts.stride(2) != 1:
+            raise ValueError(f"readouts must be (batch, tokens, {self.D}) with unit inner stride")
+        B, n, D = readouts.shape
+        x = readouts if readouts.dtype == torch.float32 else readouts.float()
+        rows = torch.arange(n, dtype=torch.int32, device=readouts.device)
+        _C.call("mmt_rows_mean_fwd", _C.ptr(x), x.stride(0), x.stride(1), B, D, _C.ptr(rows), n,
+                _C.ptr(out), out.stride(0), _C.stream_ptr())
+        return out
+
+    def denoise_loss(self, readouts: torch.Tensor, actions: torch.Tensor, train: bool = True, *,
+                     rng=None, sample_offset: int = 0) -> torch.Tensor:
+        """Reference :110-143: t ~ U{0..steps-1}, eps ~ N(0, 1) from the 'diffusion' counter
+        stream (rng, keyed by the global sample index), noisy = sqrt(abar) a + sqrt(1 - abar) eps,
+        loss = mean_b sum_a 0.5 (pred - eps)^2. Returns the loss (1,) fp32 on the device."""
+        self._ensure(readouts.device, int(readouts.shape[-1]))
+        if rng is None:
+            raise ValueError("denoise_loss needs the diffusion rng (rng=)")
+        B = readouts.shape[0]
+        if tuple(actions.shape) != (B, self.A):
+            raise ValueError(f"actions must be ({B}, {self.A})")
+        cat = self.new_cat(B, readouts.device)
+        self._mean_into(readouts, self.readout_slot(cat))
+        loss, _ = self.loss_forward(cat, actions.float().contiguous(), rng, sample_offset)
+        return loss
+
+    def predict_denoise_term(self, readouts: torch.Tensor, time: torch.Tensor,
+                             noisy_actions: torch.Tensor, train: bool = True) -> torch.Tensor:
+        """Reference :88-107: OctoDenoise(noisy, time, mean(readouts)) -> (B, A) fp32."""
+        self._ensure(readouts.device, int(readouts.shape[-1]))
+        e = torch.empty((readouts.shape[0], self.D), dtype=torch.bfloat16, device=readouts.device)
+        return self.predict_denoise_term_mean(self._mean_into(readouts, e), time,
+                                              noisy_actions.float().contiguous())
+
+    def predict_action(self, readouts: torch.Tensor, train: bool = True, *, rng=None,
+                       sample_offset: int = 0, z: torch.Tensor | None = None,
+                       return_noise: bool = False):
+        """Reference :146-209: the 32-step DDPM sampler from the readouts (B, n, D)."""
+        self._ensure(readouts.device, int(readouts.shape[-1]))
+        e = torch.empty((readouts.shape[0], self.D), dtype=torch.bfloat16, device=readouts.device)
+        return self.predict_action_mean(self._mean_into(readouts, e), rng, sample_offset, z,
+                                        return_noise)
 
     def consts(self, device):
         if device not in self._dev_consts:
@@ -110,8 +208,8 @@ class DiffusionActionHead:
         return dcat[:, self.A + self.time_dim:]
 
     # ------------------------------------------------------------------ predict_denoise_term
-    def predict_denoise_term(self, readout_mean: torch.Tensor, time: torch.Tensor,
-                             noisy_actions: torch.Tensor) -> torch.Tensor:
+    def predict_denoise_term_mean(self, readout_mean: torch.Tensor, time: torch.Tensor,
+                                  noisy_actions: torch.Tensor) -> torch.Tensor:
         """Reference :88-107 (``OctoDenoise(noisy, time, mean(readouts))``) for given integer
         times (B,) or (B, 1) and noisy actions (B, A) fp32. Returns eps_hat (B, A) fp32."""
         B = readout_mean.shape[0]
@@ -167,8 +265,8 @@ class DiffusionActionHead:
         ht = self.t1.fwd(feats, act=K.ACT_RELU)
         return self.t2.fwd(ht)
 
-    def predict_action(self, readout_mean: torch.Tensor, rng=None, sample_offset: int = 0,
-                       z: torch.Tensor | None = None, return_noise: bool = False):
+    def predict_action_mean(self, readout_mean: torch.Tensor, rng=None, sample_offset: int = 0,
+                            z: torch.Tensor | None = None, return_noise: bool = False):
         """Reference :146-209 (the 32-step DDPM loop of jax.lax.scan) on the device.
         readout_mean: (B, D) bf16 = mean of the readout tokens (:102). The initial sample z is
         drawn from the counter stream (rng = the (seed, step) device tensor, keyed by the global

@@ -32,8 +32,10 @@ import torch
 from .. import _kernels as K
 from ..layers import (DROP_ATTN, DROP_ATTN_OUT, DROP_MLP_HIDDEN, DROP_MLP_OUT, Dense, wgrad_overlap,
                       SeqLayerNorm)
+from ..config_loader import LayerSpec
+from ..module_api import Bindable, init_from_spec, merge_param, sget, spec
 from ..params import ParamStore, he_normal, normal
-from ..tokenizers.token_sequencer import LayerSets
+from ..tokenizers.token_sequencer import LayerSets, sets_from_mask
 
 
 @dataclass
@@ -69,35 +71,164 @@ def side_stream(device) -> torch.cuda.Stream:
     return _SIDE[key]
 
 
-class MLPBlock:
-    """attention.py:20-39."""
+class MLPBlock(Bindable):
+    """attention.py:20-39: ``MLPBlock(dense, activation, norm, dense_out)(inputs, train=False)``
+    = Dense -> activation -> Dropout (``norm``) -> Dense -> Dropout. The fields are the reference's
+    config nodes (flax.linen.Dense features, flax.linen.relu, flax.linen.Dropout rate); the input
+    width is taken from the first call (nn.compact), or from ``bind``. On the device: the NT GEMM
+    with a fused bias + relu + dropout epilogue, then the GEMM with bias + dropout."""
 
-    def __init__(self, store: ParamStore, name: str, in_f: int, hidden: int, out_f: int,
-                 dropout_rate: float = 0.1, fp8: bool = False):
-        self.dense = Dense(store, f"{name}/Dense_0", in_f, hidden, fp8=fp8)
-        self.dense_out = Dense(store, f"{name}/Dense_1", hidden, out_f, fp8=fp8)
-        self.rate = dropout_rate
+    fp8 = False
+
+    def __init__(self, dense=None, activation=None, norm=None, dense_out=None):
+        self.dense_spec, self.activation, self.norm, self.dense_out_spec = \
+            spec(dense), spec(activation), spec(norm), spec(dense_out)
+        act = getattr(self.activation, "target", "flax.linen.relu") if self.activation is not None \
+            else "flax.linen.relu"
+        if not act.endswith(".relu"):
+            raise NotImplementedError(f"MLPBlock activation {act!r}: the fused GEMM epilogue is relu")
+        self.rate = float(sget(self.norm, "rate", 0.0))
+        self.dense = self.dense_out = None
+
+    @classmethod
+    def create(cls, store: ParamStore, name: str, in_f: int, hidden: int, out_f: int,
+               dropout_rate: float = 0.1, fp8: bool = False) -> "MLPBlock":
+        """The block from its dimensions, declared in ``store`` (the Octo model's path)."""
+        m = cls(LayerSpec("flax.linen.Dense", {"features": hidden}),
+                LayerSpec("flax.linen.relu", partial=True),
+                LayerSpec("flax.linen.Dropout", {"rate": dropout_rate}),
+                LayerSpec("flax.linen.Dense", {"features": out_f}))
+        m.fp8 = fp8
+        return m.bind(store, name, in_f)
+
+    def _declare(self, store, name, in_f):
+        hidden = int(sget(self.dense_spec, "features"))
+        out_f = int(sget(self.dense_out_spec, "features"))
+        self.dense = Dense(store, f"{name}/Dense_0", in_f, hidden, fp8=self.fp8,
+                           kernel_init=init_from_spec(sget(self.dense_spec, "kernel_init"), (in_f, hidden)),
+                           bias_init=init_from_spec(sget(self.dense_spec, "bias_init"), (hidden,), normal(0.01)))
+        self.dense_out = Dense(store, f"{name}/Dense_1", hidden, out_f, fp8=self.fp8,
+                               kernel_init=init_from_spec(sget(self.dense_out_spec, "kernel_init"), (hidden, out_f)),
+                               bias_init=init_from_spec(sget(self.dense_out_spec, "bias_init"), (out_f,), normal(0.01)))
+
+    def __call__(self, inputs: torch.Tensor, train: bool = False, *, rng=None, layer: int = 0,
+                 sample_offset: int = 0) -> torch.Tensor:
+        """inputs (..., in) fp32 / bf16 device tensor -> (..., out) fp32. train=True applies the
+        two dropouts with the counter RNG ``rng`` (a (seed, step) int32 device tensor, the
+        'dropout' collection of the reference), keyed by (layer, site, row)."""
+        self._ensure(inputs.device, int(inputs.shape[-1]))
+        lead = inputs.shape[:-1]
+        x2 = inputs.reshape(-1, inputs.shape[-1])
+        if x2.dtype != torch.bfloat16:
+            x2 = K.cast_f32_bf16(x2.float().contiguous(),
+                                 torch.empty(x2.shape, dtype=torch.bfloat16, device=x2.device))
+        drop = self.rate > 0.0 and train
+        if drop and rng is None:
+            raise ValueError("MLPBlock(train=True) needs the dropout rng (rng=)")
+        kp = 1.0 - self.rate
+
+        def epi(site):
+            return dict(rng=rng, drop_layer=layer, drop_site=site, keep_prob=kp,
+                        drop_row_offset=sample_offset) if drop else {}
+        h = self.dense.fwd(x2.contiguous(), act=K.ACT_RELU, **epi(DROP_MLP_HIDDEN))
+        y = self.dense_out.fwd(h, out_mode=K.OUT_F32, **epi(DROP_MLP_OUT))
+        return y.view(*lead, y.shape[-1])
 
 
-class Encoder1DBlock:
-    """attention.py:41-69 (+ ToMe between the attention residual and LN1)."""
+class Encoder1DBlock(Bindable):
+    """attention.py:41-69 (+ ToMe between the attention residual and LN1 on the Octo path).
 
-    def __init__(self, store: ParamStore, name: str, D: int, num_heads: int, mlp_dim: int,
-                 eps: float = 1e-6, dropout_rate: float = 0.1, attn_dropout_rate: float = 0.1,
-                 fp8: bool = False):
-        if D % num_heads:
+    ``Encoder1DBlock(layer_norm, dropout, self_attention, mlp_block, train=None, mask=None)`` with
+    the reference's config nodes: flax.linen.LayerNorm (epsilon; reduction over the SEQUENCE
+    axis, reduction_axes [1], vanilla_decoder.yaml:5-13), flax.linen.Dropout (rate),
+    flax.linen.SelfAttention (num_heads, qkv_features = the input width, dropout_rate,
+    kernel_init, bias_init) and an MLPBlock node (or MLPBlock). ``__call__(inputs, mask=None,
+    train=None) -> (x, None)`` as the reference (train / mask from the constructor or the call,
+    flax merge_param); the dense mask is converted to the token-set table the kernels evaluate
+    (token_sequencer.sets_from_mask). Differentiable through torch autograd: the backward runs
+    the block's explicit backward kernels and accumulates the parameter gradients in the store's
+    flat gradient buffer (the ``grads`` of the reference's value_and_grad)."""
+
+    fp8 = False
+
+    def __init__(self, layer_norm=None, dropout=None, self_attention=None, mlp_block=None,
+                 train=None, mask=None):
+        self.layer_norm, self.dropout, self.self_attention = spec(layer_norm), spec(dropout), \
+            spec(self_attention)
+        mlp = spec(mlp_block)
+        if mlp is None:
+            raise ValueError("Encoder1DBlock needs an mlp_block")
+        if not isinstance(mlp, MLPBlock):
+            raise TypeError(f"mlp_block must be an MLPBlock node, got {type(mlp).__name__}")
+        self.mlp = mlp
+        self.train, self.mask = train, mask
+        ra = sget(self.layer_norm, "reduction_axes", [1])
+        ra = list(ra) if isinstance(ra, (list, tuple)) else [ra]
+        if ra != [1]:
+            raise NotImplementedError(f"LayerNorm reduction_axes {ra}: the build normalises over the "
+                                      "sequence axis, reduction_axes [1] (vanilla_decoder.yaml:10)")
+        self.eps = float(sget(self.layer_norm, "epsilon", 1e-6))
+        self.rate = float(sget(self.dropout, "rate", 0.0))
+        self.H = int(sget(self.self_attention, "num_heads", 1))
+        self.attn_rate = float(sget(self.self_attention, "dropout_rate", 0.0))
+
+    @classmethod
+    def create(cls, store: ParamStore, name: str, D: int, num_heads: int, mlp_dim: int,
+               eps: float = 1e-6, dropout_rate: float = 0.1, attn_dropout_rate: float = 0.1,
+               fp8: bool = False) -> "Encoder1DBlock":
+        """The block from its dimensions, declared in ``store`` (the Octo model's path)."""
+        blk = cls(LayerSpec("flax.linen.LayerNorm", {"epsilon": eps, "reduction_axes": [1],
+                                                     "feature_axes": [-1]}),
+                  LayerSpec("flax.linen.Dropout", {"rate": dropout_rate}),
+                  LayerSpec("flax.linen.SelfAttention", {"num_heads": num_heads, "qkv_features": D,
+                                                         "dropout_rate": attn_dropout_rate}),
+                  MLPBlock(LayerSpec("flax.linen.Dense", {"features": mlp_dim}),
+                           LayerSpec("flax.linen.relu", partial=True),
+                           LayerSpec("flax.linen.Dropout", {"rate": dropout_rate}),
+                           LayerSpec("flax.linen.Dense", {"features": D})))
+        blk.fp8 = fp8
+        return blk.bind(store, name, D)
+
+    def _declare(self, store: ParamStore, name: str, D: int):
+        qkv_f = sget(self.self_attention, "qkv_features")
+        if qkv_f is not None and int(qkv_f) != D:
+            raise ValueError(f"qkv_features {qkv_f} != the input width {D} (the fused QKV projection)")
+        if D % self.H:
             raise ValueError("qkv_features must be divisible by num_heads")
-        self.D, self.H, self.Dh, self.M = D, num_heads, D // num_heads, mlp_dim
-        self.ln0 = SeqLayerNorm(store, f"{name}/LayerNorm_0", D, eps)
-        self.qkv = Dense(store, f"{name}/SelfAttention_0/qkv", D, 3 * D, kernel_init=he_normal((D, D)),
-                         fp8=fp8)
-        self.out = Dense(store, f"{name}/SelfAttention_0/out", D, D, kernel_init=he_normal((D, D)),
-                         fp8=fp8)
-        self.ln1 = SeqLayerNorm(store, f"{name}/LayerNorm_1", D, eps)
-        self.mlp = MLPBlock(store, f"{name}/MLPBlock_0", D, mlp_dim, D, dropout_rate, fp8=fp8)
-        self.rate = dropout_rate
-        self.attn_rate = attn_dropout_rate
+        self.D, self.Dh = D, D // self.H
+        sa = self.self_attention
+        kinit = lambda: init_from_spec(sget(sa, "kernel_init"), (D, D))   # noqa: E731
+        binit = init_from_spec(sget(sa, "bias_init"), (D,), normal(0.01))
+        self.ln0 = SeqLayerNorm(store, f"{name}/LayerNorm_0", D, self.eps)
+        self.qkv = Dense(store, f"{name}/SelfAttention_0/qkv", D, 3 * D, kernel_init=kinit(),
+                         bias_init=binit, fp8=self.fp8)
+        self.out = Dense(store, f"{name}/SelfAttention_0/out", D, D, kernel_init=kinit(),
+                         bias_init=binit, fp8=self.fp8)
+        self.ln1 = SeqLayerNorm(store, f"{name}/LayerNorm_1", D, self.eps)
+        self.mlp.fp8 = self.fp8
+        self.mlp.bind(store, f"{name}/MLPBlock_0", D)
+        if self.mlp.dense_out.out_f != D:
+            raise ValueError("mlp_block.dense_out.features must equal the input width (residual)")
+        self.M = self.mlp.dense.out_f
         self.scale = self.Dh ** -0.5
+
+    def __call__(self, inputs: torch.Tensor, mask=None, train=None, *, rng=None, layer: int = 0,
+                 sample_offset: int = 0):
+        """inputs (B, L, D) -> (x, None), x fp32 (B, L, D). ``mask``: the dense reference mask
+        (or a token-set table); ``rng``: the 'dropout' collection, a (seed, step) int32 device
+        tensor (needed when train and a rate > 0); ``layer`` / ``sample_offset`` key the dropout
+        streams like the Octo path (block index, global index of the first sample)."""
+        train = bool(merge_param("train", self.train, train))
+        mask = merge_param("mask", self.mask, mask)
+        if inputs.dim() != 3:
+            raise ValueError(f"inputs must be (batch, length, features), got {tuple(inputs.shape)}")
+        self._ensure(inputs.device, int(inputs.shape[-1]))
+        ctx = LayerCtx(layer=layer, sets=None, table=set_table_of(mask, inputs.shape[1]),
+                       train=train, rng=rng, sample_offset=sample_offset)
+        if train and (self.rate > 0 or self.attn_rate > 0) and rng is None:
+            raise ValueError("Encoder1DBlock(train=True) needs the dropout rng (rng=)")
+        x = inputs.float().contiguous()
+        return _EncoderBlockFn.apply(x, self, ctx), None
 
     # ------------------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, ctx: LayerCtx, size: Optional[torch.Tensor]):
@@ -206,7 +337,8 @@ class Encoder1DBlock:
         # dX of the LN-fed Dense in bf16 (the LN backward accumulates in fp32): halves its traffic
         dy1 = self.mlp.dense.bwd(dz1, sv["y1"].view(B * L2, D), dy_colsum=cs)
         Lo = sv["o_in"].shape[1]
-        if sv["tome"] is not None and Lo <= 512 and sv["x1"].dtype == torch.float32:
+        if (sv["tome"] is not None and K.ln_unmerge_ok(Lo, L2)
+                and sv["x1"].dtype == torch.float32):
             # LayerNorm_1 backward + unmerge + attention-output dropout backward in one pass (the
             # merged-layout gradient never reaches HBM)
             dx1, dzo = K.ln_unmerge_dropout_bwd(
@@ -243,16 +375,118 @@ class Encoder1DBlock:
         return self.ln0.bwd(dy0.view(B, L, D), sv["x"], sv["mu0"], sv["rs0"], addend=dx1), None
 
 
-class StackedEncoder1DBlock:
-    """attention.py:87-119 (nn.scan over identical blocks). With ToMe the sequence shrinks per
-    block, so the stack is a Python loop over per-block parameter sets (names Block_{i})."""
+def set_table_of(mask, L: int) -> K.SetTable:
+    """The kernels' token-set table for a reference mask (dense array / tensor), a LayerSets, or
+    an existing SetTable."""
+    if isinstance(mask, K.SetTable):
+        sets = mask
+    else:
+        ls = mask if isinstance(mask, LayerSets) else sets_from_mask(mask)
+        sets = K.SetTable(ls.starts, ls.lens, ls.vis, ls.causal)
+    if sets.L != L:
+        raise ValueError(f"mask covers {sets.L} tokens, inputs have {L}")
+    return sets
 
-    def __init__(self, store: ParamStore, name: str, num_blocks: int, D: int, num_heads: int,
-                 mlp_dim: int, eps: float = 1e-6, dropout_rate: float = 0.1,
-                 attn_dropout_rate: float = 0.1, fp8: bool = False):
-        self.blocks = [Encoder1DBlock(store, f"{name}/Block_{i}", D, num_heads, mlp_dim, eps,
-                                      dropout_rate, attn_dropout_rate, fp8)
-                       for i in range(num_blocks)]
+
+class _EncoderBlockFn(torch.autograd.Function):
+    """One Encoder1DBlock under torch autograd: forward/backward are the block's explicit
+    kernel schedules; parameter gradients go to the store's flat gradient buffer."""
+
+    @staticmethod
+    def forward(fctx, x, blk, ctx):
+        y, sv, _ = blk.forward(x, ctx, None)
+        fctx.blk, fctx.ctx, fctx.sv = blk, ctx, sv
+        return y
+
+    @staticmethod
+    def backward(fctx, dy):
+        dx, _ = fctx.blk.backward(dy.float().contiguous(), fctx.sv, fctx.ctx)
+        fctx.sv = None
+        return dx, None, None
+
+
+class _StackFn(torch.autograd.Function):
+    """posembed_input + the blocks under torch autograd (StackedEncoder1DBlock.__call__)."""
+
+    @staticmethod
+    def forward(fctx, x, stack, ctxs):
+        y, saved = stack.forward(stack.pos(x), ctxs)
+        fctx.stack, fctx.ctxs, fctx.saved = stack, ctxs, saved
+        return y
+
+    @staticmethod
+    def backward(fctx, dy):
+        dx = fctx.stack.backward(dy.float().contiguous(), fctx.saved, fctx.ctxs)
+        fctx.stack.pos.backward(dx)      # d(pos_embedding) += column sums over the batch
+        fctx.saved = None
+        return dx, None, None
+
+
+class StackedEncoder1DBlock(Bindable):
+    """attention.py:87-119: ``StackedEncoder1DBlock(num_blocks, encoder_1d_block)(x, train=False,
+    mask=None)`` = x + posembed_input (AddPositionEmbedding, normal(0.02)), then num_blocks
+    Encoder1DBlocks built from the ``encoder_1d_block`` node (nn.scan over identical blocks in the
+    reference). With ToMe the sequence shrinks per block, so the stack is a Python loop over
+    per-block parameter sets (names Block_{i}); the Octo path drives ``forward`` / ``backward``
+    with per-layer contexts (token-set tables, ToMe / pruning) directly."""
+
+    def __init__(self, num_blocks: int = 1, encoder_1d_block=None):
+        self.num_blocks = int(num_blocks)
+        node = encoder_1d_block
+        if isinstance(node, Encoder1DBlock):
+            raise TypeError("encoder_1d_block must be the block's config node (one block per layer "
+                            "is built from it)")
+        self.block_node = node
+        self.blocks: List[Encoder1DBlock] = []
+        self.pos = None
+
+    def _make_block(self) -> Encoder1DBlock:
+        node = self.block_node
+        if node is None:
+            raise ValueError("StackedEncoder1DBlock needs encoder_1d_block")
+        if isinstance(node, dict):
+            kw = {k: v for k, v in node.items() if k not in ("_target_", "_partial_", "_recursive_")}
+            return Encoder1DBlock(**kw)
+        return Encoder1DBlock(node.layer_norm, node.dropout, node.self_attention, node.mlp)
+
+    @classmethod
+    def create(cls, store: ParamStore, name: str, num_blocks: int, D: int, num_heads: int,
+               mlp_dim: int, eps: float = 1e-6, dropout_rate: float = 0.1,
+               attn_dropout_rate: float = 0.1, fp8: bool = False) -> "StackedEncoder1DBlock":
+        """The stack's blocks declared in ``store`` (the Octo model's path; its posembed_input
+        is declared by the model, which adds it inside the fused sequence assembly)."""
+        st = cls(num_blocks, None)
+        st.blocks = [Encoder1DBlock.create(store, f"{name}/Block_{i}", D, num_heads, mlp_dim, eps,
+                                           dropout_rate, attn_dropout_rate, fp8)
+                     for i in range(num_blocks)]
+        st._store, st._name = store, name
+        return st
+
+    def _declare(self, store: ParamStore, name: str, L: int, D: int):
+        from ..tokenizers.readout.readout import AddPositionEmbedding
+        self.pos = AddPositionEmbedding(normal(0.02)).bind(store, f"{name}/posembed_input", L, D)
+        self.blocks = [self._make_block().bind(store, f"{name}/Block_{i}", D)
+                       for i in range(self.num_blocks)]
+
+    def __call__(self, x: torch.Tensor, train: bool = False, mask=None, *, rng=None,
+                 sample_offset: int = 0) -> torch.Tensor:
+        """x (B, L, D) -> (B, L, D) fp32: posembed_input, then the blocks with the same mask
+        (train / mask forwarded to every block, attention.py:111-117)."""
+        if x.dim() != 3:
+            raise ValueError(f"x must be (batch, length, features), got {tuple(x.shape)}")
+        B, L, D = x.shape
+        self._ensure(x.device, L, D)
+        if self.pos is None:
+            raise RuntimeError("this stack was built by create() without posembed_input; call "
+                               "forward() with per-layer contexts")
+        if mask is None:
+            raise ValueError('"mask" must be set (merge_param of Encoder1DBlock, attention.py:55)')
+        table = set_table_of(mask, L)
+        if train and rng is None:
+            raise ValueError("StackedEncoder1DBlock(train=True) needs the dropout rng (rng=)")
+        ctxs = [LayerCtx(layer=i, sets=None, table=table, train=bool(train), rng=rng,
+                         sample_offset=sample_offset) for i in range(self.num_blocks)]
+        return _StackFn.apply(x.float().contiguous(), self, ctxs)
 
     def forward(self, x, ctxs: List[LayerCtx]):
         saved = []

@@ -25,6 +25,8 @@
 // LDS and prefetched through registers one tile ahead: one barrier per tile.
 #include <math.h>
 
+#include <algorithm>
+
 #include <type_traits>
 
 #include "common.h"
@@ -186,10 +188,12 @@ __device__ __forceinline__ bf16x8 row_frag_global(const bf16_t* rowp, bool valid
 // 256 B per wave), instead of a bit extraction per score.
 __host__ __device__ __forceinline__ int lp_of(int L) { return (L + 63) & ~63; }
 __device__ __forceinline__ int key_of_pos(int p) { return (p & ~7) | ((p & 1) << 2) | ((p >> 1) & 3); }
+// v ? keep : 0 with the condition straight from the SGPR pair (one v_cndmask). Written with the
+// inverse-ballot builtin, not inline asm: the compiler's hazard recognizer does not look inside
+// an asm statement, and a v_cndmask in asm reading a v_exp_f32 result in the next cycle read the
+// stale register (gfx950 trans-forwarding hazard: wrong P on some lanes, non-deterministically).
 __device__ __forceinline__ float sel_keep(float v, uint64_t m) {
-  float r;
-  asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(v), "s"(m));
-  return r;
+  return __builtin_amdgcn_inverse_ballot_w64(m) ? v : 0.f;
 }
 // The N lane masks of one (word, tile or 32-wide sub-tile at t0): wave-uniform address, so
 // these are scalar loads (indices into m[] must be compile-time constants to stay in SGPRs).
@@ -204,12 +208,17 @@ struct TileMasks {
   }
 };
 
-// Pack accumulator registers 8s..8s+7 to a bf16 operand fragment.
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+// two floats -> one dword of two bf16 (RNE): a single v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t pk2(float a, float b) {
+  const float2v v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
+}
+// Pack accumulator registers 8s..8s+7 to a bf16 operand fragment (4 v_cvt_pk_bf16_f32).
 __device__ __forceinline__ bf16x8 pack_frag(const floatx16& x, int s) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (__bf16)x[8 * s + j];
-  return r;
+  const uint4 u = make_uint4(pk2(x[8 * s], x[8 * s + 1]), pk2(x[8 * s + 2], x[8 * s + 3]),
+                             pk2(x[8 * s + 4], x[8 * s + 5]), pk2(x[8 * s + 6], x[8 * s + 7]));
+  return __builtin_bit_cast(bf16x8, u);
 }
 
 // Column sums of output accumulators (rows = head dims d = 32 dsub + rbit(r) + 4 hh, columns =
@@ -536,6 +545,303 @@ __global__ __launch_bounds__(64 * NW, DH > 128 ? 1 : 2) void attn_fwd_kernel(
       if (WS) wsum[((int64_t)b * g.H + h) * L + q] = ld[i] * inv;  // sum_k of the dropped weights
     }
   }
+}
+
+// ===================================================== forward, K/V resident in LDS (Dh = 64)
+// For the short sequences of the training step (L <= 320: every OCTO-small / tiny layer) the
+// whole K and V of one (sample, head) fit in LDS (2 x 40 KB at L = 320), so a workgroup loads
+// them ONCE by DMA (buffer/global_load ... lds, no VGPR staging, no per-tile barrier) and its 4
+// waves then sweep their query blocks with no further synchronisation. Two such workgroups fill
+// the 160 KB of a CU: one computes while the other's DMA is in flight. Each wave keeps the
+// complete score row of its 32 queries in registers (<= 10 tiles x 16 fp32), so the softmax is
+// exact and two-pass (row max over all keys, then exp / sum / dropout / pack / P.V per tile):
+// no online rescale of O and no per-tile max bookkeeping.
+//   LDS image: K rows [0, 32 NTILE) then V rows, 128 B per row, 16-B chunk c of row r stored at
+//   chunk c ^ res_sw(r): conflict-free for the K row reads (ds_read_b128, 16 rows per lane group)
+//   AND the V transposed reads (ds_read_b64_tr_b16, 4 rows x 64 B per 32-lane half).
+//   Rows >= L are copies of row L - 1 (finite; their scores are masked and P = 0 there).
+// Query blocks are dealt to the 4 waves by the host (longest-first on the visible-tile counts).
+constexpr int RES_TILES = 10;  // 32-key tiles: L <= 320
+constexpr int RES_NW = 4;
+constexpr int RES_SLOTS = 4;   // query blocks per wave (<= 10 blocks over 4 waves)
+
+struct ResPlan {
+  uint32_t tword[MAX_SETS][RES_TILES];  // visible keys [32 t, 32 t + 32) of query set s (bit j)
+  uint8_t wblk[RES_NW][RES_SLOTS];      // query blocks of each wave, 0xff-terminated
+};
+
+// max / sum of a lane's value and lane l ^ 32's (the two half-waves): one v_permlane32_swap
+// (lanes 0-31 of its first result keep their own value, lanes 32-63 get lane l - 32's; the
+// second result the other way round), no LDS round trip
+__device__ __forceinline__ float halves_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float halves_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+__host__ __device__ __forceinline__ int res_sw(int row) {
+  return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+}
+
+template <int NTILE, bool DROP, bool WS>
+__global__ __launch_bounds__(64 * RES_NW, 2) void attn_fwd_res_kernel(
+    Geo g, AttnMask mask, ResPlan plan, const uint32_t* __restrict__ drop_q, int drop_lp,
+    float drop_scale, bf16_t* __restrict__ o, int64_t o_s_b, int64_t o_s_t, float* __restrict__ lse,
+    float* __restrict__ wsum) {
+  constexpr int DH = 64, NS = 4, ROWS = 32 * NTILE;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * ROWS * DH];  // [K | V] images
+  const int bh = blockIdx.x, b = bh / g.H, h = bh - b * g.H;
+  const int lane = threadIdx.x & 63, hh = lane >> 5, lr = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int L = g.L, D = g.H * DH;
+  const bf16_t* base = g.qkv + (int64_t)b * g.s_b;
+  // ---- DMA K and V into LDS: one wave-instruction = 8 rows x 128 B
+  {
+    const bf16_t* kb = base + D + h * DH;
+    constexpr int PIECES = ROWS / 8;  // per tensor
+    for (int p = wave; p < 2 * PIECES; p += RES_NW) {
+      const int t = p >= PIECES, pr = p - t * PIECES;
+      const int row = 8 * pr + (lane >> 3);
+      const int c = (lane & 7) ^ res_sw(row);
+      const bf16_t* src = kb + t * D + (int64_t)min(row, L - 1) * g.s_t + 8 * c;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(smem + t * ROWS * DH + pr * 512),
+                                       16, 0, 0);
+    }
+  }
+  const float c2 = g.scale * LOG2E;
+  // per-lane LDS byte offsets of the K row fragments (row lr of a tile, chunk 2s + hh)
+  const int swr = res_sw(lr);
+  int koff[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) koff[s] = lr * 128 + 16 * ((2 * s + hh) ^ swr);
+  // V transposed-read offsets: rows 4 hh + (i >> 2) (+ 8), column 16 (g & 1) + 4 (i & 3) (+ 32 dd)
+  const int ti = lane & 15, tq = ti >> 2, tp = ti & 3, tg = lane >> 4;
+  const char* smc = reinterpret_cast<const char*>(smem);
+  const char* Vimg = smc + ROWS * DH * 2;
+  // the first query block's Q fragments, in flight with the DMA
+  int slot = 0;
+  int blk = plan.wblk[wave][0];
+  bf16x8 qf[NS];
+  auto load_q = [&](int bk) {
+    const int qq = 32 * bk + lr;
+    const bool ok = qq < L;
+    const bf16_t* qp = base + (int64_t)(ok ? qq : L - 1) * g.s_t + h * DH;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) qf[s] = row_frag_global(qp, ok, s, lane);
+  };
+  if (blk != 0xff) load_q(blk);
+  __syncthreads();  // the DMA landed (vmcnt(0) + barrier)
+
+  while (blk != 0xff) {  // wave-uniform
+    const int q0 = 32 * blk, q = q0 + lr;
+    const bool qv = q < L;
+    const int qc = qv ? q : L - 1;
+    const int sq = set_of(mask, qc);
+    const int sq0 = __builtin_amdgcn_readfirstlane(sq);
+    const bool causal_any = mask.causal != 0u;
+    // one query set over the block and no causal set: the visibility words are wave-uniform
+    const bool uni = !causal_any && __all(sq == sq0);
+    // visibility word of every key tile for this lane's query, fetched ONCE per block (a
+    // divergent kernarg read inside the tile loop made the compiler wait vmcnt(0) per tile,
+    // which also drained the next block's Q prefetch)
+    uint32_t vws[NTILE];
+    if (uni) {
+#pragma unroll
+      for (int t = 0; t < NTILE; ++t) vws[t] = plan.tword[sq0][t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < NTILE; ++t) {
+        uint32_t vw = plan.tword[sq][t];
+        if ((mask.causal >> sq) & 1u) {  // keys of its own set after q
+          const int a0 = max(q + 1 - 32 * t, 0), e0 = min(mask.start[sq] + mask.len[sq] - 32 * t, 32);
+          if (a0 < e0) vw &= ~(uint32_t)(bit_range(a0, e0));
+        }
+        vws[t] = vw;
+      }
+    }
+    // the row in two chunks of CH tiles (one O rescale between them) keeps the score registers
+    // at CH x 16 (10 tiles in one chunk spill)
+    constexpr int CH = NTILE > 6 ? (NTILE + 1) / 2 : NTILE;
+    floatx16 oacc[2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
+    float mrow = -INFINITY;
+    float l4[4] = {0.f, 0.f, 0.f, 0.f}, ld4[4] = {0.f, 0.f, 0.f, 0.f};  // 4 chains, not 1
+    int nblk = 0xff;
+    auto chunk = [&](auto t0c) {
+      constexpr int T0 = decltype(t0c)::value;
+      constexpr int TN = T0 + CH < NTILE ? T0 + CH : NTILE;
+      floatx16 S[CH];
+      bool act[CH];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = T0; t < TN; ++t) {
+        const uint32_t vw = vws[t];
+        act[t - T0] = !__all(vw == 0u);
+        if (act[t - T0]) {
+          floatx16 acc;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(smc + t * 4096 + koff[s]);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], acc, 0, 0, 0);
+          }
+          if (!__all(vw == 0xffffffffu)) {  // partially visible: masked scores -> -inf
+            const uint32_t w = vw >> (4 * hh);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int mk = bitmask_of(w, rbit(r));
+              acc[r] = __int_as_float((__float_as_int(acc[r]) & mk) | (~mk & (int)0xff800000u));
+            }
+          }
+          float m8[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) m8[r] = fmaxf(acc[2 * r], acc[2 * r + 1]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) m8[r] = fmaxf(m8[r], m8[r + 4]);
+          mx = fmaxf(mx, fmaxf(fmaxf(m8[0], m8[1]), fmaxf(m8[2], m8[3])));
+          S[t - T0] = acc;
+        }
+      }
+      if constexpr (TN == NTILE) {
+        // next block's Q under this block's last softmax and P.V (qf is dead now)
+        nblk = slot + 1 < RES_SLOTS ? plan.wblk[wave][slot + 1] : 0xff;
+        if (nblk != 0xff) load_q(nblk);
+      }
+      mx = halves_max(mx);
+      const float mn = fmaxf(mrow, mx);
+      const float mc = mn == -INFINITY ? 0.f : mn * c2;
+      if constexpr (T0 > 0) {  // rescale what the earlier chunk accumulated
+        const float alpha = fast_exp2(mrow * c2 - mc);  // mrow = -inf -> 0
+        if (!__all(alpha == 1.f)) {
+#pragma unroll
+          for (int d = 0; d < 2; ++d)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            l4[i] *= alpha;
+            ld4[i] *= alpha;
+          }
+        }
+      }
+      mrow = mn;
+#pragma unroll
+      for (int t = T0; t < TN; ++t) {
+        if (!act[t - T0]) continue;  // wave-uniform
+        TileMasks<16> dm;
+        if constexpr (DROP) dm.load(drop_q, drop_lp, blk, 32 * t);
+        floatx16 p;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float e = fast_exp2(fmaf(S[t - T0][r], c2, -mc));
+          l4[r & 3] += e;
+          if constexpr (DROP) e = sel_keep(e, dm.m[r]);
+          if constexpr (WS) ld4[r & 3] += e;
+          p[r] = e;
+        }
+        const bf16x8 p0 = pack_frag(p, 0), p1 = pack_frag(p, 1);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            // A = V^T[d][key]: keys 32 t + 16 ks + 4 hh + tq (+ 8), columns 32 d + 16 (tg & 1) + 4 tp
+            const int col = 32 * d + 16 * (tg & 1) + 4 * tp;
+            const int r1 = 32 * t + 16 * ks + 4 * hh + tq, r2 = r1 + 8;
+            const short4v va = tr_read(reinterpret_cast<const bf16_t*>(
+                Vimg + r1 * 128 + 16 * ((col >> 3) ^ res_sw(r1)) + 2 * (col & 7)));
+            const short4v vb = tr_read(reinterpret_cast<const bf16_t*>(
+                Vimg + r2 * 128 + 16 * ((col >> 3) ^ res_sw(r2)) + 2 * (col & 7)));
+            const short8v vv = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
+            oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vv),
+                                                              ks ? p1 : p0, oacc[d], 0, 0, 0);
+          }
+        }
+      }
+    };
+    chunk(std::integral_constant<int, 0>{});
+    if constexpr (CH < NTILE) chunk(std::integral_constant<int, CH>{});
+    const float mx = mrow;
+    const float mc = mx == -INFINITY ? 0.f : mx * c2;
+    (void)mc;
+    float l = (l4[0] + l4[1]) + (l4[2] + l4[3]);
+    float ld = (ld4[0] + ld4[1]) + (ld4[2] + ld4[3]);
+    l = halves_sum(l);
+    if constexpr (WS) ld = halves_sum(ld);
+    const float inv = l > 0.f ? drop_scale / l : 0.f;
+    // O rows: lane pairs (q, hh) hold d = 32 dd + 8 r4 + 4 hh + {0..3}; one permlane32 swap per
+    // dword pairs r4 / r4 + 1 so that each lane stores 16 contiguous bytes (T21)
+    bf16_t* orow = o + (int64_t)b * o_s_b + (int64_t)qc * o_s_t + h * DH;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; r4 += 2) {
+        const uint32_t a0 = pk2(oacc[d][4 * r4] * inv, oacc[d][4 * r4 + 1] * inv);
+        const uint32_t a1 = pk2(oacc[d][4 * r4 + 2] * inv, oacc[d][4 * r4 + 3] * inv);
+        const uint32_t b0 = pk2(oacc[d][4 * r4 + 4] * inv, oacc[d][4 * r4 + 5] * inv);
+        const uint32_t b1 = pk2(oacc[d][4 * r4 + 6] * inv, oacc[d][4 * r4 + 7] * inv);
+        const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+        const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+        if (qv)
+          *reinterpret_cast<uint4*>(orow + 32 * d + 8 * r4 + 8 * hh) =
+              make_uint4(x0[0], x1[0], x0[1], x1[1]);
+      }
+    if (qv && lane < 32) {
+      const int64_t ri = ((int64_t)b * g.H + h) * L + q;
+      lse[ri] = l > 0.f ? mc * LN2 + logf(l) : -INFINITY;
+      if (WS) wsum[ri] = ld * inv;  // sum_k of the dropped weights
+    }
+    ++slot;
+    blk = nblk;
+  }
+}
+
+// Host plan of the resident forward: per-(query set, key tile) visibility words and the query
+// blocks of each wave (longest-processing-time first on the number of visible key tiles).
+static bool res_plan(const AttnMask& m, int L, ResPlan& plan) {
+  const int nt = (L + 31) / 32;
+  if (nt > RES_TILES) return false;
+  memset(&plan, 0, sizeof(plan));
+  for (int s = 0; s < m.n_sets; ++s)
+    for (int t = 0; t < nt; ++t) {
+      uint32_t w = 0;
+      for (int i = 0; i < m.n_sets; ++i) {
+        if (!((m.vis[s] >> i) & 1u) || m.len[i] <= 0) continue;
+        const int a = std::max(m.start[i] - 32 * t, 0), e = std::min(m.start[i] + m.len[i] - 32 * t, 32);
+        for (int j = a; j < e; ++j) w |= 1u << j;
+      }
+      plan.tword[s][t] = w;
+    }
+  memset(plan.wblk, 0xff, sizeof(plan.wblk));
+  int cost[RES_TILES], order[RES_TILES];
+  for (int i = 0; i < nt; ++i) {
+    // key tiles any query of block i sees (its query sets' words; causal sets: all of theirs)
+    uint32_t any[RES_TILES] = {0};
+    for (int s = 0; s < m.n_sets; ++s)
+      if (m.len[s] > 0 && m.start[s] < std::min(L, 32 * i + 32) && m.start[s] + m.len[s] > 32 * i)
+        for (int t = 0; t < nt; ++t) any[t] |= plan.tword[s][t];
+    cost[i] = 1;  // the block's fixed work (Q load, O store)
+    for (int t = 0; t < nt; ++t) cost[i] += any[t] ? 4 : 0;
+    order[i] = i;
+  }
+  std::sort(order, order + nt, [&](int a, int b) { return cost[a] > cost[b] || (cost[a] == cost[b] && a < b); });
+  int load[RES_NW] = {0}, cnt[RES_NW] = {0};
+  for (int k = 0; k < nt; ++k) {
+    int best = -1;
+    for (int w = 0; w < RES_NW; ++w)
+      if (cnt[w] < RES_SLOTS && (best < 0 || load[w] < load[best])) best = w;
+    if (best < 0) return false;
+    plan.wblk[best][cnt[best]++] = (uint8_t)order[k];
+    load[best] += cost[order[k]];
+  }
+  return true;
 }
 
 // =============================================================================== bwd: dQ
@@ -951,6 +1257,12 @@ int fill_mask(AttnMask& m, int n_sets, const int32_t* starts, const int32_t* len
 
 // forward query blocks per wave (0: automatic); MMT_ATTN_NQ=1..2 forces it (benchmarks)
 static const int g_attn_nq = getenv("MMT_ATTN_NQ") ? atoi(getenv("MMT_ATTN_NQ")) : 0;
+// the K/V-resident forward for Dh 64, 32 < L <= 320 (MMT_ATTN_RES=0: the streaming kernel;
+// read per call so one process can A/B both)
+static bool attn_res_enabled() {
+  const char* e = getenv("MMT_ATTN_RES");
+  return !e || atoi(e) != 0;
+}
 
 #define ATTN_DISPATCH(DH_, ...)                                  \
   do {                                                           \
@@ -1021,6 +1333,37 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   // (b, h)); beyond 256 rows one (3 blocks per wave spill registers; measured at B = 256:
   // L = 292 117.6 / 150.5 / 122.6 us for 1 / 2 / 3 blocks, L = 212 73.1 / 71.5 / 78.2,
   // L = 132 48.1 / 44.0 / 48.8). Dh 128 / 256 keep one (registers).
+  if (attn_res_enabled() && Dh == 64 && !bias && L > 32 && L <= 32 * RES_TILES) {
+    ResPlan plan;
+    if (res_plan(m, L, plan)) {
+      const int ntile = ((L + 63) / 64) * 2;  // even tile counts are instantiated
+#define RES1(NT_, DR_, WS_)                                                                       \
+  hipLaunchKernelGGL((attn_fwd_res_kernel<NT_, DR_, WS_>), dim3(B * H), dim3(64 * RES_NW), 0,     \
+                     as_stream(stream), g, m, plan, drop_bits, lp, dscale, (bf16_t*)o, o_s_b,     \
+                     o_s_t, lse, wsum)
+#define RES2(NT_)                                          \
+  do {                                                     \
+    if (drop_bits) {                                       \
+      if (wsum) RES1(NT_, true, true);                     \
+      else RES1(NT_, true, false);                         \
+    } else {                                               \
+      if (wsum) RES1(NT_, false, true);                    \
+      else RES1(NT_, false, false);                        \
+    }                                                      \
+  } while (0)
+      switch (ntile) {
+        case 2: RES2(2); break;
+        case 4: RES2(4); break;
+        case 6: RES2(6); break;
+        case 8: RES2(8); break;
+        default: RES2(10); break;
+      }
+#undef RES2
+#undef RES1
+      MMT_CHECK_LAUNCH("mmt_attn_fwd");
+      return MMT_OK;
+    }
+  }
   int nq = g_attn_nq > 0 ? std::min(g_attn_nq, 2) : (L <= 32 ? 1 : L <= 2 * QB ? 2 : 1);
   if (Dh > 64) nq = 1;
   dim3 grid((L + QB * nq - 1) / (QB * nq), H, B);

@@ -23,6 +23,9 @@ COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-un
                 "-munsafe-fp-atomics"]
 # Files whose bit-exact contract forbids FMA contraction (ToMe canonical arithmetic).
 NO_CONTRACT = {"tome.hip"}
+# Per-file extra flags. attention.hip: no NaN semantics (every NaN there would be a bug) and the
+# IEEE mode bit off, so fmaxf on MFMA outputs is one v_max (no canonicalising v_max x, x first).
+EXTRA = {"attention.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"]}
 
 
 def _hipcc() -> str:
@@ -47,6 +50,7 @@ def _compile(src: Path) -> Path:
         return obj
     flags = list(COMMON_FLAGS)
     flags.append("-ffp-contract=off" if src.name in NO_CONTRACT else "-ffp-contract=fast")
+    flags += EXTRA.get(src.name, [])
     cmd = [_hipcc(), *flags, "-I", str(ROOT / "include"), "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:

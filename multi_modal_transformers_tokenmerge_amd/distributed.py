@@ -93,6 +93,11 @@ class DDPStep:
         self.S = max(1, min(stages, model.cfg.num_blocks)) if self.distributed else 1
         self.regions = model.grad_regions(self.S) if self.S > 1 else None
         self.use_graph = use_graph
+        if self.distributed and getattr(state.allreduce, "grad_scale", 1.0) != reducer.grad_scale:
+            # the 1/N average lives in AdamW's grad_scale (state.allreduce): a reducer given only
+            # here would leave the gradients summed over the ranks, never averaged
+            raise ValueError("DDPStep: pass the same GradAllReducer to create_octo_train_state "
+                             "(state.allreduce) so AdamW averages the summed gradients")
         self.loss_buf = torch.zeros(1, device=model.device)
         self.graphs = []
         self._st = {}
@@ -125,10 +130,31 @@ class DDPStep:
                                async_op=True, group=self.reducer.group)
 
     # --------------------------------------------------------------------- capture
+    def _snapshot(self):
+        st, s = self.model.store, self.state
+        snap = [t.clone() for t in (st.flat, st.flat_bf16, st.m, st.v, s.rng)]
+        if s.metrics is not None:
+            snap += [s.metrics.total.clone(), s.metrics.count.clone()]
+        return snap
+
+    def _restore(self, snap):
+        st, s = self.model.store, self.state
+        dst = [st.flat, st.flat_bf16, st.m, st.v, s.rng]
+        if s.metrics is not None:
+            dst += [s.metrics.total, s.metrics.count]
+        for d, v in zip(dst, snap):
+            d.copy_(v)
+        st.refresh_transposed()
+        st.refresh_fp8()
+
     def build(self, warm: int = 2):
-        """Warm caches and the allocator outside capture, then capture the step's graphs."""
+        """Warm caches and the allocator outside capture, then capture the step's graphs. The
+        warm-up steps train: parameters, AdamW moments, the step counter and the metrics are
+        snapshotted before them and restored after, so build() leaves the training state as it
+        found it (the captured graphs then start from that state)."""
         if not self.use_graph:
             return self
+        snap = self._snapshot()
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -138,6 +164,9 @@ class DDPStep:
                     self.reducer(self.model.store.flat_grad)
                 self._opt()
         torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self._restore(snap)
+        del snap
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
 

@@ -41,9 +41,14 @@ KIND_TEXT, KIND_IMAGE, KIND_READOUT = 0, 1, 2
 
 class Octo:
     """Reference octo.py:55-198. ``Octo(config, device)`` declares, initialises (seeded, Flax
-    initialisers) and uploads every parameter."""
+    initialisers) and uploads every parameter. ``config``: a preset / model_configs name, an
+    OctoConfig, or a composed reference-schema dict (``config_loader.compose("octo_base")``,
+    the DictConfig the reference's Octo(config) takes)."""
 
     def __init__(self, config: OctoConfig | str = "octo-small", device="cuda", seed: int = 0):
+        if isinstance(config, dict):   # a composed reference-schema config (config_loader.compose)
+            from ...config_loader import octo_config_from_yaml
+            config = octo_config_from_yaml(config)
         self.cfg = cfg = get_config(config) if isinstance(config, str) else config
         self.device = torch.device(device)
         D = cfg.token_embedding_dim
@@ -59,9 +64,9 @@ class Octo:
             raise ValueError("text_tokens must equal the text set sizes of input_sequence")
         store = self.store = ParamStore()
         # ---- tokenizers
-        self.image_tokenizer = ImageTokenizer(store, "ImageTokenizer_0", cfg.image_size,
-                                              cfg.patch_size, True, cfg.position_interval, D,
-                                              resnet=cfg.stem)
+        self.image_tokenizer = ImageTokenizer(cfg.image_size, cfg.patch_size, True,
+                                              cfg.position_interval, "patch_encoding", D,
+                                              resnet=cfg.stem).bind(store, "ImageTokenizer_0")
         NP = self.image_tokenizer.num_patches
         for ts in sets0:
             if isinstance(ts, Image) and ts.num_tokens != NP:
@@ -71,18 +76,19 @@ class Octo:
             self.text_proj = Dense(store, "TextProjection_0", cfg.t5.d_model, D)
         # readouts = AddPositionEmbedding(zeros) (octo.py:103-108); the add itself is fused into
         # the sequence assembly kernel, the module owns the parameter
-        self.readout_encoder = AddPositionEmbedding(store, "AddPositionEmbedding_0", self.n_readout, D)
+        self.readout_encoder = AddPositionEmbedding().bind(store, "AddPositionEmbedding_0",
+                                                           self.n_readout, D)
         self.readout_pe = self.readout_encoder.pe
         # ---- backbone (posembed_input of StackedEncoder1DBlock, attention.py:97-100)
         self.pos_embed = store.add("StackedEncoder1DBlock_0/posembed_input/pos_embedding",
                                    (self.L0, D), normal(0.02))
-        self.stack = StackedEncoder1DBlock(store, "StackedEncoder1DBlock_0", cfg.num_blocks, D,
-                                           cfg.num_heads, cfg.mlp_dim, cfg.layer_norm_eps,
-                                           cfg.dropout_rate, cfg.attention_dropout_rate,
-                                           fp8=cfg.fp8)
+        self.stack = StackedEncoder1DBlock.create(store, "StackedEncoder1DBlock_0", cfg.num_blocks,
+                                                  D, cfg.num_heads, cfg.mlp_dim, cfg.layer_norm_eps,
+                                                  cfg.dropout_rate, cfg.attention_dropout_rate,
+                                                  fp8=cfg.fp8)
         # ---- head
-        self.head = DiffusionActionHead(store, "diffusion_action_head", D, cfg.action_space_dim,
-                                        cfg.diffusion_steps)
+        self.head = DiffusionActionHead.create(store, "diffusion_action_head", D,
+                                               cfg.action_space_dim, cfg.diffusion_steps)
         self.continuous_head = self.categorical_head = None
         if "continuous" in cfg.action_heads:
             self.continuous_head = ContinuousActionHead(store, "continuous_action_head", D,
@@ -225,7 +231,7 @@ class Octo:
                                        sample_offset=0, train=True):
         """Reference :130-137: readouts -> readout mean -> OctoDenoise (diffusion.py:88-107)."""
         xL, _ = self.generate_readouts(text_tokens, images, train, rng, sample_offset)
-        return self.head.predict_denoise_term(self._readout_mean(xL), time, noisy_actions)
+        return self.head.predict_denoise_term_mean(self._readout_mean(xL), time, noisy_actions)
 
     def predict_diffusion_action(self, text_tokens, images, rng, sample_offset=0, train=True,
                                  z: Optional[torch.Tensor] = None, return_noise=False,
@@ -239,7 +245,7 @@ class Octo:
         _C.call("mmt_rows_mean_fwd", _C.ptr(xL), xL.stride(0), xL.stride(1), B, self.D,
                 _C.ptr(self.readout_rows), self.readout_rows.numel(), _C.ptr(e), e.stride(0),
                 _C.stream_ptr())
-        return self.head.predict_action(e, rng, sample_offset, z, return_noise)
+        return self.head.predict_action_mean(e, rng, sample_offset, z, return_noise)
 
     # ------------------------------------------------------------------ other action heads
     def _readout_mean(self, xL):

@@ -20,8 +20,10 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from ... import _kernels as K
+from ... import _C, _kernels as K
+from ...config_loader import LayerSpec
 from ...layers import Dense
+from ...module_api import Bindable, init_from_spec, sget, spec
 from ...params import ParamStore, const, he_normal, normal, variance_scaling_normal
 
 
@@ -51,42 +53,105 @@ def encode_patch_position(image_hw: int, patch_size: int, num_tokens: int, train
     return rt[0], ct[0]
 
 
-class ResNetV2Block:
-    """Reference :140-178 / gato_resnet.yaml:41-104 parameters."""
+class ResNetV2Block(Bindable):
+    """Reference :140-178: ``ResNetV2Block(num_blocks, input_conv, input_pool, resnet_norm,
+    resnet_activation, resnet_conv, output_dense)(x)`` with the gato_resnet.yaml:41-104 nodes
+    (Conv 12x12 s2 VALID, max_pool 3x3 s1 VALID, GroupNorm, gelu, Conv 3x3 SAME, Dense); x are
+    the normalised patches (B, I, NP, p, p, C) -> (B, I, NP, D). The input channels / patch size
+    come from the first call or ``bind(store, name, in_channels, patch_size, embedding_dim)``."""
 
-    def __init__(self, store: ParamStore, name: str, in_channels: int, features: int = 64,
-                 conv_kernel=(12, 12), conv_stride=2, pool=(3, 3), num_blocks: int = 2,
-                 num_groups: int = 32, gn_eps: float = 1e-6, embedding_dim: int = 384,
-                 patch_size: int = 16):
-        kh, kw = conv_kernel
-        self.kh, self.kw, self.stride = kh, kw, conv_stride
-        self.oh = (patch_size - kh) // conv_stride + 1
-        self.ow = (patch_size - kw) // conv_stride + 1
-        if pool[0] != pool[1] or self.oh < pool[0] or self.ow < pool[1]:
-            raise ValueError(f"pool {pool} on a {self.oh}x{self.ow} conv map")
-        self.kp = pool[0]
-        self.ph, self.pw = self.oh - pool[0] + 1, self.ow - pool[1] + 1
+    def __init__(self, num_blocks: int = 2, input_conv=None, input_pool=None, resnet_norm=None,
+                 resnet_activation=None, resnet_conv=None, output_dense=None):
+        conv, pool, norm = spec(input_conv), spec(input_pool), spec(resnet_norm)
+        rconv, act, dense = spec(resnet_conv), spec(resnet_activation), spec(output_dense)
+        self.num_blocks = int(num_blocks)
+        self.features = int(sget(conv, "features", 64))
+        kh, kw = (int(v) for v in sget(conv, "kernel_size", (12, 12)))
+        strides = tuple(int(v) for v in sget(conv, "strides", (2, 2)))
+        if strides[0] != strides[1] or str(sget(conv, "padding", "VALID")).upper() != "VALID":
+            raise NotImplementedError("input_conv: equal strides, VALID padding (gato_resnet.yaml:44-50)")
+        self.kh, self.kw, self.stride = kh, kw, strides[0]
+        pw = tuple(int(v) for v in sget(pool, "window_shape", (3, 3)))
+        if tuple(int(v) for v in sget(pool, "strides", (1, 1))) != (1, 1) or pw[0] != pw[1]:
+            raise NotImplementedError("input_pool: square window, stride 1 (gato_resnet.yaml:60-65)")
+        self.kp = pw[0]
+        self.G = int(sget(norm, "num_groups", 32))
+        self.eps = float(sget(norm, "epsilon", 1e-6))
+        if act is not None and not getattr(act, "target", "gelu").endswith("gelu"):
+            raise NotImplementedError("resnet_activation: the fused GroupNorm kernels apply gelu")
+        if rconv is not None and (int(sget(rconv, "features", self.features)) != self.features or
+                                  tuple(int(v) for v in sget(rconv, "kernel_size", (3, 3))) != (3, 3)):
+            raise NotImplementedError("resnet_conv: 3x3 SAME with the input_conv's features")
+        self.out_features = sget(dense, "features")
+        self.specs = dict(conv=conv, rconv=rconv, dense=dense)
+        self.ks = 3
+        self.C = self.features
+
+    @classmethod
+    def from_hparams(cls, features: int = 64, conv_kernel=(12, 12), conv_stride: int = 2,
+                     pool=(3, 3), num_blocks: int = 2, num_groups: int = 32, gn_eps: float = 1e-6,
+                     embedding_dim: int | None = None) -> "ResNetV2Block":
+        """The block from OctoConfig.stem's hyper-parameters (config_loader.octo_config_from_yaml)."""
+        return cls(num_blocks,
+                   LayerSpec("flax.linen.Conv", {"features": features, "kernel_size": list(conv_kernel),
+                                                 "strides": [conv_stride, conv_stride], "padding": "VALID"}),
+                   LayerSpec("flax.linen.max_pool", {"window_shape": list(pool), "strides": [1, 1],
+                                                     "padding": "VALID"}, partial=True),
+                   LayerSpec("flax.linen.GroupNorm", {"num_groups": num_groups, "epsilon": gn_eps}),
+                   LayerSpec("flax.linen.gelu", partial=True),
+                   LayerSpec("flax.linen.Conv", {"features": features, "kernel_size": [3, 3],
+                                                 "strides": [1, 1], "padding": "SAME"}),
+                   LayerSpec("flax.linen.Dense", {"features": embedding_dim}))
+
+    def _declare(self, store: ParamStore, name: str, in_channels: int, patch_size: int,
+                 embedding_dim: int | None = None):
+        D = int(self.out_features or embedding_dim or 0)
+        if embedding_dim is not None and self.out_features is not None and int(self.out_features) != embedding_dim:
+            raise ValueError(f"output_dense features {self.out_features} != embedding_dim {embedding_dim}")
+        if D <= 0:
+            raise ValueError("ResNetV2Block needs output_dense.features (or the tokenizer's embedding_dim)")
+        kh, kw, features = self.kh, self.kw, self.features
+        self.patch_size, self.D = patch_size, D
+        self.oh = (patch_size - kh) // self.stride + 1
+        self.ow = (patch_size - kw) // self.stride + 1
+        if self.oh < self.kp or self.ow < self.kp:
+            raise ValueError(f"pool {self.kp} on a {self.oh}x{self.ow} conv map")
+        self.ph, self.pw = self.oh - self.kp + 1, self.ow - self.kp + 1
         self.general = (self.ph, self.pw) != (1, 1)   # else the 1x1 centre-tap form
-        self.ks = 3                                   # resnet_conv 3x3 SAME (gato_resnet.yaml:88-92)
         self.win = self.oh * self.ow
-        self.C, self.G, self.eps = features, num_groups, gn_eps
-        self.num_blocks = num_blocks
         K_in = kh * kw * in_channels
+        sc, sr, sd = self.specs["conv"], self.specs["rconv"], self.specs["dense"]
         # input_conv (Conv 12x12 s2 VALID, he_normal over (kh, kw, cin, cout) -> fan_in = K_in)
         self.conv = Dense(store, f"{name}/Conv_0", K_in, features,
-                          kernel_init=he_normal((K_in, features)), bias_init=normal(0.01))
+                          kernel_init=init_from_spec(sget(sc, "kernel_init"), (K_in, features)),
+                          bias_init=init_from_spec(sget(sc, "bias_init"), (features,), normal(0.01)))
         self.gn, self.convs = [], []
-        for i in range(num_blocks):
+        for i in range(self.num_blocks):
             self.gn.append((store.add(f"{name}/GroupNorm_{i}/scale", (features,), const(1.0)),
                             store.add(f"{name}/GroupNorm_{i}/bias", (features,), const(0.0))))
             # 3x3 SAME conv: the full (9C, C) kernel on a larger map; on a 1x1 map only the centre
             # tap acts (fan_in of the full kernel either way)
             cin = 9 * features if self.general else features
             self.convs.append(Dense(store, f"{name}/Conv_{i + 1}", cin, features,
-                                    kernel_init=he_normal((9 * features, features))))
+                                    kernel_init=init_from_spec(sget(sr, "kernel_init"), (9 * features, features)),
+                                    bias_init=init_from_spec(sget(sr, "bias_init"), (features,), normal(0.01))))
         flat = self.ph * self.pw * features                 # flatten (h, w, c) (:174-175)
-        self.out = Dense(store, f"{name}/Dense_0", flat, embedding_dim,
-                         kernel_init=he_normal((flat, embedding_dim)))
+        self.out = Dense(store, f"{name}/Dense_0", flat, D,
+                         kernel_init=init_from_spec(sget(sd, "kernel_init"), (flat, D)),
+                         bias_init=init_from_spec(sget(sd, "bias_init"), (D,), normal(0.01)))
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        """x (B, I, NP, p, p, C) normalised patch pixels (fp32) -> tokens (B, I, NP, D) fp32."""
+        if x.dim() != 6 or x.shape[3] != x.shape[4]:
+            raise ValueError(f"patches must be (B, I, NP, p, p, C), got {tuple(x.shape)}")
+        B, I, NP, p, _, C = x.shape
+        self._ensure(x.device, C, p)
+        if (p, C) != (self.patch_size, self.conv.in_f // (self.kh * self.kw)):
+            raise ValueError(f"patches {p}x{p}x{C} do not match the bound block")
+        pix = x.float().contiguous().view(B * I * NP, 1, p, p, C)  # one patch per "image"
+        A = K.patch_im2col(pix, p, self.kh, self.kw, self.stride, normalize=False)
+        tok, _ = self.forward(A, B, I * NP)
+        return tok.float().view(B, I, NP, -1)
 
     def fused_ok(self, images: torch.Tensor, patch_size: int, normalize: bool) -> bool:
         """The 64-channel 12x12 s2 conv + 3x3 pool on 16x16 uint8 RGB patches runs as one kernel
@@ -195,30 +260,79 @@ class ResNetV2Block:
         self.conv.bwd(G, sv["A"], need_dx=False, bias_grad_done=True)
 
 
-class ImageTokenizer:
-    """Reference :216-309: patches -> ResNetV2 stem -> Dense, + row/col position embeddings."""
+class ImageTokenizer(Bindable):
+    """Reference :216-309: ``ImageTokenizer(image_size, patch_size, normalize, position_interval,
+    rng_collection, embedding_dim, row_position_embedding, col_position_embedding, resnet)
+    (image, train=True) -> (B, I, NP, D)`` = ResNetV2 patch embeddings + row / column position
+    embeddings (flax.linen.Embed nodes, position_interval x embedding_dim). ``resnet`` is the
+    ResNetV2Block node (or module, or OctoConfig.stem's hyper-parameter dict)."""
 
-    def __init__(self, store: ParamStore, name: str, image_size, patch_size: int, normalize: bool,
-                 position_interval: int, embedding_dim: int, rng_collection: str = "patch_encoding",
-                 resnet: dict | None = None):
-        self.image_size = tuple(image_size)
-        self.patch_size = patch_size
-        self.normalize = normalize
-        self.Q = position_interval
-        self.D = embedding_dim
+    def __init__(self, image_size, patch_size: int, normalize: bool = True,
+                 position_interval: int = 128, rng_collection: str = "patch_encoding",
+                 embedding_dim: int = 768, row_position_embedding=None, col_position_embedding=None,
+                 resnet=None):
+        self.image_size = tuple(int(v) for v in image_size)
+        self.patch_size = int(patch_size)
+        self.normalize = bool(normalize)
+        self.Q = int(position_interval)
+        self.D = int(embedding_dim)
         self.rng_collection = rng_collection
         H, W, C = self.image_size
         if H != W:
             raise ValueError("square images only (image_tokenizer.py:49-50)")
-        self.num_patches = (H // patch_size) ** 2
-        emb_init = variance_scaling_normal(1.0, (position_interval, embedding_dim))
-        self.row_emb = store.add(f"{name}/image_row_position_embedding/embedding",
-                                 (position_interval, embedding_dim), emb_init)
-        self.col_emb = store.add(f"{name}/image_col_position_embedding/embedding",
-                                 (position_interval, embedding_dim), emb_init)
-        self.resnet = ResNetV2Block(store, f"{name}/ResNetV2Block_0", C,
-                                    embedding_dim=embedding_dim, patch_size=patch_size,
-                                    **(resnet or {}))
+        self.num_patches = (H // self.patch_size) ** 2
+        self.emb_specs = []
+        for e in (spec(row_position_embedding), spec(col_position_embedding)):
+            if e is not None and (int(sget(e, "num_embeddings", self.Q)) != self.Q or
+                                  int(sget(e, "features", self.D)) != self.D):
+                raise ValueError("position embeddings must be (position_interval, embedding_dim)")
+            self.emb_specs.append(e)
+        rs = spec(resnet)
+        if rs is None:
+            rs = ResNetV2Block.from_hparams(embedding_dim=self.D)
+        elif isinstance(rs, dict):
+            rs = ResNetV2Block.from_hparams(**rs, embedding_dim=self.D)
+        if not isinstance(rs, ResNetV2Block):
+            raise TypeError(f"resnet must be a ResNetV2Block node, got {type(rs).__name__}")
+        self.resnet = rs
+        self.row_emb = self.col_emb = None
+        self._zero_pe = {}
+
+    def _declare(self, store: ParamStore, name: str):
+        H, W, C = self.image_size
+        Q, D = self.Q, self.D
+
+        def emb_init(e):
+            return init_from_spec(sget(e, "embedding_init"), (Q, D), variance_scaling_normal(1.0, (Q, D)))
+        self.row_emb = store.add(f"{name}/image_row_position_embedding/embedding", (Q, D),
+                                 emb_init(self.emb_specs[0]))
+        self.col_emb = store.add(f"{name}/image_col_position_embedding/embedding", (Q, D),
+                                 emb_init(self.emb_specs[1]))
+        self.resnet.bind(store, f"{name}/ResNetV2Block_0", C, self.patch_size, D)
+
+    def __call__(self, image: torch.Tensor, train: bool = True, *, rng=None,
+                 sample_offset: int = 0, positions=None) -> torch.Tensor:
+        """image (B, I, H, W, C) uint8 / fp32 [0, 255] -> (B, I, NP, D) fp32 = patch embeddings +
+        row + column position embeddings (:300-307). train draws the patch positions from the
+        counter RNG ``rng`` (the 'patch_encoding' collection), keyed by the global sample index
+        sample_offset + b; eval uses the interval midpoints."""
+        self._ensure(image.device)
+        if train and rng is None and positions is None:
+            raise ValueError("ImageTokenizer(train=True) needs the patch_encoding rng (rng=)")
+        tok, (rt, ct), _ = self.forward(image, train, rng, sample_offset, positions)
+        B, NI, D = tok.shape
+        key = (NI, image.device)
+        if key not in self._zero_pe:
+            self._zero_pe[key] = (torch.zeros((NI, D), dtype=torch.float32, device=image.device),
+                                  torch.tensor([(1 << 24) | j for j in range(NI)], dtype=torch.int32,
+                                               device=image.device))
+        zpe, rows = self._zero_pe[key]
+        out = torch.empty((B, NI, D), dtype=torch.float32, device=image.device)
+        # tok + (row_emb[rt] + col_emb[ct]) in the arithmetic of the fused sequence assembly
+        _C.call("mmt_seq_assemble_fwd", B, NI, D, _C.ptr(rows), None, 1, _C.ptr(tok), NI,
+                _C.ptr(rt), _C.ptr(ct), _C.ptr(self.row_emb.data), _C.ptr(self.col_emb.data), None,
+                _C.ptr(zpe), _C.ptr(out), _C.stream_ptr())
+        return out.view(B, image.shape[1], self.num_patches, D)
 
     def check(self, images: torch.Tensor):
         if tuple(images.shape[-3:]) != self.image_size:

@@ -11,20 +11,26 @@ from __future__ import annotations
 import torch
 
 from ... import _C
-from ...params import ParamStore, he_normal
+from ...module_api import Bindable, init_from_spec, spec
+from ...params import ParamStore
 
 
-class AddPositionEmbedding:
-    """``AddPositionEmbedding(posemb_init)(inputs)`` for inputs (B, n, D) fp32 device tensors.
-    The parameter is declared in ``store`` as ``{name}/pos_embedding`` with shape (n, D) (the
-    reference's (1, n, D) without the broadcast axis); posemb_init defaults to he_normal as in
-    model_configs/tokenizers/readouts/octo.yaml."""
+class AddPositionEmbedding(Bindable):
+    """``AddPositionEmbedding(posemb_init)(inputs)`` (readout.py:8-33; the same module is
+    attention.py:71-85) for inputs (B, n, D) fp32 device tensors. The parameter ``pos_embedding``
+    has the shape (n, D) of the first call (the reference's (1, n, D) without the broadcast axis)
+    or of ``bind(store, name, n, D)``; posemb_init is the config's initializer node (he_normal in
+    model_configs/tokenizers/readouts/octo.yaml), a LayerSpec, or a ParamStore initialiser."""
 
-    def __init__(self, store: ParamStore, name: str, num_tokens: int, embedding_dim: int,
-                 posemb_init=None):
-        self.num_tokens, self.D = num_tokens, embedding_dim
-        self.pe = store.add(f"{name}/pos_embedding", (num_tokens, embedding_dim),
-                            posemb_init or he_normal((1, num_tokens, embedding_dim)))
+    def __init__(self, posemb_init=None):
+        self.posemb_init = spec(posemb_init)
+        self.pe = None
+        self.num_tokens = self.D = None
+
+    def _declare(self, store: ParamStore, name: str, num_tokens: int, embedding_dim: int):
+        self.num_tokens, self.D = int(num_tokens), int(embedding_dim)
+        self.pe = store.add(f"{name}/pos_embedding", (self.num_tokens, self.D),
+                            init_from_spec(self.posemb_init, (1, self.num_tokens, self.D)))
 
     def _check(self, inputs: torch.Tensor):
         if inputs.dim() != 3:  # the reference asserts inputs.ndim == 3 (:28-30)
@@ -36,6 +42,9 @@ class AddPositionEmbedding:
             raise ValueError("inputs must be a contiguous fp32 device tensor")
 
     def __call__(self, inputs: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        if inputs.dim() != 3:
+            raise ValueError(f"Number of dimensions should be 3, but it is: {inputs.dim()}")
+        self._ensure(inputs.device, inputs.shape[1], inputs.shape[2])
         self._check(inputs)
         out = torch.empty_like(inputs) if out is None else out
         B = inputs.shape[0]

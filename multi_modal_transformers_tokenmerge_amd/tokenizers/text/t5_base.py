@@ -99,7 +99,13 @@ class T5Tokenizer:
         return self._bias_cache[T]
 
     def __call__(self, input_ids: torch.Tensor, layer_outputs: list | None = None) -> torch.Tensor:
-        """layer_outputs: if a list, receives the residual stream after each layer (parity tests)."""
+        """input_ids (B, T) int -> last_hidden_state (B, T, d_model) bf16 (stop_gradient, :14).
+        Materialises the (seeded, randomly initialised) weights on the ids' device on the first
+        call when ``materialize`` was not called (the reference builds the module from the config
+        alone, ``T5Tokenizer()``, :10-12). layer_outputs: if a list, receives the residual stream
+        after each layer (parity tests)."""
+        if self.store.flat_bf16 is None:
+            self.materialize(input_ids.device, 1)
         c = self.cfg
         B, T = input_ids.shape
         ids = input_ids.to(torch.int32).contiguous()

@@ -257,3 +257,92 @@ class TokenSequence:
     def num_layers_until_empty(self) -> int:
         return min((ts.num_tokens // ts.tokens_compressed_per_layer
                     for ts in self.token_sequence if ts.tokens_compressed_per_layer), default=10 ** 9)
+
+
+def sets_from_mask(mask) -> LayerSets:
+    """A dense attention mask in the reference's form — ``generate_attention_mask`` repeated over
+    the batch (octo.py:66-68, 119): (B, H, L, L), (H, L, L), (B, L, L) or (L, L), bool or 0/1 — as
+    the token-set table the attention kernels evaluate (contiguous sets, per query set the key
+    sets it sees, causal sets). The mask must be the same for every batch entry and head (Flax
+    broadcasts one pattern; the kernels take one table) and must BE a block mask of at most 16
+    contiguous sets whose diagonal blocks are all-ones, all-zeros or lower-triangular (causal);
+    anything else raises ValueError. Segmentation is greedy over positions in O(L^2): token j
+    joins the open set when its row and column agree with the set's outside the set and the
+    diagonal block keeps the set's kind; the table is then checked by rebuilding the mask."""
+    if hasattr(mask, "detach"):
+        mask = mask.detach().cpu().numpy()
+    m = np.asarray(mask)
+    if m.dtype != bool:
+        m = m != 0
+    while m.ndim > 2:
+        if not (m == m[:1]).all():
+            raise ValueError("the attention mask differs across batch / heads: the kernels take one "
+                             "token-set pattern per layer")
+        m = m[0]
+    if m.ndim != 2 or m.shape[0] != m.shape[1]:
+        raise ValueError(f"attention mask must be square (.., L, L), got {m.shape}")
+    L = m.shape[0]
+    starts, lens, kinds = [], [], []
+    i = 0
+    while i < L:
+        j = i + 1
+        kind = None  # "full" | "zeros" | "causal" once the set holds two tokens
+        while j < L:
+            if kind is None:
+                blk = (m[i, i], m[i, j], m[j, i], m[j, j])
+                k = {(True, True, True, True): "full", (False, False, False, False): "zeros",
+                     (True, False, True, True): "causal"}.get(tuple(bool(v) for v in blk))
+                if k is None:
+                    break
+            else:
+                k = kind
+                row_in, col_in = m[j, i:j + 1], m[i:j, j]
+                if k == "full" and not (row_in.all() and col_in.all()):
+                    break
+                if k == "zeros" and (row_in.any() or col_in.any()):
+                    break
+                if k == "causal" and not (row_in.all() and not col_in.any()):
+                    break
+            # outside the set [i, j]: row j / column j must match row i / column i
+            if not (np.array_equal(m[j, :i], m[i, :i]) and np.array_equal(m[j, j + 1:], m[i, j + 1:])
+                    and np.array_equal(m[:i, j], m[:i, i]) and np.array_equal(m[j + 1:, j], m[j + 1:, i])):
+                break
+            kind = k
+            j += 1
+        starts.append(i)
+        lens.append(j - i)
+        kinds.append(kind or ("full" if m[i, i] else "zeros"))
+        i = j
+    n = len(starts)
+    if n > 16:
+        raise ValueError(f"the attention mask needs {n} token sets (the kernels take at most 16)")
+    vis, causal = [], []
+    for a in range(n):
+        bits = 0
+        for b in range(n):
+            if a == b:
+                on = kinds[a] != "zeros"
+            else:
+                on = bool(m[starts[a], starts[b]])
+            bits |= int(on) << b
+        vis.append(bits)
+        causal.append(kinds[a] == "causal")
+    sets = LayerSets(starts, lens, vis, causal, ["?"] * n)
+    if not np.array_equal(dense_mask_of(sets), m):
+        raise ValueError("the attention mask is not a block mask of contiguous token sets")
+    return sets
+
+
+def dense_mask_of(sets: LayerSets) -> np.ndarray:
+    """The (L, L) bool mask a token-set table stands for (inverse of sets_from_mask)."""
+    L = sets.L
+    sid = np.zeros(L, np.int64)
+    for k, (s, n) in enumerate(zip(sets.starts, sets.lens)):
+        sid[s:s + n] = k
+    vis = np.array(sets.vis, np.int64)
+    m = ((vis[sid][:, None] >> sid[None, :]) & 1).astype(bool)
+    for k, c in enumerate(sets.causal or []):
+        if c:
+            s, n = sets.starts[k], sets.lens[k]
+            m[s:s + n, s:s + n] &= np.tril(np.ones((n, n), bool))
+    return m

@@ -55,3 +55,107 @@ def test_instantiate_targets():
     assert isinstance(p, functools.partial)
     with pytest.raises(ValueError):
         C.instantiate({"_target_": "multi_modal_transformers.models.deprecated.gato.Gato"})
+
+
+def _component_nodes(cfg):
+    """The component nodes octo.py:75-87 instantiates, from a composed config of either
+    attention_blocks layout."""
+    ab = cfg["attention_blocks"]
+    stack = ab.get("stacked_encoder_1d_block") or {
+        "_target_": "multi_modal_transformers.attention_blocks.attention.StackedEncoder1DBlock",
+        "num_blocks": ab["num_blocks"], "encoder_1d_block": ab["encoder_1d_block"]}
+    heads = [h["module"] for h in cfg["action_heads"].get("heads", [])] or \
+        [cfg["action_heads"]["diffusion_action_head"]]
+    return (cfg["tokenizers"]["text"]["encoder"], cfg["tokenizers"]["images"]["encoder"],
+            cfg["tokenizers"]["readouts"]["encoder"], stack, heads)
+
+
+def _check_instantiated(cfg, D):
+    """instantiate() every component node with octo.py's _recursive_ flags; the modules take the
+    reference's constructor fields and declare their parameters lazily (here into a CPU store)."""
+    from multi_modal_transformers_tokenmerge_amd.action_heads.diffusion import DiffusionActionHead
+    from multi_modal_transformers_tokenmerge_amd.attention_blocks.attention import (
+        Encoder1DBlock, MLPBlock, StackedEncoder1DBlock)
+    from multi_modal_transformers_tokenmerge_amd.params import ParamStore
+    from multi_modal_transformers_tokenmerge_amd.tokenizers.images.image_tokenizer import (
+        ImageTokenizer, ResNetV2Block)
+    from multi_modal_transformers_tokenmerge_amd.tokenizers.readout.readout import AddPositionEmbedding
+    from multi_modal_transformers_tokenmerge_amd.tokenizers.text.t5_base import T5Tokenizer
+    text, image, readout, stack, heads = _component_nodes(cfg)
+    t5 = C.instantiate(text)                                   # octo.py:75
+    img = C.instantiate(image, _recursive_=False)              # :76
+    ro = C.instantiate(readout, _recursive_=True)              # :77
+    st = C.instantiate(stack, _recursive_=False)               # :80
+    hd = [C.instantiate(h, _recursive_=False) for h in heads]  # :83-84
+    assert isinstance(t5, T5Tokenizer) and isinstance(img, ImageTokenizer)
+    assert isinstance(img.resnet, ResNetV2Block) and isinstance(ro, AddPositionEmbedding)
+    assert isinstance(st, StackedEncoder1DBlock) and isinstance(hd[0], DiffusionActionHead)
+    blk_node = stack["encoder_1d_block"]
+    blk = C.instantiate(blk_node, _recursive_=False)
+    mlp = C.instantiate(blk_node["mlp_block"], _recursive_=False)
+    assert isinstance(blk, Encoder1DBlock) and isinstance(blk.mlp, MLPBlock) and isinstance(mlp, MLPBlock)
+    store = ParamStore()
+    img.bind(store, "ImageTokenizer_0")
+    ro.bind(store, "AddPositionEmbedding_0", 8, D)
+    L = 40
+    st.bind(store, "StackedEncoder1DBlock_0", L, D)
+    hd[0].bind(store, "diffusion_action_head", D)
+    names = {p.name: p.shape for p in store.params}
+    H = blk.H
+    b0 = "StackedEncoder1DBlock_0/Block_0"
+    assert names[f"{b0}/SelfAttention_0/qkv/kernel"] == (3 * D, D)
+    assert names[f"{b0}/MLPBlock_0/Dense_0/kernel"][1] == D
+    assert names["StackedEncoder1DBlock_0/posembed_input/pos_embedding"] == (L, D)
+    assert names["AddPositionEmbedding_0/pos_embedding"] == (8, D)
+    assert names["ImageTokenizer_0/image_row_position_embedding/embedding"] == (img.Q, D)
+    assert sum(1 for n in names if n.startswith("StackedEncoder1DBlock_0/Block_")) == 12 * st.num_blocks
+    assert D % H == 0 and blk.attn_rate == 0.1 and blk.rate == 0.1 and blk.eps == 1e-6
+    store.materialize("cpu", 0)   # the Flax initialisers run on the host
+    return store
+
+
+def test_instantiate_every_component_node_ref_octo_base():
+    """every component node of ref_octo_base.yaml (the reference's octo_base geometry)
+    instantiates into the build's module with the reference constructor and lazy parameters."""
+    _check_instantiated(C.compose("ref_octo_base"), 768)
+
+
+def test_instantiate_reference_yaml_files():
+    """The reference's OWN model_configs (octo_base.yaml + its component YAMLs, the layout
+    vanilla_decoder.yaml:1-4 defines) composed and instantiated as octo.py:75-84 does. Read at
+    test time from /root/reference when present (never shipped; skipped elsewhere)."""
+    from pathlib import Path
+    ref = Path("/root/reference/multi_modal_transformers/model_configs")
+    if not (ref / "octo_base.yaml").exists():
+        pytest.skip("reference configs not present")
+    cfg = C.compose("octo_base", config_dir=ref)
+    _check_instantiated(cfg, 768)
+    with pytest.raises(KeyError):     # octo.py:67 reads a key the shipped YAMLs do not define
+        C._get_path(cfg, "attention_blocks.stacked_encoder_1d_block")
+
+
+def test_set_table_from_reference_mask():
+    """token_sequencer.sets_from_mask: the dense mask generate_attention_mask builds (repeated
+    over batch and heads, octo.py:66-68, 119) -> the kernels' token-set table, including causal
+    Text sets; masks that are not such a block pattern are rejected."""
+    import numpy as np
+    from multi_modal_transformers_tokenmerge_amd.tokenizers.token_sequencer import (
+        TokenSequence, dense_mask_of, sets_from_mask)
+    for seq in ("[TaskDescriptionPrefix{32}] [Image{256};Readout{4}]",
+                "[TaskDescriptionPrefix{16}] [Image{25};Readout{4}]*2",
+                "[Text{5}] [Image{9};Readout{2}]*3", "[Image{16};Readout{4}]"):
+        ts = TokenSequence(seq)
+        m = ts.generate_attention_mask(repeats=3, square=True)
+        got = sets_from_mask(np.repeat(m[None], 2, 0))
+        want = ts.set_table(0)
+        assert (got.starts, got.lens, got.vis, got.causal) == (want.starts, want.lens, want.vis, want.causal)
+        assert (dense_mask_of(got) == m[0]).all()
+    m = TokenSequence("[Image{8};Readout{2}]").generate_attention_mask(1, square=True)[0]
+    hole = m.copy()
+    hole[3, 1] = False                      # still a block mask (singleton sets): exact table
+    assert (dense_mask_of(sets_from_mask(hole)) == hole).all()
+    with pytest.raises(ValueError):         # differs across heads
+        sets_from_mask(np.stack([m, hole]))
+    rnd = np.random.default_rng(0).random((40, 40)) < 0.5
+    with pytest.raises(ValueError):         # no table of <= 16 contiguous sets
+        sets_from_mask(rnd)

@@ -154,7 +154,7 @@ def test_sampler_oracle_quirks_and_coefficients():
     from multi_modal_transformers_tokenmerge_amd.action_heads.diffusion import DiffusionActionHead
     from multi_modal_transformers_tokenmerge_amd.params import ParamStore
     from oracle import sampler_ref as SR
-    head = DiffusionActionHead(ParamStore(), "h", 16, 8, 32)
+    head = DiffusionActionHead.create(ParamStore(), "h", 16, 8, 32)
     assert head.betas_np[-1] == pytest.approx(0.999)
     coef = SR.sampler_coefficients(head.betas_np, head.alpha_hats_np)
     np.testing.assert_allclose(head.sampler_coef(torch.device("cpu")).numpy(), coef, rtol=1e-5)

@@ -1,0 +1,158 @@
+"""GPU: the reference's class-level module API built by config_loader.instantiate
+from ref_octo_base.yaml (the reference's octo_base geometry: D 768, 3 heads of 256, 1 block,
+2 x 280 px cameras, patch 56, 16 text tokens) gives the Octo path's results on the same
+parameters:
+
+* T5Tokenizer()(ids), ImageTokenizer(...)(image, train), AddPositionEmbedding(...)(zeros),
+  TokenSequence.assemble_embeddings, StackedEncoder1DBlock(...)(x, train, mask) with the dense
+  reference mask == Octo.generate_readouts, bit for bit (octo.py:91-126);
+* DiffusionActionHead(...).denoise_loss(readouts, actions) == the Octo loss, bit for bit
+  (octo.py:139-145, diffusion.py:110-143);
+* torch autograd through StackedEncoder1DBlock.__call__ == the Octo stack's explicit backward
+  (dW products bit for bit; atomically accumulated bias / LN / embedding gradients to rounding);
+* Encoder1DBlock / MLPBlock __call__ against plain fp32 torch on the same bf16-rounded weights.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _class_level(cfg, model, dev):
+    from multi_modal_transformers_tokenmerge_amd import config_loader as C
+    from multi_modal_transformers_tokenmerge_amd.params import ParamStore
+    D = model.D
+    t5 = C.instantiate(cfg["tokenizers"]["text"]["encoder"])
+    img = C.instantiate(cfg["tokenizers"]["images"]["encoder"], _recursive_=False)
+    ro = C.instantiate(cfg["tokenizers"]["readouts"]["encoder"], _recursive_=True)
+    st = C.instantiate(cfg["attention_blocks"]["stacked_encoder_1d_block"], _recursive_=False)
+    head = C.instantiate(cfg["action_heads"]["heads"][0]["module"], _recursive_=False)
+    store = ParamStore()
+    img.bind(store, "ImageTokenizer_0")
+    ro.bind(store, "AddPositionEmbedding_0", model.n_readout, D)
+    st.bind(store, "StackedEncoder1DBlock_0", model.L0, D)
+    head.bind(store, "diffusion_action_head", D)
+    store.materialize(dev, 123)
+    store.load_state_dict(model.store.state_dict())     # the Octo model's parameters, by name
+    return t5, img, ro, st, head, store
+
+
+@pytest.fixture(scope="module")
+def ref_setup(dev):
+    from multi_modal_transformers_tokenmerge_amd import config_loader as C
+    from multi_modal_transformers_tokenmerge_amd.models.octo.octo import Octo
+    cfg = C.compose("ref_octo_base")
+    model = Octo(cfg, dev, seed=0)
+    g = np.random.default_rng(3)
+    B = 2
+    images = torch.from_numpy(g.integers(0, 256, (B, model.n_images, 280, 280, 3), dtype=np.uint8)).to(dev)
+    text = torch.from_numpy(g.integers(0, 32128, (B, model.n_text), dtype=np.int32)).to(dev)
+    actions = torch.from_numpy(g.uniform(-1, 1, (B, 8)).astype(np.float32)).to(dev)
+    return cfg, model, _class_level(cfg, model, dev), images, text, actions
+
+
+def test_instantiated_stack_equals_generate_readouts(dev, ref_setup):
+    from multi_modal_transformers_tokenmerge_amd.tokenizers.token_sequencer import TokenEmbeddings
+    cfg, model, (t5, img, ro, st, head, store), images, text, actions = ref_setup
+    rng = torch.tensor([21, 4], dtype=torch.int32, device=dev)
+    B = images.shape[0]
+    xL, _ = model.generate_readouts(text, images, train=True, rng=rng, sample_offset=0)
+    # the reference's generate_readouts, module by module (octo.py:98-120)
+    text_emb = t5(text)
+    image_emb = img(images, train=True, rng=rng).reshape(B, -1, model.D)
+    readouts = ro(torch.zeros((B, model.n_readout, model.D), device=dev))
+    emb = model.seq.assemble_embeddings(TokenEmbeddings(text=text_emb.float(), images=image_emb,
+                                                        readouts=readouts))
+    heads = cfg["attention_blocks"]["stacked_encoder_1d_block"]["encoder_1d_block"]["self_attention"]["num_heads"]
+    mask = np.repeat(model.seq.generate_attention_mask(repeats=heads, square=True)[None], B, axis=0)
+    x = st(emb, train=True, mask=mask, rng=rng)
+    torch.cuda.synchronize()
+    assert x.shape == xL.shape
+    assert torch.equal(x, xL)
+    # readout rows -> DiffusionActionHead.denoise_loss == Octo.compute_diffusion_denoise_loss
+    ridx = torch.from_numpy(model.seq.get_modality_idx("readouts")).to(dev)
+    loss_ref, _ = model.compute_diffusion_denoise_loss(text, images, actions, True, rng, 0)
+    loss = head.denoise_loss(x.index_select(1, ridx), actions, rng=rng)
+    torch.cuda.synchronize()
+    assert torch.equal(loss, loss_ref), (float(loss), float(loss_ref))
+    with pytest.raises(ValueError):       # flax merge_param: the mask is mandatory
+        st(emb, train=True, mask=None, rng=rng)
+
+
+def test_stack_autograd_matches_explicit_backward(dev, ref_setup):
+    from multi_modal_transformers_tokenmerge_amd.layers import wgrad_overlap
+    cfg, model, (t5, img, ro, st, head, store), images, text, actions = ref_setup
+    rng = torch.tensor([8, 1], dtype=torch.int32, device=dev)
+    B, L, D = images.shape[0], model.L0, model.D
+    g = torch.Generator().manual_seed(5)
+    x0 = torch.randn((B, L, D), generator=g).to(dev)
+    dy = torch.randn((B, L, D), generator=g).to(dev)
+    mask = model.seq.generate_attention_mask(repeats=3, square=True)
+    # class level: autograd
+    store.zero_grad()
+    x = x0.clone().requires_grad_()
+    st(x, train=True, mask=mask, rng=rng).backward(dy)
+    # Octo level: posembed add, explicit stack forward / backward on the same inputs
+    model.store.zero_grad()
+    xin = x0 + model.pos_embed.data[None]
+    ctxs = model.layer_ctxs(True, rng, 0)
+    xo, saved = model.stack.forward(xin.contiguous(), ctxs)
+    with wgrad_overlap(dev):
+        dx = model.stack.backward(dy.contiguous(), saved, ctxs)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(x.grad, dx, rtol=0, atol=0)
+    mine = {p.name: p.grad for p in store.params}
+    for p in model.store.params:
+        if not p.name.startswith("StackedEncoder1DBlock_0/Block_"):
+            continue
+        if p.name.endswith("/kernel"):
+            assert torch.equal(mine[p.name], p.grad), p.name
+        else:
+            torch.testing.assert_close(mine[p.name], p.grad, rtol=1e-5, atol=1e-6)
+    # posembed_input gradient = column sums of dx over the batch
+    torch.testing.assert_close(mine["StackedEncoder1DBlock_0/posembed_input/pos_embedding"],
+                               dx.sum(0), rtol=1e-5, atol=1e-5)
+
+
+def test_encoder_block_and_mlp_call_vs_torch(dev):
+    """Encoder1DBlock(...)(x, mask, train=False) and MLPBlock(...)(x) built from config nodes
+    with lazily created parameters, against fp32 torch on the same (bf16-rounded) weights."""
+    from multi_modal_transformers_tokenmerge_amd import config_loader as C
+    cfg = C.compose("octo_tiny")
+    node = cfg["attention_blocks"]["stacked_encoder_1d_block"]["encoder_1d_block"]
+    blk = C.instantiate(node, _recursive_=False)
+    B, L, D = 3, 20, cfg["token_embedding_dim"]
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn((B, L, D), generator=g).to(dev)
+    mask = np.ones((L, L), bool)
+    y, aux = blk(x, mask=mask, train=False)
+    assert aux is None and y.shape == (B, L, D) and y.dtype == torch.float32
+    p = {k.split("Encoder1DBlock_0/")[1]: v.float() for k, v in blk.params.items()}
+    bf = lambda t: t.bfloat16().float()  # noqa: E731  the kernels read bf16 weights / activations
+
+    def seqln(v, s, b):                  # LayerNorm over the sequence axis (reduction_axes [1])
+        mu = v.mean(1, keepdim=True)
+        var = ((v - mu) ** 2).mean(1, keepdim=True)
+        return (v - mu) / torch.sqrt(var + 1e-6) * s + b
+    H = blk.H
+    Dh = D // H
+    y0 = bf(seqln(x, p["LayerNorm_0/scale"], p["LayerNorm_0/bias"]))
+    qkv = bf(y0 @ bf(p["SelfAttention_0/qkv/kernel"]).T + p["SelfAttention_0/qkv/bias"])
+    q, k, v = qkv.view(B, L, 3, H, Dh).unbind(2)
+    a = torch.softmax(torch.einsum("bqhd,bkhd->bhqk", q, k) * Dh ** -0.5, -1)
+    o = bf(torch.einsum("bhqk,bkhd->bqhd", a, v).reshape(B, L, D))
+    x1 = x + o @ bf(p["SelfAttention_0/out/kernel"]).T + p["SelfAttention_0/out/bias"]
+    y1 = bf(seqln(x1, p["LayerNorm_1/scale"], p["LayerNorm_1/bias"]))
+    hmid = bf(torch.relu(y1 @ bf(p["MLPBlock_0/Dense_0/kernel"]).T + p["MLPBlock_0/Dense_0/bias"]))
+    ref = x1 + hmid @ bf(p["MLPBlock_0/Dense_1/kernel"]).T + p["MLPBlock_0/Dense_1/bias"]
+    rel = ((y - ref).norm() / ref.norm()).item()
+    assert rel < 1e-2, rel
+    with pytest.raises(ValueError):        # train must be set (constructor or call)
+        blk(x, mask=mask)
+    mlp = C.instantiate(node["mlp_block"], _recursive_=False)
+    z = mlp(x)                              # train=False default: no dropout
+    q = {k.split("MLPBlock_0/")[1]: v.float() for k, v in mlp.params.items()}
+    hz = bf(torch.relu(bf(x) @ bf(q["Dense_0/kernel"]).T + q["Dense_0/bias"]))
+    zr = hz @ bf(q["Dense_1/kernel"]).T + q["Dense_1/bias"]
+    assert ((z - zr).norm() / zr.norm()).item() < 1e-2

@@ -15,7 +15,7 @@ def _head(dev, D, seed=3):
     from multi_modal_transformers_tokenmerge_amd.action_heads.diffusion import DiffusionActionHead
     from multi_modal_transformers_tokenmerge_amd.params import ParamStore
     store = ParamStore()
-    head = DiffusionActionHead(store, "diffusion_action_head", D, 8, 32)
+    head = DiffusionActionHead.create(store, "diffusion_action_head", D, 8, 32)
     store.materialize(dev, seed=seed)
     return head
 
@@ -30,7 +30,7 @@ def test_sampler_matches_oracle(dev, D, B):
     g = torch.Generator().manual_seed(D + B)
     readout = (torch.randn((B, D), generator=g) * 0.5).to(torch.bfloat16).to(dev)
     rng = torch.tensor([1234, 7], dtype=torch.int32, device=dev)
-    actions, z = head.predict_action(readout, rng, sample_offset=100, return_noise=True)
+    actions, z = head.predict_action_mean(readout, rng, sample_offset=100, return_noise=True)
     temb = head.time_embeddings(dev)
     torch.cuda.synchronize()
 
@@ -57,24 +57,24 @@ def test_sampler_injected_noise_and_determinism(dev):
     B = 17
     readout = torch.randn((B, 384), device=dev).to(torch.bfloat16)
     rng = torch.tensor([99, 3], dtype=torch.int32, device=dev)
-    a1, z1 = head.predict_action(readout, rng, sample_offset=0, return_noise=True)
-    a2, z2 = head.predict_action(readout, rng, sample_offset=0, return_noise=True)
+    a1, z1 = head.predict_action_mean(readout, rng, sample_offset=0, return_noise=True)
+    a2, z2 = head.predict_action_mean(readout, rng, sample_offset=0, return_noise=True)
     assert torch.equal(a1, a2) and torch.equal(z1, z2)
     # the same z injected reproduces the drawn run exactly
-    a3 = head.predict_action(readout, None, z=z1.clone())
+    a3 = head.predict_action_mean(readout, None, z=z1.clone())
     assert torch.equal(a1, a3)
     # per-sample streams are keyed by the global sample index: a shifted batch matches
-    a4, z4 = head.predict_action(readout[5:], rng, sample_offset=5, return_noise=True)
+    a4, z4 = head.predict_action_mean(readout[5:], rng, sample_offset=5, return_noise=True)
     assert torch.equal(z4, z1[5:]) and torch.equal(a4, a1[5:])
 
 
 def test_sampler_rejects_bad_shapes(dev):
     head = _head(dev, 192)
     with pytest.raises(ValueError):
-        head.predict_action(torch.zeros((4, 191), dtype=torch.bfloat16, device=dev), None,
+        head.predict_action_mean(torch.zeros((4, 191), dtype=torch.bfloat16, device=dev), None,
                             z=torch.zeros((4, 8), device=dev))
     with pytest.raises(ValueError):
-        head.predict_action(torch.zeros((4, 192), dtype=torch.bfloat16, device=dev))
+        head.predict_action_mean(torch.zeros((4, 192), dtype=torch.bfloat16, device=dev))
 
 
 def test_octo_predict_diffusion_action(dev):
@@ -99,7 +99,7 @@ def test_predict_denoise_term_matches_oracle(dev):
     readout = (torch.randn((B, 384), generator=g) * 0.5).to(torch.bfloat16).to(dev)
     t = torch.randint(0, 32, (B,), generator=g, dtype=torch.int32)
     noisy = torch.randn((B, 8), generator=g)
-    eps = head.predict_denoise_term(readout, t.to(dev), noisy.to(dev))
+    eps = head.predict_denoise_term_mean(readout, t.to(dev), noisy.to(dev))
     temb = _np(head.time_embeddings(dev))
     torch.cuda.synchronize()
     w1, b1 = _np(head.d1.w.bf16), _np(head.d1.b.data)

@@ -197,3 +197,37 @@ def test_ln_unmerge_dropout_bwd_fused(dev, n, L, D, s0, t, r, drop):
     assert torch.equal(a_z.view(n, L, D), b_z)
     for i in range(3):
         torch.testing.assert_close(grads[i + 3], grads[i], rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("L2", [384, 385])
+def test_ln_unmerge_gate_boundary(dev, L2):
+    """The Python gate of the fused LN-1 backward + unmerge (K.ln_unmerge_ok, used by
+    Encoder1DBlock.backward) mirrors the C entry point's limits: at 384 merged rows the fused
+    kernel runs and equals the three-kernel path; at 385 the gate says no and the C entry refuses
+    (MMTError), so the block takes the three-kernel path instead of failing mid-backward."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    from multi_modal_transformers_tokenmerge_amd._C import MMTError
+    n, D, r, s0 = 2, 64, 16, 32
+    L = L2 + r
+    t = L - s0 - 4
+    g = torch.Generator().manual_seed(L2)
+    metric = torch.randn((n, t, 64), generator=g).bfloat16().to(dev)
+    unm, src, dst = K.tome_match(metric, r)
+    x = torch.randn((n, L, D), generator=g).to(dev)
+    gamma, beta = torch.randn(D, generator=g).to(dev), torch.randn(D, generator=g).to(dev)
+    x1, size_out, pos, _, mu, rs = K.tome_merge_seqnorm_fwd(x, s0, t, r, unm, src, dst, gamma, beta, 1e-6)
+    dy = torch.randn((n, L2, D), generator=g).bfloat16().to(dev)
+    grads = [torch.zeros(D, device=dev) for _ in range(5)]
+    dx = K.seqnorm_bwd(dy, x1, mu, rs, gamma, grads[0], grads[1])
+    a_g = K.tome_merge_bwd(dx, s0, t, r, pos, None, size_out)
+    a_z = K.dropout_bwd(a_g.reshape(n * L, D), None, 3, 1, 1.0)
+    tome = (s0, t, r, pos, None, size_out)
+    assert K.ln_unmerge_ok(L, L2) == (L2 <= 384)
+    if K.ln_unmerge_ok(L, L2):
+        b_g, b_z = K.ln_unmerge_dropout_bwd(dy, x1, mu, rs, gamma, grads[2], grads[3], None, tome,
+                                            None, 3, 1, 1.0, 0)
+        assert torch.equal(a_g, b_g) and torch.equal(a_z.view(n, L, D), b_z)
+    else:
+        with pytest.raises(MMTError):
+            K.ln_unmerge_dropout_bwd(dy, x1, mu, rs, gamma, grads[2], grads[3], None, tome, None, 3,
+                                     1, 1.0, 0)

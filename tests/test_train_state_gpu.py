@@ -66,7 +66,7 @@ def test_add_position_embedding(dev):
     from multi_modal_transformers_tokenmerge_amd.params import ParamStore
     from multi_modal_transformers_tokenmerge_amd.tokenizers.readout.readout import AddPositionEmbedding
     store = ParamStore()
-    mod = AddPositionEmbedding(store, "AddPositionEmbedding_0", 8, 64)
+    mod = AddPositionEmbedding().bind(store, "AddPositionEmbedding_0", 8, 64)
     store.materialize(dev, 0)
     x = torch.randn((3, 8, 64), device=dev)
     y = mod(x)
@@ -79,3 +79,59 @@ def test_add_position_embedding(dev):
     torch.testing.assert_close(mod.pe.grad, dout.sum(0), rtol=1e-6, atol=1e-6)
     with pytest.raises(ValueError):
         mod(torch.zeros((8, 64), device=dev))
+
+
+def test_wgrad_overlap_schedule_same_gradients(dev):
+    """The side-stream weight-gradient schedule (layers.wgrad_overlap: dW GEMMs forked onto a
+    second stream at each Dense.bwd, joined per block with lag 0 / 1 and at the end of the
+    backward) changes only WHEN work runs: every gradient equals the single-stream backward's,
+    eager and HIP-graph captured. The dW products (split-K slabs + ordered combine) are
+    deterministic and compared bit for bit; bias / LayerNorm / embedding gradients accumulate
+    per-workgroup partials with fp32 atomics (arrival order varies run to run), compared to
+    rounding."""
+    from multi_modal_transformers_tokenmerge_amd.layers import wgrad_overlap
+    from multi_modal_transformers_tokenmerge_amd.models.octo.config import get_config
+    from multi_modal_transformers_tokenmerge_amd.models.octo import octo as O
+    from oracle.parity import _inputs
+    cfg = get_config("octo-tiny", num_blocks=3, token_compression_sequence="[Image{4};Readout{0}]")
+    model = O.Octo(cfg, dev, seed=0)
+    images, _, actions = _inputs(model, 4)
+    img, act = torch.from_numpy(images).to(dev), torch.from_numpy(actions).to(dev)
+    rng = torch.tensor([11, 3], dtype=torch.int32, device=dev)
+
+    def fwd_bwd():
+        model.store.zero_grad()
+        _, st = model.compute_diffusion_denoise_loss(None, img, act, True, rng, 0)
+        model.backward(st)
+
+    def run(enabled, lag, graph):
+        old = (wgrad_overlap.enabled, wgrad_overlap.lag)
+        wgrad_overlap.enabled, wgrad_overlap.lag = enabled, lag
+        try:
+            if graph:
+                side = torch.cuda.Stream()
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    fwd_bwd()
+                torch.cuda.current_stream().wait_stream(side)
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    fwd_bwd()
+                g.replay()
+            else:
+                fwd_bwd()
+            torch.cuda.synchronize()
+            return model.store.flat_grad.clone()
+        finally:
+            wgrad_overlap.enabled, wgrad_overlap.lag = old
+
+    ref = run(False, 0, False)
+    kernels = [p for p in model.store.params if p.name.endswith("/kernel")]
+    for enabled, lag, graph in ((True, 0, False), (True, 1, False), (True, 1, True),
+                                (False, 0, True), (True, 2, True)):
+        got = run(enabled, lag, graph)
+        for p in kernels:
+            sl = slice(p.offset, p.offset + p.numel)
+            assert torch.equal(got[sl], ref[sl]), (p.name, enabled, lag, graph)
+        torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-6)

@@ -19,6 +19,7 @@ import csv
 import glob
 import json
 import os
+import re
 import statistics
 
 
@@ -27,10 +28,13 @@ def per_dispatch(d: str, counter: str, kernel: str) -> list[float]:
     if not files:
         raise SystemExit(f"no counter_collection csv under {d}")
     vals: dict[str, float] = {}
+    # the probe's kernel name as a whole identifier ("seqnorm_fwd_kernel" must not match
+    # "tome_merge_seqnorm_fwd_kernel"; a trailing "_" / "<" is a prefix match: "Cijk_")
+    pat = re.compile(r"(?<![A-Za-z0-9_])" + re.escape(kernel))
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if row.get("Counter_Name") != counter or kernel not in row.get("Kernel_Name", ""):
+                if row.get("Counter_Name") != counter or not pat.search(row.get("Kernel_Name", "")):
                     continue
                 key = f"{f}:{row.get('Dispatch_Id')}"
                 vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
