@@ -569,6 +569,9 @@ struct ResPlan {
   uint32_t tword[MAX_SETS][RES_TILES];  // visible keys [32 t, 32 t + 32) of query set s (bit j)
   uint8_t wblk[RES_NW][RES_SLOTS];      // query blocks of each wave, 0xff-terminated
 };
+// deferred-rescale threshold of the online softmax (log2 units): P is computed against a running max
+// that may lag the true one by up to 2^8 (fp32 sums, bf16 P keep their relative precision)
+constexpr float RES_THR = 8.f;
 
 // max / sum of a lane's value and lane l ^ 32's (the two half-waves): one v_permlane32_swap
 // (lanes 0-31 of its first result keep their own value, lanes 32-63 get lane l - 32's; the
@@ -584,6 +587,18 @@ __device__ __forceinline__ float halves_sum(float v) {
 
 __host__ __device__ __forceinline__ int res_sw(int row) {
   return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+}
+
+// A = X^T fragment [d][row] of a swizzled [row][64] image for rows rbase + 16 ks (+ 8): the
+// accumulator-operand k order (transposed reads, conflict-free, see the forward).
+__device__ __forceinline__ bf16x8 res_trans(const char* img, int rbase, int dsub, int lane) {
+  const int ti = lane & 15, tq = ti >> 2, tp = ti & 3, tg = lane >> 4, hh = lane >> 5;
+  const int col = 32 * dsub + 16 * (tg & 1) + 4 * tp;
+  const int r1 = rbase + 4 * hh + tq, r2 = r1 + 8;
+  const short4v a = tr_read(reinterpret_cast<const bf16_t*>(img + r1 * 128 + 16 * ((col >> 3) ^ res_sw(r1)) + 2 * (col & 7)));
+  const short4v b = tr_read(reinterpret_cast<const bf16_t*>(img + r2 * 128 + 16 * ((col >> 3) ^ res_sw(r2)) + 2 * (col & 7)));
+  const short8v v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
 }
 
 template <int NTILE, bool DROP, bool WS>
@@ -602,6 +617,9 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_fwd_res_kernel(
   {
     const bf16_t* kb = base + D + h * DH;
     constexpr int PIECES = ROWS / 8;  // per tensor
+#if MMT_RES_ABL == 2
+    if (L < 0)
+#endif
     for (int p = wave; p < 2 * PIECES; p += RES_NW) {
       const int t = p >= PIECES, pr = p - t * PIECES;
       const int row = 8 * pr + (lane >> 3);
@@ -636,18 +654,49 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_fwd_res_kernel(
   if (blk != 0xff) load_q(blk);
   __syncthreads();  // the DMA landed (vmcnt(0) + barrier)
 
+  // epilogue of a query block: O = acc / l (x 1/keep_prob) as bf16 rows, lse, wsum
+  auto finish = [&](const floatx16 (&oacc)[2], const float (&l4)[4], const float (&ld4)[4], float mc,
+                    int q, bool qv) {
+    float l = (l4[0] + l4[1]) + (l4[2] + l4[3]);
+    float ld = (ld4[0] + ld4[1]) + (ld4[2] + ld4[3]);
+    l = halves_sum(l);
+    if constexpr (WS) ld = halves_sum(ld);
+    const float inv = l > 0.f ? drop_scale / l : 0.f;
+    bf16_t* orow = o + (int64_t)b * o_s_b + (int64_t)(qv ? q : L - 1) * o_s_t + h * DH;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; r4 += 2) {
+        const uint32_t a0 = pk2(oacc[d][4 * r4] * inv, oacc[d][4 * r4 + 1] * inv);
+        const uint32_t a1 = pk2(oacc[d][4 * r4 + 2] * inv, oacc[d][4 * r4 + 3] * inv);
+        const uint32_t b0 = pk2(oacc[d][4 * r4 + 4] * inv, oacc[d][4 * r4 + 5] * inv);
+        const uint32_t b1 = pk2(oacc[d][4 * r4 + 6] * inv, oacc[d][4 * r4 + 7] * inv);
+        const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+        const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+#if MMT_RES_ABL == 3
+        if (qv && L < 0)
+#else
+        if (qv)
+#endif
+          *reinterpret_cast<uint4*>(orow + 32 * d + 8 * r4 + 8 * hh) = make_uint4(x0[0], x1[0], x0[1], x1[1]);
+      }
+    if (qv && lane < 32) {
+      const int64_t ri = ((int64_t)b * g.H + h) * L + q;
+      lse[ri] = l > 0.f ? mc * LN2 + logf(l) : -INFINITY;
+      if (WS) wsum[ri] = ld * inv;  // sum_k of the dropped weights
+    }
+  };
+
   while (blk != 0xff) {  // wave-uniform
     const int q0 = 32 * blk, q = q0 + lr;
     const bool qv = q < L;
     const int qc = qv ? q : L - 1;
     const int sq = set_of(mask, qc);
     const int sq0 = __builtin_amdgcn_readfirstlane(sq);
-    const bool causal_any = mask.causal != 0u;
     // one query set over the block and no causal set: the visibility words are wave-uniform
-    const bool uni = !causal_any && __all(sq == sq0);
+    const bool uni = mask.causal == 0u && __all(sq == sq0);
     // visibility word of every key tile for this lane's query, fetched ONCE per block (a
-    // divergent kernarg read inside the tile loop made the compiler wait vmcnt(0) per tile,
-    // which also drained the next block's Q prefetch)
+    // divergent kernarg read inside the tile loop made the compiler wait vmcnt(0) per tile)
     uint32_t vws[NTILE];
     if (uni) {
 #pragma unroll
@@ -663,145 +712,140 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_fwd_res_kernel(
         vws[t] = vw;
       }
     }
-    // the row in two chunks of CH tiles (one O rescale between them) keeps the score registers
-    // at CH x 16 (10 tiles in one chunk spill)
-    constexpr int CH = NTILE > 6 ? (NTILE + 1) / 2 : NTILE;
+    // tiles [0, nt): up to the last one any query of the block sees (invisible tiles before it,
+    // rare, are computed fully masked)
+    int nt = 0;
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t)
+      if (!__all(vws[t] == 0u)) nt = t + 1;
+#if MMT_RES_ABL == 1
+    nt = 0;
+#endif
+    const int nblk = slot + 1 < RES_SLOTS ? plan.wblk[wave][slot + 1] : 0xff;
+    bf16x8 qn[NS];  // the next block's Q, loaded under this block
+    {
+      const int bk = nblk != 0xff ? nblk : blk;
+      const int qq = 32 * bk + lr;
+      const bool ok = qq < L;
+      const bf16_t* qp = base + (int64_t)(ok ? qq : L - 1) * g.s_t + h * DH;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) qn[s] = row_frag_global(qp, ok, s, lane);
+    }
+    // flash-style online softmax with a deferred rescale, software-pipelined: the QK^T MFMAs of
+    // tile t + 1 and the K fragments of tile t + 2 are issued before the softmax of tile t, and
+    // tile t's V^T fragments before it, so MFMA / LDS latencies hide under the VALU work
+    bf16x8 kr[NS];
+    auto kread = [&](int t) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) kr[s] = *reinterpret_cast<const bf16x8*>(smc + t * 4096 + koff[s]);
+    };
+    auto qk = [&]() {
+      floatx16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kr[s], qf[s], acc, 0, 0, 0);
+      return acc;
+    };
+    auto maskw = [&](floatx16& acc, uint32_t vw) {  // partially visible tile: masked scores -> -inf
+      if (!__all(vw == 0xffffffffu)) {
+        const uint32_t w = vw >> (4 * hh);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int mk = bitmask_of(w, rbit(r));
+          acc[r] = __int_as_float((__float_as_int(acc[r]) & mk) | (~mk & (int)0xff800000u));
+        }
+      }
+    };
+    auto rmax = [&](const floatx16& a) {
+      float m8[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) m8[r] = fmaxf(a[2 * r], a[2 * r + 1]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) m8[r] = fmaxf(m8[r], m8[r + 4]);
+      return halves_max(fmaxf(fmaxf(m8[0], m8[1]), fmaxf(m8[2], m8[3])));
+    };
     floatx16 oacc[2];
 #pragma unroll
     for (int d = 0; d < 2; ++d)
 #pragma unroll
       for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
-    float mrow = -INFINITY;
-    float l4[4] = {0.f, 0.f, 0.f, 0.f}, ld4[4] = {0.f, 0.f, 0.f, 0.f};  // 4 chains, not 1
-    int nblk = 0xff;
-    auto chunk = [&](auto t0c) {
-      constexpr int T0 = decltype(t0c)::value;
-      constexpr int TN = T0 + CH < NTILE ? T0 + CH : NTILE;
-      floatx16 S[CH];
-      bool act[CH];
-      float mx = -INFINITY;
+    float l4[4] = {0.f, 0.f, 0.f, 0.f}, ld4[4] = {0.f, 0.f, 0.f, 0.f};
+    float mrow = -INFINITY, mc = 0.f;
+    floatx16 Sa;
+    // dropout lane masks (scalar loads), one tile ahead: waiting on them at first use stalled
+    // every tile
+    TileMasks<16> dm[2];
+    if constexpr (DROP) dm[0].load(drop_q, drop_lp, blk, 0);
+    if (nt > 0) {
+      kread(0);
+      Sa = qk();
+      if (nt > 1) kread(1);
+      maskw(Sa, vws[0]);
+      mrow = rmax(Sa);
+      mc = mrow == -INFINITY ? 0.f : mrow * c2;
+    }
 #pragma unroll
-      for (int t = T0; t < TN; ++t) {
-        const uint32_t vw = vws[t];
-        act[t - T0] = !__all(vw == 0u);
-        if (act[t - T0]) {
-          floatx16 acc;
+    for (int t = 0; t < NTILE; ++t) {
+      if (t < nt) {  // wave-uniform
+        if constexpr (DROP)
+          if (t + 1 < NTILE) dm[(t + 1) & 1].load(drop_q, drop_lp, blk, 32 * (t + 1));
+        floatx16 Sb;
+        if (t + 1 < NTILE && t + 1 < nt) {
+          Sb = qk();
+          if (t + 2 < NTILE && t + 2 < nt) kread(t + 2);
+          maskw(Sb, vws[t + 1]);
+        }
+        bf16x8 vt[2][2];
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        for (int d = 0; d < 2; ++d)
 #pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(smc + t * 4096 + koff[s]);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], acc, 0, 0, 0);
-          }
-          if (!__all(vw == 0xffffffffu)) {  // partially visible: masked scores -> -inf
-            const uint32_t w = vw >> (4 * hh);
+          for (int ks = 0; ks < 2; ++ks) vt[d][ks] = res_trans(Vimg, 32 * t + 16 * ks, d, lane);
+        if (t > 0) {
+          const float tm = rmax(Sa);
+          if (__any(tm * c2 > mc + RES_THR)) {  // rare: the row max grew past the threshold
+            const float mn = fmaxf(mrow, tm);
+            const float mcn = mn == -INFINITY ? 0.f : mn * c2;
+            const float alpha = fast_exp2(mc - mcn);
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int mk = bitmask_of(w, rbit(r));
-              acc[r] = __int_as_float((__float_as_int(acc[r]) & mk) | (~mk & (int)0xff800000u));
+            for (int d = 0; d < 2; ++d)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              l4[i] *= alpha;
+              ld4[i] *= alpha;
             }
-          }
-          float m8[8];
-#pragma unroll
-          for (int r = 0; r < 8; ++r) m8[r] = fmaxf(acc[2 * r], acc[2 * r + 1]);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) m8[r] = fmaxf(m8[r], m8[r + 4]);
-          mx = fmaxf(mx, fmaxf(fmaxf(m8[0], m8[1]), fmaxf(m8[2], m8[3])));
-          S[t - T0] = acc;
-        }
-      }
-      if constexpr (TN == NTILE) {
-        // next block's Q under this block's last softmax and P.V (qf is dead now)
-        nblk = slot + 1 < RES_SLOTS ? plan.wblk[wave][slot + 1] : 0xff;
-        if (nblk != 0xff) load_q(nblk);
-      }
-      mx = halves_max(mx);
-      const float mn = fmaxf(mrow, mx);
-      const float mc = mn == -INFINITY ? 0.f : mn * c2;
-      if constexpr (T0 > 0) {  // rescale what the earlier chunk accumulated
-        const float alpha = fast_exp2(mrow * c2 - mc);  // mrow = -inf -> 0
-        if (!__all(alpha == 1.f)) {
-#pragma unroll
-          for (int d = 0; d < 2; ++d)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            l4[i] *= alpha;
-            ld4[i] *= alpha;
+            mrow = mn;
+            mc = mcn;
           }
         }
-      }
-      mrow = mn;
-#pragma unroll
-      for (int t = T0; t < TN; ++t) {
-        if (!act[t - T0]) continue;  // wave-uniform
-        TileMasks<16> dm;
-        if constexpr (DROP) dm.load(drop_q, drop_lp, blk, 32 * t);
         floatx16 p;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float e = fast_exp2(fmaf(S[t - T0][r], c2, -mc));
+          float e = fast_exp2(fmaf(Sa[r], c2, -mc));
           l4[r & 3] += e;
-          if constexpr (DROP) e = sel_keep(e, dm.m[r]);
+          if constexpr (DROP) e = sel_keep(e, dm[t & 1].m[r]);
           if constexpr (WS) ld4[r & 3] += e;
           p[r] = e;
         }
         const bf16x8 p0 = pack_frag(p, 0), p1 = pack_frag(p, 1);
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) {
-            // A = V^T[d][key]: keys 32 t + 16 ks + 4 hh + tq (+ 8), columns 32 d + 16 (tg & 1) + 4 tp
-            const int col = 32 * d + 16 * (tg & 1) + 4 * tp;
-            const int r1 = 32 * t + 16 * ks + 4 * hh + tq, r2 = r1 + 8;
-            const short4v va = tr_read(reinterpret_cast<const bf16_t*>(
-                Vimg + r1 * 128 + 16 * ((col >> 3) ^ res_sw(r1)) + 2 * (col & 7)));
-            const short4v vb = tr_read(reinterpret_cast<const bf16_t*>(
-                Vimg + r2 * 128 + 16 * ((col >> 3) ^ res_sw(r2)) + 2 * (col & 7)));
-            const short8v vv = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
-            oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vv),
-                                                              ks ? p1 : p0, oacc[d], 0, 0, 0);
-          }
+          oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vt[d][0], p0, oacc[d], 0, 0, 0);
+          oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vt[d][1], p1, oacc[d], 0, 0, 0);
         }
+        Sa = Sb;
       }
-    };
-    chunk(std::integral_constant<int, 0>{});
-    if constexpr (CH < NTILE) chunk(std::integral_constant<int, CH>{});
-    const float mx = mrow;
-    const float mc = mx == -INFINITY ? 0.f : mx * c2;
-    (void)mc;
-    float l = (l4[0] + l4[1]) + (l4[2] + l4[3]);
-    float ld = (ld4[0] + ld4[1]) + (ld4[2] + ld4[3]);
-    l = halves_sum(l);
-    if constexpr (WS) ld = halves_sum(ld);
-    const float inv = l > 0.f ? drop_scale / l : 0.f;
-    // O rows: lane pairs (q, hh) hold d = 32 dd + 8 r4 + 4 hh + {0..3}; one permlane32 swap per
-    // dword pairs r4 / r4 + 1 so that each lane stores 16 contiguous bytes (T21)
-    bf16_t* orow = o + (int64_t)b * o_s_b + (int64_t)qc * o_s_t + h * DH;
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; r4 += 2) {
-        const uint32_t a0 = pk2(oacc[d][4 * r4] * inv, oacc[d][4 * r4 + 1] * inv);
-        const uint32_t a1 = pk2(oacc[d][4 * r4 + 2] * inv, oacc[d][4 * r4 + 3] * inv);
-        const uint32_t b0 = pk2(oacc[d][4 * r4 + 4] * inv, oacc[d][4 * r4 + 5] * inv);
-        const uint32_t b1 = pk2(oacc[d][4 * r4 + 6] * inv, oacc[d][4 * r4 + 7] * inv);
-        const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-        const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-        if (qv)
-          *reinterpret_cast<uint4*>(orow + 32 * d + 8 * r4 + 8 * hh) =
-              make_uint4(x0[0], x1[0], x0[1], x1[1]);
-      }
-    if (qv && lane < 32) {
-      const int64_t ri = ((int64_t)b * g.H + h) * L + q;
-      lse[ri] = l > 0.f ? mc * LN2 + logf(l) : -INFINITY;
-      if (WS) wsum[ri] = ld * inv;  // sum_k of the dropped weights
     }
+    finish(oacc, l4, ld4, mc, q, qv);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) qf[s] = qn[s];
     ++slot;
     blk = nblk;
   }
 }
+
 
 // Host plan of the resident forward: per-(query set, key tile) visibility words and the query
 // blocks of each wave (longest-processing-time first on the number of visible key tiles).
@@ -839,6 +883,385 @@ static bool res_plan(const AttnMask& m, int L, ResPlan& plan) {
       if (cnt[w] < RES_SLOTS && (best < 0 || load[w] < load[best])) best = w;
     if (best < 0) return false;
     plan.wblk[best][cnt[best]++] = (uint8_t)order[k];
+    load[best] += cost[order[k]];
+  }
+  return true;
+}
+
+// ===================================================== backward, resident operands (Dh = 64)
+// One workgroup per (sample, head), two phases over LDS images of the same layout as the
+// forward's (res_sw chunk swizzle, rows >= L copies of row L - 1):
+//   A (queries on the lanes): K and V resident; per query block S^T = K Q^T, dP^T = V dO^T,
+//     P = exp2(S c - lse), dS = P (keep dP / kp - delta), dQ^T += K^T dS^T (K^T by transposed
+//     reads of the K image); delta = rowsum(dO O) computed here and written for phase B;
+//   B (keys on the lanes), after a barrier that frees the images: Q and dO resident; per key
+//     block S = Q K^T, dP = dO V^T, dV^T += dO^T P_kept, dK^T += Q^T dS (dO^T, Q^T transposed
+//     reads), lse / delta of the query rows from global (L2-hot).
+// Query / key blocks are dealt to the 4 waves by the host plan. The fused-QKV bias gradient
+// (column sums of dq, dk, dv) is summed per lane over the wave's blocks, reduced over the lanes
+// at the end of each phase and written to a per-(sample, wave) slab row — plain stores, summed
+// by one column-sum launch afterwards (no atomics: bitwise reproducible).
+struct ResPlanB {
+  uint32_t qword[MAX_SETS][RES_TILES];  // phase A: keys of tile t that query set s sees
+  uint32_t kword[MAX_SETS][RES_TILES];  // phase B: queries of tile t that see key set s
+  uint8_t qblk[RES_NW][RES_SLOTS];
+  uint8_t kblk[RES_NW][RES_SLOTS];
+};
+
+// DMA of rows [0, 32 NTILE) (clamped to L - 1) of two (row stride s) bf16 tensors into the two
+// swizzled images of smem: one wave-instruction = 8 rows x 128 B
+template <int ROWS>
+__device__ __forceinline__ void res_dma2(bf16_t* smem, const bf16_t* a, int64_t sa, const bf16_t* b,
+                                         int64_t sb, int L, int wave, int lane) {
+  constexpr int PIECES = ROWS / 8;
+  for (int p = wave; p < 2 * PIECES; p += RES_NW) {
+    const int t = p >= PIECES, pr = p - t * PIECES;
+    const int row = 8 * pr + (lane >> 3);
+    const int c = (lane & 7) ^ res_sw(row);
+    const bf16_t* src = (t ? b : a) + (int64_t)min(row, L - 1) * (t ? sb : sa) + 8 * c;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(smem + t * ROWS * 64 + pr * 512),
+                                     16, 0, 0);
+  }
+}
+
+// column sums of the lanes: acc[dd][r] (d = 32 dd + rbit(r) + 4 hh, one column per lane of each
+// half) summed over the 32 lanes of each half; lane (hh, dd = (l >> 4) & 1, r = l & 15) then
+// stores its d's total to row[d]
+__device__ __forceinline__ void res_colsum_store(float (&acc)[2][16], float* row, int lane) {
+#pragma unroll
+  for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float v = acc[dd][r];
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
+      acc[dd][r] = v;
+    }
+  const int hh = lane >> 5, mdd = (lane >> 4) & 1, mr = lane & 15;
+  float out = 0.f;
+#pragma unroll
+  for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (dd == mdd && r == mr) out = acc[dd][r];
+  row[32 * mdd + rbit(mr) + 4 * hh] = out;
+}
+
+// store a wave's 32 x 64 rows from O^T-layout accumulators (lane = row), scaled, as bf16 with
+// 16-B stores (permlane32 swaps, as the forward's O)
+__device__ __forceinline__ void res_store_rows(const floatx16 (&acc)[2], float sc, bf16_t* rowp,
+                                               bool valid, int hh) {
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r4 = 0; r4 < 4; r4 += 2) {
+      const uint32_t a0 = pk2(acc[d][4 * r4] * sc, acc[d][4 * r4 + 1] * sc);
+      const uint32_t a1 = pk2(acc[d][4 * r4 + 2] * sc, acc[d][4 * r4 + 3] * sc);
+      const uint32_t b0 = pk2(acc[d][4 * r4 + 4] * sc, acc[d][4 * r4 + 5] * sc);
+      const uint32_t b1 = pk2(acc[d][4 * r4 + 6] * sc, acc[d][4 * r4 + 7] * sc);
+      const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+      const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+      if (valid)
+        *reinterpret_cast<uint4*>(rowp + 32 * d + 8 * r4 + 8 * hh) = make_uint4(x0[0], x1[0], x0[1], x1[1]);
+    }
+}
+
+template <int NTILE, bool DROP>
+__global__ __launch_bounds__(64 * RES_NW, 2) void attn_bwd_res_kernel(
+    Geo g, AttnMask mask, ResPlanB plan, const uint32_t* __restrict__ drop_q,
+    const uint32_t* __restrict__ drop_k, int drop_lp, float drop_scale,
+    const bf16_t* __restrict__ dout, int64_t d_s_b, int64_t d_s_t, const float* __restrict__ lse,
+    const bf16_t* __restrict__ o, int64_t o_s_b, int64_t o_s_t, float* __restrict__ delta,
+    bf16_t* __restrict__ dqkv, int64_t dq_s_b, int64_t dq_s_t, float* __restrict__ bias_ws) {
+  constexpr int DH = 64, NS = 4, ROWS = 32 * NTILE;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * ROWS * DH];
+  const int bh = blockIdx.x, b = bh / g.H, h = bh - b * g.H;
+  const int lane = threadIdx.x & 63, hh = lane >> 5, lr = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int L = g.L, D = g.H * DH;
+  const bf16_t* base = g.qkv + (int64_t)b * g.s_b;
+  const bf16_t* dbase = dout + (int64_t)b * d_s_b + h * DH;
+  const int64_t row_bh = (int64_t)bh * L;
+  const float c2 = g.scale * LOG2E;
+  const char* img0 = reinterpret_cast<const char*>(smem);
+  const char* img1 = img0 + ROWS * DH * 2;
+  int koff[NS];  // row-fragment offsets (row lr of a 32-row tile, chunk 2 s + hh)
+#pragma unroll
+  for (int s = 0; s < NS; ++s) koff[s] = lr * 128 + 16 * ((2 * s + hh) ^ res_sw(lr));
+  float* ws_row = bias_ws ? bias_ws + ((int64_t)b * RES_NW + wave) * 3 * D + h * DH : nullptr;
+
+  // ================= phase A: dQ (queries on the lanes), K / V resident
+  res_dma2<ROWS>(smem, base + D + h * DH, g.s_t, base + 2 * D + h * DH, g.s_t, L, wave, lane);
+  float bq[2][16];
+#pragma unroll
+  for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bq[dd][r] = 0.f;
+  bf16x8 qf[NS], df[NS], of[NS];
+  auto load_q = [&](int bk) {
+    const int qq = 32 * bk + lr;
+    const bool ok = qq < L;
+    const int qc = ok ? qq : L - 1;
+    const bf16_t* qp = base + (int64_t)qc * g.s_t + h * DH;
+    const bf16_t* dp = dbase + (int64_t)qc * d_s_t;
+    const bf16_t* op = o + (int64_t)b * o_s_b + (int64_t)qc * o_s_t + h * DH;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      qf[s] = row_frag_global(qp, ok, s, lane);
+      df[s] = row_frag_global(dp, ok, s, lane);
+      of[s] = row_frag_global(op, ok, s, lane);
+    }
+  };
+  int slot = 0, blk = plan.qblk[wave][0];
+  if (blk != 0xff) load_q(blk);
+  __syncthreads();
+  while (blk != 0xff) {  // wave-uniform
+    const int q = 32 * blk + lr;
+    const bool qv = q < L;
+    const int qc = qv ? q : L - 1;
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part = fmaf((float)of[s][j], (float)df[s][j], part);
+    const float dlt = halves_sum(part);
+    if (qv && lane < 32) delta[row_bh + q] = dlt;
+    const float lse2 = qv ? lse[row_bh + q] * LOG2E : INFINITY;
+    const int sq = set_of(mask, qc);
+    const int sq0 = __builtin_amdgcn_readfirstlane(sq);
+    const bool uni = mask.causal == 0u && __all(sq == sq0);
+    uint32_t vws[NTILE];
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t) {
+      uint32_t vw = uni ? plan.qword[sq0][t] : plan.qword[sq][t];
+      if (!uni && ((mask.causal >> sq) & 1u)) {
+        const int a0 = max(q + 1 - 32 * t, 0), e0 = min(mask.start[sq] + mask.len[sq] - 32 * t, 32);
+        if (a0 < e0) vw &= ~(uint32_t)(bit_range(a0, e0));
+      }
+      vws[t] = vw;
+    }
+    floatx16 dq[2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t) {
+      const uint32_t vw = vws[t];
+      if (__all(vw == 0u)) continue;  // wave-uniform
+      floatx16 sacc, pacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sacc[r] = 0.f;
+        pacc[r] = 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(img0 + t * 4096 + koff[s]);
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(img1 + t * 4096 + koff[s]);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc, 0, 0, 0);
+        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, df[s], pacc, 0, 0, 0);
+      }
+      TileMasks<16> dm;
+      if constexpr (DROP) dm.load(drop_q, drop_lp, blk, 32 * t);
+      const bool full = __all(vw == 0xffffffffu);
+      const uint32_t w = vw >> (4 * hh);
+      floatx16 ds;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p = fast_exp2(fmaf(sacc[r], c2, -lse2));
+        if (!full) p = __int_as_float(__float_as_int(p) & bitmask_of(w, rbit(r)));
+        float tt = pacc[r] * drop_scale;
+        if constexpr (DROP) tt = sel_keep(tt, dm.m[r]);
+        ds[r] = p * (tt - dlt);
+      }
+      const bf16x8 d0 = pack_frag(ds, 0), d1 = pack_frag(ds, 1);
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        dq[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img0, 32 * t, d, lane), d0, dq[d], 0, 0, 0);
+        dq[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img0, 32 * t + 16, d, lane), d1, dq[d], 0, 0, 0);
+      }
+    }
+    const int nblk = slot + 1 < RES_SLOTS ? plan.qblk[wave][slot + 1] : 0xff;
+    if (nblk != 0xff) load_q(nblk);
+    res_store_rows(dq, g.scale, dqkv + (int64_t)b * dq_s_b + (int64_t)qc * dq_s_t + h * DH, qv, hh);
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bq[d][r] += dq[d][r] * g.scale;
+    ++slot;
+    blk = nblk;
+  }
+  if (ws_row) res_colsum_store(bq, ws_row, lane);
+
+  // ================= phase B: dK / dV (keys on the lanes), Q / dO resident
+  __syncthreads();  // every wave is done with the K / V images; delta is written
+  res_dma2<ROWS>(smem, base + h * DH, g.s_t, dbase, d_s_t, L, wave, lane);
+  float bk[2][16], bv[2][16];
+#pragma unroll
+  for (int dd = 0; dd < 2; ++dd)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      bk[dd][r] = 0.f;
+      bv[dd][r] = 0.f;
+    }
+  bf16x8 kf[NS], vf[NS];
+  auto load_k = [&](int bk_) {
+    const int kk = 32 * bk_ + lr;
+    const bool ok = kk < L;
+    const bf16_t* kp = base + (int64_t)(ok ? kk : L - 1) * g.s_t + D + h * DH;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      kf[s] = row_frag_global(kp, ok, s, lane);
+      vf[s] = row_frag_global(kp + D, ok, s, lane);
+    }
+  };
+  slot = 0;
+  blk = plan.kblk[wave][0];
+  if (blk != 0xff) load_k(blk);
+  __syncthreads();
+  while (blk != 0xff) {
+    const int key = 32 * blk + lr;
+    const bool kv = key < L;
+    const int kc = kv ? key : L - 1;
+    const int sk = set_of(mask, kc);
+    const int sk0 = __builtin_amdgcn_readfirstlane(sk);
+    const bool uni = mask.causal == 0u && __all(sk == sk0);
+    uint32_t qws[NTILE];
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t) {
+      uint32_t qw = uni ? plan.kword[sk0][t] : plan.kword[sk][t];
+      if (!uni && ((mask.causal >> sk) & 1u)) {  // queries of its own set before the key
+        const int a0 = max(mask.start[sk] - 32 * t, 0), e0 = min(key - 32 * t, 32);
+        if (a0 < e0) qw &= ~(uint32_t)(bit_range(a0, e0));
+      }
+      if (!kv) qw = 0u;
+      qws[t] = qw;
+    }
+    floatx16 dk[2], dv[2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        dk[d][r] = 0.f;
+        dv[d][r] = 0.f;
+      }
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t) {
+      const uint32_t qw = qws[t];
+      if (__all(qw == 0u)) continue;  // wave-uniform
+      // lse (log2 units) / delta of the query rows 32 t + 8 j + 4 hh + {0..3} (float4 j)
+      float lr2[16], dr[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r0 = min(32 * t + 8 * j + 4 * hh, ((L - 1) & ~3));
+        const float4 a = *reinterpret_cast<const float4*>(lse + row_bh + r0);
+        const float4 c = *reinterpret_cast<const float4*>(delta + row_bh + r0);
+        lr2[4 * j] = a.x * LOG2E; lr2[4 * j + 1] = a.y * LOG2E;
+        lr2[4 * j + 2] = a.z * LOG2E; lr2[4 * j + 3] = a.w * LOG2E;
+        dr[4 * j] = c.x; dr[4 * j + 1] = c.y; dr[4 * j + 2] = c.z; dr[4 * j + 3] = c.w;
+      }
+      floatx16 sacc, pacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sacc[r] = 0.f;
+        pacc[r] = 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const bf16x8 qr = *reinterpret_cast<const bf16x8*>(img0 + t * 4096 + koff[s]);
+        const bf16x8 dr_ = *reinterpret_cast<const bf16x8*>(img1 + t * 4096 + koff[s]);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qr, kf[s], sacc, 0, 0, 0);
+        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dr_, vf[s], pacc, 0, 0, 0);
+      }
+      TileMasks<16> dm;
+      if constexpr (DROP) dm.load(drop_k, drop_lp, blk, 32 * t);
+      const uint32_t w = qw >> (4 * hh);
+      floatx16 pk, ds;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        // rows past L: masked by qw (their lse / delta are clamped copies)
+        float p = fast_exp2(fmaf(sacc[r], c2, -lr2[r]));
+        p = __int_as_float(__float_as_int(p) & bitmask_of(w, rbit(r)));
+        float tt = pacc[r] * drop_scale;
+        float pkr = p;
+        if constexpr (DROP) {
+          pkr = sel_keep(p, dm.m[r]);
+          tt = sel_keep(tt, dm.m[r]);
+        }
+        pk[r] = pkr;
+        ds[r] = p * (tt - dr[r]);
+      }
+      const bf16x8 p0 = pack_frag(pk, 0), p1 = pack_frag(pk, 1);
+      const bf16x8 s0 = pack_frag(ds, 0), s1 = pack_frag(ds, 1);
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img1, 32 * t, d, lane), p0, dv[d], 0, 0, 0);
+        dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img1, 32 * t + 16, d, lane), p1, dv[d], 0, 0, 0);
+        dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img0, 32 * t, d, lane), s0, dk[d], 0, 0, 0);
+        dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img0, 32 * t + 16, d, lane), s1, dk[d], 0, 0, 0);
+      }
+    }
+    const int nblk = slot + 1 < RES_SLOTS ? plan.kblk[wave][slot + 1] : 0xff;
+    if (nblk != 0xff) load_k(nblk);
+    bf16_t* kro = dqkv + (int64_t)b * dq_s_b + (int64_t)kc * dq_s_t + D + h * DH;
+    res_store_rows(dk, g.scale, kro, kv, hh);
+    res_store_rows(dv, drop_scale, kro + D, kv, hh);
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        bk[d][r] += dk[d][r] * g.scale;
+        bv[d][r] += dv[d][r] * drop_scale;
+      }
+    ++slot;
+    blk = nblk;
+  }
+  if (ws_row) {
+    res_colsum_store(bk, ws_row + D, lane);
+    res_colsum_store(bv, ws_row + 2 * D, lane);
+  }
+}
+
+// Host plan of the resident backward: the forward's query-side words and query-block deal, and
+// the key-side words (queries of tile t that see key set s) and key-block deal.
+static bool res_plan_bwd(const AttnMask& m, int L, ResPlanB& pb) {
+  ResPlan pf;
+  if (!res_plan(m, L, pf)) return false;
+  const int nt = (L + 31) / 32;
+  memset(&pb, 0, sizeof(pb));
+  memcpy(pb.qword, pf.tword, sizeof(pb.qword));
+  memcpy(pb.qblk, pf.wblk, sizeof(pb.qblk));
+  for (int s = 0; s < m.n_sets; ++s)
+    for (int t = 0; t < nt; ++t) {
+      uint32_t w = 0;
+      for (int i = 0; i < m.n_sets; ++i) {  // query set i sees key set s
+        if (!((m.vis[i] >> s) & 1u) || m.len[i] <= 0) continue;
+        const int a = std::max(m.start[i] - 32 * t, 0), e = std::min(m.start[i] + m.len[i] - 32 * t, 32);
+        for (int j = a; j < e; ++j) w |= 1u << j;
+      }
+      pb.kword[s][t] = w;
+    }
+  memset(pb.kblk, 0xff, sizeof(pb.kblk));
+  int cost[RES_TILES], order[RES_TILES];
+  for (int i = 0; i < nt; ++i) {
+    uint32_t any[RES_TILES] = {0};
+    for (int s = 0; s < m.n_sets; ++s)
+      if (m.len[s] > 0 && m.start[s] < std::min(L, 32 * i + 32) && m.start[s] + m.len[s] > 32 * i)
+        for (int t = 0; t < nt; ++t) any[t] |= pb.kword[s][t];
+    cost[i] = 1;
+    for (int t = 0; t < nt; ++t) cost[i] += any[t] ? 4 : 0;
+    order[i] = i;
+  }
+  std::sort(order, order + nt, [&](int a, int b) { return cost[a] > cost[b] || (cost[a] == cost[b] && a < b); });
+  int load[RES_NW] = {0}, cnt[RES_NW] = {0};
+  for (int k = 0; k < nt; ++k) {
+    int best = -1;
+    for (int w = 0; w < RES_NW; ++w)
+      if (cnt[w] < RES_SLOTS && (best < 0 || load[w] < load[best])) best = w;
+    if (best < 0) return false;
+    pb.kblk[best][cnt[best]++] = (uint8_t)order[k];
     load[best] += cost[order[k]];
   }
   return true;
