@@ -252,8 +252,9 @@ int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, int L, int H,
                  const uint32_t* set_vis, const uint32_t* drop_bits, float keep_prob,
                  const float* bias, void* o, int64_t o_s_b, int64_t o_s_t, float* lse,
                  float* wsum, mmt_stream_t stream);
-/* Backward: writes dq, dk, dv into dqkv (same row layout as qkv). delta: fp32 (B, H, L)
- * workspace (rowsum(dO * O)). drop_bits / drop_bits_t: the query-word and key-word images of
+/* Backward: writes dq, dk, dv into dqkv (same row layout as qkv). delta: fp32 workspace of
+ * B * H * 2 * roundup(L, 64) floats (rowsum(dO * O), and the row constants of the K/V-resident
+ * kernel used for Dh 64 and 32 < L <= 320). drop_bits / drop_bits_t: the query-word and key-word images of
  * mmt_dropout_bits (`out` / `out_t`); both or neither. bias_grad (fp32 [3 H Dh], may be NULL) += the
  * column sums of dq | dk | dv over (B, L): the bias gradient of the fused QKV projection. */
 int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, int L, int H, int Dh,

@@ -470,6 +470,11 @@ def attn_fwd(qkv: torch.Tensor, H: int, scale: float, table: SetTable | None = N
     return out, lse
 
 
+def attn_lp(L: int) -> int:
+    """Padded row length of the attention dropout words and backward workspace (roundup(L, 64))."""
+    return (L + 63) & ~63
+
+
 def attn_bwd(qkv, o, dout, lse, H: int, scale: float, table: SetTable | None = None,
              drop_bits=None, keep_prob: float = 1.0, dqkv: torch.Tensor | None = None,
              bias_grad: torch.Tensor | None = None):
@@ -481,7 +486,8 @@ def attn_bwd(qkv, o, dout, lse, H: int, scale: float, table: SetTable | None = N
         raise ValueError("o/dout need unit inner stride")
     if dqkv is None:
         dqkv = torch.empty_like(qkv)
-    delta = torch.empty((B, H, L), dtype=torch.float32, device=qkv.device)
+    # workspace: rowsum(dO O) of the tiled kernels / the row constants of the resident one
+    delta = torch.empty((B * H * 2 * attn_lp(L),), dtype=torch.float32, device=qkv.device)
     if drop_bits is not None:
         _check_attn_bits(drop_bits, L)
     bits, bits_t = (None, None) if drop_bits is None else (drop_bits[0], drop_bits[1])

@@ -550,12 +550,11 @@ __global__ __launch_bounds__(64 * NW, DH > 128 ? 1 : 2) void attn_fwd_kernel(
 // ===================================================== forward, K/V resident in LDS (Dh = 64)
 // For the short sequences of the training step (L <= 320: every OCTO-small / tiny layer) the
 // whole K and V of one (sample, head) fit in LDS (2 x 40 KB at L = 320), so a workgroup loads
-// them ONCE by DMA (buffer/global_load ... lds, no VGPR staging, no per-tile barrier) and its 4
-// waves then sweep their query blocks with no further synchronisation. Two such workgroups fill
-// the 160 KB of a CU: one computes while the other's DMA is in flight. Each wave keeps the
-// complete score row of its 32 queries in registers (<= 10 tiles x 16 fp32), so the softmax is
-// exact and two-pass (row max over all keys, then exp / sum / dropout / pack / P.V per tile):
-// no online rescale of O and no per-tile max bookkeeping.
+// them ONCE by DMA (global_load_lds, no VGPR staging, no per-tile barrier) and its 4 waves then
+// sweep their query blocks with no further synchronisation. Two such workgroups fill the 160 KB
+// of a CU. Per 32-row query block a wave makes two passes over the visible key tiles: the exact
+// row max (QK^T only), then exp / sum / dropout / pack / P.V, software-pipelined (QK^T of tile
+// t + 1 and the K fragments of tile t + 2 are issued ahead of tile t's softmax).
 //   LDS image: K rows [0, 32 NTILE) then V rows, 128 B per row, 16-B chunk c of row r stored at
 //   chunk c ^ res_sw(r): conflict-free for the K row reads (ds_read_b128, 16 rows per lane group)
 //   AND the V transposed reads (ds_read_b64_tr_b16, 4 rows x 64 B per 32-lane half).
@@ -569,9 +568,6 @@ struct ResPlan {
   uint32_t tword[MAX_SETS][RES_TILES];  // visible keys [32 t, 32 t + 32) of query set s (bit j)
   uint8_t wblk[RES_NW][RES_SLOTS];      // query blocks of each wave, 0xff-terminated
 };
-// deferred-rescale threshold of the online softmax (log2 units): P is computed against a running max
-// that may lag the true one by up to 2^8 (fp32 sums, bf16 P keep their relative precision)
-constexpr float RES_THR = 8.f;
 
 // max / sum of a lane's value and lane l ^ 32's (the two half-waves): one v_permlane32_swap
 // (lanes 0-31 of its first result keep their own value, lanes 32-63 get lane l - 32's; the
@@ -757,21 +753,30 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_fwd_res_kernel(
         }
       }
     };
-    auto rmax = [&](const floatx16& a) {
-      float m8[8];
+    // pass 1: the exact row max over the visible keys (QK^T MFMAs and a max per score), so
+    // that pass 2's probabilities are exp(s - max) as the softmax defines them: the row's
+    // largest weight enters the P.V product as an exact 1.0 (a running max that lags it
+    // rounds the dominant weights to bf16: +18 % output error measured)
+    float mrow = -INFINITY;
+    if (nt > 0) kread(0);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) m8[r] = fmaxf(a[2 * r], a[2 * r + 1]);
+    for (int t = 0; t < NTILE; ++t) {
+      if (t < nt) {  // wave-uniform
+        floatx16 S = qk();
+        if (t + 1 < NTILE && t + 1 < nt) kread(t + 1);
+        maskw(S, vws[t]);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) m8[r] = fmaxf(m8[r], m8[r + 4]);
-      return halves_max(fmaxf(fmaxf(m8[0], m8[1]), fmaxf(m8[2], m8[3])));
-    };
+        for (int r = 0; r < 16; r += 4) mrow = fmaxf(fmaxf(mrow, fmaxf(S[r], S[r + 1])), fmaxf(S[r + 2], S[r + 3]));
+      }
+    }
+    mrow = halves_max(mrow);
+    const float mc = mrow == -INFINITY ? 0.f : mrow * c2;
     floatx16 oacc[2];
 #pragma unroll
     for (int d = 0; d < 2; ++d)
 #pragma unroll
       for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
     float l4[4] = {0.f, 0.f, 0.f, 0.f}, ld4[4] = {0.f, 0.f, 0.f, 0.f};
-    float mrow = -INFINITY, mc = 0.f;
     floatx16 Sa;
     // dropout lane masks (scalar loads), one tile ahead: waiting on them at first use stalled
     // every tile
@@ -782,8 +787,6 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_fwd_res_kernel(
       Sa = qk();
       if (nt > 1) kread(1);
       maskw(Sa, vws[0]);
-      mrow = rmax(Sa);
-      mc = mrow == -INFINITY ? 0.f : mrow * c2;
     }
 #pragma unroll
     for (int t = 0; t < NTILE; ++t) {
@@ -801,25 +804,6 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_fwd_res_kernel(
         for (int d = 0; d < 2; ++d)
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) vt[d][ks] = res_trans(Vimg, 32 * t + 16 * ks, d, lane);
-        if (t > 0) {
-          const float tm = rmax(Sa);
-          if (__any(tm * c2 > mc + RES_THR)) {  // rare: the row max grew past the threshold
-            const float mn = fmaxf(mrow, tm);
-            const float mcn = mn == -INFINITY ? 0.f : mn * c2;
-            const float alpha = fast_exp2(mc - mcn);
-#pragma unroll
-            for (int d = 0; d < 2; ++d)
-#pragma unroll
-              for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              l4[i] *= alpha;
-              ld4[i] *= alpha;
-            }
-            mrow = mn;
-            mc = mcn;
-          }
-        }
         floatx16 p;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -892,15 +876,20 @@ static bool res_plan(const AttnMask& m, int L, ResPlan& plan) {
 // One workgroup per (sample, head), two phases over LDS images of the same layout as the
 // forward's (res_sw chunk swizzle, rows >= L copies of row L - 1):
 //   A (queries on the lanes): K and V resident; per query block S^T = K Q^T, dP^T = V dO^T,
-//     P = exp2(S c - lse), dS = P (keep dP / kp - delta), dQ^T += K^T dS^T (K^T by transposed
-//     reads of the K image); delta = rowsum(dO O) computed here and written for phase B;
+//     P = exp2(S c - lse), dS' = P (keep dP - delta kp), dQ^T += K^T dS'^T (K^T by transposed
+//     reads of the K image); the row constants of phase B are written here (rc below);
 //   B (keys on the lanes), after a barrier that frees the images: Q and dO resident; per key
-//     block S = Q K^T, dP = dO V^T, dV^T += dO^T P_kept, dK^T += Q^T dS (dO^T, Q^T transposed
-//     reads), lse / delta of the query rows from global (L2-hot).
+//     block S' = Q K^T + rc0, dP' = dO V^T + rc1 (the row constants are the INITIAL accumulators,
+//     float4 loads of rc), P = exp2(c S'), dV^T += dO^T P_kept, dK^T += Q^T dS' with
+//     dS' = P (keep ? dP' : rc1).
+// dS' = dS / (1 / kp): the dropout scale is folded into the dQ / dK / dV store scales.
+// rc (the `delta` workspace of mmt_attn_bwd): per (sample, head) two rows of LP = lp_of(L) floats,
+//   rc0[q] = -lse[q] / scale (-inf for q >= L: P = 0 on padded rows with no masking) and
+//   rc1[q] = -kp rowsum(dO O)[q] (0 for q >= L).
 // Query / key blocks are dealt to the 4 waves by the host plan. The fused-QKV bias gradient
-// (column sums of dq, dk, dv) is summed per lane over the wave's blocks, reduced over the lanes
-// at the end of each phase and written to a per-(sample, wave) slab row — plain stores, summed
-// by one column-sum launch afterwards (no atomics: bitwise reproducible).
+// (column sums of dq, dk, dv) is folded per block into 16 partial sums per lane, reduced over
+// the lanes and waves through LDS at the end of each phase and added with one atomic per d and
+// workgroup.
 struct ResPlanB {
   uint32_t qword[MAX_SETS][RES_TILES];  // phase A: keys of tile t that query set s sees
   uint32_t kword[MAX_SETS][RES_TILES];  // phase B: queries of tile t that see key set s
@@ -914,6 +903,9 @@ template <int ROWS>
 __device__ __forceinline__ void res_dma2(bf16_t* smem, const bf16_t* a, int64_t sa, const bf16_t* b,
                                          int64_t sb, int L, int wave, int lane) {
   constexpr int PIECES = ROWS / 8;
+#if MMT_RES_ABL == 6
+  if (L < 0)
+#endif
   for (int p = wave; p < 2 * PIECES; p += RES_NW) {
     const int t = p >= PIECES, pr = p - t * PIECES;
     const int row = 8 * pr + (lane >> 3);
@@ -925,27 +917,40 @@ __device__ __forceinline__ void res_dma2(bf16_t* smem, const bf16_t* a, int64_t 
   }
 }
 
-// column sums of the lanes: acc[dd][r] (d = 32 dd + rbit(r) + 4 hh, one column per lane of each
-// half) summed over the 32 lanes of each half; lane (hh, dd = (l >> 4) & 1, r = l & 15) then
-// stores its d's total to row[d]
-__device__ __forceinline__ void res_colsum_store(float (&acc)[2][16], float* row, int lane) {
+// Bias-gradient column sums. A block's output accumulators acc[dd][r] (head dim
+// d = 32 dd + rbit(r) + 4 hh, one column per lane) are folded into 16 partial sums per lane with
+// one v_permlane16_swap + add per pair (acc[0][r], acc[1][r]): lane l of 16-lane row
+// rho = (l >> 4) & 3 then holds, for dd = rho & 1, hh = rho >> 1, the sums of acc[dd][r] over
+// lanes (l & 15) + 32 hh + {0, 16}.
+__device__ __forceinline__ void res_bias_fold(const floatx16 (&acc)[2], float (&b16)[16]) {
 #pragma unroll
-  for (int dd = 0; dd < 2; ++dd)
+  for (int r = 0; r < 16; ++r) {
+    const auto x = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[0][r]), __float_as_uint(acc[1][r]),
+                                                    false, false);
+    b16[r] += __uint_as_float(x[0]) + __uint_as_float(x[1]);
+  }
+}
+// End of a phase: the 4 waves' folded sums (times sc) summed through LDS (`red`, 16 KB, free)
+// over the 16 lanes of each row; one atomic per d by wave 0. Every thread calls it; it starts and
+// ends with a barrier.
+__device__ __forceinline__ void res_bias_reduce(const float (&b16)[16], float sc, float* red, float* row,
+                                                int wave, int lane) {
+  __syncthreads();
+  float4* my = reinterpret_cast<float4*>(red + (wave * 64 + lane) * 16);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float v = acc[dd][r];
+  for (int i = 0; i < 4; ++i)
+    my[i] = make_float4(b16[4 * i] * sc, b16[4 * i + 1] * sc, b16[4 * i + 2] * sc, b16[4 * i + 3] * sc);
+  __syncthreads();
+  if (wave == 0) {
+    const int d = lane, hh = (d >> 2) & 1, dd = d >> 5;
+    const int r = (d & 3) | (((d & 31) >> 3) << 2), rho = 2 * hh + dd;
+    float sum = 0.f;
+    for (int w = 0; w < RES_NW; ++w)
 #pragma unroll
-      for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
-      acc[dd][r] = v;
-    }
-  const int hh = lane >> 5, mdd = (lane >> 4) & 1, mr = lane & 15;
-  float out = 0.f;
-#pragma unroll
-  for (int dd = 0; dd < 2; ++dd)
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-      if (dd == mdd && r == mr) out = acc[dd][r];
-  row[32 * mdd + rbit(mr) + 4 * hh] = out;
+      for (int j = 0; j < 16; ++j) sum += red[(w * 64 + 16 * rho + j) * 16 + r];
+    atomicAdd(row + d, sum);
+  }
+  __syncthreads();
 }
 
 // store a wave's 32 x 64 rows from O^T-layout accumulators (lane = row), scaled, as bf16 with
@@ -972,40 +977,45 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_bwd_res_kernel(
     Geo g, AttnMask mask, ResPlanB plan, const uint32_t* __restrict__ drop_q,
     const uint32_t* __restrict__ drop_k, int drop_lp, float drop_scale,
     const bf16_t* __restrict__ dout, int64_t d_s_b, int64_t d_s_t, const float* __restrict__ lse,
-    const bf16_t* __restrict__ o, int64_t o_s_b, int64_t o_s_t, float* __restrict__ delta,
-    bf16_t* __restrict__ dqkv, int64_t dq_s_b, int64_t dq_s_t, float* __restrict__ bias_ws) {
-  constexpr int DH = 64, NS = 4, ROWS = 32 * NTILE;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * ROWS * DH];
+    const bf16_t* __restrict__ o, int64_t o_s_b, int64_t o_s_t, float* __restrict__ rc,
+    bf16_t* __restrict__ dqkv, int64_t dq_s_b, int64_t dq_s_t, float* __restrict__ bias_grad) {
+  constexpr int DH = 64, NS = 4, ROWS = 32 * NTILE, LP = ROWS;
+  constexpr int IMG_BYTES = 2 * ROWS * DH * 2, RED_BYTES = RES_NW * 64 * 16 * 4;
+  __shared__ __attribute__((aligned(16))) char smem_raw[IMG_BYTES > RED_BYTES ? IMG_BYTES : RED_BYTES];
+  bf16_t* smem = reinterpret_cast<bf16_t*>(smem_raw);
   const int bh = blockIdx.x, b = bh / g.H, h = bh - b * g.H;
   const int lane = threadIdx.x & 63, hh = lane >> 5, lr = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int L = g.L, D = g.H * DH;
   const bf16_t* base = g.qkv + (int64_t)b * g.s_b;
   const bf16_t* dbase = dout + (int64_t)b * d_s_b + h * DH;
-  const int64_t row_bh = (int64_t)bh * L;
+  float* rc0 = rc + (int64_t)bh * 2 * LP;
+  float* rc1 = rc0 + LP;
   const float c2 = g.scale * LOG2E;
-  const char* img0 = reinterpret_cast<const char*>(smem);
+  const float kp = 1.f / drop_scale;
+  const char* img0 = smem_raw;
   const char* img1 = img0 + ROWS * DH * 2;
   int koff[NS];  // row-fragment offsets (row lr of a 32-row tile, chunk 2 s + hh)
 #pragma unroll
   for (int s = 0; s < NS; ++s) koff[s] = lr * 128 + 16 * ((2 * s + hh) ^ res_sw(lr));
-  float* ws_row = bias_ws ? bias_ws + ((int64_t)b * RES_NW + wave) * 3 * D + h * DH : nullptr;
+  float* brow = bias_grad ? bias_grad + h * DH : nullptr;  // += column sums of dq / dk / dv
+  const float sc_out = g.scale * drop_scale;                // dQ / dK store scale (dS' = kp dS)
 
   // ================= phase A: dQ (queries on the lanes), K / V resident
   res_dma2<ROWS>(smem, base + D + h * DH, g.s_t, base + 2 * D + h * DH, g.s_t, L, wave, lane);
-  float bq[2][16];
+  float bq[16];
 #pragma unroll
-  for (int dd = 0; dd < 2; ++dd)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) bq[dd][r] = 0.f;
+  for (int r = 0; r < 16; ++r) bq[r] = 0.f;
+  int slot = 0, blk = plan.qblk[wave][0];
+  // the block's Q / dO / O row fragments, loaded under the previous block
   bf16x8 qf[NS], df[NS], of[NS];
-  auto load_q = [&](int bk) {
+  auto load_a = [&](int bk) {
     const int qq = 32 * bk + lr;
     const bool ok = qq < L;
-    const int qc = ok ? qq : L - 1;
-    const bf16_t* qp = base + (int64_t)qc * g.s_t + h * DH;
-    const bf16_t* dp = dbase + (int64_t)qc * d_s_t;
-    const bf16_t* op = o + (int64_t)b * o_s_b + (int64_t)qc * o_s_t + h * DH;
+    const int qc_ = ok ? qq : L - 1;
+    const bf16_t* qp = base + (int64_t)qc_ * g.s_t + h * DH;
+    const bf16_t* dp = dbase + (int64_t)qc_ * d_s_t;
+    const bf16_t* op = o + (int64_t)b * o_s_b + (int64_t)qc_ * o_s_t + h * DH;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       qf[s] = row_frag_global(qp, ok, s, lane);
@@ -1013,9 +1023,8 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_bwd_res_kernel(
       of[s] = row_frag_global(op, ok, s, lane);
     }
   };
-  int slot = 0, blk = plan.qblk[wave][0];
-  if (blk != 0xff) load_q(blk);
-  __syncthreads();
+  if (blk != 0xff) load_a(blk);
+  __syncthreads();  // the DMA landed
   while (blk != 0xff) {  // wave-uniform
     const int q = 32 * blk + lr;
     const bool qv = q < L;
@@ -1025,9 +1034,29 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_bwd_res_kernel(
     for (int s = 0; s < NS; ++s)
 #pragma unroll
       for (int j = 0; j < 8; ++j) part = fmaf((float)of[s][j], (float)df[s][j], part);
-    const float dlt = halves_sum(part);
-    if (qv && lane < 32) delta[row_bh + q] = dlt;
-    const float lse2 = qv ? lse[row_bh + q] * LOG2E : INFINITY;
+    const float dkp = halves_sum(part) * kp;  // kp delta
+    // the next block's operands, in flight under this block (of is free once delta is formed)
+    const int nblk = slot + 1 < RES_SLOTS ? plan.qblk[wave][slot + 1] : 0xff;
+    bf16x8 qn[NS], dn[NS];
+    {
+      const int qq = 32 * (nblk != 0xff ? nblk : blk) + lr;
+      const bool ok = qq < L;
+      const int qc_ = ok ? qq : L - 1;
+      const bf16_t* qp = base + (int64_t)qc_ * g.s_t + h * DH;
+      const bf16_t* dp = dbase + (int64_t)qc_ * d_s_t;
+      const bf16_t* op = o + (int64_t)b * o_s_b + (int64_t)qc_ * o_s_t + h * DH;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        qn[s] = row_frag_global(qp, ok, s, lane);
+        dn[s] = row_frag_global(dp, ok, s, lane);
+        of[s] = row_frag_global(op, ok, s, lane);
+      }
+    }
+    const float lse2 = qv ? lse[(int64_t)bh * L + q] * LOG2E : INFINITY;
+    if (lane < 32) {  // phase B's row constants (padded rows: -inf / 0)
+      rc0[q] = qv ? -lse[(int64_t)bh * L + q] / g.scale : -INFINITY;
+      rc1[q] = qv ? -dkp : 0.f;
+    }
     const int sq = set_of(mask, qc);
     const int sq0 = __builtin_amdgcn_readfirstlane(sq);
     const bool uni = mask.causal == 0u && __all(sq == sq0);
@@ -1049,82 +1078,95 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_bwd_res_kernel(
 #pragma unroll
     for (int t = 0; t < NTILE; ++t) {
       const uint32_t vw = vws[t];
-      if (__all(vw == 0u)) continue;  // wave-uniform
-      floatx16 sacc, pacc;
+#if MMT_RES_ABL == 4
+      if (L < 0) {
+#else
+      if (!__all(vw == 0u)) {  // wave-uniform
+#endif
+        TileMasks<16> dm;
+        if constexpr (DROP) dm.load(drop_q, drop_lp, blk, 32 * t);
+        floatx16 sacc, pacc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sacc[r] = 0.f;
-        pacc[r] = 0.f;
-      }
+        for (int r = 0; r < 16; ++r) {
+          sacc[r] = 0.f;
+          pacc[r] = 0.f;
+        }
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(img0 + t * 4096 + koff[s]);
-        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(img1 + t * 4096 + koff[s]);
-        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc, 0, 0, 0);
-        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, df[s], pacc, 0, 0, 0);
-      }
-      TileMasks<16> dm;
-      if constexpr (DROP) dm.load(drop_q, drop_lp, blk, 32 * t);
-      const bool full = __all(vw == 0xffffffffu);
-      const uint32_t w = vw >> (4 * hh);
-      floatx16 ds;
+        for (int s = 0; s < NS; ++s) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(img0 + t * 4096 + koff[s]);
+          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(img1 + t * 4096 + koff[s]);
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc, 0, 0, 0);
+          pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, df[s], pacc, 0, 0, 0);
+        }
+        if (!__all(vw == 0xffffffffu)) {  // partially visible tile: masked scores -> -inf
+          const uint32_t w = vw >> (4 * hh);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float p = fast_exp2(fmaf(sacc[r], c2, -lse2));
-        if (!full) p = __int_as_float(__float_as_int(p) & bitmask_of(w, rbit(r)));
-        float tt = pacc[r] * drop_scale;
-        if constexpr (DROP) tt = sel_keep(tt, dm.m[r]);
-        ds[r] = p * (tt - dlt);
-      }
-      const bf16x8 d0 = pack_frag(ds, 0), d1 = pack_frag(ds, 1);
+          for (int r = 0; r < 16; ++r) {
+            const int mk = bitmask_of(w, rbit(r));
+            sacc[r] = __int_as_float((__float_as_int(sacc[r]) & mk) | (~mk & (int)0xff800000u));
+          }
+        }
+        floatx16 ds;
 #pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        dq[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img0, 32 * t, d, lane), d0, dq[d], 0, 0, 0);
-        dq[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img0, 32 * t + 16, d, lane), d1, dq[d], 0, 0, 0);
+        for (int r = 0; r < 16; ++r) {
+          const float p = fast_exp2(fmaf(sacc[r], c2, -lse2));
+          float tt = pacc[r];
+          if constexpr (DROP) tt = sel_keep(tt, dm.m[r]);
+          ds[r] = p * (tt - dkp);
+        }
+        const bf16x8 d0 = pack_frag(ds, 0), d1 = pack_frag(ds, 1);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          dq[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img0, 32 * t, d, lane), d0, dq[d], 0, 0, 0);
+          dq[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img0, 32 * t + 16, d, lane), d1, dq[d], 0, 0, 0);
+        }
       }
     }
-    const int nblk = slot + 1 < RES_SLOTS ? plan.qblk[wave][slot + 1] : 0xff;
-    if (nblk != 0xff) load_q(nblk);
-    res_store_rows(dq, g.scale, dqkv + (int64_t)b * dq_s_b + (int64_t)qc * dq_s_t + h * DH, qv, hh);
+    res_store_rows(dq, sc_out, dqkv + (int64_t)b * dq_s_b + (int64_t)qc * dq_s_t + h * DH, qv, hh);
+    if (brow) res_bias_fold(dq, bq);
 #pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) bq[d][r] += dq[d][r] * g.scale;
+    for (int s = 0; s < NS; ++s) {
+      qf[s] = qn[s];
+      df[s] = dn[s];
+    }
     ++slot;
     blk = nblk;
   }
-  if (ws_row) res_colsum_store(bq, ws_row, lane);
+  // every wave is done with the K / V images, rc is written (the reduce's first barrier)
+  if (brow) {
+    res_bias_reduce(bq, sc_out, reinterpret_cast<float*>(smem_raw), brow, wave, lane);
+  } else {
+    __syncthreads();
+  }
 
   // ================= phase B: dK / dV (keys on the lanes), Q / dO resident
-  __syncthreads();  // every wave is done with the K / V images; delta is written
   res_dma2<ROWS>(smem, base + h * DH, g.s_t, dbase, d_s_t, L, wave, lane);
-  float bk[2][16], bv[2][16];
+  float bk[16], bv[16];
 #pragma unroll
-  for (int dd = 0; dd < 2; ++dd)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      bk[dd][r] = 0.f;
-      bv[dd][r] = 0.f;
-    }
-  bf16x8 kf[NS], vf[NS];
-  auto load_k = [&](int bk_) {
-    const int kk = 32 * bk_ + lr;
-    const bool ok = kk < L;
-    const bf16_t* kp = base + (int64_t)(ok ? kk : L - 1) * g.s_t + D + h * DH;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      kf[s] = row_frag_global(kp, ok, s, lane);
-      vf[s] = row_frag_global(kp + D, ok, s, lane);
-    }
-  };
+  for (int r = 0; r < 16; ++r) {
+    bk[r] = 0.f;
+    bv[r] = 0.f;
+  }
   slot = 0;
   blk = plan.kblk[wave][0];
-  if (blk != 0xff) load_k(blk);
+  bf16x8 kf[NS], vf[NS];  // the key block's K / V row fragments
+  auto load_b = [&](int bk_, bf16x8 (&kd)[NS], bf16x8 (&vd)[NS]) {
+    const int kk = 32 * bk_ + lr;
+    const bool ok = kk < L;
+    const bf16_t* kp_ = base + (int64_t)(ok ? kk : L - 1) * g.s_t + D + h * DH;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      kd[s] = row_frag_global(kp_, ok, s, lane);
+      vd[s] = row_frag_global(kp_ + D, ok, s, lane);
+    }
+  };
+  if (blk != 0xff) load_b(blk, kf, vf);
   __syncthreads();
   while (blk != 0xff) {
     const int key = 32 * blk + lr;
     const bool kv = key < L;
     const int kc = kv ? key : L - 1;
+    const int nblk = slot + 1 < RES_SLOTS ? plan.kblk[wave][slot + 1] : 0xff;
     const int sk = set_of(mask, kc);
     const int sk0 = __builtin_amdgcn_readfirstlane(sk);
     const bool uni = mask.causal == 0u && __all(sk == sk0);
@@ -1147,80 +1189,83 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_bwd_res_kernel(
         dk[d][r] = 0.f;
         dv[d][r] = 0.f;
       }
+    // row constants of query rows 32 t + 8 j + 4 hh + {0..3} (the initial accumulators of S'
+    // and dP')
+    auto load_rc = [&](int t, floatx16& a0, floatx16& a1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 x = *reinterpret_cast<const float4*>(rc0 + 32 * t + 8 * j + 4 * hh);
+        const float4 y = *reinterpret_cast<const float4*>(rc1 + 32 * t + 8 * j + 4 * hh);
+        a0[4 * j] = x.x; a0[4 * j + 1] = x.y; a0[4 * j + 2] = x.z; a0[4 * j + 3] = x.w;
+        a1[4 * j] = y.x; a1[4 * j + 1] = y.y; a1[4 * j + 2] = y.z; a1[4 * j + 3] = y.w;
+      }
+    };
 #pragma unroll
     for (int t = 0; t < NTILE; ++t) {
       const uint32_t qw = qws[t];
-      if (__all(qw == 0u)) continue;  // wave-uniform
-      // lse (log2 units) / delta of the query rows 32 t + 8 j + 4 hh + {0..3} (float4 j)
-      float lr2[16], dr[16];
+#if MMT_RES_ABL == 5
+      if (L < 0) {
+#else
+      if (!__all(qw == 0u)) {  // wave-uniform
+#endif
+        TileMasks<16> dm;
+        if constexpr (DROP) dm.load(drop_k, drop_lp, blk, 32 * t);
+        floatx16 sacc, ca;
+        load_rc(t, sacc, ca);
+        floatx16 pacc = ca;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r0 = min(32 * t + 8 * j + 4 * hh, ((L - 1) & ~3));
-        const float4 a = *reinterpret_cast<const float4*>(lse + row_bh + r0);
-        const float4 c = *reinterpret_cast<const float4*>(delta + row_bh + r0);
-        lr2[4 * j] = a.x * LOG2E; lr2[4 * j + 1] = a.y * LOG2E;
-        lr2[4 * j + 2] = a.z * LOG2E; lr2[4 * j + 3] = a.w * LOG2E;
-        dr[4 * j] = c.x; dr[4 * j + 1] = c.y; dr[4 * j + 2] = c.z; dr[4 * j + 3] = c.w;
-      }
-      floatx16 sacc, pacc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sacc[r] = 0.f;
-        pacc[r] = 0.f;
-      }
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const bf16x8 qr = *reinterpret_cast<const bf16x8*>(img0 + t * 4096 + koff[s]);
-        const bf16x8 dr_ = *reinterpret_cast<const bf16x8*>(img1 + t * 4096 + koff[s]);
-        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qr, kf[s], sacc, 0, 0, 0);
-        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dr_, vf[s], pacc, 0, 0, 0);
-      }
-      TileMasks<16> dm;
-      if constexpr (DROP) dm.load(drop_k, drop_lp, blk, 32 * t);
-      const uint32_t w = qw >> (4 * hh);
-      floatx16 pk, ds;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        // rows past L: masked by qw (their lse / delta are clamped copies)
-        float p = fast_exp2(fmaf(sacc[r], c2, -lr2[r]));
-        p = __int_as_float(__float_as_int(p) & bitmask_of(w, rbit(r)));
-        float tt = pacc[r] * drop_scale;
-        float pkr = p;
-        if constexpr (DROP) {
-          pkr = sel_keep(p, dm.m[r]);
-          tt = sel_keep(tt, dm.m[r]);
+        for (int s = 0; s < NS; ++s) {
+          const bf16x8 qr = *reinterpret_cast<const bf16x8*>(img0 + t * 4096 + koff[s]);
+          const bf16x8 dr_ = *reinterpret_cast<const bf16x8*>(img1 + t * 4096 + koff[s]);
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qr, kf[s], sacc, 0, 0, 0);
+          pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dr_, vf[s], pacc, 0, 0, 0);
         }
-        pk[r] = pkr;
-        ds[r] = p * (tt - dr[r]);
-      }
-      const bf16x8 p0 = pack_frag(pk, 0), p1 = pack_frag(pk, 1);
-      const bf16x8 s0 = pack_frag(ds, 0), s1 = pack_frag(ds, 1);
+        if (!__all(qw == 0xffffffffu)) {  // partially visible tile: masked scores -> -inf
+          const uint32_t w = qw >> (4 * hh);
 #pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img1, 32 * t, d, lane), p0, dv[d], 0, 0, 0);
-        dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img1, 32 * t + 16, d, lane), p1, dv[d], 0, 0, 0);
-        dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img0, 32 * t, d, lane), s0, dk[d], 0, 0, 0);
-        dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img0, 32 * t + 16, d, lane), s1, dk[d], 0, 0, 0);
+          for (int r = 0; r < 16; ++r) {
+            const int mk = bitmask_of(w, rbit(r));
+            sacc[r] = __int_as_float((__float_as_int(sacc[r]) & mk) | (~mk & (int)0xff800000u));
+          }
+        }
+        floatx16 pk, ds;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fast_exp2(sacc[r] * c2);
+          if constexpr (DROP) {
+            const bool keep = __builtin_amdgcn_inverse_ballot_w64(dm.m[r]);
+            pk[r] = keep ? p : 0.f;
+            ds[r] = p * (keep ? pacc[r] : ca[r]);
+          } else {
+            pk[r] = p;
+            ds[r] = p * pacc[r];
+          }
+        }
+        const bf16x8 p0 = pack_frag(pk, 0), p1 = pack_frag(pk, 1);
+        const bf16x8 s0 = pack_frag(ds, 0), s1 = pack_frag(ds, 1);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img1, 32 * t, d, lane), p0, dv[d], 0, 0, 0);
+          dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img1, 32 * t + 16, d, lane), p1, dv[d], 0, 0, 0);
+          dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img0, 32 * t, d, lane), s0, dk[d], 0, 0, 0);
+          dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(img0, 32 * t + 16, d, lane), s1, dk[d], 0, 0, 0);
+        }
       }
     }
-    const int nblk = slot + 1 < RES_SLOTS ? plan.kblk[wave][slot + 1] : 0xff;
-    if (nblk != 0xff) load_k(nblk);
     bf16_t* kro = dqkv + (int64_t)b * dq_s_b + (int64_t)kc * dq_s_t + D + h * DH;
-    res_store_rows(dk, g.scale, kro, kv, hh);
+    res_store_rows(dk, sc_out, kro, kv, hh);
     res_store_rows(dv, drop_scale, kro + D, kv, hh);
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        bk[d][r] += dk[d][r] * g.scale;
-        bv[d][r] += dv[d][r] * drop_scale;
-      }
+    if (brow) {
+      res_bias_fold(dk, bk);
+      res_bias_fold(dv, bv);
+    }
     ++slot;
     blk = nblk;
+    if (blk != 0xff) load_b(blk, kf, vf);
   }
-  if (ws_row) {
-    res_colsum_store(bk, ws_row + D, lane);
-    res_colsum_store(bv, ws_row + 2 * D, lane);
+  if (brow) {
+    res_bias_reduce(bk, sc_out, reinterpret_cast<float*>(smem_raw), brow + D, wave, lane);
+    res_bias_reduce(bv, drop_scale, reinterpret_cast<float*>(smem_raw), brow + 2 * D, wave, lane);
   }
 }
 
@@ -1682,8 +1727,8 @@ int fill_mask(AttnMask& m, int n_sets, const int32_t* starts, const int32_t* len
 static const int g_attn_nq = getenv("MMT_ATTN_NQ") ? atoi(getenv("MMT_ATTN_NQ")) : 0;
 // the K/V-resident forward for Dh 64, 32 < L <= 320 (MMT_ATTN_RES=0: the streaming kernel;
 // read per call so one process can A/B both)
-static bool attn_res_enabled() {
-  const char* e = getenv("MMT_ATTN_RES");
+static bool attn_res_enabled(const char* var = "MMT_ATTN_RES") {
+  const char* e = getenv(var);
   return !e || atoi(e) != 0;
 }
 
@@ -1850,6 +1895,33 @@ extern "C" int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   const int lp = lp_of(L);
   const float dscale = drop_bits ? 1.f / keep_prob : 1.f;
   hipStream_t s = as_stream(stream);
+  if (attn_res_enabled("MMT_ATTN_RES_BWD") && Dh == 64 && L > 32 && L <= 32 * RES_TILES) {
+    ResPlanB plan;
+    if (res_plan_bwd(m, L, plan)) {
+      const int ntile = ((L + 63) / 64) * 2;
+#define RESB1(NT_, DR_)                                                                             \
+  hipLaunchKernelGGL((attn_bwd_res_kernel<NT_, DR_>), dim3(B * H), dim3(64 * RES_NW), 0, s, g, m,   \
+                     plan, drop_bits, drop_bits_t, lp, dscale, (const bf16_t*)dout, d_s_b, d_s_t,  \
+                     lse, (const bf16_t*)o, o_s_b, o_s_t, delta, (bf16_t*)dqkv, dq_s_b, dq_s_t,   \
+                     bias_grad)
+#define RESB2(NT_)                  \
+  do {                              \
+    if (drop_bits) RESB1(NT_, true); \
+    else RESB1(NT_, false);          \
+  } while (0)
+      switch (ntile) {
+        case 2: RESB2(2); break;
+        case 4: RESB2(4); break;
+        case 6: RESB2(6); break;
+        case 8: RESB2(8); break;
+        default: RESB2(10); break;
+      }
+#undef RESB2
+#undef RESB1
+      MMT_CHECK_LAUNCH("mmt_attn_bwd");
+      return MMT_OK;
+    }
+  }
   if (bwd_threads(L) == 128) {
     dim3 grid(((L + 63) / 64) * H * B);
     ATTN_DISPATCH(DH, ATTN_BWD_LAUNCH(DH, 128));

@@ -712,7 +712,8 @@ extern "C" int mmt_tome_match(const void* metric, int dtype, int n, int t, int h
                               int32_t* unm_idx, int32_t* src_idx, int32_t* dst_idx,
                               float* node_max, void* workspace, int64_t ws_bytes,
                               mmt_stream_t stream) {
-  MMT_CHECK_ARG(metric && unm_idx && src_idx && dst_idx && workspace, "mmt_tome_match: null pointer");
+  MMT_CHECK_ARG(metric && (unm_idx || (t + 1) / 2 == r) && src_idx && dst_idx && workspace,
+                "mmt_tome_match: null pointer");  // unm may be NULL when every A token merges
   MMT_CHECK_ARG(n > 0 && t >= 2 && heads >= 1 && c >= 1, "mmt_tome_match: bad shape n=%d t=%d", n, t);
   MMT_CHECK_ARG(t <= 2048 && c <= 512, "mmt_tome_match: t=%d c=%d beyond 2048 / 512", t, c);
   const int prot = ((flags & MMT_TOME_CLASS_TOKEN) ? 1 : 0) + ((flags & MMT_TOME_DISTILL_TOKEN) ? 1 : 0);
@@ -1013,7 +1014,8 @@ extern "C" int mmt_tome_merge_seqnorm_fwd(const float* x, int n, int L, int D, i
                                           const float* beta, float eps, void* y, int64_t y_s_n,
                                           int64_t y_s_t, float* mean, float* rstd,
                                           mmt_stream_t stream) {
-  MMT_CHECK_ARG(x && x_out && unm_idx && src_idx && dst_idx && gamma && beta && y && mean && rstd,
+  MMT_CHECK_ARG(x && x_out && (unm_idx || (t + 1) / 2 == r) && src_idx && dst_idx && gamma && beta &&
+                    y && mean && rstd,
                 "mmt_tome_merge_seqnorm_fwd: null pointer");
   MMT_CHECK_ARG(n > 0 && L > 0 && D > 0 && D % 8 == 0 && t >= 2 && set_start >= 0 &&
                     set_start + t <= L && L - r <= kFusedRows,
@@ -1038,7 +1040,8 @@ extern "C" int mmt_tome_merge_wavg_fwd(const void* x, int dtype, int n, int L, i
                                        const int32_t* src_idx, const int32_t* dst_idx, void* x_out,
                                        int64_t o_s_n, int64_t o_s_t, float* size_out,
                                        int32_t* pos_map, mmt_stream_t stream) {
-  MMT_CHECK_ARG(x && x_out && unm_idx && src_idx && dst_idx, "mmt_tome_merge_wavg_fwd: null pointer");
+  MMT_CHECK_ARG(x && x_out && (unm_idx || (t + 1) / 2 == r) && src_idx && dst_idx,
+                "mmt_tome_merge_wavg_fwd: null pointer");
   MMT_CHECK_ARG(n > 0 && L > 0 && D > 0 && t >= 2 && set_start >= 0 && set_start + t <= L,
                 "mmt_tome_merge_wavg_fwd: bad shape");
   MMT_CHECK_ARG(r > 0 && r <= t / 2 && (t + 1) / 2 - r <= 1024 && r <= 512,

@@ -289,3 +289,58 @@ def test_seqnorm_dropout_bwd_fused(dev, B, L, D, drop):
     assert torch.equal(a_z.view(B, L, D), b_z)
     for i in range(3):
         torch.testing.assert_close(grads[i + 3], grads[i], rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("B,L,H,mode,drop", [
+    (2, 33, 3, "none", True), (2, 64, 2, "none", False), (3, 65, 2, "octo", True),
+    (2, 101, 3, "causal", True), (2, 212, 6, "octo", True), (2, 292, 6, "octo", False),
+    (1, 301, 2, "causal", False), (2, 320, 2, "octo", True)])
+def test_resident_attention_vs_tiled_and_torch(dev, B, L, H, mode, drop, monkeypatch):
+    """The K/V-resident kernels (Dh 64, 32 < L <= 320: one workgroup per (sample, head), forward
+    online softmax, two-phase backward with in-kernel bias column sums) against the tiled ones
+    (MMT_ATTN_RES / MMT_ATTN_RES_BWD = 0) and against fp32 torch, on ragged L (odd, not a multiple
+    of 4 or 32), causal sets and dropout."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    Dh = 64
+    g = torch.Generator().manual_seed(L * 13 + H)
+    qkv = torch.randn((B, L, 3 * H * Dh), generator=g).bfloat16().to(dev)
+    dout = torch.randn((B, L, H * Dh), generator=g).bfloat16().to(dev)
+    scale = Dh ** -0.5
+    if mode == "none":
+        table, mask = None, None
+    elif mode == "octo":
+        starts, lens, vis = octo_small_table(min(32, L // 4), L - min(32, L // 4) - 4, 4)
+        table, mask = K.SetTable(starts, lens, vis), dense_mask(starts, lens, vis, L, dev)
+    else:  # two steps, each: T, causal I, R
+        n = (L - 7) // 2
+        starts, lens = [0, 3, 3 + n, 4 + n, 7 + n], [3, n, 1, 3, L - 7 - n]
+        vis = [0b00001, 0b00011, 0b00111, 0b01001, 0b11011]
+        causal = [False, True, False, False, True]
+        table = K.SetTable(starts, lens, vis, causal)
+        mask = dense_mask(starts, lens, vis, L, dev, causal)
+    kp = 0.9 if drop else 1.0
+    rng = torch.tensor([5, 9], dtype=torch.int32, device=dev)
+    bits = K.dropout_bits(rng, 1, 2, L, L, kp) if drop else None
+    keep = bits_to_keep(bits, L).to(dev) if drop else None
+    outs = {}
+    for res in ("1", "0"):
+        monkeypatch.setenv("MMT_ATTN_RES", res)
+        monkeypatch.setenv("MMT_ATTN_RES_BWD", res)
+        o, lse = K.attn_fwd(qkv, H, scale, table, bits, kp)
+        bg = torch.zeros(3 * H * Dh, device=dev)
+        dq = K.attn_bwd(qkv, o, dout, lse, H, scale, table, bits, kp, bias_grad=bg)
+        torch.cuda.synchronize()
+        outs[res] = (o.float(), lse, dq.float(), bg)
+    (o1, l1, d1, b1), (o0, l0, d0, b0) = outs["1"], outs["0"]
+    assert torch.isfinite(o1).all() and torch.isfinite(d1).all() and torch.isfinite(b1).all()
+    assert rel(o1, o0) < 1e-2 and (l1 - l0).abs().max().item() < 1e-3
+    for i in range(3):
+        a, b = d1.view(B, L, 3, -1)[:, :, i], d0.view(B, L, 3, -1)[:, :, i]
+        assert rel(a, b) < 2e-2, ("qkv"[i], rel(a, b))
+    torch.testing.assert_close(b1, d1.sum((0, 1)), rtol=2e-2, atol=2e-2 * float(b1.abs().max()) + 1e-3)
+    assert rel(b1, b0) < 2e-2
+    qf = qkv.float().requires_grad_()
+    ref = ref_attention(qf, H, scale, mask, keep, kp)
+    ref.backward(dout.float())
+    assert rel(o1, ref) < 1e-2
+    assert rel(d1, qf.grad) < 2e-2
