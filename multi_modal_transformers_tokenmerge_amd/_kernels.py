@@ -442,6 +442,13 @@ def attn_fwd_resident(L: int, Dh: int, bias: bool = False) -> bool:
     return os.environ.get("MMT_ATTN_RES", "1") != "0" and Dh == 64 and not bias and 32 < L <= 320
 
 
+def attn_bwd_resident(L: int, Dh: int) -> bool:
+    """Whether mmt_attn_bwd takes the two-phase K/V-resident kernel (attn_bwd_res_kernel: Dh 64,
+    32 < L <= 320; MMT_ATTN_RES_BWD=0 disables it) — csrc/attention.hip."""
+    import os
+    return os.environ.get("MMT_ATTN_RES_BWD", "1") != "0" and Dh == 64 and 32 < L <= 320
+
+
 def attn_fwd(qkv: torch.Tensor, H: int, scale: float, table: SetTable | None = None,
              drop_bits: torch.Tensor | None = None, keep_prob: float = 1.0,
              bias: torch.Tensor | None = None, out: torch.Tensor | None = None,

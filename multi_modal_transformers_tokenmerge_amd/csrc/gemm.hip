@@ -1252,6 +1252,280 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
+// Narrow-output NT kernel (the products hipBLASLt used to run: the MLP and QKV input gradients
+// 141,312 x 384 x 1536 / 149,504 x 384 x 1152, the frozen T5's FF output + residual
+// 16,384 x 768 x 3072, and the T5 FF input relu(16,384 x 3072 x 768)): C = epi(A . B^T), bf16,
+// MT x BN tiles (BN 384 or 192), K-steps of 64.
+// The A operand streams from HBM once; B (N x K, 1.2 MB at N = 384) is re-read from L2 by every
+// tile. An HBM miss costs ~3 us under full load, so A needs more than one K-step of DMA in flight
+// per CU, and with one in-order vmcnt per wave the B loads must never sit behind a younger A
+// load that the same barrier does not need. Hence separate LDS rings: NSA A stages (DMA issued
+// NSA - 1 K-steps ahead) and two B stages (one ahead), issued per K-step as [B(s+1), A(s+NSA-1)]:
+// the barrier of K-step s waits for B(s) with vmcnt(A pieces + stores younger than it), which
+// leaves A(s+NSA-2) in flight across the barrier and has retired A(s) long before.
+//  * one 512-thread workgroup per CU, persistent over a strided (XCD-contiguous, row-panel-major)
+//    tile list: the BN-column tiles of one A row panel run together on one XCD (one HBM fetch);
+//    the (tile, K-step) sequence is flattened, so the next tile's loads overlap this tile's end;
+//  * 8 waves as (MT/WM) x (BN/96), wave tile WM x 96 of v_mfma_f32_32x32x16_bf16, operands
+//    swapped so the accumulator is C^T (lane = output row, 16 columns in runs of 4);
+//  * operands DMA'd global->LDS (buffer_load ... lds, 1 KB per wave-instruction, buffer
+//    resources rebuilt per tile) into unpadded [rows][64] bf16 images, 16-B chunk c of row r at
+//    c ^ (r & 7) (source-address swizzle; conflict-free fragment ds_read_b128);
+//  * the host plans the launch so no round of the persistent grid is mostly idle (mmt_gemm);
+//  * epilogue from registers: v_permlane32_swap pairs the two half-waves' column runs into 8
+//    contiguous columns per lane (16-B residual loads and C stores).
+// Requires N % BN == 0, K % 64 == 0; rows past M read zeros and are not stored.
+constexpr int NTW_NT = 512;
+template <int MT, int BN, int EP>  // EP: 0 plain, 1 + bf16 residual, 2 relu
+__global__ __launch_bounds__(NTW_NT, 2) void gemm_ntw_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
+    int64_t ldb, bf16_t* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ R, int64_t ldr,
+    int tiles_n, int n_tiles) {
+  constexpr int WGN = BN / 96, WGM = 8 / WGN, WM = MT / WGM, MB = WM / 32, NB = 3;
+  static_assert(BN % 96 == 0 && 8 % WGN == 0 && WM % 32 == 0, "tile / wave geometry");
+  constexpr int A_ST = MT * 128, B_ST = BN * 128;
+  constexpr int NSA_FIT = (163840 - 2 * B_ST) / A_ST, NSA = NSA_FIT > 4 ? 4 : NSA_FIT;
+  static_assert(NSA >= 2, "LDS");
+  constexpr int PA = MT / 64, PB = BN / 64;  // DMA pieces (8 rows x 128 B) per wave per K-step
+  static_assert(MT % 64 == 0 && BN % 64 == 0, "pieces");
+  constexpr int E = MB * NB * 2;             // 16-B C stores per lane per tile
+  static_assert(PA * (NSA - 2 > 1 ? NSA - 2 : 1) + E < 64, "vmcnt immediate");
+  __shared__ __attribute__((aligned(16))) char smem[NSA * A_ST + 2 * B_ST];
+  char* const sA = smem;
+  char* const sB = smem + NSA * A_ST;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int nk = K / 64;
+  int first, stride, limit = n_tiles;
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    first = (int)((int64_t)n_tiles * xcd / 8) + (blockIdx.x >> 3);
+    limit = (int)((int64_t)n_tiles * (xcd + 1) / 8);
+    stride = gridDim.x >> 3;
+  } else {
+    first = blockIdx.x;
+    stride = gridDim.x;
+  }
+  const int n_mine = first < limit ? (limit - first + stride - 1) / stride : 0;
+  const int S = n_mine * nk;
+  if (S == 0) return;
+
+  // per-lane source byte offsets (row 8 j + lane / 8, swizzled chunk) of this wave's pieces
+  int voa[PA], vob[PB];
+#pragma unroll
+  for (int p = 0; p < PA; ++p) {
+    const int row = 8 * (wave * PA + p) + (lane >> 3);
+    voa[p] = row * (int)(lda * 2) + (((lane & 7) ^ (row & 7)) << 4);
+  }
+#pragma unroll
+  for (int p = 0; p < PB; ++p) {
+    const int row = 8 * (wave * PB + p) + (lane >> 3);
+    vob[p] = row * (int)(ldb * 2) + (((lane & 7) ^ (row & 7)) << 4);
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  // A and B DMA positions advance separately (A runs NSA - 2 K-steps further ahead)
+  __amdgpu_buffer_rsrc_t ra, rb;
+  auto rsrc_a = [&](int i) {
+    const int tile = first + i * stride, tm = tile / tiles_n, m0 = tm * MT;
+    ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(A + (int64_t)m0 * lda), (short)0,
+                                           (int)min((int64_t)(M - m0) * lda * 2, (int64_t)0x7ffffff0), 0x00020000);
+  };
+  auto rsrc_b = [&](int i) {
+    const int tile = first + i * stride, tm = tile / tiles_n, n0 = (tile - tm * tiles_n) * BN;
+    rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(B + (int64_t)n0 * ldb), (short)0,
+                                           (int)min((int64_t)BN * ldb * 2, (int64_t)0x7ffffff0), 0x00020000);
+  };
+  auto dma_a = [&](int st, int p, int kt) {
+#if MMT_W384_ABL != 2
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        ra, (__attribute__((address_space(3))) void*)(sA + st * A_ST + (wave * PA + p) * 1024), 16,
+        voa[p], kt * 128, 0, 0);
+#endif
+  };
+  auto dma_b = [&](int st, int p, int kt) {
+#if MMT_W384_ABL != 2 && MMT_W384_ABL != 1
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rb, (__attribute__((address_space(3))) void*)(sB + st * B_ST + (wave * PB + p) * 1024), 16,
+        vob[p], kt * 128, 0, 0);
+#endif
+  };
+#else
+  auto rsrc_a = [&](int) {};
+  auto rsrc_b = [&](int) {};
+  auto dma_a = [&](int, int, int) {};
+  auto dma_b = [&](int, int, int) {};
+#endif
+  int ai = 0, akt = 0, as = 0;  // next A K-step to load: tile index, K-step, sequence number
+  int bi = 0, bkt = 0, bs = 0;  // next B K-step to load
+  rsrc_a(0);
+  rsrc_b(0);
+  auto next_a = [&]() {
+    ++as;
+    if (++akt == nk) {
+      akt = 0;
+      if (++ai < n_mine) rsrc_a(ai);
+    }
+  };
+  auto next_b = [&]() {
+    ++bs;
+    if (++bkt == nk) {
+      bkt = 0;
+      if (++bi < n_mine) rsrc_b(bi);
+    }
+  };
+
+  floatx16 acc[MB][NB];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const int l31 = lane & 31, h = lane >> 5;
+  int a_off[MB], b_off[NB];  // fragment row byte offsets; the rows' swizzle is l31 & 7
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) a_off[mb] = (wm * WM + 32 * mb + l31) * 128;
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) b_off[nb] = (wn * 96 + 32 * nb + l31) * 128;
+  const int sw = l31 & 7;
+
+  // the K-step in A stage sta / B stage stb; the DMA of the next B K-step and of the A K-step
+  // NSA - 1 ahead (in that order) goes between the MFMA groups, so the SIMD partner wave keeps
+  // issuing MFMAs while this one issues DMA
+  constexpr int PP = PA + PB;
+  auto compute = [&](int sta, int stb, bool nb_ok, bool na_ok) {
+    const char* SA = sA + sta * A_ST;
+    const char* SB = sB + stb * B_ST;
+    const int nbs = bs & 1, nas = as % NSA;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int c = ((2 * ks + h) ^ sw) << 4;
+      bf16x8 af[MB], bfr[NB];
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) af[mb] = *reinterpret_cast<const bf16x8*>(SA + a_off[mb] + c);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) bfr[nb] = *reinterpret_cast<const bf16x8*>(SB + b_off[nb] + c);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) {
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#if MMT_W384_ABL == 3
+          if (M < 0)
+#endif
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[nb], af[mb], acc[mb][nb], 0, 0, 0);
+        const int g = ks * MB + mb;  // DMA pieces over the (ks, mb) MFMA groups: B first, then A
+        if (g < PB) {
+          if (nb_ok) dma_b(nbs, g, bkt);
+        } else if (g < PP) {
+          if (na_ok) dma_a(nas, g - PB, akt);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int g = 4 * MB; g < PP; ++g) {
+      if (g < PB) {
+        if (nb_ok) dma_b(nbs, g, bkt);
+      } else {
+        if (na_ok) dma_a(nas, g - PB, akt);
+      }
+    }
+  };
+
+  // lane (row l31, half h) holds, per 32-column block, columns 8 g + 4 h + i (acc[4 g + i]);
+  // v_permlane32_swap of the g = 2 j and 2 j + 1 runs gives it 8 contiguous columns
+  // 16 j + 8 h .. + 7
+  auto epilogue = [&](int tile) {
+    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int gr = tm * MT + wm * WM + 32 * mb + l31;
+      const bool ok = gr < M;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float v[8];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[mb][nb][8 * j + i]),
+                                                            __float_as_uint(acc[mb][nb][8 * j + 4 + i]),
+                                                            false, false);
+            v[i] = __uint_as_float(x[0]);
+            v[4 + i] = __uint_as_float(x[1]);
+          }
+          const int gc = tn * BN + wn * 96 + 32 * nb + 16 * j + 8 * h;
+          if constexpr (EP == 1) {
+            const uint4 u = *reinterpret_cast<const uint4*>(R + (int64_t)(ok ? gr : M - 1) * ldr + gc);
+            const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              v[2 * q] += __uint_as_float(w[q] << 16);
+              v[2 * q + 1] += __uint_as_float(w[q] & 0xffff0000u);
+            }
+          }
+          if constexpr (EP == 2)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+          uint4 o;
+          o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+          o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+          if (ok) *reinterpret_cast<uint4*>(C + (int64_t)gr * ldc + gc) = o;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[mb][nb][r] = 0.f;
+      }
+    }
+  };
+
+  // prologue, issue order B(0), A(0) .. A(NSA - 2)
+#pragma unroll
+  for (int p = 0; p < PB; ++p) dma_b(0, p, bkt);
+  next_b();
+#pragma unroll
+  for (int q = 0; q < NSA - 1; ++q)
+    if (q < S) {
+#pragma unroll
+      for (int p = 0; p < PA; ++p) dma_a(q, p, akt);
+      next_a();
+    }
+  bool stored = false;  // the previous K-step ended a full tile: its E stores are the youngest
+  int i = 0, kt = 0;    // the computed K-step's tile and K-step
+  for (int s = 0; s < S; ++s) {
+    // K-step s needs B(s) and A(s). Younger than B(s): for s = 0 the prologue's A(1 ..
+    // NSA - 2), otherwise A(s + NSA - 2) (issued right after it, if it exists) and the stores
+    // of an epilogue at the end of K-step s - 1.
+    // (with NSA = 2, A(s + NSA - 2) is A(s) itself: nothing may stay in flight)
+    const int ya = s == 0 ? min(NSA - 2, S - 1) : (NSA >= 3 && s + NSA - 2 < S ? 1 : 0);
+    if (ya == 0) {
+      if (stored) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(E) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (ya == 1) {
+      if (stored) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PA + E) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PA) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PA * (NSA - 2 > 1 ? NSA - 2 : 1)) : "memory");
+    }
+    asm volatile("s_barrier" ::: "memory");  // K-step s landed for every wave; its predecessor's stages free
+    const bool nb_ok = bs < S, na_ok = as < S;
+    compute(s % NSA, s & 1, nb_ok, na_ok);
+    if (nb_ok) next_b();
+    if (na_ok) next_a();
+    stored = false;
+    if (++kt == nk) {
+      const int tile = first + i * stride;
+      epilogue(tile);
+      stored = EP != 1 && (tile / tiles_n) * MT + MT <= M;
+      kt = 0;
+      ++i;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Weight-gradient (TN) split-K partial products with direct global->LDS loads: slab[z] =
 // A[k0:k1]^T . B[k0:k1] for A [K][M] (dY, rows = tokens) and B [K][N] (X), both MN-contiguous.
 // 256 x 192 output tile, 8 waves as 4 (M) x 2 (N) of 64 x 96 (2 x 3 MFMA 32x32x16 blocks, the
@@ -1627,6 +1901,59 @@ int nt_bn(int M, int N, int K, int transA, int transB, int batch, int out_kind, 
   return bn && tm256 * (N / bn) >= cu_count() ? bn : 0;
 }
 
+// Whether the narrow-output NT kernel (gemm_ntw_kernel) runs this launch: products the library
+// (hipBLASLt) used to take — narrow outputs over a long reduction (N <= 768, K >= 1152) and the
+// bias-free relu product of the frozen T5 (N >= 2048, K <= 1024); g_variant 8 forces it wherever
+// it applies. Epilogues: none, bf16 residual, relu.
+bool ntw_ok(int M, int N, int K, int transA, int transB, int batch, int out_kind, const Epi& e) {
+  if (transA || !transB || batch != 1 || out_kind != 0 || N % 192 != 0 || K % 64 != 0) return false;
+  if (e.bias || e.rng || e.gate || e.relu_bits || e.gate_bits || e.colsum || e.alpha != 1.f ||
+      e.beta != 0.f || (e.residual && e.res_f32) || (e.residual && e.act != MMT_ACT_NONE) ||
+      (e.act != MMT_ACT_NONE && e.act != MMT_ACT_RELU))
+    return false;
+  if (g_variant >= 0 && g_variant != 8) return false;
+  if (g_variant == 8) return true;
+  const bool narrow = N <= 768 && K >= 1152 && e.act == MMT_ACT_NONE;
+  const bool relu = e.act == MMT_ACT_RELU && !e.residual && N >= 2048 && K <= 1024;
+  return (narrow || relu) && M >= 8192;
+}
+
+// Launch plan of gemm_ntw_kernel: tile width bn (192 / 384), `rows_big` rows in full rounds of
+// the persistent grid on 256-row tiles, the rest on tiles of mt2 rows. A tile's time is taken as
+// proportional to its operand bytes per K-step, (MT + BN) x 128, so a last round of a few big
+// tiles is replaced by one of smaller tiles when that ends sooner.
+struct NtwPlan {
+  int bn, rows_big, mt2;
+};
+NtwPlan ntw_plan(int M, int N) {
+  const int n_cu = cu_count();
+  static const int force_mt = getenv("MMT_NTW_MT") ? atoi(getenv("MMT_NTW_MT")) : 0;  // tuning knobs
+  static const int force_bn = getenv("MMT_NTW_BN") ? atoi(getenv("MMT_NTW_BN")) : 384;
+  // 384-wide tiles (B re-read once per 256 rows) measured faster than 192-wide ones (A re-read
+  // through L2 by two tiles, three A stages in flight): 204 vs 218 us at 138,496 x 384 x 1536
+  const int bn = (force_bn == 192 || N % 384 != 0) ? 192 : 384;
+  if (force_mt == 64 || force_mt == 128 || force_mt == 192 || force_mt == 256)
+    if (bn == 384 || force_mt % 128 == 0) return {bn, 0, force_mt};
+  const int tn = N / bn;
+  const int panels_per_round = n_cu % tn == 0 ? n_cu / tn : 0;
+  const int max_rounds = panels_per_round ? M / (256 * panels_per_round) : 0;
+  NtwPlan best{bn, 0, 256};
+  int64_t best_cost = INT64_MAX;
+  for (int r = 0; r <= max_rounds; ++r) {
+    const int rows_big = r * panels_per_round * 256, rem = M - rows_big;
+    for (int mt : {64, 128, 192, 256}) {
+      if (bn == 192 && mt % 128 != 0) continue;  // 4 x 2 waves of 32-row multiples
+      const int64_t tiles = rem > 0 ? (int64_t)((rem + mt - 1) / mt) * tn : 0;
+      const int64_t cost = (int64_t)r * (256 + bn) + ((tiles + n_cu - 1) / n_cu) * (mt + bn);
+      if (cost < best_cost) {
+        best_cost = cost;
+        best = {bn, rows_big, mt};
+      }
+    }
+  }
+  return best;
+}
+
 }  // namespace
 
 extern "C" int mmt_gemm_colsum_rows(int M, int N, int K, int transA, int transB, int c_mode,
@@ -1699,6 +2026,47 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
                       (uintptr_t)workspace % 16 == 0,
                   "mmt_gemm: split-K needs a 16-B aligned workspace of split_k*M*N floats");
     out_kind = 2;
+  }
+  // narrow-output NT kernel (products formerly on hipBLASLt)
+  if (ntw_ok(M, N, K, transA, transB, batch, out_kind, epi)) {
+    const NtwPlan plan = ntw_plan(M, N);
+    const int ep = epi.residual ? 1 : epi.act == MMT_ACT_RELU ? 2 : 0;
+    auto launch = [&](int mt, int r0, int rows) {
+      const int tn = N / plan.bn, n_tiles = ((rows + mt - 1) / mt) * tn;
+      int grid = std::min(n_tiles, cu_count());
+      if (grid > 8) grid &= ~7;  // XCD-contiguous tile ranges need a multiple of 8 workgroups
+      const bf16_t* a = (const bf16_t*)A + (int64_t)r0 * lda;
+      bf16_t* c = (bf16_t*)C + (int64_t)r0 * ldc;
+      const bf16_t* r = epi.residual ? (const bf16_t*)epi.residual + (int64_t)r0 * epi.ld_res : nullptr;
+#define GW(MTV, BNV)                                                                                  \
+  do {                                                                                                 \
+    if (ep == 0)                                                                                       \
+      hipLaunchKernelGGL((gemm_ntw_kernel<MTV, BNV, 0>), dim3(grid), dim3(NTW_NT), 0, s, rows, N, K, a, \
+                         lda, (const bf16_t*)B, ldb, c, ldc, r, epi.ld_res, tn, n_tiles);              \
+    else if (ep == 1)                                                                                  \
+      hipLaunchKernelGGL((gemm_ntw_kernel<MTV, BNV, 1>), dim3(grid), dim3(NTW_NT), 0, s, rows, N, K, a, \
+                         lda, (const bf16_t*)B, ldb, c, ldc, r, epi.ld_res, tn, n_tiles);              \
+    else                                                                                               \
+      hipLaunchKernelGGL((gemm_ntw_kernel<MTV, BNV, 2>), dim3(grid), dim3(NTW_NT), 0, s, rows, N, K, a, \
+                         lda, (const bf16_t*)B, ldb, c, ldc, r, epi.ld_res, tn, n_tiles);              \
+  } while (0)
+      if (plan.bn == 384) {
+        switch (mt) {
+          case 64: GW(64, 384); break;
+          case 128: GW(128, 384); break;
+          case 192: GW(192, 384); break;
+          default: GW(256, 384); break;
+        }
+      } else {
+        if (mt == 128) GW(128, 192);
+        else GW(256, 192);
+      }
+#undef GW
+    };
+    if (plan.rows_big > 0) launch(256, 0, plan.rows_big);
+    if (M > plan.rows_big) launch(plan.mt2, plan.rows_big, M - plan.rows_big);
+    MMT_CHECK_LAUNCH("mmt_gemm(ntw)");
+    return MMT_OK;
   }
   // Persistent 256 x BN NT kernel (variant -1 auto, 5/6/7 force BN 256/192/128)
   const int bn = (epi.bias && N > NT_BIAS_LDS) ? 0 : nt_bn(M, N, K, transA, transB, batch, out_kind, final_kind);

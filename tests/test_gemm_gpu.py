@@ -177,3 +177,30 @@ def test_library_relu_product(dev):
     _close_bf16(ours, ref)
     if Kn.library_relu_gemm_ok(M, N, K):
         _close_bf16(Kn.library_relu_gemm_nt(a, b), ref)
+
+
+@pytest.mark.parametrize("M,N,K,ep,variant", [
+    (8200, 384, 1536, "none", -1), (138496, 384, 1536, "none", -1), (8192, 768, 3072, "res", -1),
+    (9000, 3072, 768, "relu", -1), (300, 384, 128, "none", 8), (70, 768, 64, "res", 8),
+    (1000, 1152, 192, "relu", 8)])
+def test_narrow_nt_kernel(dev, M, N, K, ep, variant):
+    """gemm_ntw_kernel (the products formerly on hipBLASLt: N <= 768 over K >= 1152, the T5 relu
+    product; variant 8 forces it on any N % 192 == 0, K % 64 == 0 launch): ragged row counts,
+    the two-launch plan (full rounds of 256-row tiles + one round of smaller tiles at M = 138,496),
+    residual and relu epilogues, against fp32 torch on the same bf16 operands."""
+    from multi_modal_transformers_tokenmerge_amd import _C
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    g = torch.Generator().manual_seed(M + N + K)
+    a, b = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    r = _mk((M, N), dev, g) if ep == "res" else None
+    act = Kn.ACT_RELU if ep == "relu" else Kn.ACT_NONE
+    _C.call("mmt_gemm_set_variant", variant)
+    try:
+        out = Kn.gemm(a, b, False, True, residual=r, act=act)
+        torch.cuda.synchronize()
+    finally:
+        _C.call("mmt_gemm_set_variant", -1)
+    ref = a.float() @ b.float().t() + (r.float() if r is not None else 0.0)
+    if ep == "relu":
+        ref = ref.clamp_min(0)
+    _close_bf16(out, ref)
