@@ -168,19 +168,21 @@ def kernel_probes(model, B, reps=20):
                                   keep_prob=0.9),
         "mfma", 2.0 * M * Mh * D, f"M={M} N={Mh} K={D}, 2MNK", _gemm_bytes(M, Mh, D, extra=4 * Mh))
     # 2. MLP input gradient dy1 = dz1 . W1 (NT on the transposed shadow): N = 384, K = 1536 — a
-    # plain product, which the step runs on hipBLASLt (K.library_gemm_ok); the library kernel's
-    # name is Cijk_..., matched by that prefix in the PMC passes
+    # plain narrow product: gemm_ntw_kernel (hipBLASLt with MMT_BLASLT=1, name Cijk_..., matched
+    # by that prefix in the PMC passes)
     dz1 = rnd(M, Mh)
     dy1 = torch.empty((M, D), dtype=torch.bfloat16, device=dev)
     if K.library_gemm_ok(M, D, Mh):
         add("mlp_dx", "Cijk_",
             lambda: K.library_gemm_nt(dz1, blk.mlp.dense.w.bf16_t, out=dy1),
-            "mfma", 2.0 * M * D * Mh, f"M={M} N={D} K={Mh}, 2MNK (hipBLASLt, as in the step)",
+            "mfma", 2.0 * M * D * Mh, f"M={M} N={D} K={Mh}, 2MNK (hipBLASLt, MMT_BLASLT=1)",
             _gemm_bytes(M, D, Mh))
     else:
-        add("mlp_dx", "gemm_glds_nt_kernel<0>",
+        add("mlp_dx", "gemm_ntw_kernel",
             lambda: K.gemm(dz1, blk.mlp.dense.w.bf16_t, trans_b=True, out=dy1),
-            "mfma", 2.0 * M * D * Mh, f"M={M} N={D} K={Mh}, 2MNK", _gemm_bytes(M, D, Mh))
+            "mfma", 2.0 * M * D * Mh,
+            f"M={M} N={D} K={Mh}, 2MNK (one or two launches of the narrow-output NT kernel)",
+            _gemm_bytes(M, D, Mh))
     # 3. MLP Dense_0 weight gradient dW += dz1^T . y1 (TN, split-K fp32 slabs + combine)
     wgrad = torch.zeros((Mh, D), dtype=torch.float32, device=dev)
     add("mlp_dw", "gemm_tn_dma_kernel",

@@ -228,17 +228,17 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
     return out
 
 
-_BLASLT = os.environ.get("MMT_BLASLT", "1") != "0"  # benchmarking knob: every product on libmmt_hip
+# MMT_BLASLT=1: the plain narrow products and the T5 relu product on hipBLASLt (a comparison knob:
+# by default every product of the step runs on libmmt_hip's kernels — gemm_ntw_kernel for these)
+_BLASLT = os.environ.get("MMT_BLASLT", "0") == "1"
 
 
 def library_gemm_ok(M: int, N: int, K: int) -> bool:
-    """Plain (epilogue-free) NT products that hipBLASLt runs faster than this library's kernels
-    (tools/blaslt_probe.py, B = 512 shapes, graph-timed): narrow outputs (N <= 768) over a long
-    reduction (K >= 1152) — the MLP input gradient 141,312 x 384 x 1536 (208 vs 241 us), the QKV
-    input gradient 149,504 x 384 x 1152 (156 vs 187 us) and the frozen T5's FF output + residual
-    16,384 x 768 x 3072 (80 vs 98 us). Shorter reductions (out-projection input gradient, T5
-    attention output) are faster here; everything with a fused epilogue beyond a residual stays
-    on libmmt_hip."""
+    """With MMT_BLASLT=1 only: the plain narrow NT products (N <= 768, K >= 1152) go to hipBLASLt —
+    the MLP input gradient 141,312 x 384 x 1536, the QKV input gradient 149,504 x 384 x 1152 and
+    the frozen T5's FF output + residual 16,384 x 768 x 3072. By default libmmt_hip's
+    gemm_ntw_kernel runs them (tools/w384_probe.py: 204 / 173 / 90 us vs the library's
+    200 / 152 / 81; the whole step 36.14 vs 35.96 ms)."""
     return _BLASLT and N <= 768 and K >= 1152 and M >= 8192
 
 
@@ -256,8 +256,8 @@ _ZERO_BIAS: dict = {}
 
 
 def library_relu_gemm_ok(M: int, N: int, K: int) -> bool:
-    """Bias-free relu products that hipBLASLt's fused relu epilogue runs faster: the frozen T5's
-    FF input 16,384 x 3072 x 768 (73 vs 99 us, bit-identical outputs; tools/blaslt_probe.py)."""
+    """With MMT_BLASLT=1 only: the frozen T5's FF input relu(16,384 x 3072 x 768) on hipBLASLt's
+    relu epilogue (73 us vs gemm_ntw_kernel's 89)."""
     return _BLASLT and hasattr(torch, "_addmm_activation") and N >= 2048 and K <= 1024 and M >= 8192
 
 
