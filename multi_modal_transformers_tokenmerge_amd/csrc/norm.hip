@@ -13,6 +13,7 @@
 // over the sequence). The residual stream x and its gradient are therefore fp32 (x_dtype /
 // res_dtype = MMT_F32 on the training path); y is emitted in bf16 for the MFMA GEMMs.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -26,6 +27,14 @@ constexpr int NT = 256;  // = 8 column vectors x RG
 
 __device__ __forceinline__ void load8(const bf16_t* p, float* f) {
   const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f[2 * q] = __uint_as_float(w[q] << 16);
+    f[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void unpack8(const uint4 u, float* f) {
   const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -137,7 +146,10 @@ struct DropZ {
   int64_t zs_b, zs_t;
   float* colsum;
 };
-template <typename TDY, typename TX, bool DZ = false>
+// RPT > 0 (bf16 dy, fp32 x, L <= 32 RPT): single pass over HBM — each thread keeps its RPT rows
+// of x (fp32) and dy (packed bf16) in registers from the statistics pass to the gradient pass
+// (the two-pass form re-reads both: 1.43x the algorithmic bytes measured at B = 512).
+template <typename TDY, typename TX, bool DZ = false, int RPT = 0>
 __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
     const TDY* __restrict__ dy, int64_t ds_b, int64_t ds_t, const TX* __restrict__ x,
     int64_t xs_b, int64_t xs_t, int L, int D, const float* __restrict__ mean,
@@ -159,21 +171,47 @@ __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
   const TX* xb = x + (int64_t)b * xs_b + col;
   const TDY* db = dy + (int64_t)b * ds_b + col;
   float part[4][8] = {};  // sum g, sum g*xhat, sum dy*xhat, sum dy
-  if (cok)
+  constexpr int RR = RPT > 0 ? RPT : 1;
+  [[maybe_unused]] float rx[RR][8];  // RPT: this thread's rows of x and dy, kept for pass 2
+  [[maybe_unused]] uint4 rdy[RR];
+  auto stat = [&](const float* fx, const float* fd) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float xh = (fx[e] - mu[e]) * rs[e];
+      const float g = fd[e] * ga[e];
+      part[0][e] += g;
+      part[1][e] += g * xh;
+      part[2][e] += fd[e] * xh;
+      part[3][e] += fd[e];
+    }
+  };
+  if constexpr (RPT > 0) {
+    static_assert(std::is_same<TDY, bf16_t>::value && std::is_same<TX, float>::value, "RPT form");
+    // every load unconditional (rows past L clamped, their dy zeroed: no contribution), so
+    // they are all in flight together: a load under a per-row branch waits vmcnt(0) each
+    if (cok) {
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        const int l = min(rg + j * RG, L - 1);
+        load8(xb + (int64_t)l * xs_t, rx[j]);
+        rdy[j] = *reinterpret_cast<const uint4*>(db + (int64_t)l * ds_t);
+      }
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        if (rg + j * RG >= L) rdy[j] = make_uint4(0u, 0u, 0u, 0u);
+        float fd[8];
+        unpack8(rdy[j], fd);
+        stat(rx[j], fd);
+      }
+    }
+  } else if (cok) {
     for (int l = rg; l < L; l += RG) {
       float fx[8], fd[8];
       load8(xb + (int64_t)l * xs_t, fx);
       load8(db + (int64_t)l * ds_t, fd);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float xh = (fx[e] - mu[e]) * rs[e];
-        const float g = fd[e] * ga[e];
-        part[0][e] += g;
-        part[1][e] += g * xh;
-        part[2][e] += fd[e] * xh;
-        part[3][e] += fd[e];
-      }
+      stat(fx, fd);
     }
+  }
   reduce_rows<4>(part, red);
   if (threadIdx.x < CW && c0 + threadIdx.x < D) {
     atomicAdd(dgamma + c0 + threadIdx.x, red[2 * RG * CW + threadIdx.x]);
@@ -190,17 +228,28 @@ __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
   const TX* ab = addend ? addend + (int64_t)b * as_b + col : nullptr;
   [[maybe_unused]] float cs[8] = {};
   [[maybe_unused]] const uint32_t key = DZ && dz.rng ? stream_key(dz.rng[0], dz.rng[1], dz.layer, dz.site) : 0u;
-  for (int l = rg; cok && l < L; l += RG) {
+#pragma unroll(RPT > 0 ? RPT : 1)
+  for (int j = 0, l = rg; cok && (RPT > 0 ? j < RPT : l < L); ++j, l += RG) {
+    // RPT: a fixed trip count and unconditional (row-clamped) addend loads; only the stores of
+    // rows past L are skipped
+    const int la = RPT > 0 ? min(l, L - 1) : l;
     float fx[8], fd[8], fa[8];
-    load8(xb + (int64_t)l * xs_t, fx);
-    load8(db + (int64_t)l * ds_t, fd);
-    if (ab) load8(ab + (int64_t)l * as_t, fa);
+    if constexpr (RPT > 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) fx[e] = rx[j][e];
+      unpack8(rdy[j], fd);
+    } else {
+      load8(xb + (int64_t)l * xs_t, fx);
+      load8(db + (int64_t)l * ds_t, fd);
+    }
+    if (ab) load8(ab + (int64_t)la * as_t, fa);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float xh = (fx[e] - mu[e]) * rs[e];
       const float g = fd[e] * ga[e];
       fx[e] = rs[e] * (g - mg[e] - xh * mgx[e]) + (ab ? fa[e] : 0.f);
     }
+    if (RPT > 0 && l >= L) continue;
     store8(dxb + (int64_t)l * dxs_t, fx);
     if constexpr (DZ) {
       float f[8];
@@ -239,7 +288,10 @@ __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
 // with its column sums (the out-projection bias gradient). Same expressions as the three kernels
 // (this file's compilation): bit-identical g_in, z and LN gradients; the column-sum atomics
 // differ in order only.
+// RPT > 0 (L2 <= 32 RPT): passes 1 and 2 read x1 / dy1 once, kept in registers (as the
+// RPT form of seqnorm_bwd_kernel).
 constexpr int kUnmergeMax = 512;  // unmerged rows per sample of the fused form
+template <int RPT = 0>
 __global__ __launch_bounds__(NT) void ln_unmerge_dropout_bwd_kernel(
     const bf16_t* __restrict__ dy, int64_t ds_b, int64_t ds_t, const float* __restrict__ x,
     int64_t xs_b, int64_t xs_t, int L2, int D, const float* __restrict__ mean,
@@ -281,21 +333,46 @@ __global__ __launch_bounds__(NT) void ln_unmerge_dropout_bwd_kernel(
   const float* xb = x + (int64_t)b * xs_b + col;
   const bf16_t* db = dy + (int64_t)b * ds_b + col;
   float part[4][8] = {};  // pass 1 (seqnorm_bwd_kernel)
-  if (cok)
+  constexpr int RR = RPT > 0 ? RPT : 1;
+  [[maybe_unused]] float rx[RR][8];
+  [[maybe_unused]] uint4 rdy[RR];
+  auto stat = [&](const float* fx, const float* fd) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float xh = (fx[e] - mu[e]) * rs[e];
+      const float g = fd[e] * ga[e];
+      part[0][e] += g;
+      part[1][e] += g * xh;
+      part[2][e] += fd[e] * xh;
+      part[3][e] += fd[e];
+    }
+  };
+  if constexpr (RPT > 0) {
+    // every load unconditional (rows past L2 clamped, their dy zeroed: no contribution), so
+    // they are all in flight together: a load under a per-row branch waits vmcnt(0) each
+    if (cok) {
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        const int l = min(rg + j * RG, L2 - 1);
+        load8(xb + (int64_t)l * xs_t, rx[j]);
+        rdy[j] = *reinterpret_cast<const uint4*>(db + (int64_t)l * ds_t);
+      }
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        if (rg + j * RG >= L2) rdy[j] = make_uint4(0u, 0u, 0u, 0u);
+        float fd[8];
+        unpack8(rdy[j], fd);
+        stat(rx[j], fd);
+      }
+    }
+  } else if (cok) {
     for (int l = rg; l < L2; l += RG) {
       float fx[8], fd[8];
       load8(xb + (int64_t)l * xs_t, fx);
       load8(db + (int64_t)l * ds_t, fd);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float xh = (fx[e] - mu[e]) * rs[e];
-        const float g = fd[e] * ga[e];
-        part[0][e] += g;
-        part[1][e] += g * xh;
-        part[2][e] += fd[e] * xh;
-        part[3][e] += fd[e];
-      }
+      stat(fx, fd);
     }
+  }
   reduce_rows<4>(part, red);
   if (threadIdx.x < CW && c0 + threadIdx.x < D) {
     atomicAdd(dgamma + c0 + threadIdx.x, red[2 * RG * CW + threadIdx.x]);
@@ -309,18 +386,26 @@ __global__ __launch_bounds__(NT) void ln_unmerge_dropout_bwd_kernel(
   }
   __syncthreads();  // red is read; the panel reuses it
   const float* ab = addend ? addend + (int64_t)b * as_b + col : nullptr;
-  if (cok)
-    for (int l = rg; l < L2; l += RG) {  // pass 2: merged-layout input gradient into LDS
+#pragma unroll(RPT > 0 ? RPT : 1)
+  for (int j = 0, l = rg; cok && (RPT > 0 ? j < RPT : l < L2); ++j, l += RG) {  // pass 2: into LDS
+      const int la = RPT > 0 ? min(l, L2 - 1) : l;
       float fx[8], fd[8], fa[8];
-      load8(xb + (int64_t)l * xs_t, fx);
-      load8(db + (int64_t)l * ds_t, fd);
-      if (ab) load8(ab + (int64_t)l * as_t, fa);
+      if constexpr (RPT > 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) fx[e] = rx[j][e];
+        unpack8(rdy[j], fd);
+      } else {
+        load8(xb + (int64_t)l * xs_t, fx);
+        load8(db + (int64_t)l * ds_t, fd);
+      }
+      if (ab) load8(ab + (int64_t)la * as_t, fa);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float xh = (fx[e] - mu[e]) * rs[e];
         const float g = fd[e] * ga[e];
         fx[e] = rs[e] * (g - mg[e] - xh * mgx[e]) + (ab ? fa[e] : 0.f);
       }
+      if (RPT > 0 && l >= L2) continue;  // rows past L2: no panel row
       store8(panel + l * CW + cv * 8, fx);
     }
   __syncthreads();
@@ -402,6 +487,16 @@ inline bool is_dt(int d) { return d == MMT_F32 || d == MMT_BF16; }
 
 }  // namespace
 
+// rows per thread of the single-pass (register-resident) LayerNorm backward for L rows, 0 for the
+// two-pass form (L > 320, or MMT_SNB_RPT=0)
+static int snb_rpt(int L) {
+  static const bool on = !getenv("MMT_SNB_RPT") || atoi(getenv("MMT_SNB_RPT")) != 0;
+  if (!on) return 0;
+  for (int r : {4, 6, 8, 10})
+    if (L <= RG * r) return r;
+  return 0;
+}
+
 extern "C" int mmt_seqnorm_fwd(const void* x, int x_dtype, int64_t xs_b, int64_t xs_t, int B,
                                int L, int D, const float* gamma, const float* beta, float eps,
                                void* y, int64_t ys_b, int64_t ys_t, float* mean, float* rstd,
@@ -442,7 +537,18 @@ extern "C" int mmt_seqnorm_bwd(const void* dy, int dy_dtype, int64_t ds_b, int64
   hipLaunchKernelGGL((seqnorm_bwd_kernel<TDY, TX>), grid, dim3(NT), 0, s, (const TDY*)dy, ds_b, \
                      ds_t, (const TX*)x, xs_b, xs_t, L, D, mean, rstd, gamma, (const TX*)addend,  \
                      as_b, as_t, (TX*)dx, dxs_b, dxs_t, dgamma, dbeta)
-  if (dy_dtype == MMT_F32 && x_dtype == MMT_F32) SNB(float, float);
+  const int rpt = snb_rpt(L);
+  if (dy_dtype == MMT_BF16 && x_dtype == MMT_F32 && rpt) {
+#define SNBR(R)                                                                                     \
+  hipLaunchKernelGGL((seqnorm_bwd_kernel<bf16_t, float, false, R>), grid, dim3(NT), 0, s,           \
+                     (const bf16_t*)dy, ds_b, ds_t, (const float*)x, xs_b, xs_t, L, D, mean, rstd,  \
+                     gamma, (const float*)addend, as_b, as_t, (float*)dx, dxs_b, dxs_t, dgamma, dbeta)
+    if (rpt == 4) SNBR(4);
+    else if (rpt == 6) SNBR(6);
+    else if (rpt == 8) SNBR(8);
+    else SNBR(10);
+#undef SNBR
+  } else if (dy_dtype == MMT_F32 && x_dtype == MMT_F32) SNB(float, float);
   else if (dy_dtype == MMT_BF16 && x_dtype == MMT_F32) SNB(bf16_t, float);
   else if (dy_dtype == MMT_F32 && x_dtype == MMT_BF16) SNB(float, bf16_t);
   else SNB(bf16_t, bf16_t);
@@ -507,16 +613,27 @@ extern "C" int mmt_ln_unmerge_dropout_bwd(
                 "mmt_ln_unmerge_dropout_bwd: strides must be multiples of 8");
   MMT_CHECK_ARG(!rng || (keep_prob > 0.f && keep_prob <= 1.f), "mmt_ln_unmerge_dropout_bwd: keep_prob");
   const size_t dyn = sizeof(float) * (size_t)std::max(L2 * CW, 4 * RG * CW);
-  static const bool attr_ = (hipFuncSetAttribute((const void*)ln_unmerge_dropout_bwd_kernel,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 96 * 1024), true);
-  (void)attr_;
   dim3 grid(B, (D + CW - 1) / CW);
-  hipLaunchKernelGGL(ln_unmerge_dropout_bwd_kernel, grid, dim3(NT), dyn, as_stream(stream),
-                     (const bf16_t*)dy, ds_b, ds_t, x, xs_b, xs_t, L2, D, mean, rstd, gamma, addend,
-                     as_b, as_t, dgamma, dbeta, L, set_start, t, r, size_in, size_out, pos_map,
-                     g_in, gs_b, gs_t, rng, layer, site, rng ? keep_threshold16(keep_prob) : 0u,
-                     rng ? 1.f / keep_prob : 1.f, row_offset, (bf16_t*)z, zs_b, zs_t, bias_grad);
+  const int rpt = snb_rpt(L2);
+#define LUD(R)                                                                                      \
+  do {                                                                                              \
+    static const bool attr_ = (hipFuncSetAttribute((const void*)ln_unmerge_dropout_bwd_kernel<R>,   \
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,      \
+                                                   96 * 1024), true);                               \
+    (void)attr_;                                                                                    \
+    hipLaunchKernelGGL((ln_unmerge_dropout_bwd_kernel<R>), grid, dim3(NT), dyn, as_stream(stream),  \
+                       (const bf16_t*)dy, ds_b, ds_t, x, xs_b, xs_t, L2, D, mean, rstd, gamma,      \
+                       addend, as_b, as_t, dgamma, dbeta, L, set_start, t, r, size_in, size_out,    \
+                       pos_map, g_in, gs_b, gs_t, rng, layer, site,                                  \
+                       rng ? keep_threshold16(keep_prob) : 0u, rng ? 1.f / keep_prob : 1.f,          \
+                       row_offset, (bf16_t*)z, zs_b, zs_t, bias_grad);                               \
+  } while (0)
+  if (rpt == 4) LUD(4);
+  else if (rpt == 6) LUD(6);
+  else if (rpt == 8) LUD(8);
+  else if (rpt == 10) LUD(10);
+  else LUD(0);
+#undef LUD
   MMT_CHECK_LAUNCH("mmt_ln_unmerge_dropout_bwd");
   return MMT_OK;
 }
@@ -538,9 +655,17 @@ extern "C" int mmt_seqnorm_dropout_bwd(const void* dy, int64_t ds_b, int64_t ds_
   DropZ dz{rng, layer, site, rng ? keep_threshold16(keep_prob) : 0u, rng ? 1.f / keep_prob : 1.f,
            row_offset, (bf16_t*)z, zs_b, zs_t, colsum};
   dim3 grid(B, (D + CW - 1) / CW);
-  hipLaunchKernelGGL((seqnorm_bwd_kernel<bf16_t, float, true>), grid, dim3(NT), 0,
-                     as_stream(stream), (const bf16_t*)dy, ds_b, ds_t, x, xs_b, xs_t, L, D, mean,
-                     rstd, gamma, addend, as_b, as_t, dx, dxs_b, dxs_t, dgamma, dbeta, dz);
+  const int rpt = snb_rpt(L);
+#define SDZ(R)                                                                                      \
+  hipLaunchKernelGGL((seqnorm_bwd_kernel<bf16_t, float, true, R>), grid, dim3(NT), 0,               \
+                     as_stream(stream), (const bf16_t*)dy, ds_b, ds_t, x, xs_b, xs_t, L, D, mean,   \
+                     rstd, gamma, addend, as_b, as_t, dx, dxs_b, dxs_t, dgamma, dbeta, dz)
+  if (rpt == 4) SDZ(4);
+  else if (rpt == 6) SDZ(6);
+  else if (rpt == 8) SDZ(8);
+  else if (rpt == 10) SDZ(10);
+  else SDZ(0);
+#undef SDZ
   MMT_CHECK_LAUNCH("mmt_seqnorm_dropout_bwd");
   return MMT_OK;
 }
