@@ -12,7 +12,8 @@ cross-queue waits, small launches, AdamW — amortise; see DESIGN.md "Batch").
 One step = zero grads -> forward (frozen T5, image stem, 12 ToMe blocks, diffusion loss) ->
 backward -> [gradient all-reduce over RCCL] -> fused AdamW -> device step counter, on synthetic
 inputs resident in HBM (numpy default_rng(0) shapes of SURVEY §8d). The N=1 step is one HIP graph
-replay; with N>1 the backward runs as --overlap-stages block-range graphs, each stage's gradient
+replay; with N>1 the backward runs as --overlap-stages graphs (default auto: ~24 MB gradient
+regions, block 0 alone last), each stage's gradient
 region all-reduced asynchronously on the RCCL stream while the later stages compute, and the AdamW
 graph waits for them (distributed.DDPStep; --no-graph launches the same schedule eagerly).
 Timing: barrier + synchronize on both sides of exactly K steps, max over ranks.
@@ -346,9 +347,10 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--overlap-stages", type=int, default=3,
-                    help="N > 1: backward split into this many block ranges, each range's gradient "
-                         "all-reduce overlapped with the rest of the backward (1 = no overlap)")
+    ap.add_argument("--overlap-stages", default="auto",
+                    help="N > 1: backward stages, each stage's gradient region all-reduced while "
+                         "the rest of the backward runs: an int (block ranges; 1 = no overlap) or "
+                         "auto[:MB] (~MB-megabyte regions, default 24, block 0 alone last)")
     ap.add_argument("--no-probes", action="store_true",
                     help="skip the per-kernel roofline probes (rocprofv3 traces of the step alone)")
     ap.add_argument("--probe-only", action="store_true",
@@ -377,7 +379,8 @@ def main():
     use_graph = not args.no_graph
     # N > 1: the backward runs as --overlap-stages block-range stages, each stage's gradient
     # region all-reduced asynchronously while the later stages compute (distributed.DDPStep)
-    step = DDPStep(model, state, txt, img, act, reducer, stages=args.overlap_stages,
+    ov = args.overlap_stages
+    step = DDPStep(model, state, txt, img, act, reducer, stages=int(ov) if ov.isdigit() else ov,
                    use_graph=use_graph).build()
     loss_buf = step.loss_buf
 

@@ -76,7 +76,9 @@ __device__ __forceinline__ void reduce_rows(float (*part)[8], float* red /*[NV][
   __syncthreads();
 }
 
-template <typename TX>
+// RPT > 0 (fp32 x, L <= 32 RPT): one read of x — each thread keeps its RPT rows in registers
+// from the statistics pass to the normalisation pass, every load unconditional (row-clamped).
+template <typename TX, int RPT = 0>
 __global__ __launch_bounds__(NT) void seqnorm_fwd_kernel(
     const TX* __restrict__ x, int64_t xs_b, int64_t xs_t, int L, int D,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
@@ -90,7 +92,22 @@ __global__ __launch_bounds__(NT) void seqnorm_fwd_kernel(
   const bool cok = col < D;
   const TX* xb = x + (int64_t)b * xs_b + col;
   float part[2][8] = {};
-  if (cok)
+  constexpr int RR = RPT > 0 ? RPT : 1;
+  [[maybe_unused]] float rx[RR][8];
+  if constexpr (RPT > 0) {
+    if (cok) {
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) load8(xb + (int64_t)min(rg + j * RG, L - 1) * xs_t, rx[j]);
+#pragma unroll
+      for (int j = 0; j < RPT; ++j)
+        if (rg + j * RG < L)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            part[0][e] += rx[j][e];
+            part[1][e] += rx[j][e] * rx[j][e];
+          }
+    }
+  } else if (cok) {
     for (int l = rg; l < L; l += RG) {
       float f[8];
       load8(xb + (int64_t)l * xs_t, f);
@@ -100,6 +117,7 @@ __global__ __launch_bounds__(NT) void seqnorm_fwd_kernel(
         part[1][e] += f[e] * f[e];
       }
     }
+  }
   reduce_rows<2>(part, red);
   if (threadIdx.x < CW && c0 + threadIdx.x < D) {
     const int c = c0 + threadIdx.x;
@@ -121,12 +139,24 @@ __global__ __launch_bounds__(NT) void seqnorm_fwd_kernel(
     add[e] = s_add[cv * 8 + e];
   }
   bf16_t* yb = y + (int64_t)b * ys_b + col;
-  for (int l = rg; l < L; l += RG) {
-    float f[8];
-    load8(xb + (int64_t)l * xs_t, f);
+  if constexpr (RPT > 0) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = f[e] * mul[e] + add[e];
-    store8(yb + (int64_t)l * ys_t, f);
+    for (int j = 0; j < RPT; ++j) {
+      const int l = rg + j * RG;
+      if (l >= L) break;
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = rx[j][e] * mul[e] + add[e];
+      store8(yb + (int64_t)l * ys_t, f);
+    }
+  } else {
+    for (int l = rg; l < L; l += RG) {
+      float f[8];
+      load8(xb + (int64_t)l * xs_t, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = f[e] * mul[e] + add[e];
+      store8(yb + (int64_t)l * ys_t, f);
+    }
   }
 }
 
@@ -507,7 +537,18 @@ extern "C" int mmt_seqnorm_fwd(const void* x, int x_dtype, int64_t xs_b, int64_t
                     xs_b % 8 == 0 && ys_b % 8 == 0,
                 "mmt_seqnorm_fwd: D and strides must be multiples of 8");
   dim3 grid(B, (D + CW - 1) / CW);
-  if (x_dtype == MMT_F32)
+  const int rpt = snb_rpt(L);
+  if (x_dtype == MMT_F32 && rpt) {
+#define SNF(R)                                                                                       \
+  hipLaunchKernelGGL((seqnorm_fwd_kernel<float, R>), grid, dim3(NT), 0, as_stream(stream),          \
+                     (const float*)x, xs_b, xs_t, L, D, gamma, beta, eps, (bf16_t*)y, ys_b, ys_t,    \
+                     mean, rstd)
+    if (rpt == 4) SNF(4);
+    else if (rpt == 6) SNF(6);
+    else if (rpt == 8) SNF(8);
+    else SNF(10);
+#undef SNF
+  } else if (x_dtype == MMT_F32)
     hipLaunchKernelGGL(seqnorm_fwd_kernel<float>, grid, dim3(NT), 0, as_stream(stream),
                        (const float*)x, xs_b, xs_t, L, D, gamma, beta, eps, (bf16_t*)y, ys_b, ys_t,
                        mean, rstd);

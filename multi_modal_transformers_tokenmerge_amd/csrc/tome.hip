@@ -834,7 +834,11 @@ static int check_vec(int dtype, int D, int64_t a, int64_t b, int64_t c2, int64_t
 // without FMA contraction: bit-identical merged rows), stores them and accumulates the LN sums;
 // pass 2 re-reads the just-written rows and writes y (bf16). Saves the LN's separate read of the
 // merged sequence and a launch. fp32 residual stream, Lout <= kFusedRows.
+// RPT > 0 (Lout <= 32 RPT): every thread first issues the primary-row loads of all its RPT output
+// rows (row-clamped, unconditional: a load under a per-row branch waits vmcnt(0) each), keeps the
+// merged rows in registers and writes y from them (no re-read of the merged rows).
 constexpr int kFusedRows = 512, kFRG = 32;
+template <int RPT = 0>
 __global__ __launch_bounds__(256) void tome_merge_seqnorm_fwd_kernel(
     const float* __restrict__ x, int L, int D, int64_t xs_n, int64_t xs_t, int set_start, int t,
     int r, int flags, const float* __restrict__ size_in, const int32_t* __restrict__ unm_g,
@@ -912,52 +916,72 @@ __global__ __launch_bounds__(256) void tome_merge_seqnorm_fwd_kernel(
   const float* xb = x + (int64_t)n * xs_n + col;
   float* ob = out + (int64_t)n * os_n + col;
   float part[2][8] = {};
-  if (cok)
+  // the merge of output row o into v (tome_merge_fwd_kernel's arithmetic), v holding its
+  // primary row on entry; then its store and LN sums
+  auto merge_row = [&](int o, float* v) {
+    const int jr = m_j[o];
+    if (jr != -2) {
+      const float sp = m_sp[o];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] * sp;
+      const int cnt = m_cnt[o];
+      if (cnt <= kMergeSeg) {
+        for (int k = 0; k < cnt; ++k) {
+          float w[8];
+          Vec<float>::load(xb + (int64_t)m_list[o][k] * xs_t, w);
+          Vec<float>::load(xb + (int64_t)m_list[o][k] * xs_t + 4, w + 4);
+          const float ss = m_ss[o][k];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = v[e] + w[e] * ss;
+        }
+      } else {
+        for (int i = 0; i < r; ++i) {
+          if (s_dst[i] != jr) continue;
+          const int st = 2 * s_src[i];
+          const float ss = (sb && !plain) ? sb[st] : 1.f;
+          float w[8];
+          Vec<float>::load(xb + (int64_t)(set_start + st) * xs_t, w);
+          Vec<float>::load(xb + (int64_t)(set_start + st) * xs_t + 4, w + 4);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = v[e] + w[e] * ss;
+        }
+      }
+      if (!plain) {
+        const float S = m_S[o];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = __fdiv_rn(v[e], S);
+      }
+    }
+    Vec<float>::store(ob + (int64_t)o * os_t, v);
+    Vec<float>::store(ob + (int64_t)o * os_t + 4, v + 4);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      part[0][e] += v[e];
+      part[1][e] = __builtin_fmaf(v[e], v[e], part[1][e]);
+    }
+  };
+  constexpr int RR = RPT > 0 ? RPT : 1;
+  [[maybe_unused]] float rv[RR][8];
+  if constexpr (RPT > 0) {
+    if (cok) {
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        const int o = min(rg + j * kFRG, Lout - 1);
+        Vec<float>::load(xb + (int64_t)m_prim[o] * xs_t, rv[j]);
+        Vec<float>::load(xb + (int64_t)m_prim[o] * xs_t + 4, rv[j] + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < RPT; ++j)
+        if (rg + j * kFRG < Lout) merge_row(rg + j * kFRG, rv[j]);
+    }
+  } else if (cok) {
     for (int o = rg; o < Lout; o += kFRG) {
       float v[8];
       Vec<float>::load(xb + (int64_t)m_prim[o] * xs_t, v);
       Vec<float>::load(xb + (int64_t)m_prim[o] * xs_t + 4, v + 4);
-      const int jr = m_j[o];
-      if (jr != -2) {
-        const float sp = m_sp[o];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = v[e] * sp;
-        const int cnt = m_cnt[o];
-        if (cnt <= kMergeSeg) {
-          for (int k = 0; k < cnt; ++k) {
-            float w[8];
-            Vec<float>::load(xb + (int64_t)m_list[o][k] * xs_t, w);
-            Vec<float>::load(xb + (int64_t)m_list[o][k] * xs_t + 4, w + 4);
-            const float ss = m_ss[o][k];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = v[e] + w[e] * ss;
-          }
-        } else {
-          for (int i = 0; i < r; ++i) {
-            if (s_dst[i] != jr) continue;
-            const int st = 2 * s_src[i];
-            const float ss = (sb && !plain) ? sb[st] : 1.f;
-            float w[8];
-            Vec<float>::load(xb + (int64_t)(set_start + st) * xs_t, w);
-            Vec<float>::load(xb + (int64_t)(set_start + st) * xs_t + 4, w + 4);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = v[e] + w[e] * ss;
-          }
-        }
-        if (!plain) {
-          const float S = m_S[o];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = __fdiv_rn(v[e], S);
-        }
-      }
-      Vec<float>::store(ob + (int64_t)o * os_t, v);
-      Vec<float>::store(ob + (int64_t)o * os_t + 4, v + 4);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        part[0][e] += v[e];
-        part[1][e] = __builtin_fmaf(v[e], v[e], part[1][e]);
-      }
+      merge_row(o, v);
     }
+  }
 #pragma unroll
   for (int vv = 0; vv < 2; ++vv)
 #pragma unroll
@@ -990,10 +1014,16 @@ __global__ __launch_bounds__(256) void tome_merge_seqnorm_fwd_kernel(
     add[e] = s_add[cv * 8 + e];
   }
   bf16_t* yb = y + (int64_t)n * ys_n + col;
-  for (int o = rg; o < Lout; o += kFRG) {
+#pragma unroll(RPT > 0 ? RPT : 1)
+  for (int j = 0, o = rg; o < Lout && (RPT == 0 || j < RPT); ++j, o += kFRG) {
     float f[8];
-    Vec<float>::load(ob + (int64_t)o * os_t, f);
-    Vec<float>::load(ob + (int64_t)o * os_t + 4, f + 4);
+    if constexpr (RPT > 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = rv[j][e];
+    } else {
+      Vec<float>::load(ob + (int64_t)o * os_t, f);
+      Vec<float>::load(ob + (int64_t)o * os_t + 4, f + 4);
+    }
     uint32_t wds[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1026,10 +1056,18 @@ extern "C" int mmt_tome_merge_seqnorm_fwd(const float* x, int n, int L, int D, i
                     y_s_t % 8 == 0 && y_s_n % 8 == 0,
                 "mmt_tome_merge_seqnorm_fwd: strides must be multiples of 8");
   dim3 grid(n, (D + 63) / 64);
-  hipLaunchKernelGGL(tome_merge_seqnorm_fwd_kernel, grid, dim3(256), 0, as_stream(stream), x, L, D,
-                     x_s_n, x_s_t, set_start, t, r, flags, size_in, unm_idx, src_idx, dst_idx,
-                     x_out, o_s_n, o_s_t, size_out, pos_map, gamma, beta, eps, (bf16_t*)y, y_s_n,
-                     y_s_t, mean, rstd);
+  const int Lo = L - r;
+  static const bool rpt_on = !getenv("MMT_SNB_RPT") || atoi(getenv("MMT_SNB_RPT")) != 0;
+  const int rpt = !rpt_on ? 0 : Lo <= 128 ? 4 : Lo <= 192 ? 6 : Lo <= 256 ? 8 : Lo <= 320 ? 10 : 0;
+#define TMS(R) hipLaunchKernelGGL((tome_merge_seqnorm_fwd_kernel<R>), grid, dim3(256), 0, as_stream(stream), ARGS_)
+#define ARGS_ x, L, D, x_s_n, x_s_t, set_start, t, r, flags, size_in, unm_idx, src_idx, dst_idx, x_out, o_s_n, o_s_t, size_out, pos_map, gamma, beta, eps, (bf16_t*)y, y_s_n, y_s_t, mean, rstd
+  if (rpt == 4) TMS(4);
+  else if (rpt == 6) TMS(6);
+  else if (rpt == 8) TMS(8);
+  else if (rpt == 10) TMS(10);
+  else TMS(0);
+#undef ARGS_
+#undef TMS
   MMT_CHECK_LAUNCH("mmt_tome_merge_seqnorm_fwd");
   return MMT_OK;
 }

@@ -75,23 +75,27 @@ class DDPStep:
     zero grads -> forward -> backward -> gradient all-reduce -> fused AdamW -> step counter.
 
     * world size 1: the whole step is ONE HIP graph (no host work between kernels);
-    * world size N > 1 with stages S > 1: the backward runs as S block-range stages
-      (Octo.backward_stage; the heads and last blocks first). After stage k the flat-gradient
-      region it finalised (Octo.grad_regions) is all-reduced asynchronously on the collective
-      stream while the later stages compute; AdamW (its own graph) waits for all of them, so only
-      the last region (first blocks + stem/embeddings) is exposed;
+    * world size N > 1: the backward runs as S block-range stages (Octo.backward_stage /
+      stage_bounds; the heads and last blocks first; by default "auto": ~24 MB gradient regions
+      from the top and a last stage of block 0 alone). After stage k the flat-gradient region it
+      finalised (Octo.grad_regions) is all-reduced asynchronously on the collective stream while
+      the later stages compute; AdamW (its own graph) waits for all of them, so only the last
+      region (block 0 + the tokenizers / stem, exposed_bytes) is all-reduced with nothing to
+      hide behind;
     * S = 1: one forward/backward graph, then a blocking bucketed all-reduce (GradAllReducer);
     * use_graph False: the same schedules launched eagerly (the overlap still applies).
     The 1/N average is AdamW's grad_scale (reducer.grad_scale)."""
 
     def __init__(self, model, state, txt, img, act, reducer: GradAllReducer | None = None,
-                 stages: int = 3, use_graph: bool = True):
+                 stages="auto", use_graph: bool = True):
         self.model, self.state = model, state
         self.txt, self.img, self.act = txt, img, act
         self.reducer = reducer
         self.distributed = reducer is not None and reducer.world_size > 1
-        self.S = max(1, min(stages, model.cfg.num_blocks)) if self.distributed else 1
-        self.regions = model.grad_regions(self.S) if self.S > 1 else None
+        # the backward's stage split (Octo.stage_bounds: an int, a list or "auto[:MB]")
+        self.bounds = model.stage_bounds(stages) if self.distributed else [model.cfg.num_blocks, 0]
+        self.S = len(self.bounds) - 1
+        self.regions = model.grad_regions(self.bounds) if self.S > 1 else None
         self.use_graph = use_graph
         if self.distributed and getattr(state.allreduce, "grad_scale", 1.0) != reducer.grad_scale:
             # the 1/N average lives in AdamW's grad_scale (state.allreduce): a reducer given only
@@ -119,10 +123,18 @@ class DDPStep:
                                                         s.sample_offset)
             self.loss_buf.copy_(loss)
             self._st["st"] = st
-        m.backward_stage(self._st["st"], k, self.S)
+        m.backward_stage(self._st["st"], k, self.bounds)
 
     def _opt(self):
         self.state.apply_gradients()
+
+    @property
+    def exposed_bytes(self) -> int:
+        """fp32 gradient bytes all-reduced after the backward's last stage (not overlapped)."""
+        if not self.distributed:
+            return 0
+        lo, hi = self.regions[-1] if self.regions else (0, self.model.store.n)
+        return 4 * (hi - lo)
 
     def _reduce_async(self, k):
         lo, hi = self.regions[k]

@@ -301,17 +301,48 @@ class Octo:
         return loss, st
 
     # ------------------------------------------------------------------ staged backward
-    def _stage_bounds(self, n_stages: int) -> List[int]:
-        nb = self.cfg.num_blocks
-        return [nb * (n_stages - i) // n_stages for i in range(n_stages + 1)]  # nb .. 0
+    def _block_offset(self, j: int) -> int:
+        """Flat index of block j's first parameter (store.n for j = num_blocks)."""
+        if j >= self.cfg.num_blocks:
+            return self.store.n
+        return self.store.by_name[f"StackedEncoder1DBlock_0/Block_{j}/LayerNorm_0/scale"].offset
 
-    def grad_regions(self, n_stages: int) -> List[tuple]:
+    def stage_bounds(self, stages) -> List[int]:
+        """Block boundaries nb = b[0] > b[1] > ... > b[S] = 0 of a backward split into S stages
+        (stage i runs blocks [b[i+1], b[i]); stage 0 also the heads, the last stage the tokens).
+        `stages`: an int S (blocks split evenly), an explicit list, or "auto[:MB]": gradient
+        regions of ~MB megabytes (default 24) from the top, and a last stage of block 0 alone, so
+        the region all-reduced after the backward ends (block 0 and everything declared before
+        it: the tokenizers, the stem) is the smallest possible."""
+        nb = self.cfg.num_blocks
+        if isinstance(stages, (list, tuple)):
+            return list(stages)
+        if isinstance(stages, str):
+            mb = float(stages.split(":", 1)[1]) if ":" in stages else 24.0
+            target = mb * (1 << 20)
+            bounds, acc = [nb], 0.0
+            for j in range(nb - 1, 0, -1):
+                acc += 4.0 * (self._block_offset(j + 1) - self._block_offset(j))
+                if acc >= target:
+                    bounds.append(j)
+                    acc = 0.0
+            if nb > 1 and bounds[-1] != 1:
+                bounds.append(1)
+            bounds.append(0)
+            return bounds
+        n = max(1, min(int(stages), nb))
+        return [nb * (n - i) // n for i in range(n + 1)]  # nb .. 0
+
+    def _stage_bounds(self, n_stages) -> List[int]:
+        return self.stage_bounds(n_stages)
+
+    def grad_regions(self, stages) -> List[tuple]:
         """Flat-gradient index ranges that are final after each backward stage (stage 0: the
         heads and the last blocks, declared last in the store; the last stage: the first blocks
-        and everything declared before them)."""
-        b = self._stage_bounds(n_stages)
-        off = [self.store.by_name[f"StackedEncoder1DBlock_0/Block_{j}/LayerNorm_0/scale"].offset
-               if j < self.cfg.num_blocks else self.store.n for j in b]
+        and everything declared before them). `stages` as in stage_bounds."""
+        b = self.stage_bounds(stages)
+        n_stages = len(b) - 1
+        off = [self._block_offset(j) for j in b]
         regions = []
         for i in range(n_stages):
             hi = self.store.n if i == 0 else off[i]
@@ -319,10 +350,11 @@ class Octo:
             regions.append((lo, hi))
         return regions
 
-    def backward_stage(self, st: Dict, stage: int, n_stages: int):
-        """Stage `stage` of a backward split into n_stages block ranges (the heads run in stage
-        0, the stem / embeddings in the last): backward(st) == all stages in order."""
-        b = self._stage_bounds(n_stages)
+    def backward_stage(self, st: Dict, stage: int, stages):
+        """Stage `stage` of a backward split as stage_bounds(stages) (the heads run in stage 0,
+        the stem / embeddings in the last): backward(st) == all stages in order."""
+        b = self.stage_bounds(stages)
+        n_stages = len(b) - 1
         with wgrad_overlap(self.device):  # dW products beside the critical path; joined here
             if stage == 0:
                 st["_dx"] = self._backward_head(st)

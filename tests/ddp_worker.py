@@ -1,8 +1,9 @@
 """One rank of the 2-process data-parallel GPU test (tests/test_ddp_gpu.py); both ranks share the
 one GPU and talk over gloo. Not collected by pytest (no test_ prefix).
 
-Checks, on the bench's own step (distributed.DDPStep: staged backward graphs with each stage's
-gradient region all-reduced asynchronously):
+Checks, on the bench's own step (distributed.DDPStep: staged backward graphs — one per block
+here, the "auto" plan with a tiny region target — with each stage's gradient region all-reduced
+asynchronously):
   async_vs_sync  : the overlapped all-reduce result equals the one-piece backward + blocking
                    bucketed all-reduce from the same parameters and RNG state;
   shards_vs_full : (rank 0) the all-reduced sum / 2 equals ONE process's gradient of the whole
@@ -52,7 +53,10 @@ def main():
     img, act = img_all[sl].contiguous(), act_all[sl].contiguous()
     red = GradAllReducer(N, bucket_bytes=1 << 20)
     state = create_octo_train_state(model, seed=11, allreduce=red, sample_offset=di.rank * B)
-    step = DDPStep(model, state, None, img, act, red, stages=3, use_graph=True).build(warm=1)
+    # the bench's default plan ("auto": byte-sized gradient regions, block 0 alone last); a tiny
+    # region target gives every block its own stage and region here
+    step = DDPStep(model, state, None, img, act, red, stages="auto:0.001", use_graph=True).build(warm=1)
+    assert step.bounds == [4, 3, 2, 1, 0], step.bounds
     step()                                   # a real step, then freeze params + RNG
     torch.cuda.synchronize()
     P = model.store.flat.clone()
@@ -75,7 +79,8 @@ def main():
     red(model.store.flat_grad)               # blocking bucketed all-reduce
     torch.cuda.synchronize()
     g_sync = model.store.flat_grad.clone()
-    rep = dict(rank=di.rank, async_vs_sync=rel_by_tensor(model, g_async, g_sync))
+    rep = dict(rank=di.rank, async_vs_sync=rel_by_tensor(model, g_async, g_sync),
+               stages=step.S, exposed_bytes=step.exposed_bytes)
     dist.barrier()
     if di.rank == 0:
         restore()

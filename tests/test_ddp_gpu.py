@@ -5,8 +5,8 @@
   per-sample random streams are keyed by the global sample index, and the gradients each sample
   contributes are bitwise the same, so only fp32 summation order differs).
 * test_two_rank_staged_allreduce: two processes on the one GPU over gloo run the bench's step
-  (distributed.DDPStep: backward in 3 block-range graphs, each finished gradient region
-  all-reduced asynchronously) — the result equals the one-piece backward + blocking all-reduce,
+  (distributed.DDPStep: the backward in one graph per block — the "auto" stage plan — each
+  finished gradient region all-reduced asynchronously) — the result equals the one-piece backward + blocking all-reduce,
   and sum / 2 equals one process's gradient of the whole global batch (tests/ddp_worker.py).
 """
 import json

@@ -203,3 +203,28 @@ def test_continuous_head_oracle_gradient():
         zp = z.copy(); zp[i] += eps
         num[i] = (HR.continuous(zp, y, 5.0)[1] - loss) / eps
     np.testing.assert_allclose(dz, num, rtol=1e-4, atol=1e-6)
+
+
+def test_ddp_stage_plan_regions_cover_the_store():
+    """distributed.DDPStep's backward split (Octo.stage_bounds / grad_regions) on the CPU-built
+    model: "auto[:MB]" gives byte-sized regions from the top and block 0 alone in the last stage;
+    for every plan the regions tile [0, n) without overlap, stage 0 holds the heads (the top of
+    the store) and the last stage everything below block 1."""
+    import torch
+    from multi_modal_transformers_tokenmerge_amd.models.octo.config import get_config
+    from multi_modal_transformers_tokenmerge_amd.models.octo.octo import Octo
+    m = Octo(get_config("octo-small-tome16"), torch.device("cpu"), seed=0)
+    nb = m.cfg.num_blocks
+    for plan in ("auto", "auto:12", "auto:0.001", 1, 3, nb, [nb, 6, 1, 0]):
+        b = m.stage_bounds(plan)
+        assert b[0] == nb and b[-1] == 0 and all(x > y for x, y in zip(b, b[1:])), (plan, b)
+        regs = m.grad_regions(b)
+        assert regs[0][1] == m.store.n and regs[-1][0] == 0
+        assert all(regs[i][0] == regs[i + 1][1] for i in range(len(regs) - 1))
+        if isinstance(plan, str):
+            assert b[-2] == 1  # block 0 alone in the last stage
+    b = m.stage_bounds("auto")
+    exposed = 4 * (m.grad_regions(b)[-1][1] - m.grad_regions(b)[-1][0])
+    even = 4 * (m.grad_regions(3)[-1][1] - m.grad_regions(3)[-1][0])
+    assert exposed < even / 3, (exposed, even)
+    assert m.stage_bounds("auto:0.001") == list(range(nb, -1, -1))
