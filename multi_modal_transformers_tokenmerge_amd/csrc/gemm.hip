@@ -1705,7 +1705,19 @@ __global__ void splitk_epilogue_kernel(const float* __restrict__ ws, int split, 
     const float* p = ws + (int64_t)gr * N + gc;
     float v[8];
     ldw<8>(p, v);
-    for (int k = 1; k < split; ++k) {
+    // slabs 4 at a time: their loads in flight together (a one-slab loop waited a full L2 / MALL
+    // round trip per slab); the adds keep the slab order
+    int k = 1;
+    for (; k + 4 <= split; k += 4) {
+      float t[4][8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ldw<8>(p + (k + j) * slab, t[j]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += t[j][e];
+    }
+    for (; k < split; ++k) {
       float t[8];
       ldw<8>(p + k * slab, t);
 #pragma unroll
