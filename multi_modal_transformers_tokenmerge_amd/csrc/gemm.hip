@@ -1690,6 +1690,149 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
   }
 }
 
+// Weight-gradient TN split-K with a deep DMA ring (the default TN path; gemm_tn_dma_kernel with
+// MMT_TN_RING=0). The 256 x 192 tile of gemm_tn_dma_kernel streams both operands from HBM (dY and
+// X rows of the workgroup's K chunk, each slice shared by only 2 / 6 tiles through L2), and with
+// 56 KB per 64-deep K-step only two stages fit in LDS: one K-step in flight against an HBM
+// latency of ~2-3 us under load made every K-step 1.9 us (0.73 us of MFMAs; 29 GB/s per CU).
+// Here the K-steps are 32 deep (28 KB: [32][256] + [32][192] k-row images, the same chunk
+// swizzles and transposed fragment reads) in an NSR-stage ring, NSR - 1 K-steps (112 KB at
+// NSR = 5) in flight: the DMA of K-step s + NSR - 1 is issued right after the barrier of K-step s
+// into the stage K-step s - 1 used. Pieces per K-step: A 16 (two k-rows each), B 12 (1 KB of the
+// [32][192] image): waves 0-3 issue 2 + 2, waves 4-7 2 + 1 (wave-uniform vmcnt immediates).
+template <int NSR>
+__global__ __launch_bounds__(TN_NT, 1) void gemm_tn_ring_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
+    int64_t ldb, float* __restrict__ slab, int split_k, int k_chunk, int tiles_n) {
+  constexpr int BK = 32;
+  constexpr int A_ROWB = TN_BM * 2, B_ROWB = TN_BN * 2;            // bytes per k-row
+  constexpr int A_BYTES = BK * A_ROWB, B_BYTES = BK * B_ROWB, STAGE = A_BYTES + B_BYTES;
+  static_assert(NSR >= 2 && NSR * STAGE <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[NSR * STAGE];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1, hl = lane >> 5;
+  const int tiles = ((M + TN_BM - 1) / TN_BM) * tiles_n;
+  const int wi = xcd_remap(blockIdx.x, gridDim.x);
+  const int z = wi / tiles, t = wi - z * tiles;
+  const int tm = t / tiles_n;
+  const int m0 = tm * TN_BM, n0 = (t - tm * tiles_n) * TN_BN;
+  const int kbeg = z * k_chunk, kend = min(K, kbeg + k_chunk);
+  const int nk = max(0, (kend - kbeg + BK - 1) / BK);
+  auto swA = [](int r) { return 4 * (r & 3); };
+  auto swB = [](int r) { return 2 * (r & 3); };
+  const bool wide = wave < 4;  // 2 B pieces per K-step (else 1)
+  int voa[2], vob[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int j = 2 * wave + p, row = 2 * j + (lane >> 5), c = (lane & 31) ^ swA(row);
+    voa[p] = row * (int)(lda * 2) + c * 16;
+  }
+  const int jb0 = wide ? 2 * wave : 8 + (wave - 4);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int j = jb0 + p, e = j * 64 + lane, row = e / 24, c = (e % 24) ^ swB(row);
+    vob[p] = row * (int)(ldb * 2) + c * 16;
+  }
+  auto piece_a = [&](int kt, int p) {
+    const int k0 = kbeg + kt * BK;
+    dma16_asm(A + (int64_t)k0 * lda + m0, ((int64_t)(K - k0) * lda - m0) * 2,
+              smem + (kt % NSR) * STAGE + (2 * wave + p) * 1024, voa[p]);
+  };
+  auto piece_b = [&](int kt, int p) {
+    const int k0 = kbeg + kt * BK;
+    dma16_asm(B + (int64_t)k0 * ldb + n0, ((int64_t)(K - k0) * ldb - n0) * 2,
+              smem + (kt % NSR) * STAGE + A_BYTES + (jb0 + p) * 1024, vob[p]);
+  };
+  auto issue = [&](int kt) {
+    piece_a(kt, 0);
+    piece_a(kt, 1);
+    piece_b(kt, 0);
+    if (wide) piece_b(kt, 1);
+  };
+  // wait until at most n younger K-steps' pieces are in flight (n <= NSR - 2)
+  auto wait_younger = [&](int n) {
+    if (wide) {
+      if (n >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else if (n == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (n >= 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+      else if (n == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (n == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+  static_assert(NSR - 2 <= 3, "wait_younger covers up to 3 younger K-steps");
+
+  floatx16 acc[2][3];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[a][b][q] = 0.f;
+  const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g16 = lane >> 4;
+  auto frag = [&](const char* S, int rowb, int rbase, int ks) {
+    const int col = rbase + 16 * (g16 & 1) + 4 * p4;
+    const int k1 = ks * 16 + 8 * hl + q4;
+    const int cofs = (col & 7) * 2;
+    const int s1 = rowb == A_ROWB ? swA(k1) : swB(k1);
+    const int s2 = rowb == A_ROWB ? swA(k1 + 4) : swB(k1 + 4);
+    const short4v v1 = tr_read(reinterpret_cast<const bf16_t*>(
+        S + k1 * rowb + ((((col >> 3) ^ s1)) << 4) + cofs));
+    const short4v v2 = tr_read(reinterpret_cast<const bf16_t*>(
+        S + (k1 + 4) * rowb + ((((col >> 3) ^ s2)) << 4) + cofs));
+    short __attribute__((ext_vector_type(8))) v = {v1[0], v1[1], v1[2], v1[3],
+                                                   v2[0], v2[1], v2[2], v2[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
+#pragma unroll
+  for (int q = 0; q < NSR - 1; ++q)
+    if (q < nk) issue(q);
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_younger(min(NSR - 2, nk - 1 - kt));
+    asm volatile("s_barrier" ::: "memory");  // K-step kt landed for every wave; kt - 1's stage free
+    if (kt + NSR - 1 < nk) issue(kt + NSR - 1);
+    const char* As = smem + (kt % NSR) * STAGE;
+    const char* Bs = As + A_BYTES;
+    bf16x8 af[2][2], bfr[2][3];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) af[0][a] = frag(As, A_ROWB, wm * 64 + a * 32, 0);
+#pragma unroll
+    for (int b = 0; b < 3; ++b) bfr[0][b] = frag(Bs, B_ROWB, wn * 96 + b * 32, 0);
+#pragma unroll
+    for (int a = 0; a < 2; ++a) af[1][a] = frag(As, A_ROWB, wm * 64 + a * 32, 1);
+#pragma unroll
+    for (int b = 0; b < 3; ++b) bfr[1][b] = frag(Bs, B_ROWB, wn * 96 + b * 32, 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b)  // operands swapped: the accumulator holds C^T
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[ks][b], af[ks][a], acc[a][b], 0, 0, 0);
+  }
+  float* out = slab + (int64_t)z * M * N;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int gr = m0 + wm * 64 + a * 32 + (lane & 31);
+    if (gr >= M) continue;
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int gc = n0 + wn * 96 + b * 32 + 8 * g + 4 * hl;
+        if (gc >= N) continue;
+        *reinterpret_cast<float4*>(out + (int64_t)gr * N + gc) =
+            make_float4(acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2],
+                        acc[a][b][4 * g + 3]);
+      }
+  }
+}
+
 // Split-K combine: v = sum_s slab[s][m][n] (fp32), then the GEMM epilogue, 8 columns per thread.
 template <int OUT>
 __global__ void splitk_epilogue_kernel(const float* __restrict__ ws, int split, int M, int N,
@@ -1728,6 +1871,247 @@ __global__ void splitk_epilogue_kernel(const float* __restrict__ ws, int split, 
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Warp-specialised wide NT kernel (the bf16-output forward / gated products of the step: QKV,
+// MLP up with bias + relu + dropout + relu_bits, the gated MLP input gradient with column sums).
+// Why: in gemm_nt256_kernel every wave both issues the K-step DMA and stores its epilogue, and
+// vmcnt retires loads and stores in one in-order counter, so the DMA wait after a tile's epilogue
+// also waits for that epilogue's stores to be acknowledged (with every CU writing at once: K-steps
+// 1.9 us instead of 1.04; the stores, not the MFMAs, set the pace of the K = 384 products). Here
+// the roles are split by wave:
+//  * waves 4-7 (loaders) issue every DMA piece (buffer_load ... lds, inline asm) and never store:
+//    their vmcnt counts DMA only; three LDS stages, two K-steps in flight;
+//  * waves 0-3 (one per SIMD) run the MFMAs and the epilogue; their stores are never waited for.
+//    One s_barrier per K-step (all 8 waves): the loaders arrive after their K-step s DMA landed,
+//    the compute waves after they finished reading K-step s - 1's stage (which the loaders refill
+//    with K-step s + 2 right after the barrier).
+// Tile 256 (M) x 128 (N): compute wave wm owns rows 64 wm .. + 63 and all 128 columns, with the
+// per-wave fragment geometry, B-row permutation, swizzles and epilogue of nt256's BN = 256 wave
+// (16x16x32 MFMA, operands swapped, lane = 4 rows x 32 columns in runs of 8): its outputs, its
+// relu_bits / gate_bits words and its column sums are laid out exactly as nt256's (a 256-wide
+// nt256 tile = two adjacent tiles here), and the column-sum slab is summed over the same 4 waves
+// in the same order (bit-identical results).
+// Requires !transA, transB, K % 64 == 0, N % 128 == 0, bf16 output, N <= WS_BIAS with a bias.
+constexpr int WS_NT = 512, WS_BIAS = 2048;
+template <bool CS, bool GBITS>
+__global__ __launch_bounds__(WS_NT, 1) void gemm_ntws_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
+    int64_t ldb, bf16_t* __restrict__ C, int64_t ldc, int tiles_n, int n_tiles, Epi epi) {
+  constexpr int W = 128, NF = 8, Q = 32, NS = 3;
+  constexpr int A_BYTES = 256 * 128, STAGE = A_BYTES + W * 128;  // 48 KB
+  constexpr int PIECES = STAGE / 1024, PL = PIECES / 4;          // 48 pieces, 12 per loader
+  constexpr int CS_FLOATS = CS ? 4 * W : 0;
+  // ONE LDS object (a second one makes the compiler drain vmcnt before LDS reads)
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + 4 * (WS_BIAS + CS_FLOATS)];
+  float* const s_bias = reinterpret_cast<float*>(smem + NS * STAGE);
+  float (*const s_cs)[W] = reinterpret_cast<float (*)[W]>(s_bias + WS_BIAS);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nk = K / 64;
+  int first, stride, limit = n_tiles;
+  if ((gridDim.x & 7) == 0) {  // each XCD a contiguous eighth of the row-panel-major tile list
+    const int xcd = blockIdx.x & 7;
+    first = (int)((int64_t)n_tiles * xcd / 8) + (blockIdx.x >> 3);
+    limit = (int)((int64_t)n_tiles * (xcd + 1) / 8);
+    stride = gridDim.x >> 3;
+  } else {
+    first = xcd_remap(blockIdx.x, gridDim.x);
+    stride = gridDim.x;
+  }
+  const int n_mine = first < limit ? (limit - first + stride - 1) / stride : 0;
+  const int S = n_mine * nk;
+  if (S == 0) return;  // workgroup-uniform
+  auto fA = [](int r) { return r & 6; };
+  auto fB = [](int r) { return (r & 2) | (((r >> 3) & 1) << 2); };
+
+  if (wave >= 4) {
+    // ------------------------------------------------------------------ loader waves
+    const int lw = wave - 4;
+    // loader lw: A pieces 8 lw .. 8 lw + 7 (rows 8 j .. 8 j + 7 of the 256-row panel) and B pieces
+    // 4 lw .. 4 lw + 3 (of the 128-row panel); the lane's 16-B chunk of its row at the row's
+    // swizzle (source side; the LDS destination is lane-linear)
+    constexpr int PLA = 8, PLB = 4;
+    static_assert(PLA + PLB == PL, "pieces");
+    int voa[PLA], vob[PLB];
+#pragma unroll
+    for (int i = 0; i < PLA; ++i) {
+      const int row = 8 * (lw * PLA + i) + (lane >> 3);
+      voa[i] = row * (int)(lda * 2) + (((lane & 7) ^ fA(row)) << 4);
+    }
+#pragma unroll
+    for (int i = 0; i < PLB; ++i) {
+      const int row = 8 * (lw * PLB + i) + (lane >> 3);
+      vob[i] = row * (int)(ldb * 2) + (((lane & 7) ^ fB(row)) << 4);
+    }
+    auto issue = [&](int s) {  // K-step s of this workgroup's sequence into stage s % 3
+      const int i = s / nk, kt = s - i * nk;
+      const int tile = first + i * stride, tm = tile / tiles_n;
+      const int m0 = tm * 256, n0 = (tile - tm * tiles_n) * W, k0 = kt * 64;
+      char* S0 = smem + (s % NS) * STAGE;
+      const bf16_t* pa = A + (int64_t)m0 * lda + k0;  // rows past M read zeros (buffer range)
+      const int64_t ra = ((int64_t)(M - m0) * lda - k0) * 2;
+      const bf16_t* pb = B + (int64_t)n0 * ldb + k0;
+      const int64_t rb = ((int64_t)W * ldb - k0) * 2;
+#pragma unroll
+      for (int p = 0; p < PLA; ++p) dma16_asm(pa, ra, S0 + (lw * PLA + p) * 1024, voa[p]);
+#pragma unroll
+      for (int p = 0; p < PLB; ++p) dma16_asm(pb, rb, S0 + A_BYTES + (lw * PLB + p) * 1024, vob[p]);
+    };
+    issue(0);
+    if (S > 1) issue(1);
+    for (int s = 0; s < S; ++s) {
+      // K-step s landed (K-step s + 1's pieces, issued after it, may stay in flight)
+      if (s + 1 < S) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PL) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_barrier" ::: "memory");
+      if (s + 2 < S) issue(s + 2);  // into the stage K-step s - 1 used (read before this barrier)
+      if (CS && (s % nk) == nk - 1) asm volatile("s_barrier" ::: "memory");  // the tile's colsum sync
+    }
+    return;
+  }
+
+  // -------------------------------------------------------------------- compute waves
+  const int wm = wave;
+  if (epi.bias)  // N <= WS_BIAS (host); published by the loop's first barrier
+    for (int i = threadIdx.x; i < N; i += 256) s_bias[i] = epi.bias[i];
+  uint32_t key = 0;
+  if (epi.rng) key = stream_key(epi.rng[0], epi.rng[1], epi.drop_layer, epi.drop_site);
+  Epi rest = epi;  // dropout / residual through epilogue_w; the rest inline (nt256 order)
+  rest.alpha = 1.f;
+  rest.bias = nullptr;
+  rest.act = MMT_ACT_NONE;
+  rest.gate = nullptr;
+  rest.relu_bits = nullptr;
+  rest.gate_bits = nullptr;
+  constexpr bool RBITS = !CS && !GBITS;
+
+  const int l15 = lane & 15, lq = lane >> 4;
+  int a_off[4], a_sw[4], b_off[NF], b_sw[NF];
+#pragma unroll
+  for (int mf = 0; mf < 4; ++mf) {
+    const int r = wm * 64 + mf * 16 + l15;
+    a_off[mf] = r * 128;
+    a_sw[mf] = fA(r);
+  }
+#pragma unroll
+  for (int nf = 0; nf < NF; ++nf) {
+    const int r = 32 * (nf >> 1) + 8 * (l15 >> 2) + 4 * (nf & 1) + (l15 & 3);
+    b_off[nf] = A_BYTES + r * 128;
+    b_sw[nf] = fB(r);
+  }
+  typedef float floatx4 __attribute__((ext_vector_type(4)));
+  floatx4 acc[4][NF];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < NF; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int st) {
+    const char* S0 = smem + st * STAGE;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = 4 * h + lq;
+      bf16x8 af[4], bfr[NF];
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf)
+        af[mf] = *reinterpret_cast<const bf16x8*>(S0 + a_off[mf] + ((c ^ a_sw[mf]) << 4));
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf)
+        bfr[nf] = *reinterpret_cast<const bf16x8*>(S0 + b_off[nf] + ((c ^ b_sw[nf]) << 4));
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf)
+          acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nf], af[mf], acc[mf][nf], 0, 0, 0);
+    }
+  };
+
+  // epilogue of `tile` (nt256's 256-wide epilogue for one wave, wn = 0, tile width 128); gbw: the
+  // tile's gate_bits word, loaded at the tile's first K-step
+  auto epilogue = [&](int tile, const uint4& gbw) {
+    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    const int gc0 = tn * W + 8 * lq;
+    float cs[CS ? Q : 1];
+    if constexpr (CS)
+#pragma unroll
+      for (int j = 0; j < Q; ++j) cs[j] = 0.f;
+    const int64_t bidx = (int64_t)(tm * 64 + wm * 16 + l15) * (N / 32) + (tn * 4 + lq);
+    uint32_t rbw[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf) {
+      const int gr = tm * 256 + wm * 64 + mf * 16 + l15;
+      if (gr < M) {
+#pragma unroll
+        for (int c8 = 0; c8 < Q / 8; ++c8) {
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = acc[mf][(8 * c8 + e) >> 2][e & 3] * epi.alpha;
+          const int gc = gc0 + 32 * c8;
+          if (epi.bias) {
+            const float4 b0 = *reinterpret_cast<const float4*>(s_bias + gc);
+            const float4 b1 = *reinterpret_cast<const float4*>(s_bias + gc + 4);
+            v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+            v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+          }
+          if (epi.act == MMT_ACT_RELU)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+          if (GBITS) {
+            const uint32_t w = (mf == 0 ? gbw.x : mf == 1 ? gbw.y : mf == 2 ? gbw.z : gbw.w) >> (8 * c8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= ((w >> e) & 1u) ? epi.gate_scale : 0.f;
+          }
+          epilogue_w<8>(rest, key, N, gr, gc, v);
+          if (RBITS && epi.relu_bits)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) rbw[mf] |= (v[e] > 0.f ? 1u : 0u) << (8 * c8 + e);
+          if constexpr (CS)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cs[8 * c8 + e] += __uint_as_float((uint32_t)f2bf(v[e]) << 16);
+          store_w<0, 8>(C, (int64_t)gr * ldc + gc, 0.f, v);
+        }
+      }
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf) acc[mf][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (RBITS && epi.relu_bits)
+      reinterpret_cast<uint4*>(epi.relu_bits)[bidx] = make_uint4(rbw[0], rbw[1], rbw[2], rbw[3]);
+    if constexpr (CS) {
+#pragma unroll
+      for (int j = 0; j < Q; ++j) {  // sum over the 16 row lanes of each DPP row (as nt256)
+        float x = cs[j];
+        x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xf, 0xf, false));
+        x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xf, 0xf, false));
+        x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xf, 0xf, false));
+        x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xf, 0xf, false));
+        cs[j] = x;
+      }
+      if (l15 == 0)
+#pragma unroll
+        for (int j = 0; j < Q; ++j) s_cs[wm][32 * (j >> 3) + 8 * lq + (j & 7)] = cs[j];
+      // the loaders meet this barrier after the tile's last K-step too (LDS only: no vmcnt)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (threadIdx.x < W)
+        epi.colsum[(int64_t)tm * N + tn * W + threadIdx.x] =
+            s_cs[0][threadIdx.x] + s_cs[1][threadIdx.x] + s_cs[2][threadIdx.x] + s_cs[3][threadIdx.x];
+    }
+  };
+
+  uint4 gbw = make_uint4(0u, 0u, 0u, 0u);
+  for (int s = 0; s < S; ++s) {
+    const int i = s / nk, kt = s - i * nk;
+    if (GBITS && kt == 0) {  // the tile's gate word, needed at its epilogue
+      const int tile = first + i * stride, tm = tile / tiles_n, tn = tile - tm * tiles_n;
+      gbw = reinterpret_cast<const uint4*>(epi.gate_bits)[(int64_t)(tm * 64 + wm * 16 + l15) * (N / 32) +
+                                                          (tn * 4 + lq)];
+    }
+    // this wave's reads of K-step s - 1 are consumed (complete); LDS writes (bias) published
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    compute(s % NS);
+    if (kt == nk - 1) epilogue(first + i * stride, gbw);
+  }
+}
 
 // ---------------------------------------------------------------------------------------------
 // FP8 (OCP e4m3) forward GEMM for the fp8 weight path (BASELINE configs[4]): C = epilogue(
@@ -2080,8 +2464,32 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     MMT_CHECK_LAUNCH("mmt_gemm(ntw)");
     return MMT_OK;
   }
+  // Warp-specialised wide NT kernel: bf16 outputs of N % 128 == 0 with the nt256 epilogues that
+  // the step uses (bias, relu, dropout, relu_bits, gate_bits, colsum, bf16 / fp32 residual).
+  // MMT_NTWS: 0 off, 1 (default) where nt256 would take 192-wide tiles (N % 256 != 0: the QKV
+  // projection, 209 vs 247 us at B = 512), 2 everywhere (the 256-wide nt256 tiles measured
+  // faster: MLP up 284 vs 299 us, gated dX 252 vs 289; tools/ntws_bench.py)
+  static const int g_ntws = getenv("MMT_NTWS") ? atoi(getenv("MMT_NTWS")) : 1;
+  if (g_ntws && (g_ntws == 2 || N % 256 != 0) && g_variant < 0 && !transA && transB && batch == 1 &&
+      out_kind == 0 && final_kind == 0 &&
+      K % 64 == 0 && N % 128 == 0 && N >= 1024 && M >= 4096 && !epi.gate && epi.beta == 0.f &&
+      (!epi.bias || N <= WS_BIAS) && !(epi.colsum && epi.relu_bits)) {
+    const int tn = N / 128, n_tiles = ((M + 255) / 256) * tn;
+    int grid = std::min(n_tiles, cu_count());
+    if (grid > 8) grid &= ~7;
+#define GWS(CSV, GBV)                                                                                   \
+  hipLaunchKernelGGL((gemm_ntws_kernel<CSV, GBV>), dim3(grid), dim3(WS_NT), 0, s, M, N, K,              \
+                     (const bf16_t*)A, lda, (const bf16_t*)B, ldb, (bf16_t*)C, ldc, tn, n_tiles, epi)
+    if (epi.colsum && epi.gate_bits) GWS(true, true);
+    else if (epi.colsum) GWS(true, false);
+    else if (epi.gate_bits) GWS(false, true);
+    else GWS(false, false);
+#undef GWS
+    MMT_CHECK_LAUNCH("mmt_gemm(ntws)");
+    return MMT_OK;
+  }
   // Persistent 256 x BN NT kernel (variant -1 auto, 5/6/7 force BN 256/192/128)
-  const int bn = (epi.bias && N > NT_BIAS_LDS) ? 0 : nt_bn(M, N, K, transA, transB, batch, out_kind, final_kind);
+  const int bn =(epi.bias && N > NT_BIAS_LDS) ? 0 : nt_bn(M, N, K, transA, transB, batch, out_kind, final_kind);
   MMT_CHECK_ARG(!(epi.relu_bits || epi.gate_bits) || (bn == 256 && final_kind == 0),
                 "mmt_gemm: relu_bits / gate_bits need the 256-wide bf16 nt path (mmt_gemm_colsum_rows)");
   if (bn) {
@@ -2161,8 +2569,18 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
   if (pipe == 3 && out_kind == 2 && transA && !transB && batch == 1 && g_tn_dma) {
     const int tn = (N + TN_BN - 1) / TN_BN;
     const int work = ((M + TN_BM - 1) / TN_BM) * tn * split_k;
-    hipLaunchKernelGGL(gemm_tn_dma_kernel, dim3(work), dim3(TN_NT), 0, s, M, N, K,
-                       (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
+    // the deep-ring kernel unless MMT_TN_RING=0 or variant 9 (the two-stage kernel, same MFMA
+    // order: bit-identical slabs)
+    static const int g_tn_ring = getenv("MMT_TN_RING") ? atoi(getenv("MMT_TN_RING")) : 5;
+    if (g_tn_ring == 5 && g_variant != 9)
+      hipLaunchKernelGGL(gemm_tn_ring_kernel<5>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
+                         (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
+    else if (g_tn_ring == 3 && g_variant != 9)
+      hipLaunchKernelGGL(gemm_tn_ring_kernel<3>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
+                         (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
+    else
+      hipLaunchKernelGGL(gemm_tn_dma_kernel, dim3(work), dim3(TN_NT), 0, s, M, N, K,
+                         (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
     MMT_CHECK_LAUNCH("mmt_gemm(tn dma)");
   } else {
 #define GL(TA, TB, OUT)                          \

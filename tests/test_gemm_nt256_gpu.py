@@ -1,6 +1,8 @@
 """GPU numerics of the persistent 256 x BN NT GEMM (gemm_nt256_kernel) for each tile width, with
 partial last row tiles, several tiles per workgroup (persistent walk) and every epilogue, against
 a torch fp32 reference of the same bf16 operands (same bars as tests/test_gemm_gpu.py)."""
+import os
+
 import pytest
 import torch
 
@@ -182,3 +184,55 @@ def test_bits_rejected_off_the_256_path(dev):
     a, w = torch.zeros((M, K), dtype=torch.bfloat16, device=dev), torch.zeros((N, K), dtype=torch.bfloat16, device=dev)
     with pytest.raises(ValueError):
         Kn.gemm(a, w, False, True, relu_bits=torch.empty((512, N // 32), dtype=torch.int32, device=dev))
+
+
+@pytest.mark.parametrize("M,N,K", [(4133, 1536, 384), (70656, 1536, 384), (9000, 1152, 384),
+                                   (5000, 1024, 1536)])
+def test_ntws_matches_nt256(dev, M, N, K):
+    """The warp-specialised wide NT kernel (gemm_ntws_kernel, the automatic choice for these bf16
+    products) against gemm_nt256_kernel forced by variant 5 / 6 (BN 256 / 192): the same MFMA
+    order per output element, so every epilogue the step uses must agree bit for bit — outputs,
+    relu_bits and the per-256-row column-sum slab."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn, _C
+    if N % 256 == 0 and os.environ.get("MMT_NTWS", "1") != "2":
+        pytest.skip("the warp-specialised kernel takes N % 256 == 0 only with MMT_NTWS=2")
+    g = torch.Generator().manual_seed(M + N + K)
+    a, w = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    bias = torch.randn(N, generator=g).to(dev)
+    rng = torch.tensor([99, 4], dtype=torch.int32, device=dev)
+    rows = -(-M // 256)
+    ref_variant = 5 if N % 256 == 0 else 6
+
+    def both(**kw):
+        bits_ = kw.pop("bits", None)
+        cs_ = kw.pop("cs", None)
+        outs = []
+        for v in (-1, ref_variant):
+            _C.call("mmt_gemm_set_variant", v)
+            try:
+                extra = {}
+                if bits_ is not None:
+                    extra["relu_bits"] = torch.full_like(bits_, -1)
+                if cs_ is not None:
+                    extra["colsum"] = torch.full((rows, N), float("nan"), device=dev)
+                o = Kn.gemm(a, w, False, True, split_k=1, **kw, **extra)
+                outs.append((o, extra))
+            finally:
+                _C.call("mmt_gemm_set_variant", -1)
+        return outs
+
+    (o1, _), (o2, _) = both()
+    assert torch.equal(o1, o2)
+    _close_bf16(o1, a.float() @ w.float().t())
+    (o1, _), (o2, _) = both(bias=bias)
+    assert torch.equal(o1, o2)
+    if N % 256 == 0 and Kn.gemm_bits_supported(M, N, K):  # relu_bits / gate_bits / colsum
+        bits = torch.empty((rows * 256, N // 32), dtype=torch.int32, device=dev)
+        (o1, e1), (o2, e2) = both(bias=bias, act=Kn.ACT_RELU, rng=rng, drop_layer=2, drop_site=2,
+                                  keep_prob=0.9, drop_row_offset=3 * M, bits=bits)
+        assert torch.equal(o1, o2)
+        assert torch.equal(e1["relu_bits"], e2["relu_bits"])  # every word written
+        gbits = e1["relu_bits"]
+        (o1, e1), (o2, e2) = both(gate_bits=gbits, gate_scale=1 / 0.9, cs=True)
+        assert torch.equal(o1, o2)
+        assert torch.equal(e1["colsum"], e2["colsum"])
