@@ -1595,7 +1595,20 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
   }
   // buffer ranges end at row K (zeros past it); the panel base moves with the K-step
   auto piece = [&](int kt, int st, int p) {
+#if MMT_TN_ABL == 1 || MMT_TN_ABL == 4  // ablation builds (tools/build_abl_tn.sh): no DMA
+    if (K > 0) return;
+#endif
+#if MMT_TN_ABL == 6  // ablation: B pieces only
+    if (p < GA) return;
+#endif
+#if MMT_TN_ABL == 7  // ablation: A pieces only
+    if (p >= GA) return;
+#endif
+#if MMT_TN_ABL == 5  // ablation: every split reads the first K chunk (L2-shared)
+    const int k0 = kt * 64;
+#else
     const int k0 = kbeg + kt * 64;
+#endif
     char* S0 = smem + st * STAGE;
     if (p < GA)
       dma16_asm(A + (int64_t)k0 * lda + m0, ((int64_t)(K - k0) * lda - m0) * 2,
@@ -1651,7 +1664,11 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int cu = ks & 1;
+#if MMT_TN_ABL == 3 || MMT_TN_ABL == 4  // ablation: fragments of k-slice 0 reused (no further reads)
+      if (ks < 3 && K < 0) {
+#else
       if (ks < 3) {
+#endif
 #pragma unroll
         for (int a = 0; a < 2; ++a) af[cu ^ 1][a] = frag(As, A_ROWB, wm * 64 + a * 32, ks + 1);
 #pragma unroll
@@ -1661,7 +1678,11 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
       for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 3; ++b)  // operands swapped: the accumulator holds C^T
+#if MMT_TN_ABL == 2  // ablation: no MFMAs (fragments kept live)
+          asm volatile("" ::"v"(bfr[cu][b]), "v"(af[cu][a]));
+#else
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[cu][b], af[cu][a], acc[a][b], 0, 0, 0);
+#endif
       // the next K-step's DMA into the other stage (free since this K-step's barrier), spread
       // over the k-slices so the SIMD partner wave keeps issuing MFMAs
       if (nxt) {
@@ -1672,149 +1693,6 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
     }
   }
   // fp32 slab z: lane (m = lane & 31, h) of block (a, b) holds row m, columns 8g + 4h + {0..3}
-  float* out = slab + (int64_t)z * M * N;
-#pragma unroll
-  for (int a = 0; a < 2; ++a) {
-    const int gr = m0 + wm * 64 + a * 32 + (lane & 31);
-    if (gr >= M) continue;
-#pragma unroll
-    for (int b = 0; b < 3; ++b)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int gc = n0 + wn * 96 + b * 32 + 8 * g + 4 * hl;
-        if (gc >= N) continue;
-        *reinterpret_cast<float4*>(out + (int64_t)gr * N + gc) =
-            make_float4(acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2],
-                        acc[a][b][4 * g + 3]);
-      }
-  }
-}
-
-// Weight-gradient TN split-K with a deep DMA ring (the default TN path; gemm_tn_dma_kernel with
-// MMT_TN_RING=0). The 256 x 192 tile of gemm_tn_dma_kernel streams both operands from HBM (dY and
-// X rows of the workgroup's K chunk, each slice shared by only 2 / 6 tiles through L2), and with
-// 56 KB per 64-deep K-step only two stages fit in LDS: one K-step in flight against an HBM
-// latency of ~2-3 us under load made every K-step 1.9 us (0.73 us of MFMAs; 29 GB/s per CU).
-// Here the K-steps are 32 deep (28 KB: [32][256] + [32][192] k-row images, the same chunk
-// swizzles and transposed fragment reads) in an NSR-stage ring, NSR - 1 K-steps (112 KB at
-// NSR = 5) in flight: the DMA of K-step s + NSR - 1 is issued right after the barrier of K-step s
-// into the stage K-step s - 1 used. Pieces per K-step: A 16 (two k-rows each), B 12 (1 KB of the
-// [32][192] image): waves 0-3 issue 2 + 2, waves 4-7 2 + 1 (wave-uniform vmcnt immediates).
-template <int NSR>
-__global__ __launch_bounds__(TN_NT, 1) void gemm_tn_ring_kernel(
-    int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
-    int64_t ldb, float* __restrict__ slab, int split_k, int k_chunk, int tiles_n) {
-  constexpr int BK = 32;
-  constexpr int A_ROWB = TN_BM * 2, B_ROWB = TN_BN * 2;            // bytes per k-row
-  constexpr int A_BYTES = BK * A_ROWB, B_BYTES = BK * B_ROWB, STAGE = A_BYTES + B_BYTES;
-  static_assert(NSR >= 2 && NSR * STAGE <= 163840, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[NSR * STAGE];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 1, wn = wave & 1, hl = lane >> 5;
-  const int tiles = ((M + TN_BM - 1) / TN_BM) * tiles_n;
-  const int wi = xcd_remap(blockIdx.x, gridDim.x);
-  const int z = wi / tiles, t = wi - z * tiles;
-  const int tm = t / tiles_n;
-  const int m0 = tm * TN_BM, n0 = (t - tm * tiles_n) * TN_BN;
-  const int kbeg = z * k_chunk, kend = min(K, kbeg + k_chunk);
-  const int nk = max(0, (kend - kbeg + BK - 1) / BK);
-  auto swA = [](int r) { return 4 * (r & 3); };
-  auto swB = [](int r) { return 2 * (r & 3); };
-  const bool wide = wave < 4;  // 2 B pieces per K-step (else 1)
-  int voa[2], vob[2];
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int j = 2 * wave + p, row = 2 * j + (lane >> 5), c = (lane & 31) ^ swA(row);
-    voa[p] = row * (int)(lda * 2) + c * 16;
-  }
-  const int jb0 = wide ? 2 * wave : 8 + (wave - 4);
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int j = jb0 + p, e = j * 64 + lane, row = e / 24, c = (e % 24) ^ swB(row);
-    vob[p] = row * (int)(ldb * 2) + c * 16;
-  }
-  auto piece_a = [&](int kt, int p) {
-    const int k0 = kbeg + kt * BK;
-    dma16_asm(A + (int64_t)k0 * lda + m0, ((int64_t)(K - k0) * lda - m0) * 2,
-              smem + (kt % NSR) * STAGE + (2 * wave + p) * 1024, voa[p]);
-  };
-  auto piece_b = [&](int kt, int p) {
-    const int k0 = kbeg + kt * BK;
-    dma16_asm(B + (int64_t)k0 * ldb + n0, ((int64_t)(K - k0) * ldb - n0) * 2,
-              smem + (kt % NSR) * STAGE + A_BYTES + (jb0 + p) * 1024, vob[p]);
-  };
-  auto issue = [&](int kt) {
-    piece_a(kt, 0);
-    piece_a(kt, 1);
-    piece_b(kt, 0);
-    if (wide) piece_b(kt, 1);
-  };
-  // wait until at most n younger K-steps' pieces are in flight (n <= NSR - 2)
-  auto wait_younger = [&](int n) {
-    if (wide) {
-      if (n >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      else if (n == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      if (n >= 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-      else if (n == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else if (n == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  };
-  static_assert(NSR - 2 <= 3, "wait_younger covers up to 3 younger K-steps");
-
-  floatx16 acc[2][3];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 3; ++b)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[a][b][q] = 0.f;
-  const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g16 = lane >> 4;
-  auto frag = [&](const char* S, int rowb, int rbase, int ks) {
-    const int col = rbase + 16 * (g16 & 1) + 4 * p4;
-    const int k1 = ks * 16 + 8 * hl + q4;
-    const int cofs = (col & 7) * 2;
-    const int s1 = rowb == A_ROWB ? swA(k1) : swB(k1);
-    const int s2 = rowb == A_ROWB ? swA(k1 + 4) : swB(k1 + 4);
-    const short4v v1 = tr_read(reinterpret_cast<const bf16_t*>(
-        S + k1 * rowb + ((((col >> 3) ^ s1)) << 4) + cofs));
-    const short4v v2 = tr_read(reinterpret_cast<const bf16_t*>(
-        S + (k1 + 4) * rowb + ((((col >> 3) ^ s2)) << 4) + cofs));
-    short __attribute__((ext_vector_type(8))) v = {v1[0], v1[1], v1[2], v1[3],
-                                                   v2[0], v2[1], v2[2], v2[3]};
-    return __builtin_bit_cast(bf16x8, v);
-  };
-
-#pragma unroll
-  for (int q = 0; q < NSR - 1; ++q)
-    if (q < nk) issue(q);
-  for (int kt = 0; kt < nk; ++kt) {
-    wait_younger(min(NSR - 2, nk - 1 - kt));
-    asm volatile("s_barrier" ::: "memory");  // K-step kt landed for every wave; kt - 1's stage free
-    if (kt + NSR - 1 < nk) issue(kt + NSR - 1);
-    const char* As = smem + (kt % NSR) * STAGE;
-    const char* Bs = As + A_BYTES;
-    bf16x8 af[2][2], bfr[2][3];
-#pragma unroll
-    for (int a = 0; a < 2; ++a) af[0][a] = frag(As, A_ROWB, wm * 64 + a * 32, 0);
-#pragma unroll
-    for (int b = 0; b < 3; ++b) bfr[0][b] = frag(Bs, B_ROWB, wn * 96 + b * 32, 0);
-#pragma unroll
-    for (int a = 0; a < 2; ++a) af[1][a] = frag(As, A_ROWB, wm * 64 + a * 32, 1);
-#pragma unroll
-    for (int b = 0; b < 3; ++b) bfr[1][b] = frag(Bs, B_ROWB, wn * 96 + b * 32, 1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b)  // operands swapped: the accumulator holds C^T
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[ks][b], af[ks][a], acc[a][b], 0, 0, 0);
-  }
   float* out = slab + (int64_t)z * M * N;
 #pragma unroll
   for (int a = 0; a < 2; ++a) {
@@ -2569,18 +2447,8 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
   if (pipe == 3 && out_kind == 2 && transA && !transB && batch == 1 && g_tn_dma) {
     const int tn = (N + TN_BN - 1) / TN_BN;
     const int work = ((M + TN_BM - 1) / TN_BM) * tn * split_k;
-    // the deep-ring kernel unless MMT_TN_RING=0 or variant 9 (the two-stage kernel, same MFMA
-    // order: bit-identical slabs)
-    static const int g_tn_ring = getenv("MMT_TN_RING") ? atoi(getenv("MMT_TN_RING")) : 5;
-    if (g_tn_ring == 5 && g_variant != 9)
-      hipLaunchKernelGGL(gemm_tn_ring_kernel<5>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
-                         (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
-    else if (g_tn_ring == 3 && g_variant != 9)
-      hipLaunchKernelGGL(gemm_tn_ring_kernel<3>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
-                         (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
-    else
-      hipLaunchKernelGGL(gemm_tn_dma_kernel, dim3(work), dim3(TN_NT), 0, s, M, N, K,
-                         (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
+    hipLaunchKernelGGL(gemm_tn_dma_kernel, dim3(work), dim3(TN_NT), 0, s, M, N, K,
+                       (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
     MMT_CHECK_LAUNCH("mmt_gemm(tn dma)");
   } else {
 #define GL(TA, TB, OUT)                          \

@@ -103,28 +103,6 @@ def test_gemm_tn_splitk_weight_gradient(dev, M, N, K):
     torch.testing.assert_close(dw, ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
 
 
-@pytest.mark.parametrize("M,N,K", [(1536, 384, 141312), (1152, 384, 9997), (384, 1536, 12288),
-                                   (640, 200, 30000)])
-def test_tn_ring_matches_two_stage(dev, M, N, K):
-    """The deep-ring TN kernel (32-deep K-steps, 5 stages; the default) against the two-stage
-    64-deep kernel (variant 9): the same k-slice order per accumulator, so the fp32 weight
-    gradients agree bit for bit, ragged tiles and a partial last K-step included."""
-    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn, _C
-    from multi_modal_transformers_tokenmerge_amd.layers import split_k_for
-    g = torch.Generator().manual_seed(M + N + K + 1)
-    dy, x = _mk((K, M), dev, g), _mk((K, N), dev, g)
-    outs = []
-    for v in (-1, 9):
-        _C.call("mmt_gemm_set_variant", v)
-        try:
-            dw = torch.zeros(M, N, device=dev)
-            Kn.gemm(dy, x, trans_a=True, out=dw, out_mode=Kn.OUT_F32_ACCUM, split_k=split_k_for(M, N, K))
-            outs.append(dw)
-        finally:
-            _C.call("mmt_gemm_set_variant", -1)
-    assert torch.equal(outs[0], outs[1])
-
-
 def test_gemm_rejects_bad_shapes(dev):
     from multi_modal_transformers_tokenmerge_amd import _kernels as Kn, _C
     a = torch.zeros((16, 12), dtype=torch.bfloat16, device=dev)
