@@ -104,6 +104,18 @@ __host__ __device__ __forceinline__ bool keep_elem(uint32_t key, uint32_t idx, u
   return ((pair_draw(key, idx >> 1) >> ((idx & 1u) << 4)) & 0xffffu) < thresh16;
 }
 
+// ---------------------------------------------------------------- sequence-LN launch grids
+// The (sample, 64-column block) workgroups of the sequence-axis LayerNorm family: column blocks
+// fastest (MMT_LN_COLFIRST = 1: the D / 64 workgroups of one sample run together and read its
+// whole rows, one DRAM page run per token row) or samples fastest (0: a sample's column blocks run
+// B workgroups apart, each reading a 256-B piece of every row).
+#ifndef MMT_LN_COLFIRST
+#define MMT_LN_COLFIRST 1
+#endif
+__device__ __forceinline__ int ln_sample() { return MMT_LN_COLFIRST ? blockIdx.y : blockIdx.x; }
+__device__ __forceinline__ int ln_colblk() { return MMT_LN_COLFIRST ? blockIdx.x : blockIdx.y; }
+inline dim3 ln_grid(int n, int cblocks) { return MMT_LN_COLFIRST ? dim3(cblocks, n) : dim3(n, cblocks); }
+
 // ---------------------------------------------------------------- wave helpers (wave64)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

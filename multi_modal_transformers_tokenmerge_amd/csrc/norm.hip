@@ -86,7 +86,7 @@ __global__ __launch_bounds__(NT) void seqnorm_fwd_kernel(
     float* __restrict__ rstd_out) {
   __shared__ float red[2 * RG * CW];
   __shared__ float s_mul[CW], s_add[CW];
-  const int b = blockIdx.x, c0 = blockIdx.y * CW;
+  const int b = ln_sample(), c0 = ln_colblk() * CW;
   const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;
   const int col = c0 + cv * 8;
   const bool cok = col < D;
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
     int64_t as_b, int64_t as_t, TX* dx, int64_t dxs_b, int64_t dxs_t,
     float* __restrict__ dgamma, float* __restrict__ dbeta, DropZ dz = DropZ{}) {
   __shared__ float red[4 * RG * CW];
-  const int b = blockIdx.x, c0 = blockIdx.y * CW;
+  const int b = ln_sample(), c0 = ln_colblk() * CW;
   const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;
   const int col = c0 + cv * 8;
   const bool cok = col < D;
@@ -337,7 +337,7 @@ __global__ __launch_bounds__(NT) void ln_unmerge_dropout_bwd_kernel(
   __shared__ float u_s[kUnmergeMax], u_S[kUnmergeMax];
   float* red = dyn_f;
   float* panel = dyn_f;  // reused after the reduction: merged-layout gradient [L2][64]
-  const int b = blockIdx.x, c0 = blockIdx.y * CW;
+  const int b = ln_sample(), c0 = ln_colblk() * CW;
   const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;
   const int col = c0 + cv * 8;
   const bool cok = col < D;
@@ -536,7 +536,7 @@ extern "C" int mmt_seqnorm_fwd(const void* x, int x_dtype, int64_t xs_b, int64_t
   MMT_CHECK_ARG(B > 0 && L > 0 && D > 0 && D % 8 == 0 && xs_t % 8 == 0 && ys_t % 8 == 0 &&
                     xs_b % 8 == 0 && ys_b % 8 == 0,
                 "mmt_seqnorm_fwd: D and strides must be multiples of 8");
-  dim3 grid(B, (D + CW - 1) / CW);
+  const dim3 grid = ln_grid(B, (D + CW - 1) / CW);
   const int rpt = snb_rpt(L);
   if (x_dtype == MMT_F32 && rpt) {
 #define SNF(R)                                                                                       \
@@ -572,7 +572,7 @@ extern "C" int mmt_seqnorm_bwd(const void* dy, int dy_dtype, int64_t ds_b, int64
   MMT_CHECK_ARG(B > 0 && L > 0 && D > 0 && D % 8 == 0 && ds_t % 8 == 0 && xs_t % 8 == 0 &&
                     dxs_t % 8 == 0 && (!addend || as_t % 8 == 0),
                 "mmt_seqnorm_bwd: D and strides must be multiples of 8");
-  dim3 grid(B, (D + CW - 1) / CW);
+  const dim3 grid = ln_grid(B, (D + CW - 1) / CW);
   hipStream_t s = as_stream(stream);
 #define SNB(TDY, TX)                                                                             \
   hipLaunchKernelGGL((seqnorm_bwd_kernel<TDY, TX>), grid, dim3(NT), 0, s, (const TDY*)dy, ds_b, \
@@ -654,7 +654,7 @@ extern "C" int mmt_ln_unmerge_dropout_bwd(
                 "mmt_ln_unmerge_dropout_bwd: strides must be multiples of 8");
   MMT_CHECK_ARG(!rng || (keep_prob > 0.f && keep_prob <= 1.f), "mmt_ln_unmerge_dropout_bwd: keep_prob");
   const size_t dyn = sizeof(float) * (size_t)std::max(L2 * CW, 4 * RG * CW);
-  dim3 grid(B, (D + CW - 1) / CW);
+  const dim3 grid = ln_grid(B, (D + CW - 1) / CW);
   const int rpt = snb_rpt(L2);
 #define LUD(R)                                                                                      \
   do {                                                                                              \
@@ -695,7 +695,7 @@ extern "C" int mmt_seqnorm_dropout_bwd(const void* dy, int64_t ds_b, int64_t ds_
   MMT_CHECK_ARG(!rng || (keep_prob > 0.f && keep_prob <= 1.f), "mmt_seqnorm_dropout_bwd: keep_prob");
   DropZ dz{rng, layer, site, rng ? keep_threshold16(keep_prob) : 0u, rng ? 1.f / keep_prob : 1.f,
            row_offset, (bf16_t*)z, zs_b, zs_t, colsum};
-  dim3 grid(B, (D + CW - 1) / CW);
+  const dim3 grid = ln_grid(B, (D + CW - 1) / CW);
   const int rpt = snb_rpt(L);
 #define SDZ(R)                                                                                      \
   hipLaunchKernelGGL((seqnorm_bwd_kernel<bf16_t, float, true, R>), grid, dim3(NT), 0,               \

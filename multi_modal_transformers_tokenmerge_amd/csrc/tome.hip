@@ -856,12 +856,12 @@ __global__ __launch_bounds__(256) void tome_merge_seqnorm_fwd_kernel(
   __shared__ float m_ss[kFusedRows][kMergeSeg];
   __shared__ float red[2 * kFRG * 64];
   __shared__ float s_mul[64], s_add[64];
-  const int n = blockIdx.x, c0 = blockIdx.y * 64;
+  const int n = ln_sample(), c0 = ln_colblk() * 64;
   const int ta = (t + 1) / 2, nu = ta - r;
   const bool dis = flags & MMT_TOME_DISTILL_TOKEN;
   const bool plain = flags & MMT_TOME_PLAIN_SUM;
   const bool scatter = !(flags & MMT_TOME_NO_SCATTER);
-  const bool lead = blockIdx.y == 0;  // writes the sizes and the position map
+  const bool lead = ln_colblk() == 0;  // writes the sizes and the position map
   for (int k = threadIdx.x; k < nu; k += blockDim.x) s_unm[k] = unm_g[(int64_t)n * nu + k];
   for (int k = threadIdx.x; k < r; k += blockDim.x) {
     s_src[k] = src_g[(int64_t)n * r + k];
@@ -1055,7 +1055,7 @@ extern "C" int mmt_tome_merge_seqnorm_fwd(const float* x, int n, int L, int D, i
   MMT_CHECK_ARG(x_s_t % 8 == 0 && x_s_n % 8 == 0 && o_s_t % 8 == 0 && o_s_n % 8 == 0 &&
                     y_s_t % 8 == 0 && y_s_n % 8 == 0,
                 "mmt_tome_merge_seqnorm_fwd: strides must be multiples of 8");
-  dim3 grid(n, (D + 63) / 64);
+  const dim3 grid = ln_grid(n, (D + 63) / 64);
   const int Lo = L - r;
   static const bool rpt_on = !getenv("MMT_SNB_RPT") || atoi(getenv("MMT_SNB_RPT")) != 0;
   const int rpt = !rpt_on ? 0 : Lo <= 128 ? 4 : Lo <= 192 ? 6 : Lo <= 256 ? 8 : Lo <= 320 ? 10 : 0;

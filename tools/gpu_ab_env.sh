@@ -7,7 +7,8 @@ mkdir -p gpurun_out
 VAR=$1; VALS=$2; ROUNDS=${3:-2}; shift 3
 for r in $(seq 1 $ROUNDS); do
   for v in $VALS; do
-    env $VAR=$v timeout -k 10 300 python bench.py --no-cpu-baseline --no-probes "$@" > gpurun_out/ab_${VAR}_${v}_$r.log 2>&1 || exit 1
-    echo "$VAR=$v round $r $(grep -o '"value": [0-9.]*' gpurun_out/ab_${VAR}_${v}_$r.log)" >> gpurun_out/ab_${VAR}.txt
+    tag=$(basename "$v")
+    env $VAR=$v timeout -k 10 300 python bench.py --no-cpu-baseline --no-probes "$@" > gpurun_out/ab_${VAR}_${tag}_$r.log 2>&1 || exit 1
+    echo "$VAR=$tag round $r $(grep -o '"value": [0-9.]*' gpurun_out/ab_${VAR}_${tag}_$r.log)" >> gpurun_out/ab_${VAR}.txt
   done
 done
