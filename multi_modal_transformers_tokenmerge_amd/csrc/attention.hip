@@ -1269,6 +1269,305 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_bwd_res_kernel(
   }
 }
 
+// ============================ backward, all four operands resident, both phases concurrent
+// attn_bwd_res_kernel reads K, V, Q and dO twice (a DMA into one phase's images and row
+// fragments from HBM in the other: 1.55x the algorithmic bytes at L = 292) and runs its phases
+// one after the other, each behind its own DMA; ablations at L = 292, B = 512: 513 us of which
+// 110 us are phase-A tiles, 174 us phase-B tiles and ~230 us memory not overlapped with them.
+// Here one 8-wave workgroup per (sample, head) holds K, V, Q and dO (4 x 40 KB at L <= 320:
+// the CU's 160 KB) loaded once; after a prologue that writes the row constants rc of every
+// query row (delta = rowsum(dO O) from the dO image and O rows, the same summation order as
+// the two-phase kernel), waves 0-3 run phase A (dQ, queries on the lanes, the forward's query
+// deal) and waves 4-7 phase B (dK / dV, keys on the lanes) at the same time, every row
+// fragment read from the images. Same arithmetic and order per output as attn_bwd_res_kernel:
+// bit-identical dQ / dK / dV (and per-workgroup bias sums).
+template <int NTILE, bool DROP>
+__global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
+    Geo g, AttnMask mask, ResPlanB plan, const uint32_t* __restrict__ drop_q,
+    const uint32_t* __restrict__ drop_k, int drop_lp, float drop_scale,
+    const bf16_t* __restrict__ dout, int64_t d_s_b, int64_t d_s_t, const float* __restrict__ lse,
+    const bf16_t* __restrict__ o, int64_t o_s_b, int64_t o_s_t, float* __restrict__ rc,
+    bf16_t* __restrict__ dqkv, int64_t dq_s_b, int64_t dq_s_t, float* __restrict__ bias_grad) {
+  constexpr int DH = 64, NS = 4, ROWS = 32 * NTILE, LP = ROWS, IMG = ROWS * DH * 2;
+  __shared__ __attribute__((aligned(16))) char smem_raw[4 * IMG];  // K | V | Q | dO images
+  bf16_t* smem = reinterpret_cast<bf16_t*>(smem_raw);
+  const int bh = blockIdx.x, b = bh / g.H, h = bh - b * g.H;
+  const int lane = threadIdx.x & 63, hh = lane >> 5, lr = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int L = g.L, D = g.H * DH;
+  const bf16_t* base = g.qkv + (int64_t)b * g.s_b;
+  const bf16_t* dbase = dout + (int64_t)b * d_s_b + h * DH;
+  float* rc0 = rc + (int64_t)bh * 2 * LP;
+  float* rc1 = rc0 + LP;
+  const float c2 = g.scale * LOG2E;
+  const float kp = 1.f / drop_scale;
+  const char* imgK = smem_raw;
+  const char* imgV = imgK + IMG;
+  const char* imgQ = imgV + IMG;
+  const char* imgD = imgQ + IMG;
+  int koff[NS];  // row-fragment offsets (row lr of a 32-row tile, chunk 2 s + hh)
+#pragma unroll
+  for (int s = 0; s < NS; ++s) koff[s] = lr * 128 + 16 * ((2 * s + hh) ^ res_sw(lr));
+  float* brow = bias_grad ? bias_grad + h * DH : nullptr;
+  const float sc_out = g.scale * drop_scale;
+
+  // ---- DMA of the four images (waves 0-3: K and V, waves 4-7: Q and dO)
+  if (wave < RES_NW)
+    res_dma2<ROWS>(smem, base + D + h * DH, g.s_t, base + 2 * D + h * DH, g.s_t, L, wave, lane);
+  else
+    res_dma2<ROWS>(smem + 2 * ROWS * DH, base + h * DH, g.s_t, dbase, d_s_t, L, wave - RES_NW, lane);
+  __syncthreads();  // the DMA landed (vmcnt(0) + barrier)
+  // ---- row constants of every query row: rc0 = -lse / scale (-inf past L), rc1 = -kp delta
+  //      (0 past L); delta as the two-phase kernel forms it: chunks 0, 2, 4, 6 and 1, 3, 5, 7
+  //      of the row as two fmaf chains, then their sum
+  if (threadIdx.x < ROWS) {
+    const int q = threadIdx.x;
+    float v0 = -INFINITY, v1 = 0.f;
+    if (q < L) {
+      const bf16_t* orow = o + (int64_t)b * o_s_b + (int64_t)q * o_s_t + h * DH;
+      float part[2] = {0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const bf16x8 of = *reinterpret_cast<const bf16x8*>(orow + 8 * c);
+        const bf16x8 df = *reinterpret_cast<const bf16x8*>(imgD + q * 128 + 16 * (c ^ res_sw(q)));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part[c & 1] = fmaf((float)of[j], (float)df[j], part[c & 1]);
+      }
+      v0 = -lse[(int64_t)bh * L + q] / g.scale;
+      v1 = -((part[0] + part[1]) * kp);
+    }
+    rc0[q] = v0;
+    rc1[q] = v1;
+  }
+  // rc is read by the other waves (L2, no stale L1 line: first touch in this workgroup)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // bias sums: each wave's folded partials through LDS once every wave is done with the images
+  // (two barriers in either branch), summed over the phase's 4 waves in wave order (as
+  // res_bias_reduce), one atomic per d: dq by wave 0, dk by wave 4, dv by wave 5
+  float* red = reinterpret_cast<float*>(smem_raw);  // [2][8 waves][64 lanes][16]
+  auto bias_out = [&](const float (&bs)[16], int i, float sc) {
+    float4* my = reinterpret_cast<float4*>(red + ((i * 8 + wave) * 64 + lane) * 16);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      my[j] = make_float4(bs[4 * j] * sc, bs[4 * j + 1] * sc, bs[4 * j + 2] * sc, bs[4 * j + 3] * sc);
+  };
+  auto bias_sum = [&](int i, int w0, float* dst) {
+    const int d = lane, dhh = (d >> 2) & 1, dd = d >> 5;
+    const int r = (d & 3) | (((d & 31) >> 3) << 2), rho = 2 * dhh + dd;
+    float sum = 0.f;
+    for (int w = 0; w < RES_NW; ++w)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) sum += red[((i * 8 + w0 + w) * 64 + 16 * rho + j) * 16 + r];
+    atomicAdd(dst + d, sum);
+  };
+
+  if (wave < RES_NW) {
+    float bq[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bq[r] = 0.f;
+    // ================= phase A: dQ (queries on the lanes)
+    for (int slot = 0; slot < RES_SLOTS; ++slot) {
+      const int blk = plan.qblk[wave][slot];
+      if (blk == 0xff) break;  // wave-uniform
+      const int q = 32 * blk + lr;
+      const bool qv = q < L;
+      const int qc = qv ? q : L - 1;
+      bf16x8 qf[NS], df[NS];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        qf[s] = *reinterpret_cast<const bf16x8*>(imgQ + blk * 4096 + koff[s]);
+        df[s] = *reinterpret_cast<const bf16x8*>(imgD + blk * 4096 + koff[s]);
+      }
+      const float dkp = -rc1[q];  // kp delta (0 past L)
+      const float lse2 = qv ? lse[(int64_t)bh * L + q] * LOG2E : INFINITY;
+      const int sq = set_of(mask, qc);
+      const int sq0 = __builtin_amdgcn_readfirstlane(sq);
+      const bool uni = mask.causal == 0u && __all(sq == sq0);
+      uint32_t vws[NTILE];
+#pragma unroll
+      for (int t = 0; t < NTILE; ++t) {
+        uint32_t vw = uni ? plan.qword[sq0][t] : plan.qword[sq][t];
+        if (!uni && ((mask.causal >> sq) & 1u)) {
+          const int a0 = max(q + 1 - 32 * t, 0), e0 = min(mask.start[sq] + mask.len[sq] - 32 * t, 32);
+          if (a0 < e0) vw &= ~(uint32_t)(bit_range(a0, e0));
+        }
+        vws[t] = vw;
+      }
+      floatx16 dq[2];
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
+#pragma unroll
+      for (int t = 0; t < NTILE; ++t) {
+        const uint32_t vw = vws[t];
+        if (!__all(vw == 0u)) {  // wave-uniform
+          TileMasks<16> dm;
+          if constexpr (DROP) dm.load(drop_q, drop_lp, blk, 32 * t);
+          floatx16 sacc, pacc;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            sacc[r] = 0.f;
+            pacc[r] = 0.f;
+          }
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(imgK + t * 4096 + koff[s]);
+            const bf16x8 vf = *reinterpret_cast<const bf16x8*>(imgV + t * 4096 + koff[s]);
+            sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc, 0, 0, 0);
+            pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, df[s], pacc, 0, 0, 0);
+          }
+          if (!__all(vw == 0xffffffffu)) {
+            const uint32_t w = vw >> (4 * hh);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int mk = bitmask_of(w, rbit(r));
+              sacc[r] = __int_as_float((__float_as_int(sacc[r]) & mk) | (~mk & (int)0xff800000u));
+            }
+          }
+          floatx16 ds;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float p = fast_exp2(fmaf(sacc[r], c2, -lse2));
+            float tt = pacc[r];
+            if constexpr (DROP) tt = sel_keep(tt, dm.m[r]);
+            ds[r] = p * (tt - dkp);
+          }
+          const bf16x8 d0 = pack_frag(ds, 0), d1 = pack_frag(ds, 1);
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            dq[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(imgK, 32 * t, d, lane), d0, dq[d], 0, 0, 0);
+            dq[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(imgK, 32 * t + 16, d, lane), d1, dq[d], 0, 0, 0);
+          }
+        }
+      }
+      res_store_rows(dq, sc_out, dqkv + (int64_t)b * dq_s_b + (int64_t)qc * dq_s_t + h * DH, qv, hh);
+      if (brow) res_bias_fold(dq, bq);
+    }
+    if (brow) {
+      __syncthreads();
+      bias_out(bq, 0, sc_out);
+      __syncthreads();
+      if (wave == 0) bias_sum(0, 0, brow);
+    }
+  } else {
+    // ================= phase B: dK / dV (keys on the lanes)
+    const int wb = wave - RES_NW;
+    float bk[16], bv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      bk[r] = 0.f;
+      bv[r] = 0.f;
+    }
+    for (int slot = 0; slot < RES_SLOTS; ++slot) {
+      const int blk = plan.kblk[wb][slot];
+      if (blk == 0xff) break;  // wave-uniform
+      const int key = 32 * blk + lr;
+      const bool kv = key < L;
+      const int kc = kv ? key : L - 1;
+      bf16x8 kf[NS], vf[NS];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        kf[s] = *reinterpret_cast<const bf16x8*>(imgK + blk * 4096 + koff[s]);
+        vf[s] = *reinterpret_cast<const bf16x8*>(imgV + blk * 4096 + koff[s]);
+      }
+      const int sk = set_of(mask, kc);
+      const int sk0 = __builtin_amdgcn_readfirstlane(sk);
+      const bool uni = mask.causal == 0u && __all(sk == sk0);
+      uint32_t qws[NTILE];
+#pragma unroll
+      for (int t = 0; t < NTILE; ++t) {
+        uint32_t qw = uni ? plan.kword[sk0][t] : plan.kword[sk][t];
+        if (!uni && ((mask.causal >> sk) & 1u)) {
+          const int a0 = max(mask.start[sk] - 32 * t, 0), e0 = min(key - 32 * t, 32);
+          if (a0 < e0) qw &= ~(uint32_t)(bit_range(a0, e0));
+        }
+        if (!kv) qw = 0u;
+        qws[t] = qw;
+      }
+      floatx16 dk[2], dv[2];
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          dk[d][r] = 0.f;
+          dv[d][r] = 0.f;
+        }
+#pragma unroll
+      for (int t = 0; t < NTILE; ++t) {
+        const uint32_t qw = qws[t];
+        if (!__all(qw == 0u)) {  // wave-uniform
+          TileMasks<16> dm;
+          if constexpr (DROP) dm.load(drop_k, drop_lp, blk, 32 * t);
+          floatx16 sacc, ca;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float4 x = *reinterpret_cast<const float4*>(rc0 + 32 * t + 8 * j + 4 * hh);
+            const float4 y = *reinterpret_cast<const float4*>(rc1 + 32 * t + 8 * j + 4 * hh);
+            sacc[4 * j] = x.x; sacc[4 * j + 1] = x.y; sacc[4 * j + 2] = x.z; sacc[4 * j + 3] = x.w;
+            ca[4 * j] = y.x; ca[4 * j + 1] = y.y; ca[4 * j + 2] = y.z; ca[4 * j + 3] = y.w;
+          }
+          floatx16 pacc = ca;
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            const bf16x8 qr = *reinterpret_cast<const bf16x8*>(imgQ + t * 4096 + koff[s]);
+            const bf16x8 dr_ = *reinterpret_cast<const bf16x8*>(imgD + t * 4096 + koff[s]);
+            sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qr, kf[s], sacc, 0, 0, 0);
+            pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dr_, vf[s], pacc, 0, 0, 0);
+          }
+          if (!__all(qw == 0xffffffffu)) {
+            const uint32_t w = qw >> (4 * hh);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int mk = bitmask_of(w, rbit(r));
+              sacc[r] = __int_as_float((__float_as_int(sacc[r]) & mk) | (~mk & (int)0xff800000u));
+            }
+          }
+          floatx16 pk, ds;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float p = fast_exp2(sacc[r] * c2);
+            if constexpr (DROP) {
+              const bool keep = __builtin_amdgcn_inverse_ballot_w64(dm.m[r]);
+              pk[r] = keep ? p : 0.f;
+              ds[r] = p * (keep ? pacc[r] : ca[r]);
+            } else {
+              pk[r] = p;
+              ds[r] = p * pacc[r];
+            }
+          }
+          const bf16x8 p0 = pack_frag(pk, 0), p1 = pack_frag(pk, 1);
+          const bf16x8 s0 = pack_frag(ds, 0), s1 = pack_frag(ds, 1);
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(imgD, 32 * t, d, lane), p0, dv[d], 0, 0, 0);
+            dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(imgD, 32 * t + 16, d, lane), p1, dv[d], 0, 0, 0);
+            dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(imgQ, 32 * t, d, lane), s0, dk[d], 0, 0, 0);
+            dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(imgQ, 32 * t + 16, d, lane), s1, dk[d], 0, 0, 0);
+          }
+        }
+      }
+      bf16_t* kro = dqkv + (int64_t)b * dq_s_b + (int64_t)kc * dq_s_t + D + h * DH;
+      res_store_rows(dk, sc_out, kro, kv, hh);
+      res_store_rows(dv, drop_scale, kro + D, kv, hh);
+      if (brow) {
+        res_bias_fold(dk, bk);
+        res_bias_fold(dv, bv);
+      }
+    }
+    if (brow) {
+      __syncthreads();
+      bias_out(bk, 0, sc_out);
+      bias_out(bv, 1, drop_scale);
+      __syncthreads();
+      if (wave == RES_NW) bias_sum(0, RES_NW, brow + D);
+      else if (wave == RES_NW + 1) bias_sum(1, RES_NW, brow + 2 * D);
+    }
+  }
+}
+
 // Host plan of the resident backward: the forward's query-side words and query-block deal, and
 // the key-side words (queries of tile t that see key set s) and key-block deal.
 static bool res_plan_bwd(const AttnMask& m, int L, ResPlanB& pb) {
@@ -1899,11 +2198,21 @@ extern "C" int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
     ResPlanB plan;
     if (res_plan_bwd(m, L, plan)) {
       const int ntile = ((L + 63) / 64) * 2;
+      // MMT_ATTN_BWD8=0: the two-phase 4-wave kernel (same outputs, bit for bit)
+      const bool bwd8 = attn_res_enabled("MMT_ATTN_BWD8");
 #define RESB1(NT_, DR_)                                                                             \
-  hipLaunchKernelGGL((attn_bwd_res_kernel<NT_, DR_>), dim3(B * H), dim3(64 * RES_NW), 0, s, g, m,   \
-                     plan, drop_bits, drop_bits_t, lp, dscale, (const bf16_t*)dout, d_s_b, d_s_t,  \
-                     lse, (const bf16_t*)o, o_s_b, o_s_t, delta, (bf16_t*)dqkv, dq_s_b, dq_s_t,   \
-                     bias_grad)
+  do {                                                                                              \
+    if (bwd8)                                                                                       \
+      hipLaunchKernelGGL((attn_bwd_res8_kernel<NT_, DR_>), dim3(B * H), dim3(128 * RES_NW), 0, s, g, \
+                         m, plan, drop_bits, drop_bits_t, lp, dscale, (const bf16_t*)dout, d_s_b,   \
+                         d_s_t, lse, (const bf16_t*)o, o_s_b, o_s_t, delta, (bf16_t*)dqkv, dq_s_b, \
+                         dq_s_t, bias_grad);                                                        \
+    else                                                                                            \
+      hipLaunchKernelGGL((attn_bwd_res_kernel<NT_, DR_>), dim3(B * H), dim3(64 * RES_NW), 0, s, g,  \
+                         m, plan, drop_bits, drop_bits_t, lp, dscale, (const bf16_t*)dout, d_s_b,   \
+                         d_s_t, lse, (const bf16_t*)o, o_s_b, o_s_t, delta, (bf16_t*)dqkv, dq_s_b, \
+                         dq_s_t, bias_grad);                                                        \
+  } while (0)
 #define RESB2(NT_)                  \
   do {                              \
     if (drop_bits) RESB1(NT_, true); \

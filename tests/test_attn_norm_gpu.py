@@ -344,3 +344,43 @@ def test_resident_attention_vs_tiled_and_torch(dev, B, L, H, mode, drop, monkeyp
     ref.backward(dout.float())
     assert rel(o1, ref) < 1e-2
     assert rel(d1, qf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("B,L,H,mode,drop", [
+    (2, 33, 3, "none", True), (3, 65, 2, "octo", True), (2, 101, 3, "causal", True),
+    (2, 212, 6, "octo", True), (2, 292, 6, "octo", False), (1, 301, 2, "causal", False),
+    (2, 320, 2, "octo", True)])
+def test_resident_backward_concurrent_phases_bit_identical(dev, B, L, H, mode, drop, monkeypatch):
+    """The 8-wave resident backward (K, V, Q, dO all in LDS, phase A on waves 0-3 and phase B on
+    waves 4-7 at the same time; the default) against the two-phase 4-wave kernel
+    (MMT_ATTN_BWD8=0): the same arithmetic in the same order, so dQ / dK / dV agree bit for bit
+    (the bias gradient, one fp32 atomic per workgroup, to summation order)."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    Dh = 64
+    g = torch.Generator().manual_seed(L * 7 + H)
+    qkv = torch.randn((B, L, 3 * H * Dh), generator=g).bfloat16().to(dev)
+    dout = torch.randn((B, L, H * Dh), generator=g).bfloat16().to(dev)
+    scale = Dh ** -0.5
+    if mode == "none":
+        table = None
+    elif mode == "octo":
+        starts, lens, vis = octo_small_table(min(32, L // 4), L - min(32, L // 4) - 4, 4)
+        table = K.SetTable(starts, lens, vis)
+    else:
+        n = (L - 7) // 2
+        table = K.SetTable([0, 3, 3 + n, 4 + n, 7 + n], [3, n, 1, 3, L - 7 - n],
+                           [0b00001, 0b00011, 0b00111, 0b01001, 0b11011],
+                           [False, True, False, False, True])
+    kp = 0.9 if drop else 1.0
+    rng = torch.tensor([3, 4], dtype=torch.int32, device=dev)
+    bits = K.dropout_bits(rng, 2, 0, L, L, kp) if drop else None
+    o, lse = K.attn_fwd(qkv, H, scale, table, bits, kp)
+    outs = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("MMT_ATTN_BWD8", v)
+        bg = torch.zeros(3 * H * Dh, device=dev)
+        dq = K.attn_bwd(qkv, o, dout, lse, H, scale, table, bits, kp, bias_grad=bg)
+        torch.cuda.synchronize()
+        outs[v] = (dq, bg)
+    assert torch.equal(outs["1"][0], outs["0"][0])
+    torch.testing.assert_close(outs["1"][1], outs["0"][1], rtol=1e-5, atol=1e-5)
