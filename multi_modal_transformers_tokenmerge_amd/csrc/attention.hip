@@ -893,8 +893,8 @@ static bool res_plan(const AttnMask& m, int L, ResPlan& plan) {
 struct ResPlanB {
   uint32_t qword[MAX_SETS][RES_TILES];  // phase A: keys of tile t that query set s sees
   uint32_t kword[MAX_SETS][RES_TILES];  // phase B: queries of tile t that see key set s
-  uint8_t qblk[RES_NW][RES_SLOTS];
-  uint8_t kblk[RES_NW][RES_SLOTS];
+  uint8_t qblk[2 * RES_NW][RES_SLOTS];  // query blocks of each phase-A wave (0xff-terminated)
+  uint8_t kblk[2 * RES_NW][RES_SLOTS];  // key blocks of each phase-B wave
 };
 
 // DMA of rows [0, 32 NTILE) (clamped to L - 1) of two (row stride s) bf16 tensors into the two
@@ -1277,10 +1277,14 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_bwd_res_kernel(
 // Here one 8-wave workgroup per (sample, head) holds K, V, Q and dO (4 x 40 KB at L <= 320:
 // the CU's 160 KB) loaded once; after a prologue that writes the row constants rc of every
 // query row (delta = rowsum(dO O) from the dO image and O rows, the same summation order as
-// the two-phase kernel), waves 0-3 run phase A (dQ, queries on the lanes, the forward's query
-// deal) and waves 4-7 phase B (dK / dV, keys on the lanes) at the same time, every row
-// fragment read from the images. Same arithmetic and order per output as attn_bwd_res_kernel:
-// bit-identical dQ / dK / dV (and per-workgroup bias sums).
+// the two-phase kernel), waves 0 .. RES8_NA - 1 run phase A (dQ, queries on the lanes) and the
+// rest phase B (dK / dV, keys on the lanes) at the same time, blocks dealt longest-first by
+// visible tiles, every row fragment read from the images. Same arithmetic and order per output
+// as attn_bwd_res_kernel: bit-identical dQ / dK / dV (the bias column sums add the per-wave
+// partials over 3 / 5 waves instead of 4 / 4: equal to summation order).
+// Phase-A waves of the 8 (a phase-B key block costs ~1.6x a phase-A query block: 3 + 5 waves
+// balance the two phases; the bias sums then run over 3 / 5 waves)
+constexpr int RES8_NA = 3;
 template <int NTILE, bool DROP>
 __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
     Geo g, AttnMask mask, ResPlanB plan, const uint32_t* __restrict__ drop_q,
@@ -1289,7 +1293,9 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
     const bf16_t* __restrict__ o, int64_t o_s_b, int64_t o_s_t, float* __restrict__ rc,
     bf16_t* __restrict__ dqkv, int64_t dq_s_b, int64_t dq_s_t, float* __restrict__ bias_grad) {
   constexpr int DH = 64, NS = 4, ROWS = 32 * NTILE, LP = ROWS, IMG = ROWS * DH * 2;
-  __shared__ __attribute__((aligned(16))) char smem_raw[4 * IMG];  // K | V | Q | dO images
+  constexpr int RED_BYTES = 2 * 2 * RES_NW * 64 * 16 * 4;  // the bias partials, after the phases
+  // K | V | Q | dO images (the bias partials reuse them: 64 KB, more than the images at NTILE 2)
+  __shared__ __attribute__((aligned(16))) char smem_raw[4 * IMG > RED_BYTES ? 4 * IMG : RED_BYTES];
   bf16_t* smem = reinterpret_cast<bf16_t*>(smem_raw);
   const int bh = blockIdx.x, b = bh / g.H, h = bh - b * g.H;
   const int lane = threadIdx.x & 63, hh = lane >> 5, lr = lane & 31;
@@ -1353,17 +1359,17 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
     for (int j = 0; j < 4; ++j)
       my[j] = make_float4(bs[4 * j] * sc, bs[4 * j + 1] * sc, bs[4 * j + 2] * sc, bs[4 * j + 3] * sc);
   };
-  auto bias_sum = [&](int i, int w0, float* dst) {
+  auto bias_sum = [&](int i, int w0, int nw, float* dst) {
     const int d = lane, dhh = (d >> 2) & 1, dd = d >> 5;
     const int r = (d & 3) | (((d & 31) >> 3) << 2), rho = 2 * dhh + dd;
     float sum = 0.f;
-    for (int w = 0; w < RES_NW; ++w)
+    for (int w = 0; w < nw; ++w)
 #pragma unroll
       for (int j = 0; j < 16; ++j) sum += red[((i * 8 + w0 + w) * 64 + 16 * rho + j) * 16 + r];
     atomicAdd(dst + d, sum);
   };
 
-  if (wave < RES_NW) {
+  if (wave < RES8_NA) {
     float bq[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) bq[r] = 0.f;
@@ -1450,11 +1456,11 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
       __syncthreads();
       bias_out(bq, 0, sc_out);
       __syncthreads();
-      if (wave == 0) bias_sum(0, 0, brow);
+      if (wave == 0) bias_sum(0, 0, RES8_NA, brow);
     }
   } else {
     // ================= phase B: dK / dV (keys on the lanes)
-    const int wb = wave - RES_NW;
+    const int wb = wave - RES8_NA;
     float bk[16], bv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -1562,21 +1568,62 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
       bias_out(bk, 0, sc_out);
       bias_out(bv, 1, drop_scale);
       __syncthreads();
-      if (wave == RES_NW) bias_sum(0, RES_NW, brow + D);
-      else if (wave == RES_NW + 1) bias_sum(1, RES_NW, brow + 2 * D);
+      if (wave == RES8_NA) bias_sum(0, RES8_NA, 2 * RES_NW - RES8_NA, brow + D);
+      else if (wave == RES8_NA + 1) bias_sum(1, RES8_NA, 2 * RES_NW - RES8_NA, brow + 2 * D);
     }
   }
 }
 
 // Host plan of the resident backward: the forward's query-side words and query-block deal, and
 // the key-side words (queries of tile t that see key set s) and key-block deal.
-static bool res_plan_bwd(const AttnMask& m, int L, ResPlanB& pb) {
+// Longest-processing-time deal of nt blocks (cost[i]) over nw waves, at most RES_SLOTS each.
+static bool res_deal(const int* cost, int nt, int nw, uint8_t (*blk)[RES_SLOTS]) {
+  int order[RES_TILES];
+  for (int i = 0; i < nt; ++i) order[i] = i;
+  std::sort(order, order + nt, [&](int a, int b) { return cost[a] > cost[b] || (cost[a] == cost[b] && a < b); });
+  int load[2 * RES_NW] = {0}, cnt[2 * RES_NW] = {0};
+  for (int k = 0; k < nt; ++k) {
+    int best = -1;
+    for (int w = 0; w < nw; ++w)
+      if (cnt[w] < RES_SLOTS && (best < 0 || load[w] < load[best])) best = w;
+    if (best < 0) return false;
+    blk[best][cnt[best]++] = (uint8_t)order[k];
+    load[best] += cost[order[k]];
+  }
+  return true;
+}
+
+// Cost of a block: 1 (its fixed work) + 4 per key / query tile any of its rows sees.
+static void res_costs(const AttnMask& m, int L, const uint32_t (*word)[RES_TILES], int* cost) {
+  const int nt = (L + 31) / 32;
+  for (int i = 0; i < nt; ++i) {
+    uint32_t any[RES_TILES] = {0};
+    for (int s = 0; s < m.n_sets; ++s)
+      if (m.len[s] > 0 && m.start[s] < std::min(L, 32 * i + 32) && m.start[s] + m.len[s] > 32 * i)
+        for (int t = 0; t < nt; ++t) any[t] |= word[s][t];
+    cost[i] = 1;
+    for (int t = 0; t < nt; ++t) cost[i] += any[t] ? 4 : 0;
+  }
+}
+
+// Host plan of the resident backward: the forward's query-side words, the key-side words
+// (queries of tile t that see key set s), query blocks dealt over na phase-A waves and key
+// blocks over nb phase-B waves (the two-phase kernel: 4 and 4, the forward's query deal).
+static bool res_plan_bwd(const AttnMask& m, int L, ResPlanB& pb, int na = RES_NW, int nb = RES_NW) {
   ResPlan pf;
   if (!res_plan(m, L, pf)) return false;
   const int nt = (L + 31) / 32;
   memset(&pb, 0, sizeof(pb));
   memcpy(pb.qword, pf.tword, sizeof(pb.qword));
-  memcpy(pb.qblk, pf.wblk, sizeof(pb.qblk));
+  memset(pb.qblk, 0xff, sizeof(pb.qblk));
+  memset(pb.kblk, 0xff, sizeof(pb.kblk));
+  if (na == RES_NW) {
+    memcpy(pb.qblk, pf.wblk, sizeof(pf.wblk));
+  } else {
+    int qc[RES_TILES];
+    res_costs(m, L, pb.qword, qc);
+    if (!res_deal(qc, nt, na, pb.qblk)) return false;
+  }
   for (int s = 0; s < m.n_sets; ++s)
     for (int t = 0; t < nt; ++t) {
       uint32_t w = 0;
@@ -1587,28 +1634,9 @@ static bool res_plan_bwd(const AttnMask& m, int L, ResPlanB& pb) {
       }
       pb.kword[s][t] = w;
     }
-  memset(pb.kblk, 0xff, sizeof(pb.kblk));
-  int cost[RES_TILES], order[RES_TILES];
-  for (int i = 0; i < nt; ++i) {
-    uint32_t any[RES_TILES] = {0};
-    for (int s = 0; s < m.n_sets; ++s)
-      if (m.len[s] > 0 && m.start[s] < std::min(L, 32 * i + 32) && m.start[s] + m.len[s] > 32 * i)
-        for (int t = 0; t < nt; ++t) any[t] |= pb.kword[s][t];
-    cost[i] = 1;
-    for (int t = 0; t < nt; ++t) cost[i] += any[t] ? 4 : 0;
-    order[i] = i;
-  }
-  std::sort(order, order + nt, [&](int a, int b) { return cost[a] > cost[b] || (cost[a] == cost[b] && a < b); });
-  int load[RES_NW] = {0}, cnt[RES_NW] = {0};
-  for (int k = 0; k < nt; ++k) {
-    int best = -1;
-    for (int w = 0; w < RES_NW; ++w)
-      if (cnt[w] < RES_SLOTS && (best < 0 || load[w] < load[best])) best = w;
-    if (best < 0) return false;
-    pb.kblk[best][cnt[best]++] = (uint8_t)order[k];
-    load[best] += cost[order[k]];
-  }
-  return true;
+  int kc[RES_TILES];
+  res_costs(m, L, pb.kword, kc);
+  return res_deal(kc, nt, nb, pb.kblk);
 }
 
 // =============================================================================== bwd: dQ
@@ -2195,11 +2223,11 @@ extern "C" int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   const float dscale = drop_bits ? 1.f / keep_prob : 1.f;
   hipStream_t s = as_stream(stream);
   if (attn_res_enabled("MMT_ATTN_RES_BWD") && Dh == 64 && L > 32 && L <= 32 * RES_TILES) {
+    // MMT_ATTN_BWD8=0: the two-phase 4-wave kernel (same dQ / dK / dV, bit for bit)
+    const bool bwd8 = attn_res_enabled("MMT_ATTN_BWD8");
     ResPlanB plan;
-    if (res_plan_bwd(m, L, plan)) {
+    if (bwd8 ? res_plan_bwd(m, L, plan, RES8_NA, 2 * RES_NW - RES8_NA) : res_plan_bwd(m, L, plan)) {
       const int ntile = ((L + 63) / 64) * 2;
-      // MMT_ATTN_BWD8=0: the two-phase 4-wave kernel (same outputs, bit for bit)
-      const bool bwd8 = attn_res_enabled("MMT_ATTN_BWD8");
 #define RESB1(NT_, DR_)                                                                             \
   do {                                                                                              \
     if (bwd8)                                                                                       \
