@@ -2223,7 +2223,10 @@ extern "C" int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   const float dscale = drop_bits ? 1.f / keep_prob : 1.f;
   hipStream_t s = as_stream(stream);
   if (attn_res_enabled("MMT_ATTN_RES_BWD") && Dh == 64 && L > 32 && L <= 32 * RES_TILES) {
-    // MMT_ATTN_BWD8=0: the two-phase 4-wave kernel (same dQ / dK / dV, bit for bit)
+    // the concurrent-phase kernel (MMT_ATTN_BWD8=0: the two-phase kernel; same dQ / dK / dV, bit
+    // for bit). Alone (tools/attn_bench.py, B = 512) it wins at L = 292 (464 vs 516 us) and
+    // L <= 164 (1.06-1.13x) and loses 0-6 % at L = 196 .. 276 (one workgroup per CU there);
+    // in the step it is faster at every L (all: 14.75k, per-L choice: 14.73k, two-phase: 14.66k)
     const bool bwd8 = attn_res_enabled("MMT_ATTN_BWD8");
     ResPlanB plan;
     if (bwd8 ? res_plan_bwd(m, L, plan, RES8_NA, 2 * RES_NW - RES8_NA) : res_plan_bwd(m, L, plan)) {
