@@ -1556,22 +1556,29 @@ __device__ __forceinline__ void dma16_asm(const void* base, int64_t bytes, void*
   asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
                :: "v"(voffset), "s"(r), "s"(l) : "m0", "memory");
 }
+// BM: tile height, 256 (8 waves of 64 x 96: 2 x 3 MFMA blocks) or 384 (waves of 96 x 96: 3 x 3
+// blocks; 72 KB per K-step for 1.5x the products of the 56 KB 256-row step — the kernel is bound
+// by its DMA rate, profiles/r03_tn_ablation.txt)
+template <int BM>
 __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
     int64_t ldb, float* __restrict__ slab, int split_k, int k_chunk, int tiles_n) {
-  constexpr int A_ROWB = TN_BM * 2, B_ROWB = TN_BN * 2;            // bytes per k-row
+  static_assert(BM == 256 || BM == 384, "tile height");
+  constexpr int MB = BM / 128;                                      // 32-row MFMA blocks per wave
+  constexpr int A_ROWB = BM * 2, B_ROWB = TN_BN * 2;                // bytes per k-row
+  constexpr int A_CH = A_ROWB / 16;                                 // 16-B chunks per A k-row
   constexpr int A_BYTES = 64 * A_ROWB, B_BYTES = 64 * B_ROWB, STAGE = A_BYTES + B_BYTES;
-  constexpr int GA = A_BYTES / 1024 / 8, GB = B_BYTES / 1024 / 8;   // DMA pieces per wave (4 + 3)
+  constexpr int GA = A_BYTES / 1024 / 8, GB = B_BYTES / 1024 / 8;   // DMA pieces per wave (4 / 6 + 3)
   constexpr int G = GA + GB;
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1, hl = lane >> 5;
-  const int tiles = ((M + TN_BM - 1) / TN_BM) * tiles_n;
+  const int tiles = ((M + BM - 1) / BM) * tiles_n;
   const int wi = xcd_remap(blockIdx.x, gridDim.x);
   const int z = wi / tiles, t = wi - z * tiles;
   const int tm = t / tiles_n;
-  const int m0 = tm * TN_BM, n0 = (t - tm * tiles_n) * TN_BN;
+  const int m0 = tm * BM, n0 = (t - tm * tiles_n) * TN_BN;
   const int kbeg = z * k_chunk, kend = min(K, kbeg + k_chunk);
   const int nk = max(0, (kend - kbeg + 63) / 64);
   // chunk swizzles (16-B chunks of a k-row): A rows are 512 B (every row starts on bank 0), so
@@ -1585,8 +1592,9 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
   int voff[G];
 #pragma unroll
   for (int p = 0; p < G; ++p) {
-    if (p < GA) {  // A piece j = wave * GA + p: k-rows 2j, 2j + 1 (32 chunks each)
-      const int j = wave * GA + p, row = 2 * j + (lane >> 5), c = (lane & 31) ^ swA(row);
+    if (p < GA) {  // A piece j = wave * GA + p: 1 KB of the [64][BM] image (A_CH chunks per k-row;
+                   // 768-B rows also start on bank 0: the same swizzle)
+      const int j = wave * GA + p, e = j * 64 + lane, row = e / A_CH, c = (e % A_CH) ^ swA(row);
       voff[p] = row * (int)(lda * 2) + c * 16;
     } else {       // B piece j: 1 KB of the [64][192] image (24 chunks per k-row)
       const int j = wave * GB + (p - GA), e = j * 64 + lane, row = e / 24, c = (e % 24) ^ swB(row);
@@ -1618,9 +1626,9 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
                 S0 + A_BYTES + (wave * GB + (p - GA)) * 1024, voff[p]);
   };
 
-  floatx16 acc[2][3];
+  floatx16 acc[MB][3];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < MB; ++a)
 #pragma unroll
     for (int b = 0; b < 3; ++b)
 #pragma unroll
@@ -1656,9 +1664,9 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
     const char* Bs = As + A_BYTES;
     // fragments one k-slice ahead: slice ks + 1's reads are in flight under slice ks's MFMAs (every
     // wave reaches this point together after the barrier, so the partner wave cannot cover them)
-    bf16x8 af[2][2], bfr[2][3];
+    bf16x8 af[2][MB], bfr[2][3];
 #pragma unroll
-    for (int a = 0; a < 2; ++a) af[0][a] = frag(As, A_ROWB, wm * 64 + a * 32, 0);
+    for (int a = 0; a < MB; ++a) af[0][a] = frag(As, A_ROWB, wm * (32 * MB) + a * 32, 0);
 #pragma unroll
     for (int b = 0; b < 3; ++b) bfr[0][b] = frag(Bs, B_ROWB, wn * 96 + b * 32, 0);
 #pragma unroll
@@ -1670,12 +1678,12 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
       if (ks < 3) {
 #endif
 #pragma unroll
-        for (int a = 0; a < 2; ++a) af[cu ^ 1][a] = frag(As, A_ROWB, wm * 64 + a * 32, ks + 1);
+        for (int a = 0; a < MB; ++a) af[cu ^ 1][a] = frag(As, A_ROWB, wm * (32 * MB) + a * 32, ks + 1);
 #pragma unroll
         for (int b = 0; b < 3; ++b) bfr[cu ^ 1][b] = frag(Bs, B_ROWB, wn * 96 + b * 32, ks + 1);
       }
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+      for (int a = 0; a < MB; ++a)
 #pragma unroll
         for (int b = 0; b < 3; ++b)  // operands swapped: the accumulator holds C^T
 #if MMT_TN_ABL == 2  // ablation: no MFMAs (fragments kept live)
@@ -1685,9 +1693,11 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
 #endif
       // the next K-step's DMA into the other stage (free since this K-step's barrier), spread
       // over the k-slices so the SIMD partner wave keeps issuing MFMAs
-      if (nxt) {
-        if (2 * ks < G) piece(kt + 1, st ^ 1, 2 * ks);
-        if (2 * ks + 1 < G) piece(kt + 1, st ^ 1, 2 * ks + 1);
+      if (nxt) {  // ceil(G / 4) pieces per k-slice (G = 7 at BM 256, 9 at BM 384)
+        constexpr int PPK = (G + 3) / 4;
+#pragma unroll
+        for (int q = 0; q < PPK; ++q)
+          if (PPK * ks + q < G) piece(kt + 1, st ^ 1, PPK * ks + q);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -1695,8 +1705,8 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
   // fp32 slab z: lane (m = lane & 31, h) of block (a, b) holds row m, columns 8g + 4h + {0..3}
   float* out = slab + (int64_t)z * M * N;
 #pragma unroll
-  for (int a = 0; a < 2; ++a) {
-    const int gr = m0 + wm * 64 + a * 32 + (lane & 31);
+  for (int a = 0; a < MB; ++a) {
+    const int gr = m0 + wm * (32 * MB) + a * 32 + (lane & 31);
     if (gr >= M) continue;
 #pragma unroll
     for (int b = 0; b < 3; ++b)
@@ -2446,9 +2456,17 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
   static const int g_tn_dma = getenv("MMT_TN_DMA") ? atoi(getenv("MMT_TN_DMA")) : 1;
   if (pipe == 3 && out_kind == 2 && transA && !transB && batch == 1 && g_tn_dma) {
     const int tn = (N + TN_BN - 1) / TN_BN;
-    const int work = ((M + TN_BM - 1) / TN_BM) * tn * split_k;
-    hipLaunchKernelGGL(gemm_tn_dma_kernel, dim3(work), dim3(TN_NT), 0, s, M, N, K,
-                       (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
+    // 384-row tiles where M divides (every weight gradient of the step: 384 / 1152 / 1536 rows)
+    // unless MMT_TN_BM=256; fewer, larger tiles: the split-K factor is the caller's
+    static const int g_tn_bm = getenv("MMT_TN_BM") ? atoi(getenv("MMT_TN_BM")) : 384;
+    const bool tall = g_tn_bm == 384 && M % 384 == 0 && g_variant != 9;
+    const int work = ((M + (tall ? 383 : 255)) / (tall ? 384 : 256)) * tn * split_k;
+    if (tall)
+      hipLaunchKernelGGL(gemm_tn_dma_kernel<384>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
+                         (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
+    else
+      hipLaunchKernelGGL(gemm_tn_dma_kernel<256>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
+                         (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
     MMT_CHECK_LAUNCH("mmt_gemm(tn dma)");
   } else {
 #define GL(TA, TB, OUT)                          \

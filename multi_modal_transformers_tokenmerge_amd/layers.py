@@ -70,12 +70,16 @@ class wgrad_overlap:
         return False
 
 
+_TN_BM = 256 if os.environ.get("MMT_TN_BM") == "256" else 384  # as csrc/gemm.hip's tile choice
+
+
 def split_k_for(n_out: int, k_out: int, m_red: int) -> int:
     """Split of the M-reduction of a weight-gradient GEMM so the launch fills the 256 CUs once:
-    the TN products run on the 256 x 192-tile kernel at one workgroup per CU (csrc/gemm.hip
-    gemm_big_kernel), so the split is sized for ~256 of ITS tiles (sizing it for 128 x 128 tiles
-    left 1536 x 384 at 180 workgroups)."""
-    tiles = math.ceil(n_out / 256) * math.ceil(k_out / 192)
+    the TN products run on the direct-to-LDS kernel at one workgroup per CU (csrc/gemm.hip
+    gemm_tn_dma_kernel: 384 x 192 tiles where n_out % 384 == 0, else 256 x 192), so the split is
+    sized for ~256 of ITS tiles."""
+    bm = _TN_BM if n_out % 384 == 0 else 256
+    tiles = math.ceil(n_out / bm) * math.ceil(k_out / 192)
     want = max(1, 256 // tiles)
     return int(max(1, min(want, m_red // 256, 64)))
 
