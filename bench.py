@@ -206,10 +206,10 @@ def kernel_probes(model, B, reps=20):
     do = rnd(B, L, D)
     bgrad = torch.zeros(3 * D, dtype=torch.float32, device=dev)
     res_b = K.attn_bwd_resident(L, Dh)
-    add("attn_bwd", "attn_bwd_res_kernel" if res_b else "attn_bwd_dkdv_kernel",
+    add("attn_bwd", "attn_bwd_res" if res_b else "attn_bwd_dkdv_kernel",  # res / res8 kernels
         lambda: K.attn_bwd(qkv, o, do, lse, H, scale, table, bits, kpa, bias_grad=bgrad),
         "mfma", 2.5 * fwd_flops,
-        ("one two-phase kernel (dQ; dK / dV)" if res_b else "dQ + dK/dV kernels together")
+        ("one resident kernel (dQ beside dK / dV)" if res_b else "dQ + dK/dV kernels together")
         + ": 2.5 x the forward count (flash-attention convention)",
         B * L * (3 * D + 2 * D + 3 * D) * 2 + B * H * L * 8)
     # 6. ToMe matching and merge forward of block 0 (metric = K of the image set, fp32 residual)

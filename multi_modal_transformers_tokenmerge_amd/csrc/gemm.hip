@@ -2189,6 +2189,12 @@ int nt_bn(int M, int N, int K, int transA, int transB, int batch, int out_kind, 
 // (hipBLASLt) used to take — narrow outputs over a long reduction (N <= 768, K >= 1152) and the
 // bias-free relu product of the frozen T5 (N >= 2048, K <= 1024); g_variant 8 forces it wherever
 // it applies. Epilogues: none, bf16 residual, relu.
+// MMT_NTWS (see mmt_gemm): 0 off, 1 the 192-wide-tile shapes, 2 every bf16 product it takes
+int ntws_mode() {
+  static const int m = getenv("MMT_NTWS") ? atoi(getenv("MMT_NTWS")) : 1;
+  return m;
+}
+
 bool ntw_ok(int M, int N, int K, int transA, int transB, int batch, int out_kind, const Epi& e) {
   if (transA || !transB || batch != 1 || out_kind != 0 || N % 192 != 0 || K % 64 != 0) return false;
   if (e.bias || e.rng || e.gate || e.relu_bits || e.gate_bits || e.colsum || e.alpha != 1.f ||
@@ -2198,7 +2204,7 @@ bool ntw_ok(int M, int N, int K, int transA, int transB, int batch, int out_kind
   if (g_variant >= 0 && g_variant != 8) return false;
   if (g_variant == 8) return true;
   const bool narrow = N <= 768 && K >= 1152 && e.act == MMT_ACT_NONE;
-  const bool relu = e.act == MMT_ACT_RELU && !e.residual && N >= 2048 && K <= 1024;
+  const bool relu = e.act == MMT_ACT_RELU && !e.residual && N >= 2048 && K <= 1024 && ntws_mode() != 2;
   return (narrow || relu) && M >= 8192;
 }
 
@@ -2357,7 +2363,7 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
   // MMT_NTWS: 0 off, 1 (default) where nt256 would take 192-wide tiles (N % 256 != 0: the QKV
   // projection, 209 vs 247 us at B = 512), 2 everywhere (the 256-wide nt256 tiles measured
   // faster: MLP up 284 vs 299 us, gated dX 252 vs 289; tools/ntws_bench.py)
-  static const int g_ntws = getenv("MMT_NTWS") ? atoi(getenv("MMT_NTWS")) : 1;
+  const int g_ntws = ntws_mode();
   if (g_ntws && (g_ntws == 2 || N % 256 != 0) && g_variant < 0 && !transA && transB && batch == 1 &&
       out_kind == 0 && final_kind == 0 &&
       K % 64 == 0 && N % 128 == 0 && N >= 1024 && M >= 4096 && !epi.gate && epi.beta == 0.f &&

@@ -287,54 +287,7 @@ __global__ __launch_bounds__(FUSED_NT) void tome_match_fused_kernel(
   const int lr = lane % LPR, rbase = lane - lr;
   const int nch = c / 8;
   const T* mb = metric + (int64_t)b * s_n;
-  constexpr int RPI = FUSED_NT / LPR;  // token rows per pass
-  int r0 = 0;
-  if constexpr (sizeof(T) == 2) {
-    // bf16 metric, up to 8 heads: two passes' loads (the raw 16-B chunks) issued together, so a
-    // workgroup waits one HBM round trip per two passes instead of one per pass
-    for (; heads <= 8 && r0 + RPI < t; r0 += 2 * RPI) {  // uniform trip count
-      uint4 raw[2][8];
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int tok = min(r0 + k * RPI + (int)threadIdx.x / LPR, t - 1);
-        const T* p = mb + (int64_t)tok * s_t + min(lr, nch - 1) * 8;
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          raw[k][u] = *reinterpret_cast<const uint4*>(p + (int64_t)min(u, heads - 1) * s_h);
-      }
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int tok = r0 + k * RPI + threadIdx.x / LPR;
-        const bool mine = tok < t && lr < nch;
-        float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int u = 0; u < 8; ++u)  // the heads in ascending order, as head_sum
-          if (u < heads) {
-            const uint32_t w[4] = {raw[k][u].x, raw[k][u].y, raw[k][u].z, raw[k][u].w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              m[2 * q] = m[2 * q] + __uint_as_float(w[q] << 16);
-              m[2 * q + 1] = m[2 * q + 1] + __uint_as_float(w[q] & 0xffff0000u);
-            }
-          }
-        float ss = 0.f;
-        for (int j = 0; j < nch; ++j) {
-          if (lr == j) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) ss = __fmaf_rn(m[q], m[q], ss);
-          }
-          ss = __shfl(ss, rbase + j, 64);
-        }
-        if (mine) {
-          const float nrm = __fsqrt_rn(ss);
-          float* o = ((tok & 1) ? Bs : As) + (tok >> 1) * cs + lr * 8;
-#pragma unroll
-          for (int q = 0; q < 8; ++q) o[q] = __fdiv_rn(m[q], nrm);
-        }
-      }
-    }
-  }
-  for (; r0 < t; r0 += RPI) {  // uniform trip count: the shuffles below
+  for (int r0 = 0; r0 < t; r0 += FUSED_NT / LPR) {  // uniform trip count: the shuffles below
     const int tok = r0 + threadIdx.x / LPR;
     const bool mine = tok < t && lr < nch;
     float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};

@@ -38,6 +38,16 @@ def main():
         "qkv (bias)": (2 * M0 * 1152 * 384, 6, lambda: K.gemm(x0, wq, False, True, out=q, bias=bq,
                                                                split_k=1)),
     }
+    # the frozen T5's products (B * 32 = 16,384 rows): QKV 2304 x 768 and the relu FF input
+    # 3072 x 768 (arm "nt256" = variant 6 / 8: the 192-wide nt256 tiles / the narrow kernel)
+    Mt = B * 32
+    xt, wqt = rnd(Mt, 768), rnd(2304, 768)
+    qt = torch.empty((Mt, 2304), dtype=torch.bfloat16, device=dev)
+    wf = rnd(3072, 768)
+    ft = torch.empty((Mt, 3072), dtype=torch.bfloat16, device=dev)
+    cases["t5 qkv"] = (2 * Mt * 2304 * 768, 6, lambda: K.gemm(xt, wqt, False, True, out=qt, split_k=1))
+    cases["t5 ff_in relu"] = (2 * Mt * 3072 * 768, 8, lambda: K.gemm(xt, wf, False, True, out=ft,
+                                                                       act=K.ACT_RELU, split_k=1))
     res = {k: {"ws": [], "nt256": []} for k in cases}
     for rnd_i in range(3):
         for name, (fl, var, fn) in cases.items():
