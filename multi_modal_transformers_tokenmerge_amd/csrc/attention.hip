@@ -349,7 +349,10 @@ __global__ __launch_bounds__(64 * NW, DH > 128 ? 1 : 2) void attn_fwd_kernel(
   constexpr int NS = DH / 16;   // k-steps over the head dim
   constexpr int ND = DH / 32;   // 32-row d sub-tiles of O^T
   constexpr int TILE = KT * STR;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE];  // [buf][K | V]
+  // [buf][K | V]; the one-wave form (L <= 32: one key tile) keeps a single buffer, so twice as
+  // many of its workgroups fit a CU's LDS (the T5 layers: 6,144 one-wave workgroups)
+  constexpr int NBUF = NW == 1 ? 1 : 2;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * NBUF * TILE];
   // visibility word of every (query set, 64-key tile) pair, built once per workgroup
   __shared__ uint64_t s_vis[MAX_SETS * (MAXL / KT)];
   const int b = blockIdx.z, h = blockIdx.y;
@@ -414,9 +417,17 @@ __global__ __launch_bounds__(64 * NW, DH > 128 ? 1 : 2) void attn_fwd_kernel(
       if (mask.causal) vm = causal_keys(mask, sq[i], qrow[i], kt, vm);
       if (__all(vm == 0ull)) continue;  // no query of this block sees the tile
       const int q = qrow[i];
+      // the tile's second 32-key half lies past L (the T5's L = 32, a last tile of <= 32 keys):
+      // skipped whole (its scores would all be masked, its probabilities 0)
+      const int nu = kt + 32 < L ? 2 : 1;  // wave-uniform
       floatx16 sacc[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
+        if (u >= nu) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sacc[u][r] = -INFINITY;
+          continue;
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) sacc[u][r] = 0.f;
 #pragma unroll
@@ -430,6 +441,7 @@ __global__ __launch_bounds__(64 * NW, DH > 128 ? 1 : 2) void attn_fwd_kernel(
         for (int u = 0; u < 2; ++u)
 #pragma unroll
           for (int r4 = 0; r4 < 4; ++r4) {
+            if (u >= nu) continue;
             const int k4 = kt + 32 * u + 8 * r4 + 4 * hh;
             const float4 bv = *reinterpret_cast<const float4*>(brow + min(k4, L - 4));
             const float kb = k4 < L ? LOG2E : 0.f;
@@ -442,6 +454,7 @@ __global__ __launch_bounds__(64 * NW, DH > 128 ? 1 : 2) void attn_fwd_kernel(
       if (!__all(vm == ~0ull)) {  // partially visible tile: masked scores -> -inf
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
+          if (u >= nu) continue;
           const uint32_t w = (uint32_t)(vm >> (32 * u)) >> (4 * hh);
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -453,8 +466,9 @@ __global__ __launch_bounds__(64 * NW, DH > 128 ? 1 : 2) void attn_fwd_kernel(
       float tmax = -INFINITY;
 #pragma unroll
       for (int u = 0; u < 2; ++u)
+        if (u < nu)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sacc[u][r]);
+          for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sacc[u][r]);
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float mn = fmaxf(m[i], tmax);
       const float mnc = mn == -INFINITY ? 0.f : mn * c;
@@ -465,6 +479,7 @@ __global__ __launch_bounds__(64 * NW, DH > 128 ? 1 : 2) void attn_fwd_kernel(
       const float2v cc = {c, c}, mm = {-mnc, -mnc};
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
+        if (u >= nu) continue;
         TileMasks<16> dm;  // dropout lane masks of (query word, key sub-tile): scalar loads
         if constexpr (DROP) dm.load(drop_q, drop_lp, (q0 >> 5) + wave + NW * i, kt + 32 * u);
 #pragma unroll
@@ -499,6 +514,7 @@ __global__ __launch_bounds__(64 * NW, DH > 128 ? 1 : 2) void attn_fwd_kernel(
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
+        if (u >= nu) continue;
         const bf16x8 p0 = pack_frag(sacc[u], 0), p1 = pack_frag(sacc[u], 1);
 #pragma unroll
         for (int d = 0; d < ND; ++d) {
@@ -509,14 +525,22 @@ __global__ __launch_bounds__(64 * NW, DH > 128 ? 1 : 2) void attn_fwd_kernel(
         }
       }
     }
-    if (kn < L) pf.store(smem + (buf ^ 1) * 2 * TILE, smem + (buf ^ 1) * 2 * TILE + TILE);
-    __syncthreads();
-    buf ^= 1;
+    if constexpr (NBUF == 2) {
+      if (kn < L) pf.store(smem + (buf ^ 1) * 2 * TILE, smem + (buf ^ 1) * 2 * TILE + TILE);
+      __syncthreads();
+      buf ^= 1;
+    } else {  // single buffer: refill after every wave is done with it (never taken at L <= 64)
+      __syncthreads();
+      if (kn < L) {
+        pf.store(smem, smem + TILE);
+        __syncthreads();
+      }
+    }
     kt = kn;
   }
   // O, scaled and rounded to bf16: with NQ = 2 through LDS (the idle K/V buffers: one 32-row
   // region per wave and query block) as whole-row stores (L = 212: 71.2 -> 67.9 us)
-  static_assert(NW * NQ * 32 <= 4 * KT, "O staging regions must fit the K/V buffers");
+  static_assert(NQ == 1 || NW * NQ * 32 <= 2 * NBUF * KT, "O staging regions must fit the K/V buffers");
 #pragma unroll
   for (int i = 0; i < NQ; ++i) {
     if (!live[i]) continue;  // wave-uniform

@@ -430,6 +430,41 @@ __global__ void rmsnorm_fwd_kernel(const bf16_t* __restrict__ x, int64_t rows, i
   if (row >= rows) return;
   const bf16_t* xr = x + row * D;
   float s = 0.f;
+  if (D <= 1024) {
+    // the row read once: both of a lane's chunks (and the weight's) loaded together, unconditional
+    // (a lane past D reads chunk 0 and drops it); same sums in the same order as the loop below
+    const int c0 = lane * 8, c1 = c0 + 512;
+    const bool h0 = c0 < D, h1 = c1 < D;
+    const uint4 u0 = *reinterpret_cast<const uint4*>(xr + (h0 ? c0 : 0));
+    const uint4 u1 = *reinterpret_cast<const uint4*>(xr + (h1 ? c1 : 0));
+    const uint4 w0 = *reinterpret_cast<const uint4*>(w + (h0 ? c0 : 0));
+    const uint4 w1 = *reinterpret_cast<const uint4*>(w + (h1 ? c1 : 0));
+    float f0[8], f1[8];
+    unpack8(u0, f0);
+    unpack8(u1, f1);
+    if (h0)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += f0[e] * f0[e];
+    if (h1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += f1[e] * f1[e];
+    s = wave_sum(s);
+    const float rs = rsqrtf(s / D + eps);
+    float g[8];
+    if (h0) {
+      unpack8(w0, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f0[e] = f0[e] * rs * g[e];
+      *reinterpret_cast<uint4*>(y + row * D + c0) = pack8(f0);
+    }
+    if (h1) {
+      unpack8(w1, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f1[e] = f1[e] * rs * g[e];
+      *reinterpret_cast<uint4*>(y + row * D + c1) = pack8(f1);
+    }
+    return;
+  }
   for (int c = lane * 8; c < D; c += 512) {
     float f[8];
     unpack8(*reinterpret_cast<const uint4*>(xr + c), f);
