@@ -484,9 +484,10 @@ __global__ __launch_bounds__(NT) void colsum_kernel(const T* __restrict__ x, int
                                                     const uint32_t* __restrict__ rng,
                                                     uint32_t layer, uint32_t site, uint32_t thresh,
                                                     float scale, int64_t row_offset,
-                                                    bf16_t* __restrict__ z, int64_t ldz) {
+                                                    bf16_t* __restrict__ z, int64_t ldz,
+                                                    int rows_per) {
   __shared__ float red[RG * CW];
-  const int c0 = blockIdx.x * CW, r0 = blockIdx.y * CS_ROWS;
+  const int c0 = blockIdx.x * CW, r0 = blockIdx.y * rows_per;
   const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;
   const int col = c0 + cv * 8;
   const bool cok = col < N;
@@ -494,7 +495,7 @@ __global__ __launch_bounds__(NT) void colsum_kernel(const T* __restrict__ x, int
   if (rng) key = stream_key(rng[0], rng[1], layer, site);
   float part[1][8] = {};
   if (cok)
-    for (int m = r0 + rg; m < min(M, r0 + CS_ROWS); m += RG) {
+    for (int m = r0 + rg; m < min(M, r0 + rows_per); m += RG) {
       float f[8];
       load8(x + (int64_t)m * ldx + col, f);
       if (rng) {
@@ -514,6 +515,15 @@ __global__ __launch_bounds__(NT) void colsum_kernel(const T* __restrict__ x, int
 }
 
 inline bool is_dt(int d) { return d == MMT_F32 || d == MMT_BF16; }
+
+// rows per column-sum workgroup: CS_ROWS, fewer (down to RG) when that leaves the launch under
+// ~512 workgroups (the bias-gradient slabs: 552 x 1536 floats gave 72 workgroups, 16 us)
+inline int colsum_rows(int M, int N) {
+  const int cb = (N + CW - 1) / CW;
+  int r = CS_ROWS;
+  while (r > RG && (int64_t)cb * ((M + r - 1) / r) < 512) r /= 2;
+  return r;
+}
 
 }  // namespace
 
@@ -602,14 +612,15 @@ extern "C" int mmt_colsum(const void* x, int dtype, int64_t ldx, int M, int N, f
                           mmt_stream_t stream) {
   MMT_CHECK_ARG(x && out && M > 0 && N > 0 && N % 8 == 0 && ldx % 8 == 0 && is_dt(dtype),
                 "mmt_colsum: bad args");
-  dim3 grid((N + CW - 1) / CW, (M + CS_ROWS - 1) / CS_ROWS);
+  const int rows_per = colsum_rows(M, N);
+  dim3 grid((N + CW - 1) / CW, (M + rows_per - 1) / rows_per);
   if (dtype == MMT_F32)
     hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(NT), 0, as_stream(stream), (const float*)x,
-                       ldx, M, N, out, nullptr, 0u, 0u, 0u, 1.f, (int64_t)0, nullptr, (int64_t)0);
+                       ldx, M, N, out, nullptr, 0u, 0u, 0u, 1.f, (int64_t)0, nullptr, (int64_t)0, rows_per);
   else
     hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(NT), 0, as_stream(stream),
                        (const bf16_t*)x, ldx, M, N, out, nullptr, 0u, 0u, 0u, 1.f, (int64_t)0,
-                       nullptr, (int64_t)0);
+                       nullptr, (int64_t)0, rows_per);
   MMT_CHECK_LAUNCH("mmt_colsum");
   return MMT_OK;
 }
@@ -622,16 +633,17 @@ extern "C" int mmt_dropout_bwd(const void* dy, int dtype, int64_t ldy, int M, in
                     is_dt(dtype),
                 "mmt_dropout_bwd: bad args");
   MMT_CHECK_ARG(keep_prob > 0.f && keep_prob <= 1.f, "mmt_dropout_bwd: keep_prob");
-  dim3 grid((N + CW - 1) / CW, (M + CS_ROWS - 1) / CS_ROWS);
+  const int rows_per = colsum_rows(M, N);
+  dim3 grid((N + CW - 1) / CW, (M + rows_per - 1) / rows_per);
   const uint32_t th = rng ? keep_threshold16(keep_prob) : 0u;
   const float sc = rng ? 1.f / keep_prob : 1.f;
   if (dtype == MMT_F32)
     hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(NT), 0, as_stream(stream), (const float*)dy,
-                       ldy, M, N, colsum, rng, layer, site, th, sc, row_offset, (bf16_t*)dz, ldz);
+                       ldy, M, N, colsum, rng, layer, site, th, sc, row_offset, (bf16_t*)dz, ldz, rows_per);
   else
     hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(NT), 0, as_stream(stream),
                        (const bf16_t*)dy, ldy, M, N, colsum, rng, layer, site, th, sc, row_offset,
-                       (bf16_t*)dz, ldz);
+                       (bf16_t*)dz, ldz, rows_per);
   MMT_CHECK_LAUNCH("mmt_dropout_bwd");
   return MMT_OK;
 }
