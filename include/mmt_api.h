@@ -197,9 +197,13 @@ typedef struct {
    *   f = (m / 16) & 3, n = 256 (w / 8) + 128 ((w / 4) & 1) + 8 (w & 3) + 32 c + e (c < 4,
    *   e < 8): one 16-B vector per lane of that path's epilogue (its 4 rows x 32 columns);
    * gate_bits (in): the same layout, used in place of gate (v *= bit ? gate_scale : 0), so a
-   *   backward reads M*N/8 bytes instead of the bf16 gate's 2*M*N. NULL: unused. */
+   *   backward reads M*N/8 bytes instead of the bf16 gate's 2*M*N. NULL: unused.
+   * keep_bits (in, relu_bits launches only, rng NULL): the dropout keep decisions in the same
+   *   layout (mmt_gemm_dropout_keep_bits), applied as v = bit ? v / keep_prob : 0 in place of the
+   *   counter-RNG draws — bit-identical outputs, the draws moved off the GEMM. NULL: unused. */
   uint32_t* relu_bits;
   const uint32_t* gate_bits;
+  const uint32_t* keep_bits;
 } mmt_epilogue_t;
 
 /* Tuning knob (benchmarks): 0 = 128x128 register-staged, double-buffered LDS; 1 = same, single
@@ -210,6 +214,12 @@ void mmt_gemm_set_variant(int variant);
 /* Rows of the epilogue's colsum slab for this launch shape (ceil(M / 256)), 0 when the kernel the
  * launch would use cannot write it (then take the column sums with mmt_colsum). */
 int mmt_gemm_colsum_rows(int M, int N, int K, int transA, int transB, int c_mode, int split_k);
+/* The keep_bits words of an (M, N) output's counter-RNG dropout (stream (rng, layer, site), rows
+ * offset by row_offset: the draws mmt_gemm's epilogue would make with the same fields) into out
+ * ([ceil(M/256)*256][N/32] words, 16-B aligned; N % 256 == 0). Replaces the per-element dropout
+ * draws of the MLP hidden layer (attention.py:20-39 MLPBlock, nn.Dropout after the relu). */
+int mmt_gemm_dropout_keep_bits(const uint32_t* rng, uint32_t layer, uint32_t site, int M, int N,
+                               float keep_prob, int64_t row_offset, uint32_t* out, mmt_stream_t stream);
 int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t lda, const void* B,
              int transB, int64_t ldb, void* C, int c_mode, int64_t ldc, int batch, int64_t sA,
              int64_t sB, int64_t sC, int split_k, const mmt_epilogue_t* epi, float* workspace,

@@ -21,7 +21,8 @@ class Epilogue(ctypes.Structure):
     _fields_ = [("bias", P), ("act", I), ("rng", P), ("drop_layer", U32), ("drop_site", U32),
                 ("keep_prob", F), ("drop_row_offset", L), ("gate", P), ("ld_gate", L),
                 ("gate_scale", F), ("residual", P), ("ld_res", L), ("alpha", F), ("beta", F),
-                ("res_dtype", I), ("colsum", P), ("relu_bits", P), ("gate_bits", P)]
+                ("res_dtype", I), ("colsum", P), ("relu_bits", P), ("gate_bits", P),
+                ("keep_bits", P)]
 
 
 # name -> argtypes (every entry point returns int status unless listed in _VOID)
@@ -42,6 +43,7 @@ SIGNATURES: dict[str, list] = {
     "mmt_topk_scatter_bwd": [P, I, I, I, I, L, L, P, I, P, L, L, P],
     "mmt_gemm_set_variant": [I],
     "mmt_gemm_colsum_rows": [I, I, I, I, I, I, I],
+    "mmt_gemm_dropout_keep_bits": [P, U32, U32, I, I, F, L, P, P],
     "mmt_gemm": [I, I, I, P, I, L, P, I, L, P, I, L, I, L, L, L, I, P, P, L, P],
     "mmt_quant_rows_fp8": [P, L, I, I, P, L, P, P],
     "mmt_gemm_fp8": [I, I, I, P, L, P, P, L, P, P, I, L, P, P],

@@ -143,11 +143,12 @@ ACT_NONE, ACT_RELU = 0, 1
 
 def _epi(bias=None, act=ACT_NONE, rng=None, drop_layer=0, drop_site=0, keep_prob=1.0,
          drop_row_offset=0, gate=None, gate_scale=1.0, residual=None, alpha=1.0, beta=0.0,
-         colsum=None, relu_bits=None, gate_bits=None):
+         colsum=None, relu_bits=None, gate_bits=None, keep_bits=None):
     e = _C.Epilogue()
     e.colsum = ptr(colsum)
     e.relu_bits = ptr(relu_bits)
     e.gate_bits = ptr(gate_bits)
+    e.keep_bits = ptr(keep_bits)
     e.bias = ptr(bias)
     e.act = act
     e.rng = ptr(rng)
@@ -201,7 +202,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
     bias = epi.get("bias")
     if bias is not None and (bias.numel() != N or bias.dtype != torch.float32):
         raise ValueError("gemm bias must be fp32 [N]")
-    for name in ("relu_bits", "gate_bits"):
+    if epi.get("keep_bits") is not None and (epi.get("relu_bits") is None or epi.get("rng") is not None):
+        raise ValueError("gemm keep_bits replaces rng's dropout draws in a relu_bits launch")
+    for name in ("relu_bits", "gate_bits", "keep_bits"):
         t = epi.get(name)
         if t is not None:
             if not gemm_bits_supported(M, N, K, trans_a, trans_b, out_mode, split_k):
@@ -276,6 +279,23 @@ def gemm_bits_supported(M: int, N: int, K: int, trans_a: bool = False, trans_b: 
     """Whether gemm(..., relu_bits= / gate_bits=) works for this launch (the 256-wide bf16 NT
     path, the same launches that can write epilogue column sums)."""
     return gemm_colsum_rows(M, N, K, trans_a, trans_b, out_mode, 1 if split_k is None else split_k) > 0
+
+
+def gemm_dropout_keep_bits(rng: torch.Tensor, layer: int, site: int, M: int, N: int,
+                           keep_prob: float, row_offset: int = 0, out: torch.Tensor | None = None):
+    """The counter-RNG dropout keeps of an (M, N) gemm output in the relu_bits layout: pass as
+    gemm(..., relu_bits=, keep_bits=, keep_prob=) without rng for outputs bit-identical to
+    gemm(..., rng=, drop_layer=layer, drop_site=site, drop_row_offset=row_offset) — the draws run
+    as their own kernel (e.g. on a side stream) instead of in the GEMM epilogue."""
+    _dev(rng, out)
+    rows = -(-M // 256) * 256
+    if out is None:
+        out = torch.empty((rows, N // 32), dtype=torch.int32, device=rng.device)
+    if N % 256 or out.dtype != torch.int32 or tuple(out.shape) != (rows, N // 32) or not out.is_contiguous():
+        raise ValueError(f"gemm_dropout_keep_bits: N % 256 == 0, out contiguous int32 ({rows}, {N // 32})")
+    _C.call("mmt_gemm_dropout_keep_bits", ptr(rng), layer, site, M, N, keep_prob, row_offset, ptr(out),
+            _C.stream_ptr())
+    return out
 
 
 def gemm_colsum_rows(M: int, N: int, K: int, trans_a: bool = False, trans_b: bool = True,

@@ -57,6 +57,12 @@ _SIDE = {}
 
 
 _RELU_BITS = os.environ.get("MMT_RELU_BITS", "1") != "0"  # benchmarking knob: bf16 gate instead
+# MMT_KEEP_BITS=1: the MLP hidden dropout keeps drawn by their own kernel on the side queue
+# (beside attention) and read as bits by the MLP-up GEMM's epilogue instead of drawn there
+# (bit-identical outputs). Off by default: the MLP-up GEMM did not get faster (210.4 vs 209.7 us
+# average over the step) and the step lost 0.7 % (15.10k vs 15.20k samples/s, 3 interleaved
+# rounds) to the 27-66 us draw kernel beside attention — the epilogue's draws were not its cost.
+_KEEP_BITS = os.environ.get("MMT_KEEP_BITS", "0") == "1"
 
 
 def side_stream(device) -> torch.cuda.Stream:
@@ -250,12 +256,26 @@ class Encoder1DBlock(Bindable):
         y0, mu0, rs0 = self.ln0.fwd(x)
         qkv = self.qkv.fwd(y0.view(B * L, D)).view(B, L, 3 * D)
         tome_idx = None
+        Mh = self.mlp.dense.out_f
+
+        def relu_bits_ok(rows):
+            return (train and not self.mlp.dense.fp8 and _RELU_BITS
+                    and K.gemm_bits_supported(rows, Mh, D))
+        kbits = None
         if ctx.r > 0:  # ToMe matching needs only K: it runs beside attention + out-projection
             s0, t = ctx.sets.starts[ctx.tome_set], ctx.sets.lens[ctx.tome_set]
             metric = qkv.view(B, L, 3, H, Dh)[:, s0:s0 + t, 1]     # (B, t, H, Dh): sum_h K
+            L2p = L - ctx.r  # the merged length (no pruning in this block)
+            if (_KEEP_BITS and train and kp < 1.0 and ctx.prune is None and Mh % 256 == 0
+                    and relu_bits_ok(B * L2p)):
+                kbits = torch.empty((-(-B * L2p // 256) * 256, Mh // 32), dtype=torch.int32,
+                                    device=x.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 tome_idx = K.tome_match(metric, ctx.r)
+                if kbits is not None:
+                    K.gemm_dropout_keep_bits(ctx.rng, ctx.layer, DROP_MLP_HIDDEN, B * L2p, Mh, kp,
+                                             ctx.sample_offset * L2p, out=kbits)
         if train and kpa < 1:
             # the (L, L) attention keep mask (RNG state only), on the main stream: a 7 us launch
             # costs less than the cross-queue wait it took beside the QKV GEMM (~10 us idle)
@@ -294,12 +314,13 @@ class Encoder1DBlock(Bindable):
         y1, mu1, rs1 = ln1_done if ln1_done is not None else self.ln1.fwd(x1)
         # the relu gate of the backward as 1 bit per hidden unit where the launch supports it
         # (the gated dX then reads M*Mh/8 bytes instead of h's 2*M*Mh)
-        Mh = self.mlp.dense.out_f
         hbits = (torch.empty((-(-B * L2 // 256) * 256, Mh // 32), dtype=torch.int32, device=x.device)
-                 if train and not self.mlp.dense.fp8 and _RELU_BITS and K.gemm_bits_supported(B * L2, Mh, D)
-                 else None)
-        h = self.mlp.dense.fwd(y1.view(B * L2, D), act=K.ACT_RELU, relu_bits=hbits,
-                               **drop(DROP_MLP_HIDDEN, L2))
+                 if relu_bits_ok(B * L2) else None)
+        if kbits is not None and hbits is not None and L2 == L - ctx.r:
+            hdrop = dict(keep_bits=kbits, keep_prob=kp)   # (joined with the side queue above)
+        else:
+            hdrop = drop(DROP_MLP_HIDDEN, L2)
+        h = self.mlp.dense.fwd(y1.view(B * L2, D), act=K.ACT_RELU, relu_bits=hbits, **hdrop)
         x2 = self.mlp.dense_out.fwd(h, residual=x1.view(B * L2, D), out_mode=K.OUT_F32,
                                     **drop(DROP_MLP_OUT, L2))
         saved = dict(x=x, y0=y0, mu0=mu0, rs0=rs0, qkv=qkv, o=o, o_in=o_in, lse=lse, bits=bits,

@@ -107,6 +107,7 @@ struct Epi {
   float* colsum;  // nt256 only: per-256-row-panel column sums of the stored (bf16) C, or null
   uint32_t* relu_bits;         // nt256 BN 256 only: 1 bit per output, set iff stored bf16 > 0
   const uint32_t* gate_bits;   // nt256 BN 256 only: the gate in that 1-bit form
+  const uint32_t* keep_bits;   // nt256 relu_bits launches only: dropout keeps in that layout
 };
 
 // global -> registers for one 128 x 64 (K-contig) or 64 x 128 (MN-contig) operand tile.
@@ -921,6 +922,12 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
   constexpr bool BITS = BN == 256;  // the 1-bit gate layout is this tile's lane layout (Q = 32)
   static_assert(!GBITS || BITS, "1-bit gate only on 256-wide tiles");
   constexpr bool RBITS = BITS && !CS && !GBITS;  // relu_bits writer (a forward launch)
+  // keep_bits (RBITS launches): the dropout keeps precomputed in the relu_bits layout
+  // (mmt_gemm_dropout_keep_bits) replace the epilogue's counter-hash draws; the tile's word is
+  // loaded at its first K-step and held until its epilogue
+  const bool KBITS = RBITS && OUT == 0 && epi.keep_bits;
+  if (KBITS) rest.rng = nullptr;
+  uint4 kbw = make_uint4(0u, 0u, 0u, 0u);
   // GBITS: the gate comes as bits (gate_bits); otherwise as bf16 rows (gate) — one of the two
   // compiled per instantiation (both at once spill registers in the column-sum variant)
 
@@ -1114,6 +1121,11 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] *= ((w >> e) & 1u) ? epi.gate_scale : 0.f;
           }
+          if (KBITS) {
+            const uint32_t w = (mf == 0 ? kbw.x : mf == 1 ? kbw.y : mf == 2 ? kbw.z : kbw.w) >> (8 * c8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = ((w >> e) & 1u) ? v[e] * epi.drop_scale : 0.f;
+          }
           epilogue_w<8>(rest, key, N, gr, gc, v);
           if (RBITS && epi.relu_bits)  // stored bf16 > 0 <=> v > 0 (bf16 keeps fp32's exponent range)
 #pragma unroll
@@ -1226,6 +1238,11 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
     NT_STEP(s, 1);
     asm volatile("s_barrier" ::: "memory");  // K-step s landed for every wave; stage st^1 free
     NT_STEP(s, 2);
+    if (KBITS && kt == 0) {  // after the previous tile's epilogue (its word is in kbw until then)
+      const int tile = first + i * stride, tm = tile / tiles_n, tn = tile - tm * tiles_n;
+      kbw = reinterpret_cast<const uint4*>(epi.keep_bits)[(int64_t)(tm * 64 + wm * 16 + l15) * (N / 32) +
+                                                          (tn * 8 + wn * 4 + lq)];
+    }
     if (kt == 0) NT_TRACE(i, 0);
     if (s == 0) NT_CLK(0);
     int nm0 = 0, nn0 = 0, nk0 = 0;
@@ -2198,7 +2215,7 @@ int ntws_mode() {
 
 bool ntw_ok(int M, int N, int K, int transA, int transB, int batch, int out_kind, const Epi& e) {
   if (transA || !transB || batch != 1 || out_kind != 0 || N % 192 != 0 || K % 64 != 0) return false;
-  if (e.bias || e.rng || e.gate || e.relu_bits || e.gate_bits || e.colsum || e.alpha != 1.f ||
+  if (e.bias || e.rng || e.gate || e.relu_bits || e.gate_bits || e.keep_bits || e.colsum || e.alpha != 1.f ||
       e.beta != 0.f || (e.residual && e.res_f32) || (e.residual && e.act != MMT_ACT_NONE) ||
       (e.act != MMT_ACT_NONE && e.act != MMT_ACT_RELU))
     return false;
@@ -2245,7 +2262,61 @@ NtwPlan ntw_plan(int M, int N) {
   return best;
 }
 
+// Dropout keeps of one (M, N) output in the relu_bits word layout (include/mmt_api.h): thread =
+// one 16-B word group (4 rows x 32 columns), the same keep_elem draws the nt256 epilogue makes
+// (pair counter ((row_offset + row) * N + col) / 2, 32-bit wrap included), so a launch that takes
+// them as keep_bits stores bit-identical outputs. Pure VALU (64 mixer evaluations per thread, one
+// 16-B store): it runs on a side queue beside attention.
+__global__ __launch_bounds__(256) void dropout_keep_words_kernel(const uint32_t* __restrict__ rng,
+                                                                 uint32_t layer, uint32_t site,
+                                                                 uint32_t thresh16, int M, int N,
+                                                                 int64_t row_off, uint4* __restrict__ out,
+                                                                 int64_t n_words) {
+  const uint32_t key = stream_key(rng[0], rng[1], layer, site);
+  const int wpr = N / 32;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < n_words; idx += (int64_t)gridDim.x * 256) {
+    const int64_t g = idx / wpr;
+    const int w = (int)(idx - g * wpr);
+    const int row0 = (int)(g >> 6) * 256 + (int)((g >> 4) & 3) * 64 + (int)(g & 15);
+    const int col0 = 256 * (w >> 3) + 128 * ((w >> 2) & 1) + 8 * (w & 3);
+    uint32_t o[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int r = row0 + 16 * f;
+      uint32_t word = 0u;
+      if (r < M) {
+        const uint32_t base = (uint32_t)((row_off + r) * (int64_t)N + col0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) {
+            const uint32_t d = pair_draw(key, (base + 32 * c + e) >> 1);
+            word |= ((d & 0xffffu) < thresh16 ? 1u : 0u) << (8 * c + e);
+            word |= ((d >> 16) < thresh16 ? 1u : 0u) << (8 * c + e + 1);
+          }
+      }
+      o[f] = word;
+    }
+    out[idx] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 }  // namespace
+
+extern "C" int mmt_gemm_dropout_keep_bits(const uint32_t* rng, uint32_t layer, uint32_t site, int M,
+                                          int N, float keep_prob, int64_t row_offset, uint32_t* out,
+                                          mmt_stream_t stream) {
+  MMT_CHECK_ARG(rng && out && M > 0 && N > 0 && N % 256 == 0 && keep_prob > 0.f && keep_prob <= 1.f &&
+                    (uintptr_t)out % 16 == 0,
+                "mmt_gemm_dropout_keep_bits: args (N %% 256 == 0, keep_prob in (0, 1], 16-B aligned out)");
+  const int64_t n_words = (int64_t)((M + 255) / 256) * 64 * (N / 32);
+  const int blocks = (int)std::min<int64_t>((n_words + 255) / 256, 16384);
+  hipLaunchKernelGGL(dropout_keep_words_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), rng, layer,
+                     site, keep_threshold16(keep_prob), M, N, row_offset, reinterpret_cast<uint4*>(out),
+                     n_words);
+  MMT_CHECK_LAUNCH("mmt_gemm_dropout_keep_bits");
+  return MMT_OK;
+}
 
 extern "C" int mmt_gemm_colsum_rows(int M, int N, int K, int transA, int transB, int c_mode,
                                     int split_k) {
@@ -2298,6 +2369,11 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     MMT_CHECK_ARG(!(e->gate && e->gate_bits), "mmt_gemm: gate and gate_bits are exclusive");
     MMT_CHECK_ARG(!(e->relu_bits && (e->gate_bits || e->colsum)),
                   "mmt_gemm: relu_bits is a forward output (no gate_bits / colsum in that launch)");
+    MMT_CHECK_ARG(!e->keep_bits || (e->relu_bits && !e->rng && e->keep_prob > 0.f &&
+                                    e->keep_prob <= 1.f && (uintptr_t)e->keep_bits % 16 == 0),
+                  "mmt_gemm: keep_bits needs relu_bits, no rng, keep_prob in (0, 1], 16-B alignment");
+    epi.keep_bits = e->keep_bits;
+    if (e->keep_bits) epi.drop_scale = 1.f / e->keep_prob;
     epi.colsum = e->colsum;
     MMT_CHECK_ARG((!e->gate || (e->ld_gate % 8 == 0 && (uintptr_t)e->gate % 16 == 0)) &&
                       (!e->residual || (e->ld_res % 8 == 0 && (uintptr_t)e->residual % 16 == 0)),
@@ -2368,7 +2444,7 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
   if (g_ntws && (g_ntws == 2 || N % 256 != 0) && g_variant < 0 && !transA && transB && batch == 1 &&
       out_kind == 0 && final_kind == 0 &&
       K % 64 == 0 && N % 128 == 0 && N >= 1024 && M >= 4096 && !epi.gate && epi.beta == 0.f &&
-      (!epi.bias || N <= WS_BIAS) && !(epi.colsum && epi.relu_bits)) {
+      (!epi.bias || N <= WS_BIAS) && !(epi.colsum && epi.relu_bits) && !epi.keep_bits) {
     const int tn = N / 128, n_tiles = ((M + 255) / 256) * tn;
     int grid = std::min(n_tiles, cu_count());
     if (grid > 8) grid &= ~7;
@@ -2560,6 +2636,7 @@ extern "C" int mmt_gemm_fp8(int M, int N, int K, const void* A, int64_t lda, con
     MMT_CHECK_ARG(!(e->gate && e->gate_bits), "mmt_gemm: gate and gate_bits are exclusive");
     MMT_CHECK_ARG(!(e->relu_bits && (e->gate_bits || e->colsum)),
                   "mmt_gemm: relu_bits is a forward output (no gate_bits / colsum in that launch)");
+    MMT_CHECK_ARG(!e->keep_bits, "mmt_gemm_fp8: keep_bits is a bf16 nt path epilogue (use rng)");
   }
   const int tiles_n = (N + F8_BN - 1) / F8_BN, n_work = ((M + F8_BM - 1) / F8_BM) * tiles_n;
   hipStream_t s = as_stream(stream);

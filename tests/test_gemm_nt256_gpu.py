@@ -177,6 +177,34 @@ def test_relu_bits_and_gate_bits(dev, M):
     assert torch.equal(d_a, d_c)
 
 
+@pytest.mark.parametrize("M,row_off", [(11264, 0), (11000, 7 * 11000), (149504, 512 * 292)])
+def test_keep_bits_match_epilogue_draws(dev, M, row_off):
+    """MLP hidden dropout from precomputed keep bits (gemm_dropout_keep_bits + keep_bits=): the
+    words equal the oracle's counter-RNG keeps (oracle/rng.py) under the relu_bits layout, and the
+    MLP-up output and its relu_bits are bit-identical to the epilogue-draw launch."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    N, K = 1536, 384
+    g = torch.Generator().manual_seed(M + 1)
+    y, w1 = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    bias = (torch.randn(N, generator=g) * 0.5).to(dev)
+    rng = torch.tensor([21, 5], dtype=torch.int32, device=dev)
+    kb = Kn.gemm_dropout_keep_bits(rng, 4, 2, M, N, 0.9, row_off)
+    if M <= 12000:  # the oracle's mask (numpy) at the small sizes
+        keep = torch.from_numpy(R.dropout_mask_2d(21, 5, 4, 2, M, N, row_off, 0.9)).to(dev)
+        assert torch.equal(_bits_to_mask(kb, M, N), keep)
+    rows = -(-M // 256) * 256
+    b1 = torch.empty((rows, N // 32), dtype=torch.int32, device=dev)
+    b2 = torch.empty_like(b1)
+    h1 = Kn.gemm(y, w1, False, True, bias=bias, act=Kn.ACT_RELU, rng=rng, drop_layer=4, drop_site=2,
+                 keep_prob=0.9, drop_row_offset=row_off, relu_bits=b1)
+    h2 = Kn.gemm(y, w1, False, True, bias=bias, act=Kn.ACT_RELU, keep_bits=kb, keep_prob=0.9,
+                 relu_bits=b2)
+    assert torch.equal(h1, h2)
+    assert torch.equal(b1, b2)
+    with pytest.raises(ValueError):  # keep_bits replaces rng, only in a relu_bits launch
+        Kn.gemm(y, w1, False, True, keep_bits=kb, keep_prob=0.9)
+
+
 def test_bits_rejected_off_the_256_path(dev):
     from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
     M, N, K = 300, 1536, 384
