@@ -2205,8 +2205,9 @@ int nt_bn(int M, int N, int K, int transA, int transB, int batch, int out_kind, 
 
 // Whether the narrow-output NT kernel (gemm_ntw_kernel) runs this launch: products the library
 // (hipBLASLt) used to take — narrow outputs over a long reduction (N <= 768, K >= 1152) and the
-// bias-free relu product of the frozen T5 (N >= 2048, K <= 1024); g_variant 8 forces it wherever
-// it applies. Epilogues: none, bf16 residual, relu.
+// bias-free relu product of the frozen T5 (N >= 2048, K <= 1024) — and the T5's plain QKV and
+// o-projection products where they measured faster here; g_variant 8 forces it wherever it
+// applies. Epilogues: none, bf16 residual, relu.
 // MMT_NTWS (see mmt_gemm): 0 off, 1 the 192-wide-tile shapes, 2 every bf16 product it takes
 int ntws_mode() {
   static const int m = getenv("MMT_NTWS") ? atoi(getenv("MMT_NTWS")) : 1;
@@ -2223,7 +2224,14 @@ bool ntw_ok(int M, int N, int K, int transA, int transB, int batch, int out_kind
   if (g_variant == 8) return true;
   const bool narrow = N <= 768 && K >= 1152 && e.act == MMT_ACT_NONE;
   const bool relu = e.act == MMT_ACT_RELU && !e.residual && N >= 2048 && K <= 1024 && ntws_mode() != 2;
-  return (narrow || relu) && M >= 8192;
+  // the frozen T5's other products at small batch (M = 32 B; tools/t5_small_probe.py, us per
+  // launch, automatic choice vs this kernel): the plain QKV product 2304 x 768 at M 4096 / 8192
+  // (30.1 / 46.9 vs 23.8 / 36.5; equal at 16384), the o-projection + residual 768 x 768 at
+  // M 8192 / 16384 (21.9 / 34.1 vs 20.4 / 29.0), the relu product from M 4096 (28.9 vs 25.6)
+  const bool wide_plain = e.act == MMT_ACT_NONE && !e.residual && N >= 2048 && K <= 1024;
+  const bool square_res = e.residual && N == 768 && K <= 1024;
+  return ((narrow || square_res) && M >= 8192) || (relu && M >= 4096) ||
+         (wide_plain && M >= 4096 && M <= 8192);
 }
 
 // Launch plan of gemm_ntw_kernel: tile width bn (192 / 384), `rows_big` rows in full rounds of
