@@ -858,7 +858,7 @@ __device__ __forceinline__ void dma16(const void* base, int64_t bytes, void* lds
 #endif
 }
 
-template <int BN, int OUT, int SHV, int NS, bool CS = false, bool GBITS = false>
+template <int BN, int OUT, int SHV, int NS, bool CS = false, bool GBITS = false, bool KB = false>
 __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
     int64_t ldb, void* __restrict__ Cv, int64_t ldc, int tiles_n, int n_tiles, int xcd_order,
@@ -922,10 +922,12 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
   constexpr bool BITS = BN == 256;  // the 1-bit gate layout is this tile's lane layout (Q = 32)
   static_assert(!GBITS || BITS, "1-bit gate only on 256-wide tiles");
   constexpr bool RBITS = BITS && !CS && !GBITS;  // relu_bits writer (a forward launch)
-  // keep_bits (RBITS launches): the dropout keeps precomputed in the relu_bits layout
-  // (mmt_gemm_dropout_keep_bits) replace the epilogue's counter-hash draws; the tile's word is
-  // loaded at its first K-step and held until its epilogue
-  const bool KBITS = RBITS && OUT == 0 && epi.keep_bits;
+  // KB (keep_bits launches, a separate instantiation: the runtime-checked form cost the default
+  // MLP-up kernel 3 % through scalar-register spills): the dropout keeps precomputed in the
+  // relu_bits layout (mmt_gemm_dropout_keep_bits) replace the epilogue's counter-hash draws; the
+  // tile's word is loaded at its first K-step and held until its epilogue
+  static_assert(!KB || (RBITS && OUT == 0), "keep_bits only in the bf16 relu_bits launch");
+  constexpr bool KBITS = KB;
   if (KBITS) rest.rng = nullptr;
   uint4 kbw = make_uint4(0u, 0u, 0u, 0u);
   // GBITS: the gate comes as bits (gate_bits); otherwise as bf16 rows (gate) — one of the two
@@ -2498,7 +2500,11 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
                            M, N, K, (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, tn,
                            n_tiles, g_nt_xcd_order, epi);
       } else if (final_kind == 0) {
-        if (bn == 256) GN(256, 0, NT_SH256, 2);
+        if (bn == 256 && epi.keep_bits)  // relu_bits launch (checked above)
+          hipLaunchKernelGGL((gemm_nt256_kernel<256, 0, NT_SH256, 2, false, false, true>), dim3(grid),
+                             dim3(NT3), 0, s, M, N, K, (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc,
+                             tn, n_tiles, g_nt_xcd_order, epi);
+        else if (bn == 256) GN(256, 0, NT_SH256, 2);
         else if (bn == 192) GN(192, 0, -1, 2);
         else GN(128, 0, -1, 3);
       } else {
