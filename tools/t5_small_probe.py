@@ -26,8 +26,25 @@ def time_us(fn, n=20):
     return s.elapsed_time(e) * 1e3 / n
 
 
+def split_sweep(dev, Ms):
+    """The long-K product with residual (wo 768 x 3072) at split-K 1..4 (auto_split_k's range)."""
+    for M in Ms:
+        a = torch.randn((M, 3072), device=dev).bfloat16()
+        b = torch.randn((768, 3072), device=dev).bfloat16()
+        res = torch.randn((M, 768), device=dev).bfloat16()
+        ref = None
+        for sk in (1, 2, 3, 4):
+            out = torch.empty((M, 768), device=dev, dtype=torch.bfloat16)
+            t = time_us(lambda: K.gemm(a, b, False, True, out=out, residual=res, split_k=sk))
+            d = 0.0 if ref is None else (out.float() - ref).abs().max().item()
+            ref = out.float() if ref is None else ref
+            print(f"M={M:6d} wo+res split_k={sk}: {t:7.1f} us  max|diff| vs split 1 {d:.3g}", flush=True)
+
+
 def main():
     dev = torch.device("cuda")
+    if sys.argv[1:2] == ["--split"]:
+        return split_sweep(dev, [int(x) for x in sys.argv[2:]] or [2048, 4096, 8192])
     for M in [int(x) for x in sys.argv[1:]] or [4096, 8192, 16384]:
         for name, N, Kd, kw in SHAPES:
             a = torch.randn((M, Kd), device=dev).bfloat16()
