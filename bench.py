@@ -87,7 +87,7 @@ def algorithmic_flops_per_sample(model) -> float:
     return 3 * (tr + stem) + t5
 
 
-PROBE_KERNEL = "gemm_nt256_kernel<256, 0, 0, 2, false, false>"
+PROBE_KERNEL = "gemm_nt256_kernel<256, 0, 0, 2, false, false, false>"
 
 
 def _graph_time_us(launch, reps):
