@@ -33,7 +33,9 @@ class wgrad_overlap:
     def __init__(self, device):
         key = torch.device(device).index
         if key not in wgrad_overlap._streams:
-            wgrad_overlap._streams[key] = torch.cuda.Stream(device=device)
+            # MMT_WGRAD_PRIO (benchmarking): stream priority of the dW queue (-1 high, 0 default)
+            wgrad_overlap._streams[key] = torch.cuda.Stream(
+                device=device, priority=int(os.environ.get("MMT_WGRAD_PRIO", "0")))
         self.stream = wgrad_overlap._streams[key]
 
     enabled = os.environ.get("MMT_WGRAD_OVERLAP", "1") != "0"  # benchmarking knob
