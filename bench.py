@@ -192,6 +192,21 @@ def kernel_probes(model, B, reps=20):
         "mfma", 2.0 * M * D * Mh,
         f"M={Mh} N={D} K={M}, 2MNK (split-K GEMM + its combine kernel together)",
         2 * (M * Mh + M * D) + 8 * Mh * D)
+    # 3b./3c. the residual-stream products (fp32 out = fp32 residual + dropout(x W^T + b)):
+    # MLP Dense_1 and the attention out-projection of block 0 (reference attention.py:36-37,
+    # 59-63). HBM-bound: algorithmic bytes = A (bf16) + W (bf16) read, residual (fp32) read,
+    # out (fp32) written; the bias is negligible
+    for name, rows, kin, dn in (("res_dense1", M, Mh, blk.mlp.dense_out),
+                                ("res_outproj", B * L, D, blk.out)):
+        a_in = rnd(rows, kin)
+        res_in = rnd(rows, D, dt=torch.float32)
+        out_f = torch.empty((rows, D), dtype=torch.float32, device=dev)
+        add(name, "gemm_nres_kernel" if K.nres_ok(rows, D, kin) else "gemm_glds_nt_kernel",
+            lambda a_in=a_in, res_in=res_in, out_f=out_f, dn=dn: dn.fwd(
+                a_in, out=out_f, out_mode=K.OUT_F32, residual=res_in, rng=rng, drop_layer=0,
+                drop_site=3, keep_prob=0.9),
+            "hbm", 2 * (rows * kin + D * kin) + 8 * rows * D,
+            f"M={rows} N={D} K={kin}: read A bf16 + W bf16 + residual fp32, write C fp32")
     # 4./5. attention forward and backward of block 0 (token-set mask, dropout)
     qkv = rnd(B, L, 3 * D)
     kpa = 1.0 - cfg.attention_dropout_rate
@@ -266,20 +281,38 @@ def kernel_probes(model, B, reps=20):
     return out
 
 
+def source_digest() -> str:
+    """sha256 of the kernel sources (csrc/*.hip, csrc/*.h, include/*.h): identifies the code a
+    PMC traffic pass measured, independent of rebuilds of the same sources."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    pkg = os.path.join(ROOT, "multi_modal_transformers_tokenmerge_amd", "csrc")
+    files = sorted(glob.glob(os.path.join(pkg, "*.hip")) + glob.glob(os.path.join(pkg, "*.h"))
+                   + glob.glob(os.path.join(ROOT, "include", "*.h")))
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def probe_traffic(B: int):
     """HBM bytes per launch of each probe from the committed rocprofv3 PMC passes
     (profiles/*_probe_pmc.json, written by tools/pmc_traffic.py from a FETCH_SIZE and a WRITE_SIZE
     pass over `bench.py --probe-only`: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
-    MI355X_MICROARCH.md "HBM"), the newest file measured at this per-GPU batch; {} when none is
-    committed."""
+    MI355X_MICROARCH.md "HBM"): only a file measured at this per-GPU batch on kernel sources with
+    this source_digest() counts (a pass over other code is stale: its probes report traffic
+    null). Returns ({name: bytes}, file name or None)."""
     import glob
-    found = {}
+    found, src, dig = {}, None, source_digest()
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_probe_pmc.json"))):
         with open(f) as fh:
             d = json.load(fh)
-        if d.get("batch", 256) == B:
+        if d.get("batch", 256) == B and d.get("source_digest") == dig:
             found = {k: v["hbm_bytes_per_launch"] for k, v in d.get("probes", {}).items()}
-    return found
+            src = os.path.basename(f)
+    return found, src
 
 
 def _cpu_model() -> str:
@@ -293,18 +326,17 @@ def _cpu_model() -> str:
     return "unknown CPU"
 
 
-def cpu_baseline(cfg_name, model, budget_s=20.0, B=8, max_steps=10):
-    """fp32 CPU restatement (oracle/octo_ref.py) forward+backward+AdamW on a bounded sample of the
-    same workload: B = 8, one warm-up step, then up to `max_steps` steps within
-    `budget_s`; samples/s from the MEDIAN step time. Threads: torch's intra-op pool (the box sets
-    OMP_NUM_THREADS to its CPU share), reported as `cores`."""
+def _cpu_run(cfg_name, model, train=True, budget_s=20.0, B=8, max_steps=10):
+    """The fp32 CPU restatement (oracle/octo_ref.py) on `model`'s parameters: one warm-up step,
+    then up to `max_steps` steps within `budget_s`; (samples/s from the MEDIAN step time, steps,
+    median s). train: forward + backward + AdamW; else the forward (loss) alone."""
     from oracle.octo_ref import OctoRef, sequence_spec
     cfg = model.cfg
-    threads = torch.get_num_threads()
-    params = {p.name: p.data.detach().float().cpu().clone().requires_grad_() for p in model.store.params}
+    params = {p.name: p.data.detach().float().cpu().clone().requires_grad_(train)
+              for p in model.store.params}
     t5p = ({p.name: p.bf16.float().cpu() for p in model.t5.store.params} if model.has_text else None)
     ref = OctoRef(cfg, params, t5p)
-    opt = torch.optim.AdamW(list(params.values()), lr=3e-4, weight_decay=1e-4)
+    opt = torch.optim.AdamW(list(params.values()), lr=3e-4, weight_decay=1e-4) if train else None
     g = np.random.default_rng(0)
     H = cfg.image_size[0]
     images = g.integers(0, 256, (B, model.n_images, H, H, 3)).astype(np.float32)
@@ -315,13 +347,16 @@ def cpu_baseline(cfg_name, model, budget_s=20.0, B=8, max_steps=10):
     spec = sequence_spec(cfg.input_sequence, cfg.token_compression_sequence)
 
     def step(i):
-        opt.zero_grad(set_to_none=True)
-        loss, _ = ref.forward_loss(text, images, actions, seed=1, step=i, positions=pos,
-                                   t=g.integers(0, cfg.diffusion_steps, B),
-                                   eps=g.standard_normal((B, cfg.action_space_dim)).astype(np.float32),
-                                   sequence=spec)
-        loss.backward()
-        opt.step()
+        with torch.set_grad_enabled(train):
+            if train:
+                opt.zero_grad(set_to_none=True)
+            loss, _ = ref.forward_loss(text, images, actions, seed=1, step=i, positions=pos,
+                                       t=g.integers(0, cfg.diffusion_steps, B),
+                                       eps=g.standard_normal((B, cfg.action_space_dim)).astype(np.float32),
+                                       sequence=spec)
+            if train:
+                loss.backward()
+                opt.step()
     step(0)  # warm-up
     times, t_all = [], time.perf_counter()
     while len(times) < max_steps and time.perf_counter() - t_all < budget_s:
@@ -329,18 +364,39 @@ def cpu_baseline(cfg_name, model, budget_s=20.0, B=8, max_steps=10):
         step(len(times) + 1)
         times.append(time.perf_counter() - t0)
     med = float(np.median(times))
-    return dict(value=B / med, unit="samples/s", cores=threads, kind="port",
+    return B / med, len(times), med
+
+
+def cpu_baseline(cfg_name, model, budget_s=20.0, B=8, max_steps=10):
+    """fp32 CPU restatement (oracle/octo_ref.py) forward+backward+AdamW on a bounded sample of the
+    same workload: B = 8, median step time (_cpu_run). Threads: torch's intra-op
+    pool (the box sets OMP_NUM_THREADS to its CPU share), reported as `cores`. `other` carries
+    SURVEY §8d's other two CPU samples — OCTO-tiny forward only and OCTO-small r = 0 training —
+    on smaller budgets (≈ 5 s each; CPU-built models, same restatement)."""
+    threads = torch.get_num_threads()
+    v, n, med = _cpu_run(cfg_name, model, True, budget_s, B, max_steps)
+    other = []
+    for name, train, b, budget, steps in (("octo-tiny", False, 8, 3.0, 5), ("octo-small", True, 8, 5.0, 3)):
+        try:
+            m = Octo(get_config(name), torch.device("cpu"), seed=0)
+            ov, on, omed = _cpu_run(name, m, train, budget, b, steps)
+            other.append(dict(config=name, mode="fwd+bwd+AdamW" if train else "forward", batch=b,
+                              value=round(ov, 3), unit="samples/s", steps=on,
+                              median_s_per_step=round(omed, 3)))
+        except Exception as e:  # a baseline sample must never sink the bench line
+            other.append(dict(config=name, error=f"{type(e).__name__}: {e}"))
+    return dict(value=v, unit="samples/s", cores=threads, kind="port",
                 sample=f"{cfg_name} fp32 torch-CPU restatement (oracle/octo_ref.py), fwd+bwd+AdamW "
-                       f"at B={B}: median of {len(times)} steps after 1 warm-up ({med:.2f} s/step) on "
+                       f"at B={B}: median of {n} steps after 1 warm-up ({med:.2f} s/step) on "
                        f"{threads} threads of {_cpu_model()} (the JAX reference is not importable "
-                       "offline)")
+                       "offline)", other=other)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)   # SURVEY §8d: 100 timed, 20 warm-up
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=512,
                     help="per-GPU batch (512: see DESIGN.md 'Batch'; 64 leaves the chip underfilled)")
     ap.add_argument("--config", default="octo-small-tome16")
@@ -368,7 +424,8 @@ def main():
     B = args.batch
     model = Octo(cfg, dev, seed=0)
     if args.probe_only:  # for rocprofv3 --pmc traffic passes (tools/pmc_traffic.py)
-        print(json.dumps(dict(probe_only=True, batch=B, probes=kernel_probes(model, B))), flush=True)
+        print(json.dumps(dict(probe_only=True, batch=B, source_digest=source_digest(),
+                              probes=kernel_probes(model, B))), flush=True)
         return
     if di.enabled:  # identical initial parameters on every rank (broadcast from rank 0)
         dist.broadcast(model.store.flat, 0)
@@ -390,9 +447,13 @@ def main():
     if di.enabled:
         dist.barrier()
     torch.cuda.synchronize()
+    cur = torch.cuda.current_stream()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record(cur)
+    for i in range(args.steps):
         step()
+        evs[i + 1].record(cur)  # step boundaries (a step ends with AdamW on this stream)
     torch.cuda.synchronize()
     if di.enabled:
         dist.barrier()
@@ -403,11 +464,12 @@ def main():
         elapsed = float(t.item())
     loss_val = float(loss_buf.item())
 
+    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     if di.rank == 0:
         ms = elapsed / args.steps * 1e3
         value = N * B * args.steps / elapsed
         probes = [] if args.no_probes else kernel_probes(model, B)
-        traffic = probe_traffic(B)
+        traffic, traffic_src = probe_traffic(B)
         for pr in probes:
             pr["traffic"] = traffic.get(pr["name"])
         # headline: the dominant kernel of the step trace — the weight-gradient GEMM (TN, split-K
@@ -428,6 +490,9 @@ def main():
                     shape_MNK=[N_, K_, M_], avg_launch_us=top["avg_launch_us"],
                     flops_per_launch=top["flops_per_launch"],
                     algorithmic_bytes_per_launch=2 * (M_ * N_ + M_ * K_) + 8 * N_ * K_,
+                    traffic_source=(f"profiles/{traffic_src} (source digest {source_digest()})"
+                                    if traffic_src else "no PMC pass of these kernel sources "
+                                    f"(digest {source_digest()}): traffic null"),
                     kernels=[p for p in probes if p is not top])
         fps = algorithmic_flops_per_sample(model)
         cpu = None
@@ -437,7 +502,11 @@ def main():
         line = {
             "metric": "train samples/sec OCTO-small 256px+text, ToMe r=16, 1/2/4/8 MI355X",
             "value": round(value, 2), "unit": "samples/s", "n_gpus": N, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3),
+            "median_ms_per_step": round(float(np.median(step_ms)), 3),
+            "p10_p90_ms_per_step": [round(float(np.percentile(step_ms, 10)), 3),
+                                    round(float(np.percentile(step_ms, 90)), 3)],
+            "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {"workload": f"{cfg.name} diffusion train step (fwd+bwd+AdamW), "
                                    f"{cfg.image_size[0]}px x{model.n_images} + {model.n_text}-tok text, "

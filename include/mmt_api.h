@@ -38,6 +38,11 @@ enum {
 };
 
 const char* mmt_last_error(void);
+/* ABI version of this header. 2: mmt_epilogue_t gained its trailing keep_bits field (a caller
+ * built against version 1 passes a shorter struct: mmt_gemm would read past it). Callers check
+ * mmt_version() == MMT_API_VERSION at load time and zero-initialise every mmt_epilogue_t
+ * (memset / `= {0}`) before setting the fields they use, so fields added later read as unused. */
+#define MMT_API_VERSION 2
 int mmt_version(void);
 
 /* Bytes of caller-provided device workspace an entry point needs (the library

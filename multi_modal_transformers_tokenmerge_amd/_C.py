@@ -95,6 +95,9 @@ _RESTYPE = {"mmt_workspace_size": L,      # returns a byte count (negative: erro
             "mmt_stem_conv_wgrad_slabs": I}
 
 
+API_VERSION = 2  # include/mmt_api.h MMT_API_VERSION
+
+
 class MMTError(RuntimeError):
     pass
 
@@ -125,6 +128,9 @@ def lib():
             fn = getattr(h, name)
             fn.argtypes = args
             fn.restype = None if name in _VOID else _RESTYPE.get(name, I)
+        if h.mmt_version() != API_VERSION:  # the Epilogue layout above is version 2's
+            raise ImportError(f"{path}: C ABI version {h.mmt_version()}, this binding needs "
+                              f"{API_VERSION} (include/mmt_api.h MMT_API_VERSION): rebuild it")
         _lib = h
         if os.environ.get("MMT_GEMM_VARIANT"):  # benchmarking knob (include/mmt_api.h)
             h.mmt_gemm_set_variant(int(os.environ["MMT_GEMM_VARIANT"]))

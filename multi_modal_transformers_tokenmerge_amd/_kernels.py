@@ -236,6 +236,13 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
 _BLASLT = os.environ.get("MMT_BLASLT", "0") == "1"
 
 
+def nres_ok(M: int, N: int, K: int) -> bool:
+    """Whether an fp32 residual-stream NT product (c_mode OUT_F32, fp32 residual, no activation)
+    of this shape runs on gemm_nres_kernel (csrc/gemm.hip nres_kind; MMT_NRES=0 turns it off)."""
+    return (os.environ.get("MMT_NRES", "1") != "0" and N % 384 == 0 and K % 64 == 0
+            and M >= 4096)
+
+
 def library_gemm_ok(M: int, N: int, K: int) -> bool:
     """With MMT_BLASLT=1 only: the plain narrow NT products (N <= 768, K >= 1152) go to hipBLASLt —
     the MLP input gradient 141,312 x 384 x 1536, the QKV input gradient 149,504 x 384 x 1152 and

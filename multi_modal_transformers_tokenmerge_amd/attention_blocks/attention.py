@@ -241,13 +241,17 @@ class Encoder1DBlock(Bindable):
         B, L, D = x.shape
         H, Dh = self.H, self.Dh
         train = ctx.train
+        # attention-output dropout: the block's `dropout` node; the two MLP dropouts: the
+        # mlp_block's own Dropout (`norm`) rate (reference attention.py:20-39, 60)
         kp = 1.0 - self.rate if train else 1.0
+        kpm = 1.0 - self.mlp.rate if train else 1.0
         kpa = 1.0 - self.attn_rate if train else 1.0
 
-        def drop(site, rows_per_sample):
-            if not train or kp >= 1.0:
+        def drop(site, rows_per_sample, keep=None):
+            keep = kp if keep is None else keep
+            if not train or keep >= 1.0:
                 return {}
-            return dict(rng=ctx.rng, drop_layer=ctx.layer, drop_site=site, keep_prob=kp,
+            return dict(rng=ctx.rng, drop_layer=ctx.layer, drop_site=site, keep_prob=keep,
                         drop_row_offset=ctx.sample_offset * rows_per_sample)
 
         main = torch.cuda.current_stream()
@@ -266,7 +270,7 @@ class Encoder1DBlock(Bindable):
             s0, t = ctx.sets.starts[ctx.tome_set], ctx.sets.lens[ctx.tome_set]
             metric = qkv.view(B, L, 3, H, Dh)[:, s0:s0 + t, 1]     # (B, t, H, Dh): sum_h K
             L2p = L - ctx.r  # the merged length (no pruning in this block)
-            if (_KEEP_BITS and train and kp < 1.0 and ctx.prune is None and Mh % 256 == 0
+            if (_KEEP_BITS and train and kpm < 1.0 and ctx.prune is None and Mh % 256 == 0
                     and relu_bits_ok(B * L2p)):
                 kbits = torch.empty((-(-B * L2p // 256) * 256, Mh // 32), dtype=torch.int32,
                                     device=x.device)
@@ -274,7 +278,7 @@ class Encoder1DBlock(Bindable):
             with torch.cuda.stream(side):
                 tome_idx = K.tome_match(metric, ctx.r)
                 if kbits is not None:
-                    K.gemm_dropout_keep_bits(ctx.rng, ctx.layer, DROP_MLP_HIDDEN, B * L2p, Mh, kp,
+                    K.gemm_dropout_keep_bits(ctx.rng, ctx.layer, DROP_MLP_HIDDEN, B * L2p, Mh, kpm,
                                              ctx.sample_offset * L2p, out=kbits)
         if train and kpa < 1:
             # the (L, L) attention keep mask (RNG state only), on the main stream: a 7 us launch
@@ -317,15 +321,15 @@ class Encoder1DBlock(Bindable):
         hbits = (torch.empty((-(-B * L2 // 256) * 256, Mh // 32), dtype=torch.int32, device=x.device)
                  if relu_bits_ok(B * L2) else None)
         if kbits is not None and hbits is not None and L2 == L - ctx.r:
-            hdrop = dict(keep_bits=kbits, keep_prob=kp)   # (joined with the side queue above)
+            hdrop = dict(keep_bits=kbits, keep_prob=kpm)   # (joined with the side queue above)
         else:
-            hdrop = drop(DROP_MLP_HIDDEN, L2)
+            hdrop = drop(DROP_MLP_HIDDEN, L2, kpm)
         h = self.mlp.dense.fwd(y1.view(B * L2, D), act=K.ACT_RELU, relu_bits=hbits, **hdrop)
         x2 = self.mlp.dense_out.fwd(h, residual=x1.view(B * L2, D), out_mode=K.OUT_F32,
-                                    **drop(DROP_MLP_OUT, L2))
+                                    **drop(DROP_MLP_OUT, L2, kpm))
         saved = dict(x=x, y0=y0, mu0=mu0, rs0=rs0, qkv=qkv, o=o, o_in=o_in, lse=lse, bits=bits,
                      x1=x1, y1=y1, mu1=mu1, rs1=rs1, h=h, hbits=hbits, tome=tome, prune=prune,
-                     kp=kp, kpa=kpa)
+                     kp=kp, kpm=kpm, kpa=kpa)
         return x2.view(B, L2, D), saved, new_size
 
     # ----------------------------------------------------------------------------- backward
@@ -336,14 +340,15 @@ class Encoder1DBlock(Bindable):
         dropout backward this block's LayerNorm_0 backward then produces (dz_prev)."""
         B, L2, D = dx2.shape
         L = sv["x"].shape[1]
-        kp, kpa, train = sv["kp"], sv["kpa"], ctx.train
-        dropping = train and kp < 1.0
+        kp, kpm, kpa, train = sv["kp"], sv["kpm"], sv["kpa"], ctx.train
+        dropping, dropping_m = train and kp < 1.0, train and kpm < 1.0
         dx2f = dx2.reshape(B * L2, D)                      # fp32 residual-stream gradient
         rng = ctx.rng if dropping else None
+        rng_m = ctx.rng if dropping_m else None
         # MLP out: x2 = x1 + drop3(h W2^T + b2); dropout backward = mask/scale + cast to bf16,
         # fused with the bias gradient (column sum)
         if dz2 is None:
-            dz2 = K.dropout_bwd(dx2f, rng, ctx.layer, DROP_MLP_OUT, kp,
+            dz2 = K.dropout_bwd(dx2f, rng_m, ctx.layer, DROP_MLP_OUT, kpm,
                                 row_offset=ctx.sample_offset * L2,
                                 colsum_out=self.mlp.dense_out.b.grad)
         # dh gated by (h > 0): relu + hidden-dropout backward fused into the dX GEMM epilogue,
@@ -354,7 +359,7 @@ class Encoder1DBlock(Bindable):
         cs = torch.empty((rows, Mh), dtype=torch.float32, device=dz2.device) if rows else None
         gate = dict(gate_bits=sv["hbits"]) if sv.get("hbits") is not None else dict(gate=sv["h"])
         dz1 = self.mlp.dense_out.bwd(dz2, sv["h"], bias_grad_done=True,
-                                     gate_scale=(1.0 / kp) if dropping else 1.0, colsum=cs, **gate)
+                                     gate_scale=(1.0 / kpm) if dropping_m else 1.0, colsum=cs, **gate)
         # dX of the LN-fed Dense in bf16 (the LN backward accumulates in fp32): halves its traffic
         dy1 = self.mlp.dense.bwd(dz1, sv["y1"].view(B * L2, D), dy_colsum=cs)
         Lo = sv["o_in"].shape[1]
@@ -386,7 +391,7 @@ class Encoder1DBlock(Bindable):
         dy0 = self.qkv.bwd(dqkv.view(B * L, 3 * D), sv["y0"].view(B * L, D), bias_grad_done=True)
         if prev is not None and sv["x"].dtype == torch.float32 and dy0.dtype == torch.bfloat16:
             pblk, psv, pctx = prev
-            pkp = psv["kp"]
+            pkp = psv["kpm"]  # block i-1's MLP-output dropout
             prng = pctx.rng if (pctx.train and pkp < 1.0) else None
             dx, dzp = K.seqnorm_dropout_bwd(
                 dy0.view(B, L, D), sv["x"], sv["mu0"], sv["rs0"], self.ln0.scale.data,

@@ -14,7 +14,7 @@ void set_error(const char* fmt, ...) {
 }  // namespace mmt
 
 extern "C" const char* mmt_last_error(void) { return mmt::g_err; }
-extern "C" int mmt_version(void) { return 1; }
+extern "C" int mmt_version(void) { return MMT_API_VERSION; }
 
 extern "C" int64_t mmt_workspace_size(int op, const int64_t* dims, int ndims) {
   switch (op) {

@@ -316,7 +316,7 @@ class Octo:
         it: the tokenizers, the stem) is the smallest possible."""
         nb = self.cfg.num_blocks
         if isinstance(stages, (list, tuple)):
-            return list(stages)
+            return self._check_bounds(list(stages))
         if isinstance(stages, str):
             mb = float(stages.split(":", 1)[1]) if ":" in stages else 24.0
             target = mb * (1 << 20)
@@ -329,9 +329,19 @@ class Octo:
             if nb > 1 and bounds[-1] != 1:
                 bounds.append(1)
             bounds.append(0)
-            return bounds
+            return self._check_bounds(bounds)
         n = max(1, min(int(stages), nb))
-        return [nb * (n - i) // n for i in range(n + 1)]  # nb .. 0
+        return self._check_bounds([nb * (n - i) // n for i in range(n + 1)])  # nb .. 0
+
+    def _check_bounds(self, b: List[int]) -> List[int]:
+        """A stage plan must cover blocks nb .. 0 once: b[0] == nb, b[-1] == 0, strictly
+        decreasing — otherwise gradient regions would be missing or overlap, parts of the
+        gradient never (or twice) all-reduced, and the ranks would drift apart silently."""
+        nb = self.cfg.num_blocks
+        if (len(b) < 2 or b[0] != nb or b[-1] != 0 or any(int(x) != x for x in b)
+                or any(b[i] <= b[i + 1] for i in range(len(b) - 1))):
+            raise ValueError(f"stage bounds {b}: need {nb} = b[0] > b[1] > ... > b[-1] = 0")
+        return [int(x) for x in b]
 
     def _stage_bounds(self, n_stages) -> List[int]:
         return self.stage_bounds(n_stages)

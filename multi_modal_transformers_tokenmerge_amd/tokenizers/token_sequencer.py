@@ -327,6 +327,12 @@ def sets_from_mask(mask) -> LayerSets:
             bits |= int(on) << b
         vis.append(bits)
         causal.append(kinds[a] == "causal")
+    if any(v == 0 for v in vis):
+        # a query row that sees no key: Flax fills its logits with finfo.min and returns the
+        # uniform average of V there; the kernels give a zero row (lse = -inf). Not a pattern
+        # the reference's TokenSequence produces (every set sees itself).
+        raise ValueError("the attention mask has fully masked query rows (a token set that sees "
+                         "no key): not supported")
     sets = LayerSets(starts, lens, vis, causal, ["?"] * n)
     if not np.array_equal(dense_mask_of(sets), m):
         raise ValueError("the attention mask is not a block mask of contiguous token sets")

@@ -36,7 +36,7 @@ def test_binding_table_covers_header():
 
 def test_version_and_error_without_gpu():
     from multi_modal_transformers_tokenmerge_amd import _C
-    assert _C.lib().mmt_version() >= 1
+    assert _C.lib().mmt_version() == _C.API_VERSION == 2
     # argument validation happens before any HIP call: a bad shape returns an error, no abort
     rc = _C.lib().mmt_tome_match(None, 0, 1, 8, 1, 4, 32, 4, 0, 2, 0, None, None, None, None, None,
                                  0, None)

@@ -159,3 +159,7 @@ def test_set_table_from_reference_mask():
     rnd = np.random.default_rng(0).random((40, 40)) < 0.5
     with pytest.raises(ValueError):         # no table of <= 16 contiguous sets
         sets_from_mask(rnd)
+    blind = m.copy()
+    blind[8:, :] = False                    # the Readout set sees no key: Flax would average V
+    with pytest.raises(ValueError, match="fully masked"):
+        sets_from_mask(blind)

@@ -204,3 +204,35 @@ def test_narrow_nt_kernel(dev, M, N, K, ep, variant):
     if ep == "relu":
         ref = ref.clamp_min(0)
     _close_bf16(out, ref)
+
+
+@pytest.mark.parametrize("M,N,K,alpha", [(141312, 384, 1536, 1.0), (149504, 384, 384, 1.0),
+                                         (8200, 384, 384, 0.5), (4100, 768, 128, 1.0),
+                                         (5000, 384, 64, 1.0)])
+def test_residual_stream_kernel(dev, M, N, K, alpha):
+    """gemm_nres_kernel (fp32 C = fp32 residual + dropout(alpha A.W^T + bias): the step's
+    out-projection and MLP Dense_1, reference attention.py:36-37,59-63): bit-identical to the
+    128 x 128 direct-to-LDS kernel (variant 4) on the same launch — same MFMA shape and k order per
+    output, same epilogue order — at the B = 512 block-0 shapes, ragged row ranges, two 384-column
+    tiles and one-K-step reductions; and within fp32 accumulation order of a torch reference."""
+    from multi_modal_transformers_tokenmerge_amd import _C
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    g = torch.Generator().manual_seed(M + N + K)
+    a, w = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    bias = torch.randn(N, generator=g).to(dev)
+    res = torch.randn((M, N), generator=g).to(dev)
+    rng = torch.tensor([31, 4], dtype=torch.int32, device=dev)
+    kw = dict(bias=bias, rng=rng, drop_layer=2, drop_site=3, keep_prob=0.9, drop_row_offset=3 * M,
+              residual=res, alpha=alpha, out_mode=Kn.OUT_F32)
+    out = Kn.gemm(a, w, False, True, **kw)
+    _C.call("mmt_gemm_set_variant", 4)
+    try:
+        old = Kn.gemm(a, w, False, True, **kw)
+        torch.cuda.synchronize()
+    finally:
+        _C.call("mmt_gemm_set_variant", -1)
+    assert torch.equal(out.view(torch.int32), old.view(torch.int32))
+    keep = torch.from_numpy(R.dropout_mask_2d(31, 4, 2, 3, M, N, 3 * M, 0.9)).to(dev)
+    ref = alpha * (a.float() @ w.float().t()) + bias
+    ref = torch.where(keep, ref / 0.9, torch.zeros_like(ref)) + res
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)

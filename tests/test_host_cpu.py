@@ -228,3 +228,6 @@ def test_ddp_stage_plan_regions_cover_the_store():
     even = 4 * (m.grad_regions(3)[-1][1] - m.grad_regions(3)[-1][0])
     assert exposed < even / 3, (exposed, even)
     assert m.stage_bounds("auto:0.001") == list(range(nb, -1, -1))
+    for bad in ([nb, 6, 6, 0], [nb - 1, 0], [nb, 3], [nb, 7, 9, 0], [0], [nb, 2.5, 0]):
+        with pytest.raises(ValueError):   # regions missing / overlapping: refused
+            m.stage_bounds(bad)

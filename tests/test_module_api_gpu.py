@@ -156,3 +156,63 @@ def test_encoder_block_and_mlp_call_vs_torch(dev):
     hz = bf(torch.relu(bf(x) @ bf(q["Dense_0/kernel"]).T + q["Dense_0/bias"]))
     zr = hz @ bf(q["Dense_1/kernel"]).T + q["Dense_1/bias"]
     assert ((z - zr).norm() / zr.norm()).item() < 1e-2
+
+
+def test_encoder_block_mlp_dropout_rate_is_its_own(dev):
+    """The MLP's two dropouts use the mlp_block's own Dropout rate (reference attention.py:20-39),
+    the attention-output dropout the block's `dropout` node (:60): with block rate 0 and MLP rate
+    0.5 (attention dropout off) the forward equals a torch reference with the counter-RNG masks of
+    DROP_MLP_HIDDEN / DROP_MLP_OUT at keep 0.5, and the input gradient follows the same masks and
+    1 / 0.5 scales (a reference with the scales at 1 is several times further from it)."""
+    import copy
+    from multi_modal_transformers_tokenmerge_amd import config_loader as C
+    from multi_modal_transformers_tokenmerge_amd.layers import DROP_MLP_HIDDEN, DROP_MLP_OUT
+    from oracle import rng as R
+    cfg = C.compose("octo_tiny")
+    node = copy.deepcopy(cfg["attention_blocks"]["stacked_encoder_1d_block"]["encoder_1d_block"])
+    node["dropout"]["rate"] = 0.0
+    node["self_attention"]["dropout_rate"] = 0.0
+    node["mlp_block"]["norm"]["rate"] = 0.5
+    blk = C.instantiate(node, _recursive_=False)
+    B, L, D = 2, 20, cfg["token_embedding_dim"]
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn((B, L, D), generator=g).to(dev).requires_grad_()
+    rng = torch.tensor([77, 5], dtype=torch.int32, device=dev)
+    y, _ = blk(x, mask=np.ones((L, L), bool), train=True, rng=rng, layer=1)
+    p = {k.split("Encoder1DBlock_0/")[1]: v.float() for k, v in blk.params.items()}
+    bf = lambda t: t.bfloat16().float()  # noqa: E731
+    Mh = p["MLPBlock_0/Dense_0/bias"].numel()
+    kh = torch.from_numpy(R.dropout_mask_2d(77, 5, 1, DROP_MLP_HIDDEN, B * L, Mh, 0, 0.5)).to(dev)
+    ko = torch.from_numpy(R.dropout_mask_2d(77, 5, 1, DROP_MLP_OUT, B * L, D, 0, 0.5)).to(dev)
+
+    def seqln(v, s, b):
+        mu = v.mean(1, keepdim=True)
+        var = ((v - mu) ** 2).mean(1, keepdim=True)
+        return (v - mu) / torch.sqrt(var + 1e-6) * s + b
+
+    def reference(scale):
+        xr = x.detach().clone().requires_grad_()
+        H = blk.H
+        Dh = D // H
+        y0 = seqln(xr, p["LayerNorm_0/scale"], p["LayerNorm_0/bias"])
+        qkv = y0 @ bf(p["SelfAttention_0/qkv/kernel"]).T + p["SelfAttention_0/qkv/bias"]
+        q, k, v = qkv.view(B, L, 3, H, Dh).unbind(2)
+        a = torch.softmax(torch.einsum("bqhd,bkhd->bhqk", q, k) * Dh ** -0.5, -1)
+        o = torch.einsum("bhqk,bkhd->bqhd", a, v).reshape(B, L, D)
+        x1 = xr + o @ bf(p["SelfAttention_0/out/kernel"]).T + p["SelfAttention_0/out/bias"]
+        y1 = seqln(x1, p["LayerNorm_1/scale"], p["LayerNorm_1/bias"]).reshape(B * L, D)
+        hm = torch.relu(y1 @ bf(p["MLPBlock_0/Dense_0/kernel"]).T + p["MLPBlock_0/Dense_0/bias"])
+        hm = torch.where(kh, hm * scale, torch.zeros_like(hm))
+        z = hm @ bf(p["MLPBlock_0/Dense_1/kernel"]).T + p["MLPBlock_0/Dense_1/bias"]
+        z = torch.where(ko, z * scale, torch.zeros_like(z))
+        return xr, x1 + z.view(B, L, D)
+    xr, ref = reference(2.0)
+    assert ((y - ref).norm() / ref.norm()).item() < 1e-2
+    gy = torch.randn((B, L, D), generator=g).to(dev)
+    y.backward(gy)
+    ref.backward(gy)
+    err = ((x.grad - xr.grad).norm() / xr.grad.norm()).item()
+    xw, refw = reference(1.0)            # the MLP dropout scales left at 1: the wrong keep prob
+    refw.backward(gy)
+    err_w = ((x.grad - xw.grad).norm() / xw.grad.norm()).item()
+    assert err < 8e-2 and err_w > 3 * err, (err, err_w)

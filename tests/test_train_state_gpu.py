@@ -135,3 +135,37 @@ def test_wgrad_overlap_schedule_same_gradients(dev):
             sl = slice(p.offset, p.offset + p.numel)
             assert torch.equal(got[sl], ref[sl]), (p.name, enabled, lag, graph)
         torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_ddpstep_build_leaves_training_state_unchanged(dev, fp8):
+    """distributed.DDPStep.build() trains for its warm-up steps outside capture and restores the
+    state after them: the fp32 master weights, the bf16 / transposed / e4m3 shadows (+ scales),
+    the AdamW moments, the RNG / step counter and the running loss metrics are bitwise what they
+    were before build() (world size 1, the one-graph step)."""
+    from multi_modal_transformers_tokenmerge_amd.distributed import DDPStep
+    from multi_modal_transformers_tokenmerge_amd.models.octo.config import get_config
+    from multi_modal_transformers_tokenmerge_amd.models.octo import octo as O
+    from oracle.parity import _inputs
+    model = O.Octo(get_config("octo-tiny", num_blocks=2, fp8=fp8), dev, seed=0)
+    state = O.create_octo_train_state(model, seed=7)
+    images, _, actions = _inputs(model, 4)
+    img, act = torch.from_numpy(images).to(dev), torch.from_numpy(actions).to(dev)
+    for _ in range(2):  # non-trivial moments, step counter and metrics before build()
+        state, _ = O.diffusion_train_step(model, state, None, img, act)
+    torch.cuda.synchronize()
+    st = model.store
+
+    def snap():
+        t = [st.flat, st.flat_bf16, st.m, st.v, state.rng, st.flat_bf16_t]
+        if st.flat_fp8 is not None:
+            t += [st.flat_fp8, st.fp8_scale]
+        if state.metrics is not None:
+            t += [state.metrics.total, state.metrics.count]
+        return [x.clone() for x in t]
+    before = snap()
+    assert (st.flat_fp8 is not None) == fp8
+    DDPStep(model, state, None, img, act, None).build()
+    torch.cuda.synchronize()
+    for a, b in zip(before, snap()):
+        assert torch.equal(a, b)

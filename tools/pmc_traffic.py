@@ -68,7 +68,8 @@ def main():
                               hbm_bytes_per_launch=round(hbm), algorithmic_bytes_per_launch=alg,
                               ratio_to_algorithmic=round(hbm / alg, 3) if alg else None)
     with open(a.out, "w") as fh:
-        json.dump(dict(batch=meta.get("batch", 256), probes=res), fh, indent=1)
+        json.dump(dict(batch=meta.get("batch", 256), source_digest=meta.get("source_digest"),
+                       probes=res), fh, indent=1)
     print(json.dumps(res))
 
 
