@@ -42,6 +42,7 @@ SIGNATURES: dict[str, list] = {
     "mmt_topk_gather": [P, I, I, I, I, L, L, P, L, I, P, P, P, P, L, L, P, P],
     "mmt_topk_scatter_bwd": [P, I, I, I, I, L, L, P, I, P, L, L, P],
     "mmt_gemm_set_variant": [I],
+    "mmt_gemm_set_nres": [I],
     "mmt_gemm_colsum_rows": [I, I, I, I, I, I, I],
     "mmt_gemm_dropout_keep_bits": [P, U32, U32, I, I, F, L, P, P],
     "mmt_gemm": [I, I, I, P, I, L, P, I, L, P, I, L, I, L, L, L, I, P, P, L, P],
@@ -89,7 +90,7 @@ SIGNATURES: dict[str, list] = {
     "mmt_transpose_bf16_batched": [P, P, P, I, L, P],
     "mmt_step_advance": [P, P],
 }
-_VOID = {"mmt_tome_set_match_path", "mmt_gemm_set_variant"}
+_VOID = {"mmt_tome_set_match_path", "mmt_gemm_set_variant", "mmt_gemm_set_nres"}
 _RESTYPE = {"mmt_workspace_size": L,      # returns a byte count (negative: error)
             "mmt_gemm_colsum_rows": I,    # returns a row count
             "mmt_stem_conv_wgrad_slabs": I}

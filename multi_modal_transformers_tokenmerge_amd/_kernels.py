@@ -239,7 +239,7 @@ _BLASLT = os.environ.get("MMT_BLASLT", "0") == "1"
 def nres_ok(M: int, N: int, K: int) -> bool:
     """Whether an fp32 residual-stream NT product (c_mode OUT_F32, fp32 residual, no activation)
     of this shape runs on gemm_nres_kernel (csrc/gemm.hip nres_kind; MMT_NRES=0 turns it off)."""
-    return (os.environ.get("MMT_NRES", "1") != "0" and N % 384 == 0 and K % 64 == 0
+    return (os.environ.get("MMT_NRES", "0") != "0" and N % 384 == 0 and K % 64 == 0
             and M >= 4096)
 
 

@@ -128,6 +128,28 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// One 16-B-per-lane LDS-DMA piece (buffer_load_dwordx4 ... lds, 1 KB per wave-instruction) as
+// inline asm: issued through the builtin, the compiler cannot tell LDS reads from the region
+// being filled and puts a vmcnt(0) behind every DMA. Invisible to the compiler's vmcnt
+// bookkeeping, so the caller waits for it explicitly (s_waitcnt vmcnt). Raw buffer resource:
+// stride 0, num_records = bytes (reads past it return 0); lds = this lane group's destination
+// base (lane-linear, 16 B per lane), voffset = the lane's source byte offset.
+__device__ __forceinline__ void dma16_asm(const void* base, int64_t bytes, void* lds, int voffset) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  i32x4 r;
+  // every operand but voffset is wave-uniform by contract: readfirstlane keeps it in SGPRs where
+  // the compiler cannot prove the uniformity (free when it already can)
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((uint32_t)(b >> 32) & 0xffffu));
+  r[2] = __builtin_amdgcn_readfirstlane((int)min(bytes, (int64_t)0x7ffffff0));
+  r[3] = 0x00020000;
+  const uint32_t l = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)lds));
+  asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               :: "v"(voffset), "s"(r), "s"(l) : "m0", "memory");
+}
+
 // XCD-aware bijective remap: workgroups b and b+8 share an XCD (round-robin dispatch), so give
 // each XCD a contiguous range of work ids: items that share operands (a GEMM's A row panel, the
 // key/query blocks of one attention (sample, head)) then meet in one L2. Speed only.

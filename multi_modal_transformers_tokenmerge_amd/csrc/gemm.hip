@@ -1562,19 +1562,7 @@ constexpr int TN_BM = 256, TN_BN = 192, TN_NT = 512;
 // builtin, the compiler cannot tell the transposed fragment reads (ds_read_b64_tr_b16) from the
 // stage being filled and puts a vmcnt(0) behind every DMA (the next K-step's, meant to stay in
 // flight under these MFMAs). Completion is waited for explicitly (vmcnt(0) + s_barrier at the
-// top of each K-step). Raw buffer resource: stride 0, num_records = bytes (reads past it: 0).
-__device__ __forceinline__ void dma16_asm(const void* base, int64_t bytes, void* lds, int voffset) {
-  typedef int i32x4 __attribute__((ext_vector_type(4)));
-  const uint64_t b = (uint64_t)(uintptr_t)base;
-  i32x4 r;
-  r[0] = (int)(uint32_t)b;
-  r[1] = (int)((uint32_t)(b >> 32) & 0xffffu);
-  r[2] = (int)min(bytes, (int64_t)0x7ffffff0);
-  r[3] = 0x00020000;
-  const uint32_t l = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)lds);
-  asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
-               :: "v"(voffset), "s"(r), "s"(l) : "m0", "memory");
-}
+// top of each K-step). dma16_asm: common.h.
 // BM: tile height, 256 (8 waves of 64 x 96: 2 x 3 MFMA blocks) or 384 (waves of 96 x 96: 3 x 3
 // blocks; 72 KB per K-step for 1.5x the products of the 56 KB 256-row step — the kernel is bound
 // by its DMA rate, profiles/r03_tn_ablation.txt)
@@ -2041,11 +2029,15 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ntws_kernel(
 //    operands swapped: lane = output row) run the MFMAs and the epilogue; their vmcnt holds only
 //    the epilogue's bias / residual loads and C stores: residual loads are issued three 8-column
 //    groups ahead of use, never behind a store they do not need.
-// One s_barrier per K-step for all 12 waves. Rows: each workgroup owns a contiguous range of
+// One s_barrier per K-step for all 12 waves, plus one at each tile's end (the epilogue reuses the
+// weight stage of the tile's last K-step as transpose scratch). Rows: each workgroup owns a contiguous range of
 // ~M / grid rows (balanced to a row, not to a tile), walked in 128-row chunks; rows past the
 // range read zeros (buffer range) and are not stored. Outputs are bit-identical to the 128 x 128
 // kernel (same MFMA shape and k order per output, same epilogue order).
 // LDS images as the narrow kernel: [rows][64] bf16, 16-B chunk c of row r at c ^ (r & 7).
+#ifndef MMT_NRES_ABL  // ablation builds (tools/build_abl_nres.sh): 1 no W DMA, 2 no A DMA,
+#define MMT_NRES_ABL 0  // 3 no MFMA, 4 no epilogue loads / stores, 5 no DMA at all
+#endif
 constexpr int NR_NT = 768, NR_MT = 128, NR_BN = 384, NR_NSA = 4;
 constexpr int NR_A_ST = NR_MT * 128, NR_W_ST = NR_BN * 128;  // 16 KB, 48 KB per K-step
 template <int WPATH, int EP>  // EP: 0 plain bf16 out, 1 fp32 out with bias / dropout / fp32 residual
@@ -2080,7 +2072,8 @@ __global__ __launch_bounds__(NR_NT, 1) void gemm_nres_kernel(
       const int64_t ra = ((int64_t)rows * lda - k0) * 2;  // rows past the range read zeros
       char* dst = sA + (s % NR_NSA) * NR_A_ST;
 #pragma unroll
-      for (int p = 0; p < 16; ++p) dma16_asm(pa, ra, dst + p * 1024, voa[p]);
+      for (int p = 0; p < 16; ++p)
+        if (MMT_NRES_ABL != 2 && MMT_NRES_ABL != 5) dma16_asm(pa, ra, dst + p * 1024, voa[p]);
     };
 #pragma unroll
     for (int q = 0; q < NR_NSA - 1; ++q)
@@ -2094,6 +2087,7 @@ __global__ __launch_bounds__(NR_NT, 1) void gemm_nres_kernel(
       asm volatile("s_barrier" ::: "memory");
       // into the stage K-step s - 1 used (its reads finished before this barrier)
       if (s + NR_NSA - 1 < S) issue(s + NR_NSA - 1);
+      if (s % nk == nk - 1) asm volatile("s_barrier" ::: "memory");  // the tile's epilogue sync
     }
     return;
   }
@@ -2116,13 +2110,15 @@ __global__ __launch_bounds__(NR_NT, 1) void gemm_nres_kernel(
         const int64_t rb = ((int64_t)NR_BN * ldb - (s % nk) * 64) * 2;
         char* dst = sW + (s & 1) * NR_W_ST + lw * 16 * 1024;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) dma16_asm(pb, rb, dst + i * 1024, vow[i]);
+        for (int i = 0; i < 16; ++i)
+          if (MMT_NRES_ABL != 1 && MMT_NRES_ABL != 5) dma16_asm(pb, rb, dst + i * 1024, vow[i]);
       };
       issue(0);
       for (int s = 0; s < S; ++s) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // W(s) landed
         asm volatile("s_barrier" ::: "memory");
         if (s + 1 < S) issue(s + 1);  // into the stage K-step s - 1 used
+        if (s % nk == nk - 1) asm volatile("s_barrier" ::: "memory");  // the tile's epilogue sync
       }
     } else {
       uint4 wr[16];
@@ -2146,6 +2142,7 @@ __global__ __launch_bounds__(NR_NT, 1) void gemm_nres_kernel(
           put(s + 1);  // into the stage K-step s - 1 used (compiler waits for the loads)
           if (s + 2 < S) load(s + 2);
         }
+        if (s % nk == nk - 1) asm volatile("s_barrier" ::: "memory");  // the tile's epilogue sync
       }
     }
     return;
@@ -2195,69 +2192,85 @@ __global__ __launch_bounds__(NR_NT, 1) void gemm_nres_kernel(
       for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
         for (int nb = 0; nb < 3; ++nb)
-          acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[cu][nb], af[cu][mb], acc[mb][nb], 0, 0, 0);
+          if (MMT_NRES_ABL != 3 || M < 0)
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[cu][nb], af[cu][mb], acc[mb][nb], 0, 0, 0);
     }
   };
 
-  // lane (row l31, half h) holds, per 32-column block, columns 8 g + 4 h + i (acc[4 g + i]);
-  // v_permlane32_swap of the g = 2 j and 2 j + 1 runs gives it 8 contiguous columns 16 j + 8 h ..
-  // Groups q = (mb, nb, j), 12 per tile; EP 1 loads group q + 3's bias / residual before group
-  // q's stores.
-  auto epilogue = [&](int i) {
+  // Epilogue through a per-wave LDS transpose: in the accumulator layout a lane holds one output
+  // row's columns 8 g + 4 h + i of each 32-column block, so direct global accesses touch 32 rows
+  // x 32 B per instruction (measured: the epilogue alone took 170 us of the Dense_1 launch). Each
+  // 32 x 32 fp32 block is written to the wave's own 32 x 36-float LDS region (conflict-free 16-B
+  // writes) and read back as 8 rows x 128 B per instruction (lane: row 8 k + lane / 8, columns
+  // 4 (lane & 7) ..): residual loads, C stores and the bias then move whole 128-B row segments.
+  // The region lies in the weight stage this tile's last K-step used: free until the next
+  // barrier, after which the W loaders refill it. The residual of the next block is loaded
+  // before the current block's stores (PF blocks ahead).
+  auto epilogue = [&](int i, int s) {
     const int64_t m0 = r0 + (int64_t)(i / tiles_n) * NR_MT;
     const int tn = i % tiles_n;
-    auto row_of = [&](int q) { return m0 + wm * 64 + 32 * (q / 6) + l31; };
-    auto col_of = [&](int q) { return tn * NR_BN + wn * 96 + 32 * ((q / 2) % 3) + 16 * (q & 1) + 8 * h; };
-    constexpr int PF = 3;
-    float resv[PF][8], biasv[PF][8];
+    float* stg = reinterpret_cast<float*>(sW + (s & 1) * NR_W_ST + wave * (32 * 36 * 4));
+    const int er = lane >> 3, ec = 4 * (lane & 7);
+    auto row_of = [&](int q, int k) { return m0 + wm * 64 + 32 * (q / 3) + 8 * k + er; };
+    auto col_of = [&](int q) { return tn * NR_BN + wn * 96 + 32 * (q % 3) + ec; };
+    constexpr int PF = 2;
+    float resv[PF][4][4];
     auto fetch = [&](int q) {
-      if constexpr (EP == 1) {
-        const int64_t gr = min(row_of(q), r1 - 1);  // clamped: unpredicated loads
-        const int gc = col_of(q);
-        if (epi.bias) ldw<8>(epi.bias + gc, biasv[q % PF]);
-        ldw<8>(reinterpret_cast<const float*>(epi.residual) + gr * epi.ld_res + gc, resv[q % PF]);
+      if constexpr (EP == 1 && MMT_NRES_ABL != 4) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t gr = min(row_of(q, k), r1 - 1);  // clamped: unpredicated loads
+          ldw<4>(reinterpret_cast<const float*>(epi.residual) + gr * epi.ld_res + col_of(q), resv[q % PF][k]);
+        }
       }
     };
+    float biasv[3][4];
+    if (EP == 1 && epi.bias)
+#pragma unroll
+      for (int nb = 0; nb < 3; ++nb) ldw<4>(epi.bias + col_of(nb), biasv[nb]);
 #pragma unroll
     for (int q = 0; q < PF; ++q) fetch(q);
 #pragma unroll
-    for (int q = 0; q < 12; ++q) {
-      const int mb = q / 6, nb = (q / 2) % 3, j = q & 1;
-      float v[8];
+    for (int q = 0; q < 6; ++q) {  // blocks (mb, nb) = (q / 3, q % 3)
+      const int mb = q / 3, nb = q % 3;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[mb][nb][8 * j + e]),
-                                                        __float_as_uint(acc[mb][nb][8 * j + 4 + e]),
-                                                        false, false);
-        v[e] = __uint_as_float(x[0]);
-        v[4 + e] = __uint_as_float(x[1]);
-      }
-      const int64_t gr = row_of(q);
+      for (int g4 = 0; g4 < 4; ++g4)
+        *reinterpret_cast<float4*>(stg + l31 * 36 + 8 * g4 + 4 * h) =
+            make_float4(acc[mb][nb][4 * g4], acc[mb][nb][4 * g4 + 1], acc[mb][nb][4 * g4 + 2],
+                        acc[mb][nb][4 * g4 + 3]);
+      float v[4][4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ldw<4>(stg + (8 * k + er) * 36 + ec, v[k]);
       const int gc = col_of(q);
       if constexpr (EP == 1) {
-        float rr[8], bb[8];
+        float rr[4][4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          rr[e] = resv[q % PF][e];
-          bb[e] = biasv[q % PF][e];
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rr[k][e] = resv[q % PF][k][e];
+        if (q + PF < 6) fetch(q + PF);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t gr = row_of(q, k);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[k][e] *= epi.alpha;
+          if (epi.bias)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[k][e] += biasv[nb][e];
+          epilogue_w<4>(rest, key, N, (int)gr, gc, v[k]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[k][e] += rr[k][e];
+          if (gr < r1 && (MMT_NRES_ABL != 4 || v[k][0] == 123.f)) store_w<2, 4>(Cv, gr * ldc + gc, 0.f, v[k]);
         }
-        if (q + PF < 12) fetch(q + PF);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] *= epi.alpha;
-        if (epi.bias)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += bb[e];
-        epilogue_w<8>(rest, key, N, (int)gr, gc, v);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += rr[e];
-        if (gr < r1) store_w<2, 8>(Cv, gr * ldc + gc, 0.f, v);
       } else {
-        uint4 o;
-        o.x = (uint32_t)f2bf(v[0] * epi.alpha) | ((uint32_t)f2bf(v[1] * epi.alpha) << 16);
-        o.y = (uint32_t)f2bf(v[2] * epi.alpha) | ((uint32_t)f2bf(v[3] * epi.alpha) << 16);
-        o.z = (uint32_t)f2bf(v[4] * epi.alpha) | ((uint32_t)f2bf(v[5] * epi.alpha) << 16);
-        o.w = (uint32_t)f2bf(v[6] * epi.alpha) | ((uint32_t)f2bf(v[7] * epi.alpha) << 16);
-        if (gr < r1) *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(Cv) + gr * ldc + gc) = o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t gr = row_of(q, k);
+          uint2 o;
+          o.x = (uint32_t)f2bf(v[k][0] * epi.alpha) | ((uint32_t)f2bf(v[k][1] * epi.alpha) << 16);
+          o.y = (uint32_t)f2bf(v[k][2] * epi.alpha) | ((uint32_t)f2bf(v[k][3] * epi.alpha) << 16);
+          if (gr < r1) *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(Cv) + gr * ldc + gc) = o;
+        }
       }
     }
 #pragma unroll
@@ -2272,7 +2285,11 @@ __global__ __launch_bounds__(NR_NT, 1) void gemm_nres_kernel(
     // this wave's reads of K-step s - 1 completed; K-step s landed for every wave
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     compute(s);
-    if ((s % nk) == nk - 1) epilogue(s / nk);
+    if ((s % nk) == nk - 1) {
+      // every compute wave is done reading K-step s's weight stage before any overwrites it
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      epilogue(s / nk, s);
+    }
   }
 }
 
@@ -2495,8 +2512,10 @@ bool ntw_ok(int M, int N, int K, int transA, int transB, int batch, int out_kind
 // 1 = the fp32 residual-stream products (fp32 out, fp32 residual, optional bias / dropout / alpha;
 // the step's out-projection and MLP Dense_1), 0 = the plain bf16 narrow product (MMT_NRES=2 only,
 // a comparison against gemm_ntw_kernel). MMT_NRES=0 keeps the 128 x 128 kernel.
+int g_nres = -1;  // mmt_gemm_set_nres (tests / benchmarks); -1: MMT_NRES (default 0)
 int nres_kind(int M, int N, int K, int transA, int transB, int batch, int out_kind, const Epi& e) {
-  static const int mode = getenv("MMT_NRES") ? atoi(getenv("MMT_NRES")) : 1;
+  static const int env_mode = getenv("MMT_NRES") ? atoi(getenv("MMT_NRES")) : 0;
+  const int mode = g_nres >= 0 ? g_nres : env_mode;
   if (!mode || transA || !transB || batch != 1 || K % 64 != 0 || N % NR_BN != 0 || M < 4096 ||
       g_variant >= 0)
     return -1;
@@ -2607,6 +2626,7 @@ extern "C" int mmt_gemm_colsum_rows(int M, int N, int K, int transA, int transB,
 }
 
 extern "C" void mmt_gemm_set_variant(int v) { g_variant = v; }
+extern "C" void mmt_gemm_set_nres(int mode) { g_nres = mode; }
 
 extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t lda,
                         const void* B, int transB, int64_t ldb, void* C, int c_mode, int64_t ldc,

@@ -224,13 +224,15 @@ def test_residual_stream_kernel(dev, M, N, K, alpha):
     rng = torch.tensor([31, 4], dtype=torch.int32, device=dev)
     kw = dict(bias=bias, rng=rng, drop_layer=2, drop_site=3, keep_prob=0.9, drop_row_offset=3 * M,
               residual=res, alpha=alpha, out_mode=Kn.OUT_F32)
-    out = Kn.gemm(a, w, False, True, **kw)
-    _C.call("mmt_gemm_set_variant", 4)
+    _C.call("mmt_gemm_set_nres", 1)
     try:
+        out = Kn.gemm(a, w, False, True, **kw)
+        _C.call("mmt_gemm_set_variant", 4)
         old = Kn.gemm(a, w, False, True, **kw)
         torch.cuda.synchronize()
     finally:
         _C.call("mmt_gemm_set_variant", -1)
+        _C.call("mmt_gemm_set_nres", -1)
     assert torch.equal(out.view(torch.int32), old.view(torch.int32))
     keep = torch.from_numpy(R.dropout_mask_2d(31, 4, 2, 3, M, N, 3 * M, 0.9)).to(dev)
     ref = alpha * (a.float() @ w.float().t()) + bias

@@ -5,7 +5,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for cfg in "MMT_NRES=0" "MMT_NRES=2 MMT_NRES_W=0" "MMT_NRES=2 MMT_NRES_W=1" "MMT_NRES=0 MMT_NTW_MT=128"; do
+for cfg in "MMT_NRES=0" "MMT_NRES=2 MMT_NRES_W=0"; do
   echo "== $cfg" >> gpurun_out/res_probe.txt
   env $cfg timeout -k 10 120 python tools/res_probe.py >> gpurun_out/res_probe.txt 2>&1 || exit 1
 done
