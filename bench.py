@@ -407,6 +407,9 @@ def main():
                     help="N > 1: backward stages, each stage's gradient region all-reduced while "
                          "the rest of the backward runs: an int (block ranges; 1 = no overlap) or "
                          "auto[:MB] (~MB-megabyte regions, default 24, block 0 alone last)")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="bitwise-reproducible gradients (fixed-point shadow instead of fp32 "
+                         "atomics; same as MMT_DETERMINISTIC=1)")
     ap.add_argument("--no-probes", action="store_true",
                     help="skip the per-kernel roofline probes (rocprofv3 traces of the step alone)")
     ap.add_argument("--probe-only", action="store_true",
@@ -422,6 +425,8 @@ def main():
     torch.cuda.set_device(dev)
     cfg = get_config(args.config)
     B = args.batch
+    if args.deterministic:
+        os.environ["MMT_DETERMINISTIC"] = "1"
     model = Octo(cfg, dev, seed=0)
     if args.probe_only:  # for rocprofv3 --pmc traffic passes (tools/pmc_traffic.py)
         print(json.dumps(dict(probe_only=True, batch=B, source_digest=source_digest(),
@@ -512,7 +517,8 @@ def main():
                                    f"{cfg.image_size[0]}px x{model.n_images} + {model.n_text}-tok text, "
                                    f"ToMe r={cfg.tome_r}/block, {cfg.num_blocks} blocks",
                        "global_batch": N * B, "per_gpu_batch": B, "seq_len": sets0.L,
-                       "parallelism": f"dp{N}", "hip_graph": use_graph},
+                       "parallelism": f"dp{N}", "hip_graph": use_graph,
+                       "deterministic": os.environ.get("MMT_DETERMINISTIC", "0") == "1"},
             "model_tflops_per_s": round(value * fps / 1e12, 2),
             "algorithmic_gflop_per_sample": round(fps / 1e9, 2),
             "final_loss": round(loss_val, 5),

@@ -45,6 +45,17 @@ const char* mmt_last_error(void);
 #define MMT_API_VERSION 2
 int mmt_version(void);
 
+/* Deterministic mode (SURVEY §5 "deterministic-mode reruns"). The gradient accumulations that are
+ * otherwise fp32 atomics (bias / LayerNorm / GroupNorm / embedding / Fourier gradients, the
+ * attention's QKV bias sums) go, for addresses inside the registered fp32 gradient buffer
+ * [grad, grad + n), to fx: a signed 64-bit fixed-point shadow of it (round(v * 2^36), integer
+ * atomics: order-independent). mmt_det_flush then adds fx * 2^-36 into grad and clears fx, so a
+ * step's gradients are bitwise reproducible. fx NULL turns the mode off. mmt_set_deterministic is
+ * synchronous: call it outside stream capture; fx must be zero-initialised. Replaces nothing in
+ * the reference (its XLA reductions are deterministic per backend); reproducibility only. */
+int mmt_set_deterministic(float* grad, long long* fx, int64_t n);
+int mmt_det_flush(float* grad, long long* fx, int64_t n, mmt_stream_t stream);
+
 /* Bytes of caller-provided device workspace an entry point needs (the library
  * allocates nothing; scratch comes from the caller). op / dims:
  *   MMT_WS_TOME_MATCH  {n, t, c}  (mmt_tome_match)

@@ -43,6 +43,8 @@ SIGNATURES: dict[str, list] = {
     "mmt_topk_scatter_bwd": [P, I, I, I, I, L, L, P, I, P, L, L, P],
     "mmt_gemm_set_variant": [I],
     "mmt_gemm_set_nres": [I],
+    "mmt_set_deterministic": [P, P, L],
+    "mmt_det_flush": [P, P, L, P],
     "mmt_gemm_colsum_rows": [I, I, I, I, I, I, I],
     "mmt_gemm_dropout_keep_bits": [P, U32, U32, I, I, F, L, P, P],
     "mmt_gemm": [I, I, I, P, I, L, P, I, L, P, I, L, I, L, L, L, I, P, P, L, P],

@@ -51,6 +51,7 @@ class LayerCtx:
     train: bool = True
     rng: Optional[torch.Tensor] = None
     sample_offset: int = 0         # global index of this rank's first sample (RNG counters)
+    tome_forced: Optional[tuple] = None  # injected (unm, src, dst) in place of the matching (tests)
 
 
 _SIDE = {}
@@ -276,7 +277,7 @@ class Encoder1DBlock(Bindable):
                                     device=x.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                tome_idx = K.tome_match(metric, ctx.r)
+                tome_idx = ctx.tome_forced if ctx.tome_forced is not None else K.tome_match(metric, ctx.r)
                 if kbits is not None:
                     K.gemm_dropout_keep_bits(ctx.rng, ctx.layer, DROP_MLP_HIDDEN, B * L2p, Mh, kpm,
                                              ctx.sample_offset * L2p, out=kbits)

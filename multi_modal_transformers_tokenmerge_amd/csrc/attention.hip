@@ -253,7 +253,7 @@ __device__ __forceinline__ void colsum_atomic(const floatx16 (&acc)[ND], float s
     float sum = 0.f;
 #pragma unroll
     for (int w = 0; w < NTT / 64; ++w) sum += wsum[w * ROWS + i];
-    atomicAdd(gbias + i, sum);
+    grad_add(gbias + i, sum);
   }
   __syncthreads();  // red / wsum may be reused by the next call
 }
@@ -1290,7 +1290,7 @@ __device__ __forceinline__ void res_bias_reduce(const float (&b16)[16], float sc
     for (int w = 0; w < RES_NW; ++w)
 #pragma unroll
       for (int j = 0; j < 16; ++j) sum += red[(w * 64 + 16 * rho + j) * 16 + r];
-    atomicAdd(row + d, sum);
+    grad_add(row + d, sum);
   }
   __syncthreads();
 }
@@ -1708,7 +1708,7 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
     for (int w = 0; w < nw; ++w)
 #pragma unroll
       for (int j = 0; j < 16; ++j) sum += red[((i * 8 + w0 + w) * 64 + 16 * rho + j) * 16 + r];
-    atomicAdd(dst + d, sum);
+    grad_add(dst + d, sum);
   };
 
   if (wave < RES8_NA) {
@@ -1748,12 +1748,16 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
       for (int d = 0; d < 2; ++d)
 #pragma unroll
         for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
+      // the dropout lane masks (scalar loads) one tile ahead: waited for at first use otherwise
+      TileMasks<16> dmq[2];
+      if constexpr (DROP) dmq[0].load(drop_q, drop_lp, blk, 0);
 #pragma unroll
       for (int t = 0; t < NTILE; ++t) {
         const uint32_t vw = vws[t];
+        if constexpr (DROP)
+          if (t + 1 < NTILE) dmq[(t + 1) & 1].load(drop_q, drop_lp, blk, 32 * (t + 1));
         if (!__all(vw == 0u)) {  // wave-uniform
-          TileMasks<16> dm;
-          if constexpr (DROP) dm.load(drop_q, drop_lp, blk, 32 * t);
+          const TileMasks<16>& dm = dmq[t & 1];
           floatx16 sacc, pacc;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -2670,3 +2674,7 @@ extern "C" int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
   MMT_CHECK_LAUNCH("mmt_attn_bwd");
   return MMT_OK;
 }
+
+namespace mmt {
+int det_set_attention(const DetState& st) { return det_set_unit(st); }
+}  // namespace mmt

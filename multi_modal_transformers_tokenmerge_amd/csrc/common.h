@@ -150,6 +150,50 @@ __device__ __forceinline__ void dma16_asm(const void* base, int64_t bytes, void*
                :: "v"(voffset), "s"(r), "s"(l) : "m0", "memory");
 }
 
+// ---------------------------------------------------------------- deterministic mode
+// mmt_set_deterministic (SURVEY §5 "deterministic-mode reruns"): every gradient accumulation that
+// is otherwise an fp32 atomicAdd into the flat gradient buffer (bias / LayerNorm / GroupNorm /
+// embedding / Fourier gradients: the per-workgroup partials of a column sum) becomes an integer
+// add of round(v * 2^36) into a signed 64-bit fixed-point shadow of that buffer. Integer adds
+// commute, so the sum no longer depends on the order in which workgroups arrive: the gradients
+// of a step are bitwise reproducible. mmt_det_flush adds the shadow (x 2^-36) into the fp32
+// buffer and clears it. Resolution 2^-36 (1.5e-11) per contribution, range |sum| < 2^27.
+// Each translation unit holds its own copy of the state (static __constant__), set by its
+// det_set_<unit> (core.hip's mmt_set_deterministic calls them all).
+struct DetState {
+  float* base;     // the fp32 gradient buffer whose additions go to fx (NULL: mode off)
+  long long* fx;   // fixed-point shadow, same offsets as base
+  int64_t n;       // elements
+};
+constexpr double DET_SCALE = 68719476736.0;  // 2^36
+static __constant__ DetState g_det;
+static DetState g_det_host{};  // this unit's host copy (kernel-variant choices)
+
+__device__ __forceinline__ long long det_fixed(float v) {
+  const double s = (double)v * DET_SCALE;
+  return __double2ll_rn(fmin(fmax(s, -9.0e18), 9.0e18));
+}
+// dst += v: an fp32 atomic, or in deterministic mode (dst inside the registered gradient buffer)
+// a 64-bit integer atomic on the fixed-point shadow
+__device__ __forceinline__ void grad_add(float* dst, float v) {
+  if (g_det.fx != nullptr) {
+    const int64_t i = dst - g_det.base;
+    if (i >= 0 && i < g_det.n) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(g_det.fx + i), (unsigned long long)det_fixed(v));
+      return;
+    }
+  }
+  atomicAdd(dst, v);
+}
+inline int det_set_unit(const DetState& st) {
+  g_det_host = st;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_det), &st, sizeof st) == hipSuccess ? 0 : -1;
+}
+int det_set_attention(const DetState&);
+int det_set_glue(const DetState&);
+int det_set_norm(const DetState&);
+int det_set_stem(const DetState&);
+
 // XCD-aware bijective remap: workgroups b and b+8 share an XCD (round-robin dispatch), so give
 // each XCD a contiguous range of work ids: items that share operands (a GEMM's A row panel, the
 // key/query blocks of one attention (sample, head)) then meet in one L2. Speed only.

@@ -29,3 +29,17 @@ extern "C" int64_t mmt_workspace_size(int op, const int64_t* dims, int ndims) {
       return MMT_ERR_INVALID;
   }
 }
+
+// Deterministic mode on (fx non-NULL: the fixed-point shadow of the n-float gradient buffer at
+// grad, zero-initialised by the caller) or off (fx NULL). Sets every unit's device state
+// (synchronous; call outside stream capture).
+extern "C" int mmt_set_deterministic(float* grad, long long* fx, int64_t n) {
+  MMT_CHECK_ARG(!fx || (grad && n > 0), "mmt_set_deterministic: args");
+  const mmt::DetState st{fx ? grad : nullptr, fx, fx ? n : 0};
+  if (mmt::det_set_attention(st) || mmt::det_set_glue(st) || mmt::det_set_norm(st) ||
+      mmt::det_set_stem(st)) {
+    mmt::set_error("mmt_set_deterministic: hipMemcpyToSymbol failed");
+    return MMT_ERR_HIP;
+  }
+  return MMT_OK;
+}

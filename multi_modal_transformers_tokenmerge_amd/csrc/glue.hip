@@ -96,7 +96,7 @@ __global__ void seq_assemble_bwd_kernel(int B, int L, int D, const int32_t* __re
     *reinterpret_cast<uint4*>(dimg + ((int64_t)b * NI + j) * D + d0) = pack8(v);
   } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) atomicAdd(dreadout_pe + (int64_t)j * D + d0 + e, v[e]);
+    for (int e = 0; e < 8; ++e) grad_add(dreadout_pe + (int64_t)j * D + d0 + e, v[e]);
   }
 }
 
@@ -105,6 +105,9 @@ __global__ void seq_assemble_bwd_kernel(int B, int L, int D, const int32_t* __re
 // accumulated with LDS atomics and flushed with one global atomic per table entry. Measured:
 // bound by the LDS float atomics (~50 M per step at B = 256); fewer, longer workgroups were slower.
 constexpr int EMB_COLS = 64, EMB_SPLIT = 128;
+// DET (deterministic mode): the table holds 64-bit fixed-point sums (integer LDS atomics,
+// order-independent) and each entry goes to the gradient's fixed-point shadow (grad_add).
+template <bool DET>
 __global__ __launch_bounds__(256) void embed_grad_kernel(int B, int L, int D, int NI, int Q,
                                                          const int32_t* __restrict__ img_rows,
                                                          const float* __restrict__ dx0,
@@ -112,9 +115,13 @@ __global__ __launch_bounds__(256) void embed_grad_kernel(int B, int L, int D, in
                                                          const int32_t* __restrict__ ctok,
                                                          float* __restrict__ drow_emb,
                                                          float* __restrict__ dcol_emb) {
-  extern __shared__ float tab[];  // [2][Q][EMB_COLS]
+  extern __shared__ float tab[];  // [2][Q][EMB_COLS] (DET: long long)
+  long long* tab64 = reinterpret_cast<long long*>(tab);
   const int c0 = blockIdx.x * EMB_COLS;
-  for (int i = threadIdx.x; i < 2 * Q * EMB_COLS; i += blockDim.x) tab[i] = 0.f;
+  for (int i = threadIdx.x; i < 2 * Q * EMB_COLS; i += blockDim.x) {
+    if constexpr (DET) tab64[i] = 0;
+    else tab[i] = 0.f;
+  }
   __syncthreads();
   const int64_t total = (int64_t)B * NI;
   const int64_t per = (total + gridDim.y - 1) / gridDim.y;
@@ -130,8 +137,14 @@ __global__ __launch_bounds__(256) void embed_grad_kernel(int B, int L, int D, in
       const int rt = rtok[rr], ct = ctok[rr];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        atomicAdd(&tab[rt * EMB_COLS + cv * 8 + e], v[e]);
-        atomicAdd(&tab[(Q + ct) * EMB_COLS + cv * 8 + e], v[e]);
+        if constexpr (DET) {
+          const unsigned long long q = (unsigned long long)det_fixed(v[e]);
+          atomicAdd(reinterpret_cast<unsigned long long*>(&tab64[rt * EMB_COLS + cv * 8 + e]), q);
+          atomicAdd(reinterpret_cast<unsigned long long*>(&tab64[(Q + ct) * EMB_COLS + cv * 8 + e]), q);
+        } else {
+          atomicAdd(&tab[rt * EMB_COLS + cv * 8 + e], v[e]);
+          atomicAdd(&tab[(Q + ct) * EMB_COLS + cv * 8 + e], v[e]);
+        }
       }
     }
   }
@@ -139,8 +152,20 @@ __global__ __launch_bounds__(256) void embed_grad_kernel(int B, int L, int D, in
   for (int i = threadIdx.x; i < 2 * Q * EMB_COLS; i += blockDim.x) {
     const int which = i / (Q * EMB_COLS), rem = i % (Q * EMB_COLS);
     const int tok = rem / EMB_COLS, cc = c0 + rem % EMB_COLS;
-    const float val = tab[i];
-    if (cc < D && val != 0.f) atomicAdd((which ? dcol_emb : drow_emb) + (int64_t)tok * D + cc, val);
+    float* dst = (which ? dcol_emb : drow_emb) + (int64_t)tok * D + cc;
+    if constexpr (DET) {  // the fixed-point partial straight into the shadow (exact)
+      const long long q = tab64[i];
+      const int64_t gi = dst - g_det.base;
+      if (cc < D && q != 0) {
+        if (g_det.fx != nullptr && gi >= 0 && gi < g_det.n)
+          atomicAdd(reinterpret_cast<unsigned long long*>(g_det.fx + gi), (unsigned long long)q);
+        else
+          atomicAdd(dst, (float)((double)q * (1.0 / DET_SCALE)));
+      }
+    } else {
+      const float val = tab[i];
+      if (cc < D && val != 0.f) atomicAdd(dst, val);
+    }
   }
 }
 
@@ -210,7 +235,7 @@ __global__ __launch_bounds__(256) void embed_grad_win_kernel(
     if (u < wn && cc < D) {
       const float val = part[0][u][i % EMB_COLS] + part[1][u][i % EMB_COLS] +
                         part[2][u][i % EMB_COLS] + part[3][u][i % EMB_COLS];
-      if (val != 0.f) atomicAdd(table + (int64_t)(ws + u) * D + cc, val);
+      if (val != 0.f) grad_add(table + (int64_t)(ws + u) * D + cc, val);
     }
   }
 }
@@ -395,7 +420,7 @@ __global__ void fourier_bwd_kernel(const bf16_t* __restrict__ dfeats, int B, int
       acc += tt * (cosf(h) * ds - sinf(h) * dc);
     }
   }
-  atomicAdd(dw + k, acc);
+  grad_add(dw + k, acc);
 }
 
 // loss = mean_b sum_j 0.5 (pred - eps)^2 (optax.l2_loss, diffusion.py:141-142);
@@ -560,6 +585,39 @@ __global__ void cast_f32_bf16_kernel(const float* __restrict__ a, bf16_t* __rest
 
 __global__ void step_advance_kernel(int32_t* state) { state[1] += 1; }
 
+
+// The LDS-table embedding-gradient kernel, in its deterministic form when the mode is on.
+void launch_embed_table(dim3 grid, hipStream_t s, int B, int L, int D, int NI, int Q,
+                        const int32_t* img_rows, const float* dx0, const int32_t* rtok,
+                        const int32_t* ctok, float* drow_emb, float* dcol_emb) {
+  static const bool attr_ = (hipFuncSetAttribute((const void*)embed_grad_kernel<false>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 160 * 1024) == hipSuccess &&
+                             hipFuncSetAttribute((const void*)embed_grad_kernel<true>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 160 * 1024) == hipSuccess);
+  (void)attr_;
+  if (g_det_host.fx)
+    hipLaunchKernelGGL(embed_grad_kernel<true>, grid, dim3(256), sizeof(long long) * 2 * Q * EMB_COLS,
+                       s, B, L, D, NI, Q, img_rows, dx0, rtok, ctok, drow_emb, dcol_emb);
+  else
+    hipLaunchKernelGGL(embed_grad_kernel<false>, grid, dim3(256), sizeof(float) * 2 * Q * EMB_COLS,
+                       s, B, L, D, NI, Q, img_rows, dx0, rtok, ctok, drow_emb, dcol_emb);
+}
+
+// deterministic mode: grad += shadow x 2^-36, shadow = 0 (elementwise: the result is independent
+// of every ordering)
+__global__ void det_flush_kernel(float* __restrict__ grad, long long* __restrict__ fx, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const long long q = fx[i];
+    if (q != 0) {
+      grad[i] += (float)((double)q * (1.0 / DET_SCALE));
+      fx[i] = 0;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int mmt_seq_assemble_fwd(int B, int L, int D, const int32_t* row_src, const void* text,
@@ -589,6 +647,8 @@ extern "C" int mmt_seq_assemble_bwd(int B, int L, int D, const int32_t* row_src,
   MMT_CHECK_ARG(NI == 0 || !emb || (img_rows && rtok && ctok && drow_emb && dcol_emb && Q > 0 &&
                                     2 * Q * EMB_COLS * 4 <= 160 * 1024),
                 "mmt_seq_assemble_bwd: image embedding arguments");
+  MMT_CHECK_ARG(NI == 0 || !emb || !g_det_host.fx || 2 * Q * EMB_COLS * 8 <= 160 * 1024,
+                "mmt_seq_assemble_bwd: Q too large for the deterministic table");
   const int64_t n = (int64_t)B * L * (D / 8);
   hipStream_t s = as_stream(stream);
   hipLaunchKernelGGL(seq_assemble_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0, s, B, L, D,
@@ -596,14 +656,8 @@ extern "C" int mmt_seq_assemble_bwd(int B, int L, int D, const int32_t* row_src,
                      drow_emb, dcol_emb, dreadout_pe);
   MMT_CHECK_LAUNCH("mmt_seq_assemble_bwd");
   if (NI > 0 && emb) {
-    const size_t sh = sizeof(float) * 2 * Q * EMB_COLS;
-    static const bool attr_ = (hipFuncSetAttribute((const void*)embed_grad_kernel,
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                   160 * 1024), true);
-    (void)attr_;
-    hipLaunchKernelGGL(embed_grad_kernel, dim3((D + EMB_COLS - 1) / EMB_COLS, EMB_SPLIT), dim3(256),
-                       sh, s, B, L, D, NI, Q, img_rows, (const float*)dx0, rtok, ctok, drow_emb,
-                       dcol_emb);
+    launch_embed_table(dim3((D + EMB_COLS - 1) / EMB_COLS, EMB_SPLIT), s, B, L, D, NI, Q, img_rows,
+                       (const float*)dx0, rtok, ctok, drow_emb, dcol_emb);
     MMT_CHECK_LAUNCH("mmt_seq_assemble_bwd(embedding grads)");
   }
   return MMT_OK;
@@ -633,14 +687,9 @@ extern "C" int mmt_patch_embed_grad(int B, int L, int D, int I, int Himg, int P,
   else if (wmax <= 16) EGW(16);
   else {  // wide windows: the LDS-atomic table kernel
     const int NI = I * PPD * PPD;
-    MMT_CHECK_ARG(2 * Q * EMB_COLS * 4 <= 160 * 1024, "mmt_patch_embed_grad: Q too large");
-    static const bool attr_ = (hipFuncSetAttribute((const void*)embed_grad_kernel,
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                   160 * 1024), true);
-    (void)attr_;
-    hipLaunchKernelGGL(embed_grad_kernel, dim3(chunks, EMB_SPLIT), dim3(256),
-                       sizeof(float) * 2 * Q * EMB_COLS, s, B, L, D, NI, Q, img_rows,
-                       (const float*)dx0, rtok, ctok, drow_emb, dcol_emb);
+    MMT_CHECK_ARG(2 * Q * EMB_COLS * 8 <= 160 * 1024, "mmt_patch_embed_grad: Q too large");
+    launch_embed_table(dim3(chunks, EMB_SPLIT), s, B, L, D, NI, Q, img_rows, (const float*)dx0, rtok,
+                       ctok, drow_emb, dcol_emb);
   }
 #undef EGW
   MMT_CHECK_LAUNCH("mmt_patch_embed_grad");
@@ -820,5 +869,18 @@ extern "C" int mmt_add_position_embedding(const float* x, const float* pe, float
   hipLaunchKernelGGL(add_pe_kernel, dim3(blocks), dim3(256), 0, as_stream(stream),
                      (const float4*)x, (const float4*)pe, (float4*)out, n4, per4);
   MMT_CHECK_LAUNCH("mmt_add_position_embedding");
+  return MMT_OK;
+}
+
+namespace mmt {
+int det_set_glue(const DetState& st) { return det_set_unit(st); }
+}  // namespace mmt
+
+extern "C" int mmt_det_flush(float* grad, long long* fx, int64_t n, mmt_stream_t stream) {
+  MMT_CHECK_ARG(grad && fx && n >= 0, "mmt_det_flush: args");
+  if (n == 0) return MMT_OK;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(det_flush_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), grad, fx, n);
+  MMT_CHECK_LAUNCH("mmt_det_flush");
   return MMT_OK;
 }

@@ -244,8 +244,8 @@ __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
   }
   reduce_rows<4>(part, red);
   if (threadIdx.x < CW && c0 + threadIdx.x < D) {
-    atomicAdd(dgamma + c0 + threadIdx.x, red[2 * RG * CW + threadIdx.x]);
-    atomicAdd(dbeta + c0 + threadIdx.x, red[3 * RG * CW + threadIdx.x]);
+    grad_add(dgamma + c0 + threadIdx.x, red[2 * RG * CW + threadIdx.x]);
+    grad_add(dbeta + c0 + threadIdx.x, red[3 * RG * CW + threadIdx.x]);
   }
   // (threads past D skip the loop but stay for the DZ reduction's barriers)
   float mg[8], mgx[8];
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
     __syncthreads();  // every thread has read mg / mgx out of red
     reduce_rows<1>(p1, red);
     if (dz.colsum && threadIdx.x < CW && c0 + threadIdx.x < D)
-      atomicAdd(dz.colsum + c0 + threadIdx.x, red[threadIdx.x]);
+      grad_add(dz.colsum + c0 + threadIdx.x, red[threadIdx.x]);
   }
 }
 
@@ -405,8 +405,8 @@ __global__ __launch_bounds__(NT) void ln_unmerge_dropout_bwd_kernel(
   }
   reduce_rows<4>(part, red);
   if (threadIdx.x < CW && c0 + threadIdx.x < D) {
-    atomicAdd(dgamma + c0 + threadIdx.x, red[2 * RG * CW + threadIdx.x]);
-    atomicAdd(dbeta + c0 + threadIdx.x, red[3 * RG * CW + threadIdx.x]);
+    grad_add(dgamma + c0 + threadIdx.x, red[2 * RG * CW + threadIdx.x]);
+    grad_add(dbeta + c0 + threadIdx.x, red[3 * RG * CW + threadIdx.x]);
   }
   float mg[8], mgx[8];
 #pragma unroll
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(NT) void ln_unmerge_dropout_bwd_kernel(
   for (int e = 0; e < 8; ++e) part1[0][e] = cs[e];
   reduce_rows<1>(part1, red);
   if (bias_grad && threadIdx.x < CW && c0 + threadIdx.x < D)
-    atomicAdd(bias_grad + c0 + threadIdx.x, red[threadIdx.x]);
+    grad_add(bias_grad + c0 + threadIdx.x, red[threadIdx.x]);
 }
 
 // out[n] += sum_m x[m][n]  and, with z != NULL, z = x * keep / keep_prob (keep = 1 when rng is
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(NT) void colsum_kernel(const T* __restrict__ x, int
     }
   if (!out) return;
   reduce_rows<1>(part, red);
-  if (threadIdx.x < CW && c0 + threadIdx.x < N) atomicAdd(out + c0 + threadIdx.x, red[threadIdx.x]);
+  if (threadIdx.x < CW && c0 + threadIdx.x < N) grad_add(out + c0 + threadIdx.x, red[threadIdx.x]);
 }
 
 inline bool is_dt(int d) { return d == MMT_F32 || d == MMT_BF16; }
@@ -722,3 +722,7 @@ extern "C" int mmt_seqnorm_dropout_bwd(const void* dy, int64_t ds_b, int64_t ds_
   MMT_CHECK_LAUNCH("mmt_seqnorm_dropout_bwd");
   return MMT_OK;
 }
+
+namespace mmt {
+int det_set_norm(const DetState& st) { return det_set_unit(st); }
+}  // namespace mmt

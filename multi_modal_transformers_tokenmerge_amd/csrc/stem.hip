@@ -639,8 +639,8 @@ __global__ __launch_bounds__(GN_NT) void groupnorm_gelu_bwd_kernel(
       s3 += p[2 * GN_NT + t * C + threadIdx.x];
       s4 += p[3 * GN_NT + t * C + threadIdx.x];
     }
-    atomicAdd(dgamma + threadIdx.x, s3);
-    atomicAdd(dbeta + threadIdx.x, s4);
+    grad_add(dgamma + threadIdx.x, s3);
+    grad_add(dbeta + threadIdx.x, s4);
   }
   __syncthreads();
   const float m1 = gm1[g], m2 = gm2[g];
@@ -804,8 +804,8 @@ __global__ __launch_bounds__(GN_NT) void groupnorm_gelu_bwd_reg_kernel(
       s3 += red[2][w][t];
       s4 += red[3][w][t];
     }
-    atomicAdd(dgamma + t, s3);
-    atomicAdd(dbeta + t, s4);
+    grad_add(dgamma + t, s3);
+    grad_add(dbeta + t, s4);
   }
   __syncthreads();
   float m1[4], m2[4];
@@ -1087,3 +1087,7 @@ extern "C" int mmt_col2im_same(const float* dcols, int64_t npatch, int H, int W,
   MMT_CHECK_LAUNCH("mmt_col2im_same");
   return MMT_OK;
 }
+
+namespace mmt {
+int det_set_stem(const DetState& st) { return det_set_unit(st); }
+}  // namespace mmt

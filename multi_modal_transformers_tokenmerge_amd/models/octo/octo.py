@@ -17,6 +17,8 @@ step is captured into a HIP graph and replayed (see OCTOTrainState.graphed_step)
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional
 
@@ -98,6 +100,9 @@ class Octo:
                                                           cfg.action_space_dim, cfg.num_bins,
                                                           cfg.max_action)
         store.materialize(self.device, seed)
+        # MMT_DETERMINISTIC=1: bitwise-reproducible gradients (ParamStore.set_deterministic)
+        if os.environ.get("MMT_DETERMINISTIC", "0") == "1" and torch.device(self.device).type == "cuda":
+            store.set_deterministic(True)
         self.t5 = T5Tokenizer(cfg.t5).materialize(self.device, seed + 1) if self.has_text else None
         self._build_tables()
 
@@ -184,7 +189,7 @@ class Octo:
 
     # ------------------------------------------------------------------ forward / backward
     def generate_readouts(self, text_tokens, images, train=True, rng=None, sample_offset=0,
-                          positions=None):
+                          positions=None, tome=None):
         """Reference :91-126. Returns the final sequence (B, L_final, D) and the saved state."""
         B = images.shape[0]
         D = self.D
@@ -207,16 +212,21 @@ class Octo:
                 _C.ptr(self.image_tokenizer.col_emb.data), _C.ptr(self.readout_pe.data),
                 _C.ptr(self.pos_embed.data), _C.ptr(x0), _C.stream_ptr())
         ctxs = self.layer_ctxs(train, rng, sample_offset)
+        if tome is not None:  # injected ToMe index triples (tests: the golden step fixtures)
+            for c, idx in zip(ctxs, tome):
+                c.tome_forced = idx
         xL, ssv = self.stack.forward(x0, ctxs)
         st.update(ctxs=ctxs, stack_sv=ssv, NI=NI, T=T)
         return xL, st
 
     def compute_diffusion_denoise_loss(self, text_tokens, images, actions, train=True, rng=None,
                                        sample_offset=0, inject: Optional[dict] = None):
-        """Reference :139-145. Returns (loss (1,) fp32 device tensor, saved state)."""
+        """Reference :139-145. Returns (loss (1,) fp32 device tensor, saved state). inject (tests):
+        positions (rt, ct), t, eps, tome (per block an (unm, src, dst) triple of int32 device
+        tensors or None) replace the step's own draws / matching."""
         inject = inject or {}
         xL, st = self.generate_readouts(text_tokens, images, train, rng, sample_offset,
-                                        inject.get("positions"))
+                                        inject.get("positions"), inject.get("tome"))
         B = xL.shape[0]
         cat = self.head.new_cat(B, xL.device)
         _C.call("mmt_rows_mean_fwd", _C.ptr(xL), xL.stride(0), xL.stride(1), B, self.D,
@@ -375,6 +385,8 @@ class Octo:
                 st.pop("_dx", None)
             else:
                 st["_dx"] = dx
+        if self.store.det_fx is not None:  # deterministic mode: this stage's final region
+            self.store.det_flush(*self.grad_regions(stages)[stage])
 
     def backward(self, st: Dict):
         """Reverse schedule of compute_diffusion_denoise_loss / compute_l2_loss / compute_ce_loss;

@@ -190,6 +190,43 @@ class ParamStore:
     def zero_grad(self):
         self.flat_grad.zero_()
 
+    # ------------------------------------------------------------------ deterministic mode
+    det_fx = None  # int64 fixed-point shadow of flat_grad while the mode is on
+
+    def set_deterministic(self, on: bool = True):
+        """Deterministic mode (include/mmt_api.h mmt_set_deterministic): the gradient sums that
+        are fp32 atomics otherwise go to an int64 fixed-point shadow of flat_grad (integer adds:
+        order-independent), added into flat_grad by det_flush. One store per process holds it
+        (the library keeps one registration); synchronous, so call outside graph capture."""
+        from . import _C
+        if on:
+            self.det_fx = torch.zeros(self.n, dtype=torch.int64, device=self.flat_grad.device)
+            _C.call("mmt_set_deterministic", _C.ptr(self.flat_grad), _C.ptr(self.det_fx), self.n)
+            ParamStore._det_owner = self
+        else:
+            if ParamStore._det_owner is self:
+                _C.call("mmt_set_deterministic", None, None, 0)
+                ParamStore._det_owner = None
+            self.det_fx = None
+
+    _det_owner = None
+
+    def det_flush(self, lo: int = 0, hi: int | None = None):
+        """flat_grad[lo:hi] += shadow * 2^-36, shadow[lo:hi] = 0 (no-op outside the mode)."""
+        if self.det_fx is None:
+            return
+        from . import _C
+        hi = self.n if hi is None else hi
+        _C.call("mmt_det_flush", _C.ptr(self.flat_grad[lo:]), _C.ptr(self.det_fx[lo:]), hi - lo,
+                _C.stream_ptr())
+
+    def __del__(self):
+        try:
+            if ParamStore._det_owner is self:
+                self.set_deterministic(False)
+        except Exception:  # interpreter shutdown: the library may be gone
+            pass
+
     def sync_shadow(self):
         """Re-derive the bf16 shadow after the master was modified outside AdamW."""
         self.flat_bf16.copy_(self.flat.to(torch.bfloat16))

@@ -231,3 +231,38 @@ def test_ddp_stage_plan_regions_cover_the_store():
     for bad in ([nb, 6, 6, 0], [nb - 1, 0], [nb, 3], [nb, 7, 9, 0], [0], [nb, 2.5, 0]):
         with pytest.raises(ValueError):   # regions missing / overlapping: refused
             m.stage_bounds(bad)
+
+
+def test_step_fixtures_randomness_and_position_kats():
+    """The committed step fixtures (tests/golden/step_*_golden.npz) hold the oracle's counter-stream
+    restatements (oracle/rng.py): recomputed here they agree exactly (t, positions) / bitwise
+    (eps, same numpy); the position restatement also meets SURVEY §8c KAT-3 (eval midpoints of a
+    256^2 image, patch 16) and the reference's own test_image_tokenizer.py:41-53 case
+    (128^2, patch 1: row[123] == 122, shape (16384,))."""
+    import ast
+    from pathlib import Path
+    from multi_modal_transformers_tokenmerge_amd.models.octo.config import get_config
+    g = Path(__file__).resolve().parent / "golden"
+    for f in sorted(g.glob("step_*_golden.npz")):
+        z = np.load(f)
+        cfg = get_config(str(z["config"]), **ast.literal_eval(str(z["overrides"])))
+        B, seed, step = int(z["B"]), int(z["rng_seed"]), int(z["rng_step"])
+        n_img = z["images"].shape[1]
+        patch = z["images"].shape[2] // int(round(np.sqrt(z["rt"].shape[1] / n_img)))
+        rt, ct = R.patch_positions(seed, step, 0, B, n_img, cfg.image_size[0], patch, 128)
+        np.testing.assert_array_equal(rt, z["rt"])
+        np.testing.assert_array_equal(ct, z["ct"])
+        t, eps = R.diffusion_t_eps(seed, step, B, cfg.action_space_dim, cfg.diffusion_steps)
+        np.testing.assert_array_equal(t, z["t"])
+        np.testing.assert_array_equal(eps, z["eps"])
+        assert (0 <= z["t"]).all() and (z["t"] < cfg.diffusion_steps).all()
+        from oracle import tome as T
+        for li in range(int(z["n_tome"])):  # the stored indices are the canonical match of the metric
+            metric = (z[f"tome{li}/metric_bf16"].astype(np.uint32) << 16).view(np.float32)
+            unm, src, dst, _ = T.canon_match(metric, cfg.tome_r)
+            for nm, a in (("unm", unm), ("src", src), ("dst", dst)):
+                np.testing.assert_array_equal(a, z[f"tome{li}/{nm}"])
+    rte, cte = R.patch_positions(0, 0, 0, 1, 1, 256, 16, 128, train=False)
+    assert (rte[0] == 3 + 8 * (np.arange(256) % 16)).all() and (cte[0] == 3 + 8 * (np.arange(256) // 16)).all()
+    r2, _ = R.patch_positions(0, 0, 0, 1, 1, 128, 1, 128, train=False)
+    assert r2.shape == (1, 16384) and r2[0, 123] == 122

@@ -109,7 +109,8 @@ def test_stack_autograd_matches_explicit_backward(dev, ref_setup):
         if p.name.endswith("/kernel"):
             assert torch.equal(mine[p.name], p.grad), p.name
         else:
-            torch.testing.assert_close(mine[p.name], p.grad, rtol=1e-5, atol=1e-6)
+            # bias / LayerNorm gradients: fp32 atomics (summation order varies run to run)
+            torch.testing.assert_close(mine[p.name], p.grad, rtol=2e-4, atol=1e-5)
     # posembed_input gradient = column sums of dx over the batch
     torch.testing.assert_close(mine["StackedEncoder1DBlock_0/posembed_input/pos_embedding"],
                                dx.sum(0), rtol=1e-5, atol=1e-5)
