@@ -35,6 +35,7 @@ from ..layers import (DROP_ATTN, DROP_ATTN_OUT, DROP_MLP_HIDDEN, DROP_MLP_OUT, D
 from ..config_loader import LayerSpec
 from ..module_api import Bindable, init_from_spec, merge_param, sget, spec
 from ..params import ParamStore, he_normal, normal
+from ..tracing import phase
 from ..tokenizers.token_sequencer import LayerSets, sets_from_mask
 
 
@@ -519,7 +520,8 @@ class StackedEncoder1DBlock(Bindable):
         saved = []
         size = None
         for blk, ctx in zip(self.blocks, ctxs):
-            x, sv, size = blk.forward(x, ctx, size)
+            with phase(f"fwd/block{ctx.layer}"):
+                x, sv, size = blk.forward(x, ctx, size)
             saved.append(sv)
         return x, saved
 
@@ -531,6 +533,7 @@ class StackedEncoder1DBlock(Bindable):
         for i in range(hi - 1, lo - 1, -1):
             # block i's LayerNorm_0 backward also does block i-1's MLP-output dropout backward
             prev = (self.blocks[i - 1], saved[i - 1], ctxs[i - 1]) if i - 1 >= lo else None
-            dx, dz = self.blocks[i].backward(dx, saved[i], ctxs[i], dz2=dz, prev=prev)
+            with phase(f"bwd/block{i}"):
+                dx, dz = self.blocks[i].backward(dx, saved[i], ctxs[i], dz2=dz, prev=prev)
             wgrad_overlap.block_done()
         return dx

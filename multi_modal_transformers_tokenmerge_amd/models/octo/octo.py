@@ -26,6 +26,7 @@ import numpy as np
 import torch
 
 from ... import _C, _kernels as K
+from ...tracing import phase
 from ...action_heads.categorical import CategoricalActionHead
 from ...action_heads.continuous import ContinuousActionHead
 from ...action_heads.diffusion import DiffusionActionHead
@@ -196,14 +197,16 @@ class Octo:
         st: Dict = dict(B=B, train=train, rng=rng, sample_offset=sample_offset)
         txt, T = None, max(self.n_text, 1)
         if self.has_text:
-            t5_out = self.t5(text_tokens)                                   # stop_gradient
+            with phase("fwd/t5"):
+                t5_out = self.t5(text_tokens)                               # stop_gradient
             st["t5_out"] = t5_out
             if self.text_proj is not None:
                 txt = self.text_proj.fwd(t5_out.view(B * self.n_text, -1)).view(B, self.n_text, D)
             else:
                 txt = t5_out
-        img_tok, (rt, ct), isv = self.image_tokenizer.forward(images, train, rng, sample_offset,
-                                                              positions)
+        with phase("fwd/stem"):
+            img_tok, (rt, ct), isv = self.image_tokenizer.forward(images, train, rng, sample_offset,
+                                                                  positions)
         st.update(img_sv=isv, rt=rt, ct=ct, img_tok=img_tok, txt=txt)
         x0 = torch.empty((B, self.L0, D), dtype=torch.float32, device=images.device)  # fp32 residual
         NI = img_tok.shape[1]
@@ -215,7 +218,8 @@ class Octo:
         if tome is not None:  # injected ToMe index triples (tests: the golden step fixtures)
             for c, idx in zip(ctxs, tome):
                 c.tome_forced = idx
-        xL, ssv = self.stack.forward(x0, ctxs)
+        with phase("fwd/blocks"):
+            xL, ssv = self.stack.forward(x0, ctxs)
         st.update(ctxs=ctxs, stack_sv=ssv, NI=NI, T=T)
         return xL, st
 
@@ -232,8 +236,9 @@ class Octo:
         _C.call("mmt_rows_mean_fwd", _C.ptr(xL), xL.stride(0), xL.stride(1), B, self.D,
                 _C.ptr(self.readout_rows), self.readout_rows.numel(),
                 _C.ptr(self.head.readout_slot(cat)), cat.stride(0), _C.stream_ptr())
-        loss, hsv = self.head.loss_forward(cat, actions, rng, sample_offset, inject.get("t"),
-                                           inject.get("eps"))
+        with phase("fwd/head"):
+            loss, hsv = self.head.loss_forward(cat, actions, rng, sample_offset, inject.get("t"),
+                                               inject.get("eps"))
         st.update(head_sv=hsv, xL_shape=tuple(xL.shape), xL=xL)
         return loss, st
 
@@ -377,11 +382,14 @@ class Octo:
         n_stages = len(b) - 1
         with wgrad_overlap(self.device):  # dW products beside the critical path; joined here
             if stage == 0:
-                st["_dx"] = self._backward_head(st)
-            dx = self.stack.backward(st["_dx"], st["stack_sv"], st["ctxs"], lo=b[stage + 1],
-                                     hi=b[stage])
+                with phase("bwd/head"):
+                    st["_dx"] = self._backward_head(st)
+            with phase(f"bwd/blocks[{b[stage + 1]},{b[stage]})"):
+                dx = self.stack.backward(st["_dx"], st["stack_sv"], st["ctxs"], lo=b[stage + 1],
+                                         hi=b[stage])
             if stage == n_stages - 1:
-                self._backward_tokens(st, dx)
+                with phase("bwd/tokens+stem"):
+                    self._backward_tokens(st, dx)
                 st.pop("_dx", None)
             else:
                 st["_dx"] = dx
@@ -497,6 +505,10 @@ class OCTOTrainState:
         return int(self.rng[1].item())
 
     def apply_gradients(self):
+        with phase("optimizer"):
+            self._apply_gradients()
+
+    def _apply_gradients(self):
         s = self.model.store
         tx = self.tx
         _C.call("mmt_adamw", _C.ptr(s.flat), _C.ptr(s.flat_grad), _C.ptr(s.m), _C.ptr(s.v),

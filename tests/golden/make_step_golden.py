@@ -64,8 +64,8 @@ def pack(out: dict, key: str, arr: np.ndarray):
     out[f"{key}:norm"] = np.float64(np.linalg.norm(a))
     if a.size <= WHOLE:
         out[f"{key}:all"] = a.astype(np.float32)
-    else:
-        idx = sample_index(key, a.size)
+    else:  # the same positions for the emu and f64 copies of a tensor
+        idx = sample_index(key.split("/", 1)[1], a.size)
         out[f"{key}:idx"] = idx
         out[f"{key}:val"] = a[idx].astype(np.float32)
 
