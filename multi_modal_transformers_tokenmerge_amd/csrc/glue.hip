@@ -687,7 +687,8 @@ extern "C" int mmt_patch_embed_grad(int B, int L, int D, int I, int Himg, int P,
   else if (wmax <= 16) EGW(16);
   else {  // wide windows: the LDS-atomic table kernel
     const int NI = I * PPD * PPD;
-    MMT_CHECK_ARG(2 * Q * EMB_COLS * 8 <= 160 * 1024, "mmt_patch_embed_grad: Q too large");
+    MMT_CHECK_ARG(2 * Q * EMB_COLS * (g_det_host.fx ? 8 : 4) <= 160 * 1024,
+                  "mmt_patch_embed_grad: Q too large%s", g_det_host.fx ? " for the deterministic table" : "");
     launch_embed_table(dim3(chunks, EMB_SPLIT), s, B, L, D, NI, Q, img_rows, (const float*)dx0, rtok,
                        ctok, drow_emb, dcol_emb);
   }

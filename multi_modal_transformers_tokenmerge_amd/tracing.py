@@ -10,11 +10,15 @@ import os
 
 import torch
 
-ENABLED = os.environ.get("MMT_ROCTX", "0") == "1"
+MODE = int(os.environ.get("MMT_ROCTX", "0") or 0)  # 1 ranges, 2 ranges + synchronize at each end
+ENABLED = MODE > 0
 
 
 @contextlib.contextmanager
 def phase(name: str):
+    """MMT_ROCTX=2 also synchronizes the device when a range closes, so an eager step's kernels
+    run inside the range that launched them (per-phase GPU time; the side-stream overlap of the
+    weight gradients is lost while measuring)."""
     if not ENABLED:
         yield
         return
@@ -22,4 +26,6 @@ def phase(name: str):
     try:
         yield
     finally:
+        if MODE >= 2 and not torch.cuda.is_current_stream_capturing():
+            torch.cuda.synchronize()
         torch.cuda.nvtx.range_pop()
