@@ -50,6 +50,7 @@ SIGNATURES: dict[str, list] = {
     "mmt_gemm": [I, I, I, P, I, L, P, I, L, P, I, L, I, L, L, L, I, P, P, L, P],
     "mmt_quant_rows_fp8": [P, L, I, I, P, L, P, P],
     "mmt_gemm_fp8": [I, I, I, P, L, P, P, L, P, P, I, L, P, P],
+    "mmt_gemm_xs": [I, I, I, P, L, P, L, P, L, P, P],
     "mmt_attn_fwd": [P, L, L, I, I, I, I, F, I, P, P, P, P, F, P, P, L, L, P, P, P],
     "mmt_prune_importance": [P, I, I, I, P, P],
     "mmt_gather_rows": [P, I, I, I, I, L, L, P, I, P, L, L, P],
