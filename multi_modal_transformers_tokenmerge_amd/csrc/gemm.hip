@@ -2757,6 +2757,17 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     MMT_CHECK_LAUNCH("mmt_gemm(ntw)");
     return MMT_OK;
   }
+  // activation-stationary short-K kernel (csrc/gemm_xs.hip) for the bias-only bf16 products at
+  // K = 384 (the OCTO-small QKV projection: 198 vs 220 us at B = 512, bit-identical outputs;
+  // tools/xs_bench.py). MMT_XS=0: off (A/B).
+  static const bool g_xs = !getenv("MMT_XS") || atoi(getenv("MMT_XS")) != 0;
+  if (g_xs && g_variant < 0 && !transA && transB && batch == 1 && out_kind == 0 && final_kind == 0 &&
+      K == 384 && N % 64 == 0 && N <= 1536 && M >= 32768 && epi.act == MMT_ACT_NONE && !epi.rng &&
+      !epi.gate && !epi.residual && epi.alpha == 1.f && epi.beta == 0.f && !epi.colsum &&
+      !epi.relu_bits && !epi.gate_bits && !epi.keep_bits && lda % 8 == 0 && ldb % 8 == 0 &&
+      ldc % 8 == 0 && ((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 == 0 &&
+      (!epi.bias || (uintptr_t)epi.bias % 16 == 0))
+    return mmt_gemm_xs(M, N, K, A, lda, B, ldb, C, ldc, epi.bias, stream);
   // Warp-specialised wide NT kernel: bf16 outputs of N % 128 == 0 with the nt256 epilogues that
   // the step uses (bias, relu, dropout, relu_bits, gate_bits, colsum, bf16 / fp32 residual).
   // MMT_NTWS: 0 off, 1 (default) where nt256 would take 192-wide tiles (N % 256 != 0: the QKV

@@ -59,19 +59,20 @@ __device__ __forceinline__ void store8(float* p, const float* f) {
   *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
 }
 
-template <int NV>
-__device__ __forceinline__ void reduce_rows(float (*part)[8], float* red /*[NV][RG][CW]*/) {
-  const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;
+template <int NV, int NTT = NT, int CWT = CW>
+__device__ __forceinline__ void reduce_rows(float (*part)[8], float* red /*[NV][RGT][CWT]*/) {
+  constexpr int CVN = CWT / 8, RGT = NTT / CVN;
+  const int cv = threadIdx.x % CVN, rg = threadIdx.x / CVN;
 #pragma unroll
   for (int v = 0; v < NV; ++v)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) red[(v * RG + rg) * CW + cv * 8 + e] = part[v][e];
+    for (int e = 0; e < 8; ++e) red[(v * RGT + rg) * CWT + cv * 8 + e] = part[v][e];
   __syncthreads();
-  for (int i = threadIdx.x; i < NV * CW; i += NT) {
-    const int v = i / CW, c = i % CW;
+  for (int i = threadIdx.x; i < NV * CWT; i += NTT) {
+    const int v = i / CWT, c = i % CWT;
     float s = 0.f;
-    for (int r = 0; r < RG; ++r) s += red[(v * RG + r) * CW + c];
-    red[(v * RG) * CW + c] = s;
+    for (int r = 0; r < RGT; ++r) s += red[(v * RGT + r) * CWT + c];
+    red[(v * RGT) * CWT + c] = s;
   }
   __syncthreads();
 }
@@ -179,16 +180,17 @@ struct DropZ {
 // RPT > 0 (bf16 dy, fp32 x, L <= 32 RPT): single pass over HBM — each thread keeps its RPT rows
 // of x (fp32) and dy (packed bf16) in registers from the statistics pass to the gradient pass
 // (the two-pass form re-reads both: 1.43x the algorithmic bytes measured at B = 512).
-template <typename TDY, typename TX, bool DZ = false, int RPT = 0>
-__global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
+template <typename TDY, typename TX, bool DZ = false, int RPT = 0, int NTT = NT, int CWT = CW>
+__global__ __launch_bounds__(NTT) void seqnorm_bwd_kernel(
     const TDY* __restrict__ dy, int64_t ds_b, int64_t ds_t, const TX* __restrict__ x,
     int64_t xs_b, int64_t xs_t, int L, int D, const float* __restrict__ mean,
     const float* __restrict__ rstd, const float* __restrict__ gamma, const TX* addend,
     int64_t as_b, int64_t as_t, TX* dx, int64_t dxs_b, int64_t dxs_t,
     float* __restrict__ dgamma, float* __restrict__ dbeta, DropZ dz = DropZ{}) {
-  __shared__ float red[4 * RG * CW];
-  const int b = ln_sample(), c0 = ln_colblk() * CW;
-  const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  constexpr int CVN = CWT / 8, RGT = NTT / CVN;  // column vectors, row groups
+  __shared__ float red[4 * RGT * CWT];
+  const int b = ln_sample(), c0 = ln_colblk() * CWT;
+  const int cv = threadIdx.x % CVN, rg = threadIdx.x / CVN;
   const int col = c0 + cv * 8;
   const bool cok = col < D;
   float mu[8], rs[8], ga[8];
@@ -222,44 +224,44 @@ __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
     if (cok) {
 #pragma unroll
       for (int j = 0; j < RPT; ++j) {
-        const int l = min(rg + j * RG, L - 1);
+        const int l = min(rg + j * RGT, L - 1);
         load8(xb + (int64_t)l * xs_t, rx[j]);
         rdy[j] = *reinterpret_cast<const uint4*>(db + (int64_t)l * ds_t);
       }
 #pragma unroll
       for (int j = 0; j < RPT; ++j) {
-        if (rg + j * RG >= L) rdy[j] = make_uint4(0u, 0u, 0u, 0u);
+        if (rg + j * RGT >= L) rdy[j] = make_uint4(0u, 0u, 0u, 0u);
         float fd[8];
         unpack8(rdy[j], fd);
         stat(rx[j], fd);
       }
     }
   } else if (cok) {
-    for (int l = rg; l < L; l += RG) {
+    for (int l = rg; l < L; l += RGT) {
       float fx[8], fd[8];
       load8(xb + (int64_t)l * xs_t, fx);
       load8(db + (int64_t)l * ds_t, fd);
       stat(fx, fd);
     }
   }
-  reduce_rows<4>(part, red);
-  if (threadIdx.x < CW && c0 + threadIdx.x < D) {
-    grad_add(dgamma + c0 + threadIdx.x, red[2 * RG * CW + threadIdx.x]);
-    grad_add(dbeta + c0 + threadIdx.x, red[3 * RG * CW + threadIdx.x]);
+  reduce_rows<4, NTT, CWT>(part, red);
+  if (threadIdx.x < CWT && c0 + threadIdx.x < D) {
+    grad_add(dgamma + c0 + threadIdx.x, red[2 * RGT * CWT + threadIdx.x]);
+    grad_add(dbeta + c0 + threadIdx.x, red[3 * RGT * CWT + threadIdx.x]);
   }
   // (threads past D skip the loop but stay for the DZ reduction's barriers)
   float mg[8], mgx[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     mg[e] = red[cv * 8 + e] / L;
-    mgx[e] = red[RG * CW + cv * 8 + e] / L;
+    mgx[e] = red[RGT * CWT + cv * 8 + e] / L;
   }
   TX* dxb = dx + (int64_t)b * dxs_b + col;
   const TX* ab = addend ? addend + (int64_t)b * as_b + col : nullptr;
   [[maybe_unused]] float cs[8] = {};
   [[maybe_unused]] const uint32_t key = DZ && dz.rng ? stream_key(dz.rng[0], dz.rng[1], dz.layer, dz.site) : 0u;
 #pragma unroll(RPT > 0 ? RPT : 1)
-  for (int j = 0, l = rg; cok && (RPT > 0 ? j < RPT : l < L); ++j, l += RG) {
+  for (int j = 0, l = rg; cok && (RPT > 0 ? j < RPT : l < L); ++j, l += RGT) {
     // RPT: a fixed trip count and unconditional (row-clamped) addend loads; only the stores of
     // rows past L are skipped
     const int la = RPT > 0 ? min(l, L - 1) : l;
@@ -303,8 +305,8 @@ __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
 #pragma unroll
     for (int e = 0; e < 8; ++e) p1[0][e] = cs[e];
     __syncthreads();  // every thread has read mg / mgx out of red
-    reduce_rows<1>(p1, red);
-    if (dz.colsum && threadIdx.x < CW && c0 + threadIdx.x < D)
+    reduce_rows<1, NTT, CWT>(p1, red);
+    if (dz.colsum && threadIdx.x < CWT && c0 + threadIdx.x < D)
       grad_add(dz.colsum + c0 + threadIdx.x, red[threadIdx.x]);
   }
 }
@@ -321,7 +323,7 @@ __global__ __launch_bounds__(NT) void seqnorm_bwd_kernel(
 // RPT > 0 (L2 <= 32 RPT): passes 1 and 2 read x1 / dy1 once, kept in registers (as the
 // RPT form of seqnorm_bwd_kernel).
 constexpr int kUnmergeMax = 512;  // unmerged rows per sample of the fused form
-template <int RPT = 0>
+template <int RPT = 0, int CWT = CW>
 __global__ __launch_bounds__(NT) void ln_unmerge_dropout_bwd_kernel(
     const bf16_t* __restrict__ dy, int64_t ds_b, int64_t ds_t, const float* __restrict__ x,
     int64_t xs_b, int64_t xs_t, int L2, int D, const float* __restrict__ mean,
@@ -332,13 +334,14 @@ __global__ __launch_bounds__(NT) void ln_unmerge_dropout_bwd_kernel(
     float* __restrict__ g_in, int64_t gs_b, int64_t gs_t, const uint32_t* __restrict__ rng,
     uint32_t layer, uint32_t site, uint32_t thresh, float scale, int64_t row_offset,
     bf16_t* __restrict__ z, int64_t zs_b, int64_t zs_t, float* __restrict__ bias_grad) {
-  extern __shared__ __attribute__((aligned(16))) float dyn_f[];  // [max(L2*64, 4*RG*CW)]
+  extern __shared__ __attribute__((aligned(16))) float dyn_f[];  // [max(L2*CWT, 4*RGT*CWT)]
+  constexpr int CVN = CWT / 8, RGT = NT / CVN;  // column vectors, row groups (seqnorm_bwd_kernel)
   __shared__ int32_t u_orow[kUnmergeMax];
   __shared__ float u_s[kUnmergeMax], u_S[kUnmergeMax];
   float* red = dyn_f;
-  float* panel = dyn_f;  // reused after the reduction: merged-layout gradient [L2][64]
-  const int b = ln_sample(), c0 = ln_colblk() * CW;
-  const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  float* panel = dyn_f;  // reused after the reduction: merged-layout gradient [L2][CWT]
+  const int b = ln_sample(), c0 = ln_colblk() * CWT;
+  const int cv = threadIdx.x % CVN, rg = threadIdx.x / CVN;
   const int col = c0 + cv * 8;
   const bool cok = col < D;
   for (int row = threadIdx.x; row < L; row += NT) {  // merge-backward row sources
@@ -383,41 +386,41 @@ __global__ __launch_bounds__(NT) void ln_unmerge_dropout_bwd_kernel(
     if (cok) {
 #pragma unroll
       for (int j = 0; j < RPT; ++j) {
-        const int l = min(rg + j * RG, L2 - 1);
+        const int l = min(rg + j * RGT, L2 - 1);
         load8(xb + (int64_t)l * xs_t, rx[j]);
         rdy[j] = *reinterpret_cast<const uint4*>(db + (int64_t)l * ds_t);
       }
 #pragma unroll
       for (int j = 0; j < RPT; ++j) {
-        if (rg + j * RG >= L2) rdy[j] = make_uint4(0u, 0u, 0u, 0u);
+        if (rg + j * RGT >= L2) rdy[j] = make_uint4(0u, 0u, 0u, 0u);
         float fd[8];
         unpack8(rdy[j], fd);
         stat(rx[j], fd);
       }
     }
   } else if (cok) {
-    for (int l = rg; l < L2; l += RG) {
+    for (int l = rg; l < L2; l += RGT) {
       float fx[8], fd[8];
       load8(xb + (int64_t)l * xs_t, fx);
       load8(db + (int64_t)l * ds_t, fd);
       stat(fx, fd);
     }
   }
-  reduce_rows<4>(part, red);
-  if (threadIdx.x < CW && c0 + threadIdx.x < D) {
-    grad_add(dgamma + c0 + threadIdx.x, red[2 * RG * CW + threadIdx.x]);
-    grad_add(dbeta + c0 + threadIdx.x, red[3 * RG * CW + threadIdx.x]);
+  reduce_rows<4, NT, CWT>(part, red);
+  if (threadIdx.x < CWT && c0 + threadIdx.x < D) {
+    grad_add(dgamma + c0 + threadIdx.x, red[2 * RGT * CWT + threadIdx.x]);
+    grad_add(dbeta + c0 + threadIdx.x, red[3 * RGT * CWT + threadIdx.x]);
   }
   float mg[8], mgx[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     mg[e] = red[cv * 8 + e] / L2;
-    mgx[e] = red[RG * CW + cv * 8 + e] / L2;
+    mgx[e] = red[RGT * CWT + cv * 8 + e] / L2;
   }
   __syncthreads();  // red is read; the panel reuses it
   const float* ab = addend ? addend + (int64_t)b * as_b + col : nullptr;
 #pragma unroll(RPT > 0 ? RPT : 1)
-  for (int j = 0, l = rg; cok && (RPT > 0 ? j < RPT : l < L2); ++j, l += RG) {  // pass 2: into LDS
+  for (int j = 0, l = rg; cok && (RPT > 0 ? j < RPT : l < L2); ++j, l += RGT) {  // pass 2: into LDS
       const int la = RPT > 0 ? min(l, L2 - 1) : l;
       float fx[8], fd[8], fa[8];
       if constexpr (RPT > 0) {
@@ -436,16 +439,16 @@ __global__ __launch_bounds__(NT) void ln_unmerge_dropout_bwd_kernel(
         fx[e] = rs[e] * (g - mg[e] - xh * mgx[e]) + (ab ? fa[e] : 0.f);
       }
       if (RPT > 0 && l >= L2) continue;  // rows past L2: no panel row
-      store8(panel + l * CW + cv * 8, fx);
+      store8(panel + l * CWT + cv * 8, fx);
     }
   __syncthreads();
   // pass 3: unmerge (tome_merge_bwd_kernel), dropout backward (colsum_kernel), column sums
   const uint32_t key = rng ? stream_key(rng[0], rng[1], layer, site) : 0u;
   float cs[8] = {};
   if (cok)
-    for (int row = rg; row < L; row += RG) {
+    for (int row = rg; row < L; row += RGT) {
       float f[8];
-      load8(panel + u_orow[row] * CW + cv * 8, f);
+      load8(panel + u_orow[row] * CWT + cv * 8, f);
       const float sv = u_s[row];
       if (sv >= 0.f) {
         const float S = u_S[row];
@@ -469,8 +472,8 @@ __global__ __launch_bounds__(NT) void ln_unmerge_dropout_bwd_kernel(
   float part1[1][8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) part1[0][e] = cs[e];
-  reduce_rows<1>(part1, red);
-  if (bias_grad && threadIdx.x < CW && c0 + threadIdx.x < D)
+  reduce_rows<1, NT, CWT>(part1, red);
+  if (bias_grad && threadIdx.x < CWT && c0 + threadIdx.x < D)
     grad_add(bias_grad + c0 + threadIdx.x, red[threadIdx.x]);
 }
 
@@ -537,6 +540,18 @@ static int snb_rpt(int L) {
   return 0;
 }
 
+// the 32-column (64 row groups) single-pass LayerNorm backward for 128 < L <= 320 (MMT_SNB512=1;
+// off by default): half the rows per thread of the 64-column form, whose 254-256 VGPRs hold two
+// waves per SIMD (this one ~156: three workgroups per CU instead of two). Measured slower at
+// B = 512, L = 276 (tools/ln_bench.py): seqnorm_bwd 168 vs 166 us, with dropout 205 vs 196, the
+// fused LN_1 + unmerge 220 vs 204 -- occupancy is not what bounds these kernels; the 128-B row
+// segments cost more than the extra workgroup gains.
+static int snb_rpt512(int L) {
+  static const bool on = getenv("MMT_SNB512") && atoi(getenv("MMT_SNB512")) != 0;
+  if (!on || snb_rpt(L) == 0 || L <= 128) return 0;
+  return (L + 63) / 64;
+}
+
 extern "C" int mmt_seqnorm_fwd(const void* x, int x_dtype, int64_t xs_b, int64_t xs_t, int B,
                                int L, int D, const float* gamma, const float* beta, float eps,
                                void* y, int64_t ys_b, int64_t ys_t, float* mean, float* rstd,
@@ -594,7 +609,18 @@ extern "C" int mmt_seqnorm_bwd(const void* dy, int dy_dtype, int64_t ds_b, int64
   hipLaunchKernelGGL((seqnorm_bwd_kernel<bf16_t, float, false, R>), grid, dim3(NT), 0, s,           \
                      (const bf16_t*)dy, ds_b, ds_t, (const float*)x, xs_b, xs_t, L, D, mean, rstd,  \
                      gamma, (const float*)addend, as_b, as_t, (float*)dx, dxs_b, dxs_t, dgamma, dbeta)
-    if (rpt == 4) SNBR(4);
+    const int r5 = snb_rpt512(L);
+    const dim3 grid32 = ln_grid(B, (D + 31) / 32);
+    if (r5) {
+#define SNBR5(R)                                                                                    \
+  hipLaunchKernelGGL((seqnorm_bwd_kernel<bf16_t, float, false, R, NT, 32>), grid32, dim3(NT), 0, s,     \
+                     (const bf16_t*)dy, ds_b, ds_t, (const float*)x, xs_b, xs_t, L, D, mean, rstd,  \
+                     gamma, (const float*)addend, as_b, as_t, (float*)dx, dxs_b, dxs_t, dgamma, dbeta)
+      if (r5 == 3) SNBR5(3);
+      else if (r5 == 4) SNBR5(4);
+      else SNBR5(5);
+#undef SNBR5
+    } else if (rpt == 4) SNBR(4);
     else if (rpt == 6) SNBR(6);
     else if (rpt == 8) SNBR(8);
     else SNBR(10);
@@ -665,27 +691,32 @@ extern "C" int mmt_ln_unmerge_dropout_bwd(
                     (!addend || as_t % 8 == 0),
                 "mmt_ln_unmerge_dropout_bwd: strides must be multiples of 8");
   MMT_CHECK_ARG(!rng || (keep_prob > 0.f && keep_prob <= 1.f), "mmt_ln_unmerge_dropout_bwd: keep_prob");
-  const size_t dyn = sizeof(float) * (size_t)std::max(L2 * CW, 4 * RG * CW);
-  const dim3 grid = ln_grid(B, (D + CW - 1) / CW);
+  const int r5 = snb_rpt512(L2);  // the 32-column form where seqnorm_bwd takes it (same sums)
+  const int cwt = r5 ? 32 : CW;
+  const size_t dyn = sizeof(float) * (size_t)std::max(L2 * cwt, 4 * (NT / (cwt / 8)) * cwt);
+  const dim3 grid = ln_grid(B, (D + cwt - 1) / cwt);
   const int rpt = snb_rpt(L2);
-#define LUD(R)                                                                                      \
+#define LUD(R, CWV)                                                                                 \
   do {                                                                                              \
-    static const bool attr_ = (hipFuncSetAttribute((const void*)ln_unmerge_dropout_bwd_kernel<R>,   \
+    static const bool attr_ = (hipFuncSetAttribute((const void*)ln_unmerge_dropout_bwd_kernel<R, CWV>, \
                                                    hipFuncAttributeMaxDynamicSharedMemorySize,      \
                                                    96 * 1024), true);                               \
     (void)attr_;                                                                                    \
-    hipLaunchKernelGGL((ln_unmerge_dropout_bwd_kernel<R>), grid, dim3(NT), dyn, as_stream(stream),  \
+    hipLaunchKernelGGL((ln_unmerge_dropout_bwd_kernel<R, CWV>), grid, dim3(NT), dyn, as_stream(stream), \
                        (const bf16_t*)dy, ds_b, ds_t, x, xs_b, xs_t, L2, D, mean, rstd, gamma,      \
                        addend, as_b, as_t, dgamma, dbeta, L, set_start, t, r, size_in, size_out,    \
                        pos_map, g_in, gs_b, gs_t, rng, layer, site,                                  \
                        rng ? keep_threshold16(keep_prob) : 0u, rng ? 1.f / keep_prob : 1.f,          \
                        row_offset, (bf16_t*)z, zs_b, zs_t, bias_grad);                               \
   } while (0)
-  if (rpt == 4) LUD(4);
-  else if (rpt == 6) LUD(6);
-  else if (rpt == 8) LUD(8);
-  else if (rpt == 10) LUD(10);
-  else LUD(0);
+  if (r5 == 3) LUD(3, 32);
+  else if (r5 == 4) LUD(4, 32);
+  else if (r5 == 5) LUD(5, 32);
+  else if (rpt == 4) LUD(4, CW);
+  else if (rpt == 6) LUD(6, CW);
+  else if (rpt == 8) LUD(8, CW);
+  else if (rpt == 10) LUD(10, CW);
+  else LUD(0, CW);
 #undef LUD
   MMT_CHECK_LAUNCH("mmt_ln_unmerge_dropout_bwd");
   return MMT_OK;
@@ -713,7 +744,16 @@ extern "C" int mmt_seqnorm_dropout_bwd(const void* dy, int64_t ds_b, int64_t ds_
   hipLaunchKernelGGL((seqnorm_bwd_kernel<bf16_t, float, true, R>), grid, dim3(NT), 0,               \
                      as_stream(stream), (const bf16_t*)dy, ds_b, ds_t, x, xs_b, xs_t, L, D, mean,   \
                      rstd, gamma, addend, as_b, as_t, dx, dxs_b, dxs_t, dgamma, dbeta, dz)
-  if (rpt == 4) SDZ(4);
+#define SDZ5(R)                                                                                     \
+  hipLaunchKernelGGL((seqnorm_bwd_kernel<bf16_t, float, true, R, NT, 32>), grid32, dim3(NT), 0,         \
+                     as_stream(stream), (const bf16_t*)dy, ds_b, ds_t, x, xs_b, xs_t, L, D, mean,   \
+                     rstd, gamma, addend, as_b, as_t, dx, dxs_b, dxs_t, dgamma, dbeta, dz)
+  const int r5 = snb_rpt512(L);
+  const dim3 grid32 = ln_grid(B, (D + 31) / 32);
+  if (r5 == 3) SDZ5(3);
+  else if (r5 == 4) SDZ5(4);
+  else if (r5 == 5) SDZ5(5);
+  else if (rpt == 4) SDZ(4);
   else if (rpt == 6) SDZ(6);
   else if (rpt == 8) SDZ(8);
   else if (rpt == 10) SDZ(10);

@@ -238,3 +238,33 @@ def test_residual_stream_kernel(dev, M, N, K, alpha):
     ref = alpha * (a.float() @ w.float().t()) + bias
     ref = torch.where(keep, ref / 0.9, torch.zeros_like(ref)) + res
     torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("M,N,bias", [(149504, 1152, True), (141312, 1536, False), (33001, 192, True),
+                                      (40000, 64, False), (700, 1536, True)])
+def test_activation_stationary_kernel(dev, M, N, bias):
+    """gemm_xs_kernel (csrc/gemm_xs.hip: K = 384 products with a bias-only epilogue, the step's QKV
+    projection, reference attention.py:41-69 Dense): the same fp32 sums in the same k order as the
+    128 x 128 kernel (variant 4), so bit-identical bf16 outputs — at the B = 512 shapes, ragged
+    row panels (rows past M neither read nor stored), one-chunk N and M below the dispatch floor
+    (mmt_gemm_xs called directly); and within bf16 rounding of a torch fp32 reference."""
+    from multi_modal_transformers_tokenmerge_amd import _C
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    g = torch.Generator().manual_seed(M + N)
+    K = 384
+    a, w = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    b = torch.randn(N, generator=g).to(dev) if bias else None
+    out = torch.full((M + 3, N), 7.0, dtype=torch.bfloat16, device=dev)  # rows past M: untouched
+    _C.call("mmt_gemm_xs", M, N, K, a.data_ptr(), K, w.data_ptr(), K, out.data_ptr(), N,
+            None if b is None else b.data_ptr(), _C.stream_ptr())
+    _C.call("mmt_gemm_set_variant", 4)
+    try:
+        old = Kn.gemm(a, w, False, True, bias=b)
+    finally:
+        _C.call("mmt_gemm_set_variant", -1)
+    disp = Kn.gemm(a, w, False, True, bias=b)  # mmt_gemm's own dispatch (XS where it applies)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:M], old) and torch.equal(disp, old)
+    assert bool((out[M:] == 7.0).all())
+    ref = a.float() @ w.float().t() + (b if b is not None else 0.0)
+    _close_bf16(out[:M], ref)
