@@ -45,6 +45,7 @@ from multi_modal_transformers_tokenmerge_amd.models.octo.octo import (  # noqa: 
     Octo, create_octo_train_state)
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md, chip table)
+MFMA_FP8_PEAK_TFLOPS = 5000.0    # MI355X dense fp8 (e4m3; the 10 PF figure is 2:1 sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -147,12 +148,13 @@ def kernel_probes(model, B, reps=20):
 
     def add(name, kernel, launch, bound, work, note, alg_bytes=None):
         us = _graph_time_us(launch, reps)
-        if bound == "mfma":
+        if bound in ("mfma", "mfma8"):
             ach = work / (us * 1e-6) / 1e12
+            peak = MFMA_FP8_PEAK_TFLOPS if bound == "mfma8" else MFMA_BF16_PEAK_TFLOPS
             out.append(dict(name=name, kernel=kernel, bound="mfma", avg_launch_us=round(us, 2),
                             flops_per_launch=work, achieved=round(ach, 2),
-                            peak=MFMA_BF16_PEAK_TFLOPS, unit="TFLOP/s",
-                            frac=round(ach / MFMA_BF16_PEAK_TFLOPS, 4), note=note,
+                            peak=peak, unit="TFLOP/s", dtype="fp8" if bound == "mfma8" else "bf16",
+                            frac=round(ach / peak, 4), note=note,
                             algorithmic_bytes_per_launch=alg_bytes))
         else:
             ach = work / (us * 1e-6) / 1e9
@@ -168,6 +170,23 @@ def kernel_probes(model, B, reps=20):
         lambda: blk.mlp.dense.fwd(y1, out=h, act=K.ACT_RELU, rng=rng, drop_layer=0, drop_site=2,
                                   keep_prob=0.9),
         "mfma", 2.0 * M * Mh * D, f"M={M} N={Mh} K={D}, 2MNK", _gemm_bytes(M, Mh, D, extra=4 * Mh))
+    # 1b. fp8 weight path (BASELINE configs[4]): the same product in e4m3 on
+    # v_mfma_scale_f32_32x32x64_f8f6f4 (per-row activation / per-channel weight scales), priced
+    # against the dense fp8 peak; its bf16 twin is mlp_up_fwd above (same shape and epilogue)
+    if blk.mlp.dense.fp8:
+        yq, sy = K.quant_rows_fp8(y1)
+        w8 = blk.mlp.dense.w
+        b8 = blk.mlp.dense.b.data
+        add("mlp_up_fwd_fp8", "gemm_fp8_nt_kernel",
+            lambda: K.gemm_fp8(yq, sy, w8.q8, w8.q8_scale, out=h, bias=b8, act=K.ACT_RELU, rng=rng,
+                               drop_layer=0, drop_site=2, keep_prob=0.9),
+            "mfma8", 2.0 * M * Mh * D, f"M={M} N={Mh} K={D}, 2MNK in e4m3 (+ bias, relu, dropout; "
+            "the activation quantisation is its own kernel)", M * D + Mh * D + 2 * M * Mh + 4 * (M + Mh))
+        add("mlp_up_fwd_bf16_twin", PROBE_KERNEL,
+            lambda: K.gemm(y1, w8.bf16, trans_b=True, out=h, bias=b8, act=K.ACT_RELU, rng=rng,
+                           drop_layer=0, drop_site=2, keep_prob=0.9),
+            "mfma", 2.0 * M * Mh * D, f"M={M} N={Mh} K={D}: the fp8 probe's product in bf16 (A/B)",
+            _gemm_bytes(M, Mh, D, extra=4 * Mh))
     # 2. MLP input gradient dy1 = dz1 . W1 (NT on the transposed shadow): N = 384, K = 1536 — a
     # plain narrow product: gemm_ntw_kernel (hipBLASLt with MMT_BLASLT=1, name Cijk_..., matched
     # by that prefix in the PMC passes)
@@ -247,27 +266,28 @@ def kernel_probes(model, B, reps=20):
         gam = torch.ones(D, device=dev)
         bet = torch.zeros(D, device=dev)
         nidx = (t + 1) // 2 + r           # unm + src + dst indices read
-        add("tome_merge_seqnorm_fwd", "tome_merge_seqnorm_fwd_kernel",
-            lambda: K.tome_merge_seqnorm_fwd(x1, s0, t, r, unm, src, dst, gam, bet, 1e-6),
-            "hbm", B * L * D * 4 + B * (L - r) * D * (4 + 2) + B * (t - r) * 4 + B * t * 4
-            + 2 * B * D * 4 + B * nidx * 4,
-            "read the fp32 sequence; write the merged sequence (fp32), LN_1 output (bf16), sizes, "
-            "pos_map and the LN statistics (token_compression.py:90-129 + attention.py:66)")
-        # 6c. its backward: LayerNorm_1 backward + unmerge + attention-output dropout backward
-        xm, so, pos, _, mu1, rs1 = K.tome_merge_seqnorm_fwd(x1, s0, t, r, unm, src, dst, gam, bet, 1e-6)
-        L2 = L - r
-        dy1 = rnd(B, L2, D)
-        dx2 = rnd(B, L2, D, dt=torch.float32)
-        ggam, gbet, gb = (torch.zeros(D, device=dev) for _ in range(3))
-        if K.ln_unmerge_ok(L, L2):
-            add("ln_unmerge_dropout_bwd", "ln_unmerge_dropout_bwd_kernel",
-                lambda: K.ln_unmerge_dropout_bwd(dy1, xm, mu1, rs1, gam, ggam, gbet, dx2,
-                                                 (s0, t, r, pos, None, so), rng, 0, 1, 0.9, 0,
-                                                 bias_grad=gb),
-                "hbm", B * L2 * D * (2 + 4 + 4) + B * L * D * (4 + 2) + B * t * 4 + B * (t - r) * 4
-                + 2 * B * D * 4,
-                "read dy (bf16), x and the residual gradient (fp32); write the unmerged gradient "
-                "(fp32) and the dropout output (bf16)")
+        if L - r <= 512:  # the fused forms' shapes (attention_blocks/attention.py uses them there)
+            add("tome_merge_seqnorm_fwd", "tome_merge_seqnorm_fwd_kernel",
+                lambda: K.tome_merge_seqnorm_fwd(x1, s0, t, r, unm, src, dst, gam, bet, 1e-6),
+                "hbm", B * L * D * 4 + B * (L - r) * D * (4 + 2) + B * (t - r) * 4 + B * t * 4
+                + 2 * B * D * 4 + B * nidx * 4,
+                "read the fp32 sequence; write the merged sequence (fp32), LN_1 output (bf16), sizes, "
+                "pos_map and the LN statistics (token_compression.py:90-129 + attention.py:66)")
+            # 6c. its backward: LayerNorm_1 backward + unmerge + attention-output dropout backward
+            xm, so, pos, _, mu1, rs1 = K.tome_merge_seqnorm_fwd(x1, s0, t, r, unm, src, dst, gam, bet, 1e-6)
+            L2 = L - r
+            dy1 = rnd(B, L2, D)
+            dx2 = rnd(B, L2, D, dt=torch.float32)
+            ggam, gbet, gb = (torch.zeros(D, device=dev) for _ in range(3))
+            if K.ln_unmerge_ok(L, L2):
+                add("ln_unmerge_dropout_bwd", "ln_unmerge_dropout_bwd_kernel",
+                    lambda: K.ln_unmerge_dropout_bwd(dy1, xm, mu1, rs1, gam, ggam, gbet, dx2,
+                                                     (s0, t, r, pos, None, so), rng, 0, 1, 0.9, 0,
+                                                     bias_grad=gb),
+                    "hbm", B * L2 * D * (2 + 4 + 4) + B * L * D * (4 + 2) + B * t * 4 + B * (t - r) * 4
+                    + 2 * B * D * 4,
+                    "read dy (bf16), x and the residual gradient (fp32); write the unmerged gradient "
+                    "(fp32) and the dropout output (bf16)")
     # 7. sequence-axis LayerNorm forward (fp32 residual stream -> bf16) and backward
     x = rnd(B, L1, D, dt=torch.float32)
     add("seqnorm_fwd", "seqnorm_fwd_kernel", lambda: blk.ln1.fwd(x), "hbm",
@@ -400,6 +420,8 @@ def main():
     ap.add_argument("--batch", type=int, default=512,
                     help="per-GPU batch (512: see DESIGN.md 'Batch'; 64 leaves the chip underfilled)")
     ap.add_argument("--config", default="octo-small-tome16")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="config override (A/B runs), e.g. --set fp8=0 on octo-base-hires-tome32")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
@@ -423,7 +445,12 @@ def main():
     # (local_rank modulo the visible devices: lets a 2-rank gloo rehearsal share one GPU)
     dev = torch.device("cuda", di.local_rank % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
-    cfg = get_config(args.config)
+    over = {}
+    for kv in args.set:
+        k, v = kv.split("=", 1)
+        over[k] = (v.lower() in ("1", "true", "yes")) if v.lower() in ("0", "1", "true", "false", "yes", "no") \
+            else (int(v) if v.lstrip("-").isdigit() else v)
+    cfg = get_config(args.config, **over)
     B = args.batch
     if args.deterministic:
         os.environ["MMT_DETERMINISTIC"] = "1"
@@ -518,7 +545,9 @@ def main():
                                    f"ToMe r={cfg.tome_r}/block, {cfg.num_blocks} blocks",
                        "global_batch": N * B, "per_gpu_batch": B, "seq_len": sets0.L,
                        "parallelism": f"dp{N}", "hip_graph": use_graph,
-                       "deterministic": os.environ.get("MMT_DETERMINISTIC", "0") == "1"},
+                       "deterministic": os.environ.get("MMT_DETERMINISTIC", "0") == "1",
+                       **({"overrides": over} if over else {}),
+                       **({"fp8_weight_path": True} if cfg.fp8 else {})},
             "model_tflops_per_s": round(value * fps / 1e12, 2),
             "algorithmic_gflop_per_sample": round(fps / 1e9, 2),
             "final_loss": round(loss_val, 5),

@@ -17,6 +17,7 @@
 // residual loads and C stores, no LDS round trip).
 // Split-K writes fp32 partial slabs (plain stores) reduced by a second kernel — no atomics.
 #include "common.h"
+#include "gemm_xs.h"
 
 using namespace mmt;
 
@@ -2459,6 +2460,12 @@ int cu_count() {
 }
 
 // Tile width of the persistent 256 x BN NT kernel for this launch, 0 when another kernel runs.
+// the activation-stationary kernel (csrc/gemm_xs.hip) where it applies; MMT_XS=0: off (A/B)
+bool xs_enabled() {
+  static const bool on = !getenv("MMT_XS") || atoi(getenv("MMT_XS")) != 0;
+  return on;
+}
+
 int nt_bn(int M, int N, int K, int transA, int transB, int batch, int out_kind, int final_kind) {
   if (transA || !transB || batch != 1 || out_kind == 2 || K % 64 != 0 ||
       !(g_variant < 0 || g_variant >= 5))
@@ -2760,14 +2767,15 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
   // activation-stationary short-K kernel (csrc/gemm_xs.hip) for the bias-only bf16 products at
   // K = 384 (the OCTO-small QKV projection: 198 vs 220 us at B = 512, bit-identical outputs;
   // tools/xs_bench.py). MMT_XS=0: off (A/B).
-  static const bool g_xs = !getenv("MMT_XS") || atoi(getenv("MMT_XS")) != 0;
-  if (g_xs && g_variant < 0 && !transA && transB && batch == 1 && out_kind == 0 && final_kind == 0 &&
-      K == 384 && N % 64 == 0 && N <= 1536 && M >= 32768 && epi.act == MMT_ACT_NONE && !epi.rng &&
-      !epi.gate && !epi.residual && epi.alpha == 1.f && epi.beta == 0.f && !epi.colsum &&
-      !epi.relu_bits && !epi.gate_bits && !epi.keep_bits && lda % 8 == 0 && ldb % 8 == 0 &&
-      ldc % 8 == 0 && ((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 == 0 &&
-      (!epi.bias || (uintptr_t)epi.bias % 16 == 0))
-    return mmt_gemm_xs(M, N, K, A, lda, B, ldb, C, ldc, epi.bias, stream);
+  if (xs_enabled() && g_variant < 0 && !transA && transB && batch == 1 && out_kind == 0 &&
+      final_kind == 0 && M >= 32768 && epi.act == MMT_ACT_NONE && !epi.rng && !epi.gate &&
+      !epi.residual && epi.alpha == 1.f && epi.beta == 0.f && !epi.colsum && !epi.relu_bits &&
+      !epi.gate_bits && !epi.keep_bits) {
+    XsEpi xe;
+    xe.bias = epi.bias;
+    if (xs_shape_ok(M, N, K, false, lda, ldb, ldc, A, B, C, xe))
+      return xs_launch(M, N, K, false, A, lda, B, ldb, C, ldc, 0, xe, s);
+  }
   // Warp-specialised wide NT kernel: bf16 outputs of N % 128 == 0 with the nt256 epilogues that
   // the step uses (bias, relu, dropout, relu_bits, gate_bits, colsum, bf16 / fp32 residual).
   // MMT_NTWS: 0 off, 1 (default) where nt256 would take 192-wide tiles (N % 256 != 0: the QKV
@@ -2975,8 +2983,27 @@ extern "C" int mmt_gemm_fp8(int M, int N, int K, const void* A, int64_t lda, con
                   "mmt_gemm: relu_bits is a forward output (no gate_bits / colsum in that launch)");
     MMT_CHECK_ARG(!e->keep_bits, "mmt_gemm_fp8: keep_bits is a bf16 nt path epilogue (use rng)");
   }
-  const int tiles_n = (N + F8_BN - 1) / F8_BN, n_work = ((M + F8_BM - 1) / F8_BM) * tiles_n;
   hipStream_t s = as_stream(stream);
+  // K = 768 products with a bf16 output and no gate / residual / beta (the OCTO-base QKV
+  // projection and MLP up-projection): the activation-stationary kernel on e4m3 operands
+  if (xs_enabled() && g_variant < 0 && c_mode == MMT_OUT_BF16 && M >= 4096 && !epi.gate && !epi.residual &&
+      epi.beta == 0.f && !epi.relu_bits && !epi.gate_bits && !(e && e->colsum)) {
+    XsEpi xe;
+    xe.bias = epi.bias;
+    xe.relu = epi.act == MMT_ACT_RELU;
+    xe.rng = epi.rng;
+    xe.drop_layer = epi.drop_layer;
+    xe.drop_site = epi.drop_site;
+    xe.keep_thresh16 = epi.keep_thresh16;
+    xe.drop_scale = epi.drop_scale;
+    xe.drop_row_offset = epi.drop_row_offset;
+    xe.alpha = epi.alpha;
+    xe.sa = sa;
+    xe.sb = sb;
+    if (xs_shape_ok(M, N, K, true, lda, ldb, ldc, A, B, C, xe))
+      return xs_launch(M, N, K, true, A, lda, B, ldb, C, ldc, 0, xe, s);
+  }
+  const int tiles_n = (N + F8_BN - 1) / F8_BN, n_work = ((M + F8_BM - 1) / F8_BM) * tiles_n;
   if (c_mode == MMT_OUT_BF16)
     hipLaunchKernelGGL(gemm_fp8_nt_kernel<0>, dim3(n_work), dim3(256), 0, s, M, N, K,
                        (const uint8_t*)A, lda, sa, (const uint8_t*)B, ldb, sb, C, ldc, tiles_n,

@@ -15,9 +15,16 @@
 //    cut into equal contiguous ranges, one per workgroup (every CU within one unit of the mean),
 //    and a workgroup reloads X only when its range crosses into a new panel.
 // Per 64-column chunk a CU computes 2.1 MFLOP from 48 KB of W (LDS-DMA) and 32 KB of C stores.
-// Requires K == 384, N % 64 == 0, 16-B aligned rows. Rows >= M are read as zeros, never stored.
-#include "common.h"
+// The fp8 weight path (BASELINE configs[4], mmt_gemm_fp8) runs the same kernel on e4m3 operands at
+// K = 768: a row is again 768 bytes (48 16-B units), the 24 register units hold 12 fragments of
+// v_mfma_scale_f32_32x32x64_f8f6f4 (lane (r, h) takes bytes 32h .. 32h+31 of its row's 64-byte
+// K-step, the pairing of gemm_fp8_nt_kernel), twice the bf16 FLOPs per chunk at the same cycles.
+// Epilogue (XsEpi, gemm_xs.h): fp8 row / channel scales, alpha, bias, relu, counter-RNG dropout,
+// in epilogue_w's order, bf16 out. Requires K == 384 (bf16) / 768 (fp8), N % 64 == 0, 16-B aligned
+// rows. Rows >= M are read as zeros, never stored.
+#include "gemm_xs.h"
 
+#include <algorithm>
 #include <type_traits>
 
 using namespace mmt;
@@ -28,13 +35,22 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float float2v __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef int v8i __attribute__((ext_vector_type(8)));
 
-constexpr int XS_K = 384, XS_KS = XS_K / 16;      // 24 MFMA k-steps
+constexpr int XS_RB = 768;                         // bytes per X / W row (bf16 K 384, fp8 K 768)
 constexpr int XS_ROWS = 256, XS_NC = 64;           // panel rows, chunk columns
-constexpr int XS_UNITS16 = XS_K / 8;               // 48 16-B units per W row
-constexpr int XS_SLOT = XS_NC * XS_K * 2;          // 48 KB per ring slot
+constexpr int XS_UNITS16 = XS_RB / 16;             // 48 16-B units per row
+constexpr int XS_XR = XS_RB / 32;                  // 24 register units of X per lane
+constexpr int XS_SLOT = XS_NC * XS_RB;             // 48 KB per ring slot
 constexpr int XS_PIECES = XS_SLOT / 1024 / 8;      // 6 DMA pieces per wave per chunk
 constexpr int XS_MAXN = 1536;                      // bias columns staged in LDS
+// fp8 slots: rows padded to 49 units (784 B) instead of the XOR swizzle — unit (r, c) at
+// 49 r + c is conflict-free for 16 consecutive rows (49 = 1 mod 16) and every fragment read of a
+// lane is one base address + an immediate (the XOR form's 24 per-step addresses spilled the
+// fp8 kernel's registers). 49 DMA pieces per slot: wave 0 issues 7, the others 6.
+constexpr int XS8_UPR = XS_UNITS16 + 1;            // 49 units per padded row
+constexpr int XS8_SLOT = XS_NC * XS8_UPR * 16;     // 50,176 B
+constexpr int XS8_PIECES = XS8_SLOT / 1024;        // 49
 
 __device__ __forceinline__ uint32_t xs_pk2(float a, float b) {
   const float2v v = {a, b};
@@ -51,11 +67,8 @@ __host__ __device__ __forceinline__ int xs_unit(int r, int c) {
 __device__ __forceinline__ void xs_wait_vm(int n) {
   switch (n) {
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
@@ -64,15 +77,16 @@ __device__ __forceinline__ void xs_wait_vm(int n) {
 #define XS_ABL 0  // 4 no C stores
 #endif
 
-template <int EP>  // EP 0: bf16 C (+ bias when given)
-__global__ __launch_bounds__(512, 1) void gemm_xs_kernel(int M, int N, const bf16_t* __restrict__ X,
-                                                         int64_t ldx, const bf16_t* __restrict__ W,
-                                                         int64_t ldw, bf16_t* __restrict__ C,
-                                                         int64_t ldc, const float* __restrict__ bias,
-                                                         int n_units) {
+template <bool F8>
+__global__ __launch_bounds__(512, 1) void gemm_xs_kernel(int M, int N, const char* __restrict__ X,
+                                                         int64_t ldxb, const char* __restrict__ W,
+                                                         int64_t ldwb, bf16_t* __restrict__ C,
+                                                         int64_t ldc, XsEpi e, int n_units) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  __shared__ __attribute__((aligned(16))) char ring[3 * XS_SLOT];
+  constexpr int SLOT = F8 ? XS8_SLOT : XS_SLOT;
+  __shared__ __attribute__((aligned(16))) char ring[3 * SLOT];
   __shared__ __attribute__((aligned(16))) float s_bias[XS_MAXN];
+  __shared__ __attribute__((aligned(16))) float s_sb[F8 ? XS_MAXN : 4];  // fp8 channel scales
   const int lane = threadIdx.x & 63, hh = lane >> 5, lr = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nc = N / XS_NC;
@@ -81,98 +95,176 @@ __global__ __launch_bounds__(512, 1) void gemm_xs_kernel(int M, int N, const bf1
   const int u1 = (int)((int64_t)n_units * (wg + 1) / gridDim.x);
   const int nu = u1 - u0;
   if (nu <= 0) return;
-  for (int i = threadIdx.x; i < N; i += 512) s_bias[i] = bias ? bias[i] : 0.f;
-  __syncthreads();
-
-  // DMA source offsets of this wave's pieces (fixed: the slot layout does not depend on the chunk)
-  int voff[XS_PIECES];
-#pragma unroll
-  for (int p = 0; p < XS_PIECES; ++p) {
-    const int u = (wave * XS_PIECES + p) * 64 + lane;  // physical unit this lane fills
-    const int r = u / XS_UNITS16, pc = u - r * XS_UNITS16;
-    const int c = (pc & ~15) | ((pc ^ r) & 15);
-    voff[p] = r * (int)(ldw * 2) + c * 16;
+  for (int i = threadIdx.x; i < N; i += 512) {
+    s_bias[i] = e.bias ? e.bias[i] : 0.f;
+    if constexpr (F8) s_sb[i] = e.sb[i];
   }
-  auto issue = [&](int j) {  // chunk u0 + j into slot j % 3: XS_PIECES vm ops per wave
+  __syncthreads();
+  float s_row = 1.f;  // fp8: this lane's row scale in the current panel (loaded with its X)
+  const uint32_t key = e.rng ? stream_key(e.rng[0], e.rng[1], e.drop_layer, e.drop_site) : 0u;
+
+  // DMA source offset of this lane in piece p (the slot layout does not depend on the chunk;
+  // recomputed per issue: a few VALU ops instead of six registers held across the kernel)
+  auto voff = [&](int p) {
+    if constexpr (F8) {  // padded rows: unit 48 of a row is padding (loads unit 47, never read)
+      const int u = p * 64 + lane;
+      const int r = u / XS8_UPR, c = u - r * XS8_UPR;
+      return r * (int)ldwb + min(c, XS_UNITS16 - 1) * 16;
+    } else {
+      const int u = (wave * XS_PIECES + p) * 64 + lane;  // physical unit this lane fills
+      const int r = u / XS_UNITS16, pc = u - r * XS_UNITS16;
+      const int c = (pc & ~15) | ((pc ^ r) & 15);
+      return r * (int)ldwb + c * 16;
+    }
+  };
+  // DMA pieces this wave issues per chunk (bf16: 6; fp8: 7 for wave 0, 6 for the others)
+  const int pw = F8 ? (XS8_PIECES - 1 - wave) / 8 + 1 : XS_PIECES;
+  auto issue = [&](int j) {  // chunk u0 + j into slot j % 3: pw vm ops per wave
     const int c = (u0 + j) % nc;
-    const bf16_t* base = W + (int64_t)c * XS_NC * ldw;
-    char* slot = ring + (j % 3) * XS_SLOT;
+    const char* base = W + (int64_t)c * XS_NC * ldwb;
+    char* slot = ring + (j % 3) * SLOT;
+    if constexpr (F8) {
 #pragma unroll
-    for (int p = 0; p < XS_PIECES; ++p)
-      dma16_asm(base, (int64_t)XS_NC * ldw * 2, slot + (wave * XS_PIECES + p) * 1024, voff[p]);
+      for (int k = 0; k < 7; ++k) {
+        const int p = wave + 8 * k;
+        if (p < XS8_PIECES)  // wave-uniform
+          dma16_asm(base, (int64_t)XS_NC * ldwb, slot + p * 1024, voff(p));
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < XS_PIECES; ++p)
+        dma16_asm(base, (int64_t)XS_NC * ldwb, slot + (wave * XS_PIECES + p) * 1024, voff(p));
+    }
   };
   // per-panel buffer resources: rows past M are out of range (loads read 0, stores are dropped),
   // so every load / store is issued unconditionally and the vm counts below are exact
-  auto rsrc = [&](const bf16_t* base, int panel, int64_t ld) {
+  auto rsrc = [&](const void* base, int panel, int64_t ldb) {
     const int rows = min(M - panel * XS_ROWS, XS_ROWS);
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base + (int64_t)panel * XS_ROWS * ld),
-                                             (short)0, (int)(rows * ld * 2), 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(reinterpret_cast<const char*>(base) + (int64_t)panel * XS_ROWS * ldb),
+        (short)0, (int)(rows * ldb), 0x00020000);
   };
-  bf16x8 xf[XS_KS];
-  const int xoff = (32 * wave + lr) * (int)(ldx * 2) + 16 * hh;
-  auto load_x = [&](int panel) {  // XS_KS vm ops per wave
-    const __amdgpu_buffer_rsrc_t rx = rsrc(X, panel, ldx);
+  // register unit i of this lane: bf16 — fragment i (k-step of 16: 16 B at 32 i + 16 h); fp8 —
+  // half i & 1 of fragment i >> 1 (k-step of 64 bytes: 32 B at 64 (i >> 1) + 32 h)
+  auto xoff = [&](int i) { return F8 ? 64 * (i >> 1) + 16 * (i & 1) + 32 * hh : 32 * i + 16 * hh; };
+  // bf16: 24 fragments of 16 B; fp8: 12 fragments of 32 B held as the 8-register tuples the
+  // scaled MFMA takes (assembled from two 16-B pieces would copy 8 registers per MFMA)
+  constexpr int XF = F8 ? XS_XR / 2 : XS_XR;
+  typedef typename std::conditional<F8, v8i, uint4>::type xfrag_t;
+  xfrag_t xq[XF];
+  const int xrow = (32 * wave + lr) * (int)ldxb;
+  auto ld16 = [&](const __amdgpu_buffer_rsrc_t& rx, int i) {
+    return __builtin_amdgcn_raw_buffer_load_b128(rx, xrow + xoff(i), 0, 0);
+  };
+  auto load_frag = [&](const __amdgpu_buffer_rsrc_t& rx, int f) {  // (F8 ? 2 : 1) vm ops
+    if constexpr (F8) {
+      const auto a = ld16(rx, 2 * f), b = ld16(rx, 2 * f + 1);
+      xq[f] = v8i{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
+    } else {
+      xq[f] = __builtin_bit_cast(uint4, ld16(rx, f));
+    }
+  };
+  auto load_x = [&](int panel) {  // XS_XR vm ops per wave
+    const __amdgpu_buffer_rsrc_t rx = rsrc(X, panel, ldxb);
 #pragma unroll
-    for (int s = 0; s < XS_KS; ++s)
-      xf[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx, xoff + 32 * s, 0, 0));
+    for (int f = 0; f < XF; ++f) load_frag(rx, f);
   };
   const int coff = (32 * wave + lr) * (int)(ldc * 2) + 16 * hh;
 
-  // epilogue of one 32-column block: lane row m = lr, columns 32 bq + 8 g + 4 hh + i (2 stores)
-  auto epilogue = [&](const floatx16& a, int bq, int c, const __amdgpu_buffer_rsrc_t& rc) {
-    const float* bp = s_bias + c * XS_NC + 32 * bq + 4 * hh;
+  // epilogue of one 32-column block: lane row m = lr, columns 32 bq + 8 g + 4 hh + i (2 stores);
+  // epilogue_w's arithmetic and order
+  auto epilogue = [&](const floatx16& a, int bq, int c, int panel, const __amdgpu_buffer_rsrc_t& rc) {
+    const int gr = panel * XS_ROWS + 32 * wave + lr;
+    uint32_t pk[4][2];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int col = c * XS_NC + 32 * bq + 8 * g + 4 * hh;
+      const float4 bb = *reinterpret_cast<const float4*>(s_bias + col);
+      float v[4] = {a[4 * g], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]};
+      if constexpr (F8) {
+        const float4 sw = *reinterpret_cast<const float4*>(s_sb + col);
+        v[0] = v[0] * s_row * sw.x;
+        v[1] = v[1] * s_row * sw.y;
+        v[2] = v[2] * s_row * sw.z;
+        v[3] = v[3] * s_row * sw.w;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] *= e.alpha;
+      v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+      if (e.relu)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], 0.f);
+      if (e.rng) {
+        const uint32_t base = (uint32_t)((e.drop_row_offset + gr) * (int64_t)N + col);  // even
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+          const uint32_t d = pair_draw(key, (base + i) >> 1);
+          v[i] = ((d & 0xffffu) < e.keep_thresh16) ? v[i] * e.drop_scale : 0.f;
+          v[i + 1] = ((d >> 16) < e.keep_thresh16) ? v[i + 1] * e.drop_scale : 0.f;
+        }
+      }
+      pk[g][0] = xs_pk2(v[0], v[1]);
+      pk[g][1] = xs_pk2(v[2], v[3]);
+    }
 #pragma unroll
     for (int g = 0; g < 4; g += 2) {
-      const float4 q0 = *reinterpret_cast<const float4*>(bp + 8 * g);
-      const float4 q1 = *reinterpret_cast<const float4*>(bp + 8 * g + 8);
-      const uint32_t a0 = xs_pk2(a[4 * g] + q0.x, a[4 * g + 1] + q0.y);
-      const uint32_t a1 = xs_pk2(a[4 * g + 2] + q0.z, a[4 * g + 3] + q0.w);
-      const uint32_t b0 = xs_pk2(a[4 * g + 4] + q1.x, a[4 * g + 5] + q1.y);
-      const uint32_t b1 = xs_pk2(a[4 * g + 6] + q1.z, a[4 * g + 7] + q1.w);
-      const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-      const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+      const auto x0 = __builtin_amdgcn_permlane32_swap(pk[g][0], pk[g + 1][0], false, false);
+      const auto x1 = __builtin_amdgcn_permlane32_swap(pk[g][1], pk[g + 1][1], false, false);
       typedef int i32x4 __attribute__((ext_vector_type(4)));
       const i32x4 d = {(int)x0[0], (int)x1[0], (int)x0[1], (int)x1[1]};
       if (!(XS_ABL & 4))
         __builtin_amdgcn_raw_buffer_store_b128(d, rc, coff + 2 * (c * XS_NC + 32 * bq + 8 * g), 0, 0);
     }
   };
-  // one chunk: wait + barrier, the ring DMA two chunks ahead, 2 x 24 MFMAs, the epilogue. REFILL
-  // (the panel's last chunk when the range continues): each X fragment is reloaded with the next
-  // panel's as soon as its two MFMAs have issued, so the next panel's X streams in under this
-  // chunk's MFMAs and epilogue instead of with the chunk loop stopped.
-  auto chunk = [&](int j, int c, const __amdgpu_buffer_rsrc_t& rc, auto refill_tag,
+  // one chunk: wait + barrier, the ring DMA two chunks ahead, the MFMAs, the epilogue. REFILL
+  // (the panel's last chunk when the range continues): each X unit is reloaded with the next
+  // panel's as soon as its MFMAs have issued, so the next panel's X streams in under this chunk's
+  // MFMAs and epilogue instead of with the chunk loop stopped.
+  auto chunk = [&](int j, int c, int panel, const __amdgpu_buffer_rsrc_t& rc, auto refill_tag,
                    const __amdgpu_buffer_rsrc_t& rx_next) {
     constexpr bool REFILL = decltype(refill_tag)::value;
     // chunk j landed: younger than its pieces are the last two chunks' 4 stores each and chunk
     // j + 1's pieces (exact: every vm op is unconditional; X loads are drained at each panel
     // start); then publish it. Every wave is then past chunk j - 1's fragment reads, so its slot
     // takes chunk j + 2.
-    xs_wait_vm(j < 2 ? 0 : 8 + (j + 1 < nu ? XS_PIECES : 0));
+    xs_wait_vm(j < 2 ? 0 : 8 + (j + 1 < nu ? pw : 0));
     asm volatile("s_barrier" ::: "memory");
     if (j + 2 < nu && !(XS_ABL & 1)) issue(j + 2);
-    const char* slot = ring + (j % 3) * XS_SLOT;
+    const char* slot = ring + (j % 3) * SLOT;
     floatx16 acc[2];
 #pragma unroll
     for (int bq = 0; bq < 2; ++bq)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[bq][r] = 0.f;
+    constexpr int STEPS = XF;
 #pragma unroll
-    for (int s = 0; s < XS_KS; ++s) {
-      // logical chunk 2 s + hh of row r: unit r * 48 + g + ((2 s & 15) + hh) ^ (r & 15)
-      const int g = (2 * s) & ~15, cs = (2 * s) & 15;
+    for (int s = 0; s < STEPS; ++s) {
 #pragma unroll
       for (int bq = 0; bq < 2; ++bq) {
         const int r = 32 * bq + lr;
-        const int off = (r * XS_UNITS16 + g + ((cs + hh) ^ (r & 15))) * 16;
-        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(slot + off);
-        if (!(XS_ABL & 2)) acc[bq] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, xf[s], acc[bq], 0, 0, 0);
+        if constexpr (F8) {
+          // logical units 4 s + 2 h and 4 s + 2 h + 1 of padded row r
+          const char* wp = slot + r * (XS8_UPR * 16) + 32 * hh + 64 * s;
+          const uint4 w0 = *reinterpret_cast<const uint4*>(wp);
+          const uint4 w1 = *reinterpret_cast<const uint4*>(wp + 16);
+          const v8i wf = {(int)w0.x, (int)w0.y, (int)w0.z, (int)w0.w, (int)w1.x, (int)w1.y, (int)w1.z, (int)w1.w};
+          if (!(XS_ABL & 2))
+            acc[bq] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf, xq[s], acc[bq], 0, 0, 0, 127, 0, 127);
+
+        } else {
+          // logical chunk 2 s + hh of row r
+          const bf16x8 wf = *reinterpret_cast<const bf16x8*>(slot + xs_unit(r, 2 * s + hh) * 16);
+          if (!(XS_ABL & 2))
+            acc[bq] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, __builtin_bit_cast(bf16x8, xq[s]), acc[bq], 0, 0, 0);
+        }
       }
-      if constexpr (REFILL)
-        xf[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rx_next, xoff + 32 * s, 0, 0));
+      if constexpr (REFILL) load_frag(rx_next, s);
+      // fp8: a k-step's fragment reads stay in that k-step (hoisted over all 12 k-steps, the
+      // 32-byte W fragments took 96 registers)
+      if constexpr (F8) asm volatile("" ::: "memory");
     }
 #pragma unroll
-    for (int bq = 0; bq < 2; ++bq) epilogue(acc[bq], bq, c, rc);
+    for (int bq = 0; bq < 2; ++bq) epilogue(acc[bq], bq, c, panel, rc);
   };
 
   issue(0);
@@ -180,44 +272,77 @@ __global__ __launch_bounds__(512, 1) void gemm_xs_kernel(int M, int N, const bf1
   int j = 0;  // chunk counter over the workgroup's range (ring slot j % 3)
   int panel = u0 / nc;
   load_x(panel);
+  auto load_sa = [&](int pn) {
+    if constexpr (F8) s_row = e.sa[min(pn * XS_ROWS + 32 * wave + lr, M - 1)];
+  };
+  load_sa(panel);
   for (; j < nu; ++panel) {
     // the panel's X is complete here, by a wait the compiler's vmcnt bookkeeping sees (no X wait
     // then lands inside the chunk loop, where it would also drain the ring DMA)
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0) only (expcnt 7, lgkmcnt 15: no wait)
     const int c_first = u0 + j - panel * nc;
     const int c_end = min(u1 - panel * nc, nc);
-    const bool more = u1 > (panel + 1) * nc;  // the range continues into the next panel
-    const __amdgpu_buffer_rsrc_t rc = rsrc(C, panel, ldc);
-    const __amdgpu_buffer_rsrc_t rxn = rsrc(X, more ? panel + 1 : panel, ldx);
-    for (int c = c_first; c < c_end - (more ? 1 : 0); ++c, ++j) chunk(j, c, rc, std::false_type{}, rxn);
+    // the range continues into the next panel (fp8: no refill under the last chunk — the
+    // second set of live fragments exceeds the 256 registers; the panel start waits instead)
+    const bool more = !F8 && u1 > (panel + 1) * nc;
+    const __amdgpu_buffer_rsrc_t rc = rsrc(C, panel, ldc * 2);
+    const __amdgpu_buffer_rsrc_t rxn = rsrc(X, more ? panel + 1 : panel, ldxb);
+    for (int c = c_first; c < c_end - (more ? 1 : 0); ++c, ++j) chunk(j, c, panel, rc, std::false_type{}, rxn);
     if (more) {
-      chunk(j, c_end - 1, rc, std::true_type{}, rxn);
+      chunk(j, c_end - 1, panel, rc, std::true_type{}, rxn);
       ++j;
+    } else if (j < nu) {
+      load_x(panel + 1);
     }
+    load_sa(panel + 1);  // (drained at the next panel start; never used past the range)
   }
 #endif
 }
 
 }  // namespace
 
-extern "C" int mmt_gemm_xs(int M, int N, int K, const void* X, int64_t ldx, const void* W,
-                           int64_t ldw, void* C, int64_t ldc, const float* bias,
-                           mmt_stream_t stream) {
-  MMT_CHECK_ARG(X && W && C && M > 0, "mmt_gemm_xs: bad args");
-  MMT_CHECK_ARG(K == XS_K && N % XS_NC == 0 && N > 0 && N <= XS_MAXN, "mmt_gemm_xs: needs K == %d, N %% %d == 0, N <= %d", XS_K, XS_NC, XS_MAXN);
-  MMT_CHECK_ARG((int64_t)XS_ROWS * std::max(ldx, ldc) * 2 < 0x7fffffff, "mmt_gemm_xs: row stride too large");
-  MMT_CHECK_ARG(ldx % 8 == 0 && ldw % 8 == 0 && ldc % 8 == 0 && ldx >= K && ldw >= K && ldc >= N,
-                "mmt_gemm_xs: strides (16-B rows)");
-  MMT_CHECK_ARG(((uintptr_t)X | (uintptr_t)W | (uintptr_t)C) % 16 == 0 && (!bias || (uintptr_t)bias % 16 == 0),
-                "mmt_gemm_xs: 16-B alignment");
+namespace mmt {
+
+bool xs_shape_ok(int M, int N, int K, bool f8, int64_t lda, int64_t ldb, int64_t ldc, const void* A,
+                 const void* B, const void* C, const XsEpi& e) {
+  const int esz = f8 ? 1 : 2;
+  return M > 0 && K * esz == XS_RB && N > 0 && N % XS_NC == 0 && N <= XS_MAXN && !e.residual &&
+         (lda * esz) % 16 == 0 && (ldb * esz) % 16 == 0 && ldc % 8 == 0 && lda >= K && ldb >= K &&
+         ldc >= N && (int64_t)XS_ROWS * std::max(lda * esz, ldc * 2) < 0x7fffffff &&
+         (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 == 0) &&
+         (!e.bias || (uintptr_t)e.bias % 16 == 0) && (!f8 || (e.sa && e.sb && (uintptr_t)e.sb % 16 == 0));
+}
+
+int xs_launch(int M, int N, int K, bool f8, const void* X, int64_t lda, const void* W, int64_t ldb,
+              void* C, int64_t ldc, int out_f32, const XsEpi& e, hipStream_t stream) {
+  MMT_CHECK_ARG(!out_f32 && xs_shape_ok(M, N, K, f8, lda, ldb, ldc, X, W, C, e),
+                "gemm_xs: needs %s K, N %% %d == 0, N <= %d, 16-B rows, bf16 out, no residual",
+                f8 ? "768-byte" : "384", XS_NC, XS_MAXN);
   const int panels = (M + XS_ROWS - 1) / XS_ROWS;
   const int n_units = panels * (N / XS_NC);
   int dev = 0, n_cu = 256;
   hipGetDevice(&dev);
-  hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-  const int grid = std::min(n_units, n_cu > 0 ? n_cu : 256);
-  hipLaunchKernelGGL(gemm_xs_kernel<0>, dim3(grid), dim3(512), 0, as_stream(stream), M, N,
-                     (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, (bf16_t*)C, ldc, bias, n_units);
-  MMT_CHECK_LAUNCH("mmt_gemm_xs");
+  if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+    n_cu = 256;
+  const int grid = std::min(n_units, n_cu);
+  const int esz = f8 ? 1 : 2;
+  if (f8)
+    hipLaunchKernelGGL(gemm_xs_kernel<true>, dim3(grid), dim3(512), 0, stream, M, N, (const char*)X,
+                       lda * esz, (const char*)W, ldb * esz, (bf16_t*)C, ldc, e, n_units);
+  else
+    hipLaunchKernelGGL(gemm_xs_kernel<false>, dim3(grid), dim3(512), 0, stream, M, N, (const char*)X,
+                       lda * esz, (const char*)W, ldb * esz, (bf16_t*)C, ldc, e, n_units);
+  MMT_CHECK_LAUNCH("gemm_xs");
   return MMT_OK;
+}
+
+}  // namespace mmt
+
+extern "C" int mmt_gemm_xs(int M, int N, int K, const void* X, int64_t ldx, const void* W,
+                           int64_t ldw, void* C, int64_t ldc, const float* bias,
+                           mmt_stream_t stream) {
+  MMT_CHECK_ARG(X && W && C && M > 0, "mmt_gemm_xs: bad args");
+  XsEpi e;
+  e.bias = bias;
+  return xs_launch(M, N, K, false, X, ldx, W, ldw, C, ldc, 0, e, as_stream(stream));
 }

@@ -423,16 +423,19 @@ def check_against_floor(out, k=2.0, slack_all=1e-3, slack_min=2e-3):
     assert 1 - hmin <= k * (1 - fmin) + slack_min, (hmin, fmin)
 
 
-def check_against_floor_seeds(outs, k_loss=4.0, k_cos=2.0, slack=2e-3):
+def check_against_floor_seeds(outs, k_loss=2.0, k_cos=1.5, slack=2e-3):
     """Free-running bar at full depth, over seeds. There the bf16 storage noise alone (the
     emulating oracle vs float64: the floor) moves the loss by 0.03 % .. 16 % and the global
     gradient cosine down to 0.58 .. 0.90 depending on the seed (sequence-axis LayerNorms over
     12 blocks amplify it; the merge indices are the HIP run's, injected), so one seed's HIP/floor
-    ratio is a ratio of two random draws. The bar compares medians over the seeds instead: HIP vs the emulating
-    oracle within k_loss x the floor's median loss deviation and k_cos x its median cosine
-    deficits (global and worst tensor). HIP carries noise sources the emulation does not
-    (MFMA accumulation order, fp32 atomics, exp2), measured at ~3x the floor's loss median
-    (octo-small-tome16 seeds 0-5: 5.4e-2 vs 1.8e-2)."""
+    ratio is a ratio of two random draws. The bar compares medians over the seeds instead: HIP vs
+    the emulating oracle within k_loss x the floor's median loss deviation and k_cos x its median
+    cosine deficits (global and worst tensor). Measured (round 4, tools/noise_sources.py,
+    octo-small-tome16 seeds 0-5): HIP 0.56x the floor's median loss deviation and 1.20x its
+    median global cosine deficit; the deterministic mode gives the same numbers and reruns are
+    bitwise equal at B = 2, so fp32 atomic order contributes nothing measurable here — what HIP
+    adds beyond the bf16 storage rounding is fp32 summation order (MFMA / reductions) and
+    v_exp_f32. Round 3's bar was 4x / 2x (then 3x measured in loss)."""
     import statistics as st
 
     def med(f):

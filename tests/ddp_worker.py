@@ -9,6 +9,11 @@ asynchronously):
   shards_vs_full : (rank 0) the all-reduced sum / 2 equals ONE process's gradient of the whole
                    global batch (2 x B samples, sample_offset 0) — per-sample random streams are
                    keyed by the global sample index.
+With MMT_DETERMINISTIC=1 (the deterministic mode: fixed-point accumulation at every fp32-atomic
+gradient site) also:
+  rerun_bitwise  : the staged step run twice gives the same all-reduced gradients bit for bit;
+  tome_equal     : this rank's ToMe index triples equal, bit for bit, its rows of the full global
+                   batch's triples at every merging layer.
 Writes a JSON report to argv[1].
 """
 import json
@@ -81,6 +86,21 @@ def main():
     g_sync = model.store.flat_grad.clone()
     rep = dict(rank=di.rank, async_vs_sync=rel_by_tensor(model, g_async, g_sync),
                stages=step.S, exposed_bytes=step.exposed_bytes)
+    if os.environ.get("MMT_DETERMINISTIC", "0") == "1":
+        restore()
+        step()
+        torch.cuda.synchronize()
+        rep["rerun_bitwise"] = bool(torch.equal(model.store.flat_grad, g_async))
+        restore()
+        _, st = model.compute_diffusion_denoise_loss(None, img, act, True, state.rng, state.sample_offset)
+        mine = [sv["tome"][6:9] for sv in st["stack_sv"] if sv["tome"] is not None]
+        restore()
+        _, st = model.compute_diffusion_denoise_loss(None, img_all, act_all, True, state.rng, 0)
+        full = [sv["tome"][6:9] for sv in st["stack_sv"] if sv["tome"] is not None]
+        rep["tome_layers"] = len(mine)
+        rep["tome_equal"] = len(mine) == len(full) and all(
+            torch.equal(a, b[sl]) for m, f in zip(mine, full) for a, b in zip(m, f))
+        torch.cuda.synchronize()
     dist.barrier()
     if di.rank == 0:
         restore()

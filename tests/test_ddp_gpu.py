@@ -7,7 +7,9 @@
 * test_two_rank_staged_allreduce: two processes on the one GPU over gloo run the bench's step
   (distributed.DDPStep: the backward in one graph per block — the "auto" stage plan — each
   finished gradient region all-reduced asynchronously) — the result equals the one-piece backward + blocking all-reduce,
-  and sum / 2 equals one process's gradient of the whole global batch (tests/ddp_worker.py).
+  and sum / 2 equals one process's gradient of the whole global batch (tests/ddp_worker.py); in
+  the deterministic mode also bitwise reruns and each rank's ToMe indices == its rows of the
+  global batch's.
 """
 import json
 import os
@@ -68,13 +70,17 @@ def _port():
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_staged_allreduce(dev, tmp_path):
+@pytest.mark.parametrize("det", [False, True], ids=["atomics", "deterministic"])
+def test_two_rank_staged_allreduce(dev, tmp_path, det):
+    """det: the same over the deterministic mode (MMT_DETERMINISTIC=1 in both ranks), plus: a rerun
+    of the staged step reproduces the all-reduced gradients bit for bit, and every rank's ToMe
+    indices equal its rows of the global batch's at every merging layer."""
     port = _port()
     procs, outs = [], []
     for r in range(2):
         out = tmp_path / f"rank{r}.json"
         env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MMT_DETERMINISTIC="1" if det else "0")
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "ddp_worker.py"),
                                        str(out)], env=env, cwd=ROOT))
         outs.append(out)
@@ -89,4 +95,6 @@ def test_two_rank_staged_allreduce(dev, tmp_path):
     reps = [json.loads(o.read_text()) for o in outs]
     for rep in reps:
         assert rep["async_vs_sync"] <= 1e-5, rep
+        if det:
+            assert rep["rerun_bitwise"] and rep["tome_equal"] and rep["tome_layers"] > 0, rep
     assert reps[0]["shards_vs_full"] <= 1e-4 and reps[0]["grad_norm"] > 0, reps[0]

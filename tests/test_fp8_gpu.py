@@ -77,3 +77,34 @@ def test_fp8_shadow_follows_adamw(dev):
     rq, rs = quant_rows_e4m3(p.bf16.float().cpu())
     assert torch.equal(p.q8.cpu().view(torch.float8_e4m3fn).float(), rq)
     assert torch.equal(p.q8_scale.cpu(), rs.view(-1))
+
+
+@pytest.mark.parametrize("M,N,epi", [(33920, 3072, {"act": 1, "drop": True}), (33920, 2304, {}),
+                                     (4101, 768, {"drop": True})])
+def test_fp8_activation_stationary_kernel(dev, M, N, epi):
+    """The K = 768 fp8 products on the activation-stationary kernel (csrc/gemm_xs.hip; OCTO-base
+    QKV projection and MLP up-projection, configs[4]): the same MX-fp8 MFMAs in the same k order
+    and epilogue order as gemm_fp8_nt_kernel (forced with variant 4), so bit-identical bf16
+    outputs, dropout draws included; ragged last panel (M % 256 != 0)."""
+    from multi_modal_transformers_tokenmerge_amd import _C
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    K = 768
+    g = torch.Generator().manual_seed(M + N + 1)
+    x = torch.randn((M, K), generator=g).bfloat16()
+    w = (torch.randn((N, K), generator=g) / K ** 0.5).bfloat16()
+    xq, sx = Kn.quant_rows_fp8(x.to(dev))
+    wq, sw = Kn.quant_rows_fp8(w.to(dev))
+    kw = dict(bias=(torch.randn(N, generator=g) * 0.1).to(dev))
+    if epi.get("act"):
+        kw["act"] = Kn.ACT_RELU
+    if epi.get("drop"):
+        kw.update(rng=torch.tensor([3, 4], dtype=torch.int32, device=dev), keep_prob=0.9,
+                  drop_layer=5, drop_site=2, drop_row_offset=17)
+    new = Kn.gemm_fp8(xq, sx, wq, sw, **kw)
+    _C.call("mmt_gemm_set_variant", 4)
+    try:
+        old = Kn.gemm_fp8(xq, sx, wq, sw, **kw)
+    finally:
+        _C.call("mmt_gemm_set_variant", -1)
+    torch.cuda.synchronize()
+    assert torch.equal(new, old)
