@@ -246,10 +246,11 @@ int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t lda, const 
              int64_t ws_elems, mmt_stream_t stream);
 
 /* mmt_gemm_xs: C = X . W^T (+ bias[n]) in bf16 for the short-K products (K == 384: the
- * OCTO-small QKV / MLP-up / MLP dH shapes), X [M][ldx], W [N][ldw] bf16, C [M][ldc] bf16, N % 64 == 0,
- * N <= 1536, 16-B aligned rows; bias fp32 [N] or NULL. The activation-stationary kernel of
- * csrc/gemm_xs.hip (a 256-row panel of X held in registers while W streams through LDS). Replaces
- * the same products' mmt_gemm launches (reference attention.py:20-37, 41-69 Dense layers). */
+ * OCTO-small QKV projection), X [M][ldx], W [N][ldw] bf16, C [M][ldc] bf16, N % 64 == 0, 16-B
+ * aligned rows; bias fp32 [N] or NULL. The activation-stationary kernel of csrc/gemm_xs.hip (a
+ * 256-row panel of X held in registers while W streams through LDS); mmt_gemm routes its
+ * bias-only K = 384 products and mmt_gemm_fp8 its K = 768 bf16-output products (no gate /
+ * residual) there itself (reference attention.py:20-37, 41-69 Dense layers). */
 int mmt_gemm_xs(int M, int N, int K, const void* X, int64_t ldx, const void* W, int64_t ldw,
                 void* C, int64_t ldc, const float* bias, mmt_stream_t stream);
 

@@ -87,6 +87,7 @@ class MLPBlock(Bindable):
     with a fused bias + relu + dropout epilogue, then the GEMM with bias + dropout."""
 
     fp8 = False
+    fp8_residual = False  # Dense_1 (the residual-stream product) in e4m3 too (OctoConfig.fp8_residual)
 
     def __init__(self, dense=None, activation=None, norm=None, dense_out=None):
         self.dense_spec, self.activation, self.norm, self.dense_out_spec = \
@@ -100,13 +101,13 @@ class MLPBlock(Bindable):
 
     @classmethod
     def create(cls, store: ParamStore, name: str, in_f: int, hidden: int, out_f: int,
-               dropout_rate: float = 0.1, fp8: bool = False) -> "MLPBlock":
+               dropout_rate: float = 0.1, fp8: bool = False, fp8_residual: bool = False) -> "MLPBlock":
         """The block from its dimensions, declared in ``store`` (the Octo model's path)."""
         m = cls(LayerSpec("flax.linen.Dense", {"features": hidden}),
                 LayerSpec("flax.linen.relu", partial=True),
                 LayerSpec("flax.linen.Dropout", {"rate": dropout_rate}),
                 LayerSpec("flax.linen.Dense", {"features": out_f}))
-        m.fp8 = fp8
+        m.fp8, m.fp8_residual = fp8, fp8_residual
         return m.bind(store, name, in_f)
 
     def _declare(self, store, name, in_f):
@@ -115,7 +116,7 @@ class MLPBlock(Bindable):
         self.dense = Dense(store, f"{name}/Dense_0", in_f, hidden, fp8=self.fp8,
                            kernel_init=init_from_spec(sget(self.dense_spec, "kernel_init"), (in_f, hidden)),
                            bias_init=init_from_spec(sget(self.dense_spec, "bias_init"), (hidden,), normal(0.01)))
-        self.dense_out = Dense(store, f"{name}/Dense_1", hidden, out_f, fp8=self.fp8,
+        self.dense_out = Dense(store, f"{name}/Dense_1", hidden, out_f, fp8=self.fp8 and self.fp8_residual,
                                kernel_init=init_from_spec(sget(self.dense_out_spec, "kernel_init"), (hidden, out_f)),
                                bias_init=init_from_spec(sget(self.dense_out_spec, "bias_init"), (out_f,), normal(0.01)))
 
@@ -158,6 +159,7 @@ class Encoder1DBlock(Bindable):
     flat gradient buffer (the ``grads`` of the reference's value_and_grad)."""
 
     fp8 = False
+    fp8_residual = False  # the out-projection in e4m3 too (OctoConfig.fp8_residual)
 
     def __init__(self, layer_norm=None, dropout=None, self_attention=None, mlp_block=None,
                  train=None, mask=None):
@@ -183,7 +185,7 @@ class Encoder1DBlock(Bindable):
     @classmethod
     def create(cls, store: ParamStore, name: str, D: int, num_heads: int, mlp_dim: int,
                eps: float = 1e-6, dropout_rate: float = 0.1, attn_dropout_rate: float = 0.1,
-               fp8: bool = False) -> "Encoder1DBlock":
+               fp8: bool = False, fp8_residual: bool = False) -> "Encoder1DBlock":
         """The block from its dimensions, declared in ``store`` (the Octo model's path)."""
         blk = cls(LayerSpec("flax.linen.LayerNorm", {"epsilon": eps, "reduction_axes": [1],
                                                      "feature_axes": [-1]}),
@@ -194,7 +196,7 @@ class Encoder1DBlock(Bindable):
                            LayerSpec("flax.linen.relu", partial=True),
                            LayerSpec("flax.linen.Dropout", {"rate": dropout_rate}),
                            LayerSpec("flax.linen.Dense", {"features": D})))
-        blk.fp8 = fp8
+        blk.fp8, blk.fp8_residual = fp8, fp8_residual
         return blk.bind(store, name, D)
 
     def _declare(self, store: ParamStore, name: str, D: int):
@@ -211,9 +213,9 @@ class Encoder1DBlock(Bindable):
         self.qkv = Dense(store, f"{name}/SelfAttention_0/qkv", D, 3 * D, kernel_init=kinit(),
                          bias_init=binit, fp8=self.fp8)
         self.out = Dense(store, f"{name}/SelfAttention_0/out", D, D, kernel_init=kinit(),
-                         bias_init=binit, fp8=self.fp8)
+                         bias_init=binit, fp8=self.fp8 and self.fp8_residual)
         self.ln1 = SeqLayerNorm(store, f"{name}/LayerNorm_1", D, self.eps)
-        self.mlp.fp8 = self.fp8
+        self.mlp.fp8, self.mlp.fp8_residual = self.fp8, self.fp8_residual
         self.mlp.bind(store, f"{name}/MLPBlock_0", D)
         if self.mlp.dense_out.out_f != D:
             raise ValueError("mlp_block.dense_out.features must equal the input width (residual)")
@@ -480,12 +482,13 @@ class StackedEncoder1DBlock(Bindable):
     @classmethod
     def create(cls, store: ParamStore, name: str, num_blocks: int, D: int, num_heads: int,
                mlp_dim: int, eps: float = 1e-6, dropout_rate: float = 0.1,
-               attn_dropout_rate: float = 0.1, fp8: bool = False) -> "StackedEncoder1DBlock":
+               attn_dropout_rate: float = 0.1, fp8: bool = False,
+               fp8_residual: bool = False) -> "StackedEncoder1DBlock":
         """The stack's blocks declared in ``store`` (the Octo model's path; its posembed_input
         is declared by the model, which adds it inside the fused sequence assembly)."""
         st = cls(num_blocks, None)
         st.blocks = [Encoder1DBlock.create(store, f"{name}/Block_{i}", D, num_heads, mlp_dim, eps,
-                                           dropout_rate, attn_dropout_rate, fp8)
+                                           dropout_rate, attn_dropout_rate, fp8, fp8_residual)
                      for i in range(num_blocks)]
         st._store, st._name = store, name
         return st

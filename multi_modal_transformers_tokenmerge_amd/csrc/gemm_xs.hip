@@ -43,7 +43,8 @@ constexpr int XS_UNITS16 = XS_RB / 16;             // 48 16-B units per row
 constexpr int XS_XR = XS_RB / 32;                  // 24 register units of X per lane
 constexpr int XS_SLOT = XS_NC * XS_RB;             // 48 KB per ring slot
 constexpr int XS_PIECES = XS_SLOT / 1024 / 8;      // 6 DMA pieces per wave per chunk
-constexpr int XS_MAXN = 1536;                      // bias columns staged in LDS
+// per ring slot, the chunk's 64 bias values (and fp8 channel scales) arrive by LDS-DMA with its
+// W rows: two 1-KB pieces (only their first 256 B are read), issued by waves 7 (bias) and 6 (sb)
 // fp8 slots: rows padded to 49 units (784 B) instead of the XOR swizzle — unit (r, c) at
 // 49 r + c is conflict-free for 16 consecutive rows (49 = 1 mod 16) and every fragment read of a
 // lane is one base address + an immediate (the XOR form's 24 per-step addresses spilled the
@@ -85,8 +86,7 @@ __global__ __launch_bounds__(512, 1) void gemm_xs_kernel(int M, int N, const cha
 #if defined(__HIP_DEVICE_COMPILE__)
   constexpr int SLOT = F8 ? XS8_SLOT : XS_SLOT;
   __shared__ __attribute__((aligned(16))) char ring[3 * SLOT];
-  __shared__ __attribute__((aligned(16))) float s_bias[XS_MAXN];
-  __shared__ __attribute__((aligned(16))) float s_sb[F8 ? XS_MAXN : 4];  // fp8 channel scales
+  __shared__ __attribute__((aligned(16))) char aux[3][2][1024];  // [slot][bias | sb] of the chunk
   const int lane = threadIdx.x & 63, hh = lane >> 5, lr = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nc = N / XS_NC;
@@ -95,11 +95,6 @@ __global__ __launch_bounds__(512, 1) void gemm_xs_kernel(int M, int N, const cha
   const int u1 = (int)((int64_t)n_units * (wg + 1) / gridDim.x);
   const int nu = u1 - u0;
   if (nu <= 0) return;
-  for (int i = threadIdx.x; i < N; i += 512) {
-    s_bias[i] = e.bias ? e.bias[i] : 0.f;
-    if constexpr (F8) s_sb[i] = e.sb[i];
-  }
-  __syncthreads();
   float s_row = 1.f;  // fp8: this lane's row scale in the current panel (loaded with its X)
   const uint32_t key = e.rng ? stream_key(e.rng[0], e.rng[1], e.drop_layer, e.drop_site) : 0u;
 
@@ -118,11 +113,18 @@ __global__ __launch_bounds__(512, 1) void gemm_xs_kernel(int M, int N, const cha
     }
   };
   // DMA pieces this wave issues per chunk (bf16: 6; fp8: 7 for wave 0, 6 for the others)
-  const int pw = F8 ? (XS8_PIECES - 1 - wave) / 8 + 1 : XS_PIECES;
+  const int pw = (F8 ? (XS8_PIECES - 1 - wave) / 8 + 1 : XS_PIECES) + (wave == 7 || (F8 && wave == 6) ? 1 : 0);
   auto issue = [&](int j) {  // chunk u0 + j into slot j % 3: pw vm ops per wave
     const int c = (u0 + j) % nc;
     const char* base = W + (int64_t)c * XS_NC * ldwb;
     char* slot = ring + (j % 3) * SLOT;
+    // the chunk's bias (wave 7) / fp8 channel scales (wave 6): 64 floats = lanes 0-15 of a piece
+    // (a NULL bias reads as zeros: empty buffer range); the rest of the 1-KB piece is not read
+    if (wave == 7)
+      dma16_asm(e.bias ? (const void*)(e.bias + c * XS_NC) : (const void*)W, e.bias ? XS_NC * 4 : 0,
+                aux[j % 3][0], 16 * (lane & 15));
+    if (F8 && wave == 6)
+      dma16_asm(e.sb + c * XS_NC, XS_NC * 4, aux[j % 3][1], 16 * (lane & 15));
     if constexpr (F8) {
 #pragma unroll
       for (int k = 0; k < 7; ++k) {
@@ -173,16 +175,17 @@ __global__ __launch_bounds__(512, 1) void gemm_xs_kernel(int M, int N, const cha
 
   // epilogue of one 32-column block: lane row m = lr, columns 32 bq + 8 g + 4 hh + i (2 stores);
   // epilogue_w's arithmetic and order
-  auto epilogue = [&](const floatx16& a, int bq, int c, int panel, const __amdgpu_buffer_rsrc_t& rc) {
+  auto epilogue = [&](const floatx16& a, int bq, int c, int panel, const __amdgpu_buffer_rsrc_t& rc,
+                      const float* cb, const float* csb) {
     const int gr = panel * XS_ROWS + 32 * wave + lr;
     uint32_t pk[4][2];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int col = c * XS_NC + 32 * bq + 8 * g + 4 * hh;
-      const float4 bb = *reinterpret_cast<const float4*>(s_bias + col);
+      const float4 bb = *reinterpret_cast<const float4*>(cb + 32 * bq + 8 * g + 4 * hh);
       float v[4] = {a[4 * g], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]};
       if constexpr (F8) {
-        const float4 sw = *reinterpret_cast<const float4*>(s_sb + col);
+        const float4 sw = *reinterpret_cast<const float4*>(csb + 32 * bq + 8 * g + 4 * hh);
         v[0] = v[0] * s_row * sw.x;
         v[1] = v[1] * s_row * sw.y;
         v[2] = v[2] * s_row * sw.z;
@@ -264,7 +267,9 @@ __global__ __launch_bounds__(512, 1) void gemm_xs_kernel(int M, int N, const cha
       if constexpr (F8) asm volatile("" ::: "memory");
     }
 #pragma unroll
-    for (int bq = 0; bq < 2; ++bq) epilogue(acc[bq], bq, c, panel, rc);
+    for (int bq = 0; bq < 2; ++bq)
+      epilogue(acc[bq], bq, c, panel, rc, reinterpret_cast<const float*>(aux[j % 3][0]),
+               reinterpret_cast<const float*>(aux[j % 3][1]));
   };
 
   issue(0);
@@ -306,7 +311,7 @@ namespace mmt {
 bool xs_shape_ok(int M, int N, int K, bool f8, int64_t lda, int64_t ldb, int64_t ldc, const void* A,
                  const void* B, const void* C, const XsEpi& e) {
   const int esz = f8 ? 1 : 2;
-  return M > 0 && K * esz == XS_RB && N > 0 && N % XS_NC == 0 && N <= XS_MAXN && !e.residual &&
+  return M > 0 && K * esz == XS_RB && N > 0 && N % XS_NC == 0 && !e.residual &&
          (lda * esz) % 16 == 0 && (ldb * esz) % 16 == 0 && ldc % 8 == 0 && lda >= K && ldb >= K &&
          ldc >= N && (int64_t)XS_ROWS * std::max(lda * esz, ldc * 2) < 0x7fffffff &&
          (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 == 0) &&
@@ -316,8 +321,8 @@ bool xs_shape_ok(int M, int N, int K, bool f8, int64_t lda, int64_t ldb, int64_t
 int xs_launch(int M, int N, int K, bool f8, const void* X, int64_t lda, const void* W, int64_t ldb,
               void* C, int64_t ldc, int out_f32, const XsEpi& e, hipStream_t stream) {
   MMT_CHECK_ARG(!out_f32 && xs_shape_ok(M, N, K, f8, lda, ldb, ldc, X, W, C, e),
-                "gemm_xs: needs %s K, N %% %d == 0, N <= %d, 16-B rows, bf16 out, no residual",
-                f8 ? "768-byte" : "384", XS_NC, XS_MAXN);
+                "gemm_xs: needs %s K, N %% %d == 0, 16-B rows, bf16 out, no residual",
+                f8 ? "768-byte" : "384", XS_NC);
   const int panels = (M + XS_ROWS - 1) / XS_ROWS;
   const int n_units = panels * (N / XS_NC);
   int dev = 0, n_cu = 256;

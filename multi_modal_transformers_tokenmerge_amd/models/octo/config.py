@@ -40,8 +40,12 @@ class OctoConfig:
     text_tokens: int = 32
     # ResNetV2Block hyper-parameters (gato_resnet.yaml:41-104); None = the build defaults
     stem: Optional[dict] = None
-    # fp8 weight path (BASELINE configs[4]): the encoder blocks' Dense forward products in e4m3
+    # fp8 weight path (BASELINE configs[4]): the encoder blocks' Dense forward products in e4m3 —
+    # the QKV projection and MLP Dense_0 (activation-stationary fp8 kernel, 1.8x its bf16 twin);
+    # fp8_residual also puts the residual-stream products (out-projection, MLP Dense_1, fp32
+    # residual epilogue) in e4m3, measured slower than their bf16 kernels — off
     fp8: bool = False
+    fp8_residual: bool = False
     # how token_compression_sequence's per-layer counts are realised: "tome" (bipartite soft
     # matching + merge_wavg, token_compression.py:54-129, one image set per layer) or "prune"
     # (per-set top-k on the attention importance, compressed_attention.py:302-308 +

@@ -88,7 +88,7 @@ class Octo:
         self.stack = StackedEncoder1DBlock.create(store, "StackedEncoder1DBlock_0", cfg.num_blocks,
                                                   D, cfg.num_heads, cfg.mlp_dim, cfg.layer_norm_eps,
                                                   cfg.dropout_rate, cfg.attention_dropout_rate,
-                                                  fp8=cfg.fp8)
+                                                  fp8=cfg.fp8, fp8_residual=cfg.fp8_residual)
         # ---- head
         self.head = DiffusionActionHead.create(store, "diffusion_action_head", D,
                                                cfg.action_space_dim, cfg.diffusion_steps)

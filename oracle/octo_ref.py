@@ -441,6 +441,8 @@ class OctoRef:
         y = tr("y0", rbg(seq_layernorm(x, p[f"{blk}/LayerNorm_0/scale"], p[f"{blk}/LayerNorm_0/bias"],
                                        cfg.layer_norm_eps)))
         bdense = dense_fp8 if getattr(cfg, "fp8", False) else dense
+        # the residual-stream products (out-projection, Dense_1) in e4m3 only with fp8_residual
+        rdense = dense_fp8 if getattr(cfg, "fp8", False) and getattr(cfg, "fp8_residual", False) else dense
         qkv = tr("qkv", rbg(bdense(p, f"{blk}/SelfAttention_0/qkv", y)))
         q, k, v = qkv.split(D, dim=-1)
         k, v = k.reshape(B, L, H, Dh), v.reshape(B, L, H, Dh)
@@ -488,7 +490,7 @@ class OctoRef:
             bidx = torch.arange(B)[:, None]
             o, x = o[bidx, idx], x[bidx, idx]
         Lo = o.shape[1]
-        o = gb(bdense(p, f"{blk}/SelfAttention_0/out", o))
+        o = gb(rdense(p, f"{blk}/SelfAttention_0/out", o))
         if train:
             keep = torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 1, B * Lo, D,
                                                       sample_offset * Lo, kp)).view(B, Lo, D)
@@ -519,7 +521,7 @@ class OctoRef:
                                                       sample_offset * L2, kp)).view(B, L2, -1)
             h = torch.where(keep, h / kp, torch.zeros_like(h))
         h = tr("h", rb(h))
-        z = gb(bdense(p, f"{blk}/MLPBlock_0/Dense_1", h))
+        z = gb(rdense(p, f"{blk}/MLPBlock_0/Dense_1", h))
         if train:
             keep = torch.from_numpy(R.dropout_mask_2d(seed, step, layer, 3, B * L2, D,
                                                       sample_offset * L2, kp)).view(B, L2, D)
