@@ -2429,6 +2429,8 @@ static bool attn_res_enabled(const char* var = "MMT_ATTN_RES") {
 // 4 waves (128 rows) — measured at B = 256, Dh = 64: L = 292 398 -> 380 us, L = 132 177 -> 138 us,
 // L = 212 (equal fill) 234 -> 257 us, so the smaller blocks must gain > 10 % fill.
 inline int bwd_threads(int L) {
+  static const int forced = getenv("MMT_ATTN_BWD_NT") ? atoi(getenv("MMT_ATTN_BWD_NT")) : 0;
+  if (forced == 128 || forced == 256) return forced;  // (benchmarks)
   const double f128 = (double)L / (((L + 127) / 128) * 128);
   const double f64 = (double)L / (((L + 63) / 64) * 64);
   return f64 > f128 + 0.10 ? 128 : 256;
@@ -2561,7 +2563,10 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
       return MMT_OK;
     }
   }
-  int nq = g_attn_nq > 0 ? std::min(g_attn_nq, 2) : (L <= 32 ? 1 : L <= 2 * QB ? 2 : 1);
+  // (past the K/V-resident kernel's L <= 320 the tiled kernel also takes two blocks: OCTO-base,
+  // B = 32, H = 12, tools/attn_bench.py: L = 1064 352.7 -> 312.5 us, L = 788 231.0 -> 193.1,
+  // L = 532 114.3 -> 111.1)
+  int nq = g_attn_nq > 0 ? std::min(g_attn_nq, 2) : (L <= 32 ? 1 : L <= 2 * QB ? 2 : L > 32 * RES_TILES ? 2 : 1);
   if (Dh > 64) nq = 1;
   dim3 grid((L + QB * nq - 1) / (QB * nq), H, B);
 #define FWD1(DH_, NQ_, WS_, DR_)                                                                 \

@@ -16,7 +16,10 @@ def main():
     B = 256
     Ls = (292, 212, 132)
     t5 = True
+    H = 6
     for a in sys.argv[1:]:
+        if a.startswith("--h="):
+            H = int(a.split("=")[1])
         if a.startswith("--b="):
             B = int(a.split("=")[1])
         if a.startswith("--L="):
@@ -26,7 +29,7 @@ def main():
     cases = []
     for L in Ls:  # default: layers 0, 5, 10 of the ToMe r=16 schedule
         n_img = L - 36
-        cases.append((f"octo-small L={L}", L, 6, 64,
+        cases.append((f"octo L={L}", L, H, 64,
                       K.SetTable([0, 32, 32 + n_img], [32, n_img, 4], [0b001, 0b011, 0b111]), True, False))
     if t5:
         cases.append(("t5 L=32 (bias)", 32, 12, 64, None, False, True))
