@@ -24,6 +24,7 @@ import statistics
 
 
 def per_dispatch(d: str, counter: str, kernel: str) -> list[float]:
+    """Counter value per dispatch of the kernel, in dispatch order."""
     files = glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection csv under {d}")
@@ -36,9 +37,9 @@ def per_dispatch(d: str, counter: str, kernel: str) -> list[float]:
             for row in csv.DictReader(fh):
                 if row.get("Counter_Name") != counter or not pat.search(row.get("Kernel_Name", "")):
                     continue
-                key = f"{f}:{row.get('Dispatch_Id')}"
+                key = (f, int(row.get("Dispatch_Id") or 0))
                 vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
-    return list(vals.values())
+    return [vals[k] for k in sorted(vals)]
 
 
 def main():
@@ -53,9 +54,22 @@ def main():
     meta = json.loads(line)
     probes = meta["probes"]
     res = {}
+    # probes that share a kernel (the two residual-stream products on gemm_glds_nt_kernel) ran
+    # one after the other: the k-th of them owns the k-th contiguous share of the dispatches
+    share = {}
     for p in probes:
-        fetch = per_dispatch(a.fetch_dir, "FETCH_SIZE", p["kernel"])
-        write = per_dispatch(a.write_dir, "WRITE_SIZE", p["kernel"])
+        share.setdefault(p["kernel"], []).append(p["name"])
+
+    def part(vals, p):
+        names = share[p["kernel"]]
+        n, k = len(names), names.index(p["name"])
+        if n == 1:
+            return vals
+        m = len(vals) // n
+        return vals[k * m:(k + 1) * m]
+    for p in probes:
+        fetch = part(per_dispatch(a.fetch_dir, "FETCH_SIZE", p["kernel"]), p)
+        write = part(per_dispatch(a.write_dir, "WRITE_SIZE", p["kernel"]), p)
         if not fetch or not write:
             print(f"no counter rows for {p['kernel']}")
             continue
