@@ -21,8 +21,9 @@ struct XsEpi {
   const float* sb = nullptr;  // fp8: per-channel weight scales [N]
 };
 
-// Whether the kernel takes a product: K == 384 (bf16) or 768 (fp8 bytes), N % 64 == 0, N <= 1536
-// for a bias (LDS-staged), 16-B aligned rows / operands.
+// Whether the kernel takes a product: K == 384 (bf16) or 768 (fp8 bytes), N % 64 == 0, no
+// residual, 16-B aligned rows / operands (bias and channel scales are DMA'd per 64-column chunk,
+// so any N).
 bool xs_shape_ok(int M, int N, int K, bool f8, int64_t lda, int64_t ldb, int64_t ldc, const void* A,
                  const void* B, const void* C, const XsEpi& e);
 // C = epi(X . W^T); X [M][lda], W [N][ldb] (elements: bf16, or e4m3 bytes when f8), C [M][ldc]
