@@ -203,13 +203,16 @@ def kernel_probes(model, B, reps=20):
             "mfma", 2.0 * M * D * Mh,
             f"M={M} N={D} K={Mh}, 2MNK (one or two launches of the narrow-output NT kernel)",
             _gemm_bytes(M, D, Mh))
-    # 3. MLP Dense_0 weight gradient dW += dz1^T . y1 (TN, split-K fp32 slabs + combine)
+    # 3. MLP Dense_0 weight gradient dW += dz1^T . y1 (TN, split-K fp32 slabs + combine); the
+    # standalone probe splits for the whole chip (256 workgroups), the step's launches for half of
+    # it (layers.split_k_for: they share the CUs with the main queue)
     wgrad = torch.zeros((Mh, D), dtype=torch.float32, device=dev)
+    sk = split_k_for(Mh, D, M, wgs=256)
     add("mlp_dw", "gemm_tn_dma_kernel",
-        lambda: K.gemm(dz1, y1, trans_a=True, out=wgrad, out_mode=K.OUT_F32_ACCUM,
-                       split_k=split_k_for(Mh, D, M)),
+        lambda: K.gemm(dz1, y1, trans_a=True, out=wgrad, out_mode=K.OUT_F32_ACCUM, split_k=sk),
         "mfma", 2.0 * M * D * Mh,
-        f"M={Mh} N={D} K={M}, 2MNK (split-K GEMM + its combine kernel together)",
+        f"M={Mh} N={D} K={M}, 2MNK, split-K {sk} (the GEMM + its combine kernel together; "
+        "full-chip split, the step splits for 128 workgroups)",
         2 * (M * Mh + M * D) + 8 * Mh * D)
     # 3b./3c. the residual-stream products (fp32 out = fp32 residual + dropout(x W^T + b)):
     # MLP Dense_1 and the attention out-projection of block 0 (reference attention.py:36-37,

@@ -1730,10 +1730,13 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
 }
 
 // Split-K combine: v = sum_s slab[s][m][n] (fp32, slabs in order), then the GEMM epilogue, 4
-// columns per thread with 8 slabs' loads in flight (the slabs come from the Infinity Cache: the
-// kernel is bound by loads in flight, 8 columns x 4 slabs per thread measured 37.6 us per launch
-// in the step)
-template <int OUT>
+// columns per thread with up to CB slabs' loads in flight (the slabs come from the Infinity
+// Cache: the kernel is bound by loads in flight; 8 columns x 4 slabs per thread measured 37.6 us
+// per launch in the step, 4 columns x 8 slabs less)
+#ifndef MMT_COMBINE_CB  // slab loads in flight per thread (benchmarking builds)
+#define MMT_COMBINE_CB 16
+#endif
+template <int OUT, int CB = MMT_COMBINE_CB>
 __global__ void splitk_epilogue_kernel(const float* __restrict__ ws, int split, int M, int N,
                                        void* __restrict__ Cv, int64_t ldc, Epi epi) {
   const int n4 = N / 4;
@@ -1747,21 +1750,18 @@ __global__ void splitk_epilogue_kernel(const float* __restrict__ ws, int split, 
     const float* p = ws + (int64_t)gr * N + gc;
     float v[4];
     ldw<4>(p, v);
-    int k = 1;
-    for (; k + 8 <= split; k += 8) {
-      float t[8][4];
+    // slabs 1 .. split - 1 in batches of CB, every load of a batch issued before the first add
+    // (predicated past split: no single-load tail), summed in slab order
+    for (int k = 1; k < split; k += CB) {
+      float t[CB][4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ldw<4>(p + (k + j) * slab, t[j]);
+      for (int j = 0; j < CB; ++j)
+        if (k + j < split) ldw<4>(p + (k + j) * slab, t[j]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
+      for (int j = 0; j < CB; ++j)
+        if (k + j < split)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += t[j][e];
-    }
-    for (; k < split; ++k) {
-      float t[4];
-      ldw<4>(p + k * slab, t);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] += t[e];
+          for (int e = 0; e < 4; ++e) v[e] += t[j][e];
     }
     epilogue_w<4>(epi, key, N, gr, gc, v);
     store_w<OUT, 4>(Cv, (int64_t)gr * ldc + gc, epi.beta, v);

@@ -101,16 +101,23 @@ class wgrad_overlap:
 
 
 _TN_BM = 256 if os.environ.get("MMT_TN_BM") == "256" else 384  # as csrc/gemm.hip's tile choice
+# workgroups a weight-gradient launch in the step is split for (MMT_WGRAD_WGS overrides): the
+# split-K slab bytes written and combined scale with it, the launch's CU-time does not, and the
+# launches share the chip with the main queue's backward anyway — half the chip measured +0.8-1 %
+# per step over a full-chip split (15,451 / 15,501 vs 15,326 / 15,338 samples/s; 64: -6 %)
+_WGRAD_WGS = int(os.environ.get("MMT_WGRAD_WGS", "128"))
 
 
-def split_k_for(n_out: int, k_out: int, m_red: int) -> int:
-    """Split of the M-reduction of a weight-gradient GEMM so the launch fills the 256 CUs once:
-    the TN products run on the direct-to-LDS kernel at one workgroup per CU (csrc/gemm.hip
+def split_k_for(n_out: int, k_out: int, m_red: int, wgs: int = 0) -> int:
+    """Split of the M-reduction of a weight-gradient GEMM so the launch runs ~wgs workgroups
+    (default _WGRAD_WGS = 128, half the chip: the dW launches run on the side queue beside the
+    main queue's backward; 256 fills the chip once, as the standalone bench probe does): the TN
+    products run on the direct-to-LDS kernel at one workgroup per CU (csrc/gemm.hip
     gemm_tn_dma_kernel: 384 x 192 tiles where n_out % 384 == 0, else 256 x 192), so the split is
-    sized for ~256 of ITS tiles."""
+    sized in ITS tiles."""
     bm = _TN_BM if n_out % 384 == 0 else 256
     tiles = math.ceil(n_out / bm) * math.ceil(k_out / 192)
-    want = max(1, 256 // tiles)
+    want = max(1, (wgs or _WGRAD_WGS) // tiles)
     return int(max(1, min(want, m_red // 256, 64)))
 
 

@@ -3,7 +3,7 @@
 # other objects into libmmt_hip_ablN.so (load with MMT_LIB_AB); run after the normal build
 set -e
 cd "$(dirname "$0")/../multi_modal_transformers_tokenmerge_amd/csrc"
-objs=$(ls _obj/*.o | grep -v gemm)
+objs=$(ls _obj/*.o | grep -v "/gemm.o$")
 for n in "$@"; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -munsafe-fp-atomics \
     -ffp-contract=fast -DMMT_W384_ABL=$n -I ../../include -c gemm.hip -o /tmp/gemm_abl$n.o

@@ -4,7 +4,7 @@
 # objects into libmmt_hip_tnablN.so (load with MMT_LIB_AB); run after the normal build
 set -e
 cd "$(dirname "$0")/../multi_modal_transformers_tokenmerge_amd/csrc"
-objs=$(ls _obj/*.o | grep -v gemm)
+objs=$(ls _obj/*.o | grep -v "/gemm.o$")
 for n in "$@"; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -munsafe-fp-atomics \
     -ffp-contract=fast -DMMT_TN_ABL=$n -I ../../include -c gemm.hip -o /tmp/gemm_tnabl$n.o
