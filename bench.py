@@ -88,7 +88,8 @@ def algorithmic_flops_per_sample(model) -> float:
     return 3 * (tr + stem) + t5
 
 
-PROBE_KERNEL = "gemm_nt256_kernel<256, 0, 0, 2, false, false, false>"
+PROBE_KERNEL = "gemm_xs_kernel<false, true>"  # the MLP up (relu-bit image) at K = 384
+NT256_KERNEL = "gemm_nt256_kernel<256, 0, 0, 2, false, false, false>"
 
 
 def _graph_time_us(launch, reps):
@@ -162,14 +163,18 @@ def kernel_probes(model, B, reps=20):
                             bytes_per_launch=work, achieved=round(ach, 1), peak=HBM_PEAK_GBS,
                             unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4), note=note))
 
-    # 1. MLP up-projection (bias + relu + dropout epilogue): the dominant kernel
+    # 1. MLP up-projection (bias + relu + dropout epilogue + the relu-bit image the backward
+    # gates with, as the step launches it)
     M = B * L1
     y1 = rnd(M, D)
     h = torch.empty((M, Mh), dtype=torch.bfloat16, device=dev)
-    add("mlp_up_fwd", PROBE_KERNEL,
+    hb = (torch.empty((-(-M // 256) * 256, Mh // 32), dtype=torch.int32, device=dev)
+          if K.gemm_bits_supported(M, Mh, D) and not blk.mlp.dense.fp8 else None)
+    add("mlp_up_fwd", PROBE_KERNEL if D == 384 else NT256_KERNEL,
         lambda: blk.mlp.dense.fwd(y1, out=h, act=K.ACT_RELU, rng=rng, drop_layer=0, drop_site=2,
-                                  keep_prob=0.9),
-        "mfma", 2.0 * M * Mh * D, f"M={M} N={Mh} K={D}, 2MNK", _gemm_bytes(M, Mh, D, extra=4 * Mh))
+                                  keep_prob=0.9, relu_bits=hb),
+        "mfma", 2.0 * M * Mh * D, f"M={M} N={Mh} K={D}, 2MNK (+ bias, relu, dropout, relu bits)",
+        _gemm_bytes(M, Mh, D, extra=4 * Mh) + (M * Mh // 8 if hb is not None else 0))
     # 1b. fp8 weight path (BASELINE configs[4]): the same product in e4m3 on
     # v_mfma_scale_f32_32x32x64_f8f6f4 (per-row activation / per-channel weight scales), priced
     # against the dense fp8 peak; its bf16 twin is mlp_up_fwd above (same shape and epilogue)
@@ -182,7 +187,7 @@ def kernel_probes(model, B, reps=20):
                                drop_layer=0, drop_site=2, keep_prob=0.9),
             "mfma8", 2.0 * M * Mh * D, f"M={M} N={Mh} K={D}, 2MNK in e4m3 (+ bias, relu, dropout; "
             "the activation quantisation is its own kernel)", M * D + Mh * D + 2 * M * Mh + 4 * (M + Mh))
-        add("mlp_up_fwd_bf16_twin", PROBE_KERNEL,
+        add("mlp_up_fwd_bf16_twin", PROBE_KERNEL if D == 384 else NT256_KERNEL,
             lambda: K.gemm(y1, w8.bf16, trans_b=True, out=h, bias=b8, act=K.ACT_RELU, rng=rng,
                            drop_layer=0, drop_site=2, keep_prob=0.9),
             "mfma", 2.0 * M * Mh * D, f"M={M} N={Mh} K={D}: the fp8 probe's product in bf16 (A/B)",

@@ -2461,10 +2461,11 @@ int cu_count() {
 
 // Tile width of the persistent 256 x BN NT kernel for this launch, 0 when another kernel runs.
 // the activation-stationary kernel (csrc/gemm_xs.hip) where it applies; MMT_XS=0: off (A/B)
-bool xs_enabled() {
-  static const bool on = !getenv("MMT_XS") || atoi(getenv("MMT_XS")) != 0;
-  return on;
+int xs_mode() {  // 0 off, 1 bias-only bf16 products, 2 (default) also relu / dropout / relu bits
+  static const int m = getenv("MMT_XS") ? atoi(getenv("MMT_XS")) : 2;
+  return m;
 }
+bool xs_enabled() { return xs_mode() != 0; }
 
 int nt_bn(int M, int N, int K, int transA, int transB, int batch, int out_kind, int final_kind) {
   if (transA || !transB || batch != 1 || out_kind == 2 || K % 64 != 0 ||
@@ -2764,15 +2765,25 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     MMT_CHECK_LAUNCH("mmt_gemm(ntw)");
     return MMT_OK;
   }
-  // activation-stationary short-K kernel (csrc/gemm_xs.hip) for the bias-only bf16 products at
-  // K = 384 (the OCTO-small QKV projection: 198 vs 220 us at B = 512, bit-identical outputs;
-  // tools/xs_bench.py). MMT_XS=0: off (A/B).
+  // activation-stationary short-K kernel (csrc/gemm_xs.hip) for the bf16 products at K = 384
+  // with a bias / relu / dropout / relu-bit epilogue (the OCTO-small QKV projection: 198 vs
+  // 220 us at B = 512; the MLP up-projection with relu bits; bit-identical outputs and bit
+  // images; tools/xs_bench.py). MMT_XS=0: off (A/B); MMT_XS=1: the bias-only products only.
   if (xs_enabled() && g_variant < 0 && !transA && transB && batch == 1 && out_kind == 0 &&
-      final_kind == 0 && M >= 32768 && epi.act == MMT_ACT_NONE && !epi.rng && !epi.gate &&
-      !epi.residual && epi.alpha == 1.f && epi.beta == 0.f && !epi.colsum && !epi.relu_bits &&
-      !epi.gate_bits && !epi.keep_bits) {
+      final_kind == 0 && M >= 32768 && (epi.act == MMT_ACT_NONE || epi.act == MMT_ACT_RELU) &&
+      !epi.gate && !epi.residual && epi.beta == 0.f && !epi.colsum && !epi.gate_bits &&
+      !epi.keep_bits && (xs_mode() == 2 || (epi.act == MMT_ACT_NONE && !epi.rng && !epi.relu_bits))) {
     XsEpi xe;
     xe.bias = epi.bias;
+    xe.relu = epi.act == MMT_ACT_RELU;
+    xe.rng = epi.rng;
+    xe.drop_layer = epi.drop_layer;
+    xe.drop_site = epi.drop_site;
+    xe.keep_thresh16 = epi.keep_thresh16;
+    xe.drop_scale = epi.drop_scale;
+    xe.drop_row_offset = epi.drop_row_offset;
+    xe.alpha = epi.alpha;
+    xe.relu_bits = epi.relu_bits;
     if (xs_shape_ok(M, N, K, false, lda, ldb, ldc, A, B, C, xe))
       return xs_launch(M, N, K, false, A, lda, B, ldb, C, ldc, 0, xe, s);
   }

@@ -19,11 +19,12 @@ struct XsEpi {
   int64_t ld_res = 0;
   const float* sa = nullptr;  // fp8: per-row activation scales [M]
   const float* sb = nullptr;  // fp8: per-channel weight scales [N]
+  uint32_t* relu_bits = nullptr;  // bf16: the relu-bit image (include/mmt_api.h layout), N % 256 == 0
 };
 
 // Whether the kernel takes a product: K == 384 (bf16) or 768 (fp8 bytes), N % 64 == 0, no
 // residual, 16-B aligned rows / operands (bias and channel scales are DMA'd per 64-column chunk,
-// so any N).
+// so any N); a relu-bit image only for bf16 and N % 256 == 0.
 bool xs_shape_ok(int M, int N, int K, bool f8, int64_t lda, int64_t ldb, int64_t ldc, const void* A,
                  const void* B, const void* C, const XsEpi& e);
 // C = epi(X . W^T); X [M][lda], W [N][ldb] (elements: bf16, or e4m3 bytes when f8), C [M][ldc]

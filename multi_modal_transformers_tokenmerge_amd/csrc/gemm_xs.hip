@@ -68,8 +68,11 @@ __host__ __device__ __forceinline__ int xs_unit(int r, int c) {
 __device__ __forceinline__ void xs_wait_vm(int n) {
   switch (n) {
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
     case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
@@ -78,7 +81,9 @@ __device__ __forceinline__ void xs_wait_vm(int n) {
 #define XS_ABL 0  // 4 no C stores
 #endif
 
-template <bool F8>
+// RB (bf16 only): also the relu-bit image of the output (include/mmt_api.h relu_bits layout: bit
+// set iff the stored value is > 0), two 16-bit stores per lane per chunk
+template <bool F8, bool RB = false>
 __global__ __launch_bounds__(512, 1) void gemm_xs_kernel(int M, int N, const char* __restrict__ X,
                                                          int64_t ldxb, const char* __restrict__ W,
                                                          int64_t ldwb, bf16_t* __restrict__ C,
@@ -174,11 +179,12 @@ __global__ __launch_bounds__(512, 1) void gemm_xs_kernel(int M, int N, const cha
   const int coff = (32 * wave + lr) * (int)(ldc * 2) + 16 * hh;
 
   // epilogue of one 32-column block: lane row m = lr, columns 32 bq + 8 g + 4 hh + i (2 stores);
-  // epilogue_w's arithmetic and order
+  // epilogue_w's arithmetic and order. Returns (RB) the positive-value bits, bit 4 g + i.
   auto epilogue = [&](const floatx16& a, int bq, int c, int panel, const __amdgpu_buffer_rsrc_t& rc,
                       const float* cb, const float* csb) {
     const int gr = panel * XS_ROWS + 32 * wave + lr;
     uint32_t pk[4][2];
+    uint32_t nib = 0;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int col = c * XS_NC + 32 * bq + 8 * g + 4 * hh;
@@ -206,6 +212,9 @@ __global__ __launch_bounds__(512, 1) void gemm_xs_kernel(int M, int N, const cha
           v[i + 1] = ((d >> 16) < e.keep_thresh16) ? v[i + 1] * e.drop_scale : 0.f;
         }
       }
+      if constexpr (RB)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) nib |= (v[i] > 0.f ? 1u : 0u) << (4 * g + i);
       pk[g][0] = xs_pk2(v[0], v[1]);
       pk[g][1] = xs_pk2(v[2], v[3]);
     }
@@ -218,19 +227,42 @@ __global__ __launch_bounds__(512, 1) void gemm_xs_kernel(int M, int N, const cha
       if (!(XS_ABL & 4))
         __builtin_amdgcn_raw_buffer_store_b128(d, rc, coff + 2 * (c * XS_NC + 32 * bq + 8 * g), 0, 0);
     }
+    return gr < M ? nib : 0u;  // (rows past M: no bits, as the 256-wide kernel leaves them)
+  };
+  // relu-bit image (RB): output (m, n) is bit 8 cb + e of word (g' N/32 + w) 4 + f with
+  // g' = (m / 256) 64 + ((m / 64) & 3) 16 + (m & 15), f = (m / 16) & 3 and
+  // n = 256 (w / 8) + 128 ((w / 4) & 1) + 8 (w & 3) + 32 cb + e. Chunk c (64 columns) fills bytes
+  // cb = bq + 2 (c & 1) of words w = 8 (c / 4) + 4 ((c / 2) & 1) + g, g < 4: one 16-bit half per
+  // (row, g), bits e = 4 hh + i from lane (lr, hh). Lane hh stores the halves of g = 2 hh, 2 hh + 1.
+  auto store_bits = [&](uint32_t n0, uint32_t n1, int c, const __amdgpu_buffer_rsrc_t& rb) {
+    const int rb_row = ((((wave >> 1) * 16 + (lr & 15)) * (N / 32)) * 4 + (wave & 1) * 2 + (lr >> 4)) * 4;
+    const uint32_t mine = n0 | (n1 << 16);
+    const auto sw = __builtin_amdgcn_permlane32_swap(mine, mine, false, false);
+    const uint32_t lo = sw[0], hi = sw[1];  // lane (lr, 0)'s and lane (lr, 1)'s bits in every lane
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int g = 2 * hh + k;
+      const uint32_t b0 = ((lo >> (4 * g)) & 15u) | (((hi >> (4 * g)) & 15u) << 4);
+      const uint32_t b1 = ((lo >> (16 + 4 * g)) & 15u) | (((hi >> (16 + 4 * g)) & 15u) << 4);
+      const int w = 8 * (c >> 2) + 4 * ((c >> 1) & 1) + g;
+      __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(b0 | (b1 << 8)), rb,
+                                            rb_row + w * 16 + 2 * (c & 1), 0, 0);
+    }
   };
   // one chunk: wait + barrier, the ring DMA two chunks ahead, the MFMAs, the epilogue. REFILL
   // (the panel's last chunk when the range continues): each X unit is reloaded with the next
   // panel's as soon as its MFMAs have issued, so the next panel's X streams in under this chunk's
   // MFMAs and epilogue instead of with the chunk loop stopped.
-  auto chunk = [&](int j, int c, int panel, const __amdgpu_buffer_rsrc_t& rc, auto refill_tag,
+  constexpr int SC = RB ? 6 : 4;  // stores per lane per chunk
+  auto chunk = [&](int j, int c, int panel, const __amdgpu_buffer_rsrc_t& rc,
+                   const __amdgpu_buffer_rsrc_t& rb, auto refill_tag,
                    const __amdgpu_buffer_rsrc_t& rx_next) {
     constexpr bool REFILL = decltype(refill_tag)::value;
-    // chunk j landed: younger than its pieces are the last two chunks' 4 stores each and chunk
+    // chunk j landed: younger than its pieces are the last two chunks' SC stores each and chunk
     // j + 1's pieces (exact: every vm op is unconditional; X loads are drained at each panel
     // start); then publish it. Every wave is then past chunk j - 1's fragment reads, so its slot
     // takes chunk j + 2.
-    xs_wait_vm(j < 2 ? 0 : 8 + (j + 1 < nu ? pw : 0));
+    xs_wait_vm(j < 2 ? 0 : 2 * SC + (j + 1 < nu ? pw : 0));
     asm volatile("s_barrier" ::: "memory");
     if (j + 2 < nu && !(XS_ABL & 1)) issue(j + 2);
     const char* slot = ring + (j % 3) * SLOT;
@@ -266,10 +298,12 @@ __global__ __launch_bounds__(512, 1) void gemm_xs_kernel(int M, int N, const cha
       // 32-byte W fragments took 96 registers)
       if constexpr (F8) asm volatile("" ::: "memory");
     }
+    uint32_t nb[2];
 #pragma unroll
     for (int bq = 0; bq < 2; ++bq)
-      epilogue(acc[bq], bq, c, panel, rc, reinterpret_cast<const float*>(aux[j % 3][0]),
-               reinterpret_cast<const float*>(aux[j % 3][1]));
+      nb[bq] = epilogue(acc[bq], bq, c, panel, rc, reinterpret_cast<const float*>(aux[j % 3][0]),
+                        reinterpret_cast<const float*>(aux[j % 3][1]));
+    if constexpr (RB) store_bits(nb[0], nb[1], c, rb);
   };
 
   issue(0);
@@ -289,12 +323,18 @@ __global__ __launch_bounds__(512, 1) void gemm_xs_kernel(int M, int N, const cha
     const int c_end = min(u1 - panel * nc, nc);
     // the range continues into the next panel (fp8: no refill under the last chunk — the
     // second set of live fragments exceeds the 256 registers; the panel start waits instead)
-    const bool more = !F8 && u1 > (panel + 1) * nc;
+    const bool more = !F8 && !RB && u1 > (panel + 1) * nc;
     const __amdgpu_buffer_rsrc_t rc = rsrc(C, panel, ldc * 2);
     const __amdgpu_buffer_rsrc_t rxn = rsrc(X, more ? panel + 1 : panel, ldxb);
-    for (int c = c_first; c < c_end - (more ? 1 : 0); ++c, ++j) chunk(j, c, panel, rc, std::false_type{}, rxn);
+    // the panel's 64 x N/32 relu-bit words (the image has a word row for every row of the last
+    // panel, also those past M)
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+        RB ? reinterpret_cast<char*>(e.relu_bits) + (int64_t)panel * N * 32 : reinterpret_cast<char*>(C),
+        (short)0, RB ? N * 32 : 0, 0x00020000);
+    for (int c = c_first; c < c_end - (more ? 1 : 0); ++c, ++j)
+      chunk(j, c, panel, rc, rb, std::false_type{}, rxn);
     if (more) {
-      chunk(j, c_end - 1, panel, rc, std::true_type{}, rxn);
+      chunk(j, c_end - 1, panel, rc, rb, std::true_type{}, rxn);
       ++j;
     } else if (j < nu) {
       load_x(panel + 1);
@@ -315,7 +355,9 @@ bool xs_shape_ok(int M, int N, int K, bool f8, int64_t lda, int64_t ldb, int64_t
          (lda * esz) % 16 == 0 && (ldb * esz) % 16 == 0 && ldc % 8 == 0 && lda >= K && ldb >= K &&
          ldc >= N && (int64_t)XS_ROWS * std::max(lda * esz, ldc * 2) < 0x7fffffff &&
          (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 == 0) &&
-         (!e.bias || (uintptr_t)e.bias % 16 == 0) && (!f8 || (e.sa && e.sb && (uintptr_t)e.sb % 16 == 0));
+         (!e.bias || (uintptr_t)e.bias % 16 == 0) && (!f8 || (e.sa && e.sb && (uintptr_t)e.sb % 16 == 0)) &&
+         (!e.relu_bits || (!f8 && N % 256 == 0 && (int64_t)N * 32 < 0x7fffffff &&
+                           (uintptr_t)e.relu_bits % 16 == 0));
 }
 
 int xs_launch(int M, int N, int K, bool f8, const void* X, int64_t lda, const void* W, int64_t ldb,
@@ -334,6 +376,9 @@ int xs_launch(int M, int N, int K, bool f8, const void* X, int64_t lda, const vo
   if (f8)
     hipLaunchKernelGGL(gemm_xs_kernel<true>, dim3(grid), dim3(512), 0, stream, M, N, (const char*)X,
                        lda * esz, (const char*)W, ldb * esz, (bf16_t*)C, ldc, e, n_units);
+  else if (e.relu_bits)
+    hipLaunchKernelGGL((gemm_xs_kernel<false, true>), dim3(grid), dim3(512), 0, stream, M, N,
+                       (const char*)X, lda * esz, (const char*)W, ldb * esz, (bf16_t*)C, ldc, e, n_units);
   else
     hipLaunchKernelGGL(gemm_xs_kernel<false>, dim3(grid), dim3(512), 0, stream, M, N, (const char*)X,
                        lda * esz, (const char*)W, ldb * esz, (bf16_t*)C, ldc, e, n_units);

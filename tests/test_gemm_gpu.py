@@ -268,3 +268,36 @@ def test_activation_stationary_kernel(dev, M, N, bias):
     assert bool((out[M:] == 7.0).all())
     ref = a.float() @ w.float().t() + (b if b is not None else 0.0)
     _close_bf16(out[:M], ref)
+
+
+@pytest.mark.parametrize("M,row_off", [(141312, 0), (33001, 7 * 33001)])
+def test_activation_stationary_relu_bits(dev, M, row_off):
+    """The step's MLP up-projection on gemm_xs_kernel<bf16, RB> (reference attention.py:20-39
+    MLPBlock: Dense_0 + bias, relu, dropout; mmt_gemm's own dispatch) against gemm_nt256_kernel
+    forced by variant 5: bf16 output AND the relu-bit image (include/mmt_api.h layout, every word
+    including the padded rows of the last 256-row panel) bit-identical; the image equals
+    (stored h > 0)."""
+    from multi_modal_transformers_tokenmerge_amd import _C
+    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
+    from tests.test_gemm_nt256_gpu import _bits_to_mask
+    N, K = 1536, 384
+    g = torch.Generator().manual_seed(M + 5)
+    y, w1 = _mk((M, K), dev, g), _mk((N, K), dev, g)
+    bias = (torch.randn(N, generator=g) * 0.5).to(dev)
+    rng = torch.tensor([13, 6], dtype=torch.int32, device=dev)
+    rows = -(-M // 256) * 256
+    outs = []
+    for v in (-1, 5):
+        bits = torch.full((rows, N // 32), -1, dtype=torch.int32, device=dev)
+        _C.call("mmt_gemm_set_variant", v)
+        try:
+            h = Kn.gemm(y, w1, False, True, bias=bias, act=Kn.ACT_RELU, rng=rng, drop_layer=3,
+                        drop_site=2, keep_prob=0.9, drop_row_offset=row_off, relu_bits=bits)
+        finally:
+            _C.call("mmt_gemm_set_variant", -1)
+        outs.append((h, bits))
+    torch.cuda.synchronize()
+    (h1, b1), (h2, b2) = outs
+    assert torch.equal(h1, h2)
+    assert torch.equal(b1, b2)
+    torch.testing.assert_close(_bits_to_mask(b1, M, N), h1.float() > 0, rtol=0, atol=0)
