@@ -1569,31 +1569,19 @@ constexpr int TN_BM = 256, TN_BN = 192, TN_NT = 512;
 // top of each K-step). dma16_asm: common.h.
 // BM: tile height, 256 (8 waves of 64 x 96: 2 x 3 MFMA blocks) or 384 (waves of 96 x 96: 3 x 3
 // blocks; 72 KB per K-step for 1.5x the products of the 56 KB 256-row step — the kernel is bound
-// by its DMA rate, profiles/r03_tn_ablation.txt). KS: tokens per K-step (64, or 32 for a deeper
-// ring); NS: LDS stages, the DMA running NS - 1 K-steps ahead (2 x 64 or 4 x 32 at BM 384: the
-// same 144 KB). The stage's 1-KB DMA pieces are dealt round-robin over the 8 waves (wave w issues
-// pieces w, w + 8, ...: 9 each at 384 x 64, 5 / 4 at 384 x 32).
-template <int V>
-__device__ __forceinline__ void tn_wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(V) : "memory");
-}
-template <int BM, int KS = 64, int NS = 2>
+// by its DMA rate, profiles/r03_tn_ablation.txt).
+template <int BM>
 __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
     int64_t ldb, float* __restrict__ slab, int split_k, int k_chunk, int tiles_n) {
   static_assert(BM == 256 || BM == 384, "tile height");
-  static_assert((KS == 64 || KS == 32) && NS >= 2, "ring");
   constexpr int MB = BM / 128;                                      // 32-row MFMA blocks per wave
   constexpr int A_ROWB = BM * 2, B_ROWB = TN_BN * 2;                // bytes per k-row
   constexpr int A_CH = A_ROWB / 16;                                 // 16-B chunks per A k-row
-  constexpr int A_BYTES = KS * A_ROWB, B_BYTES = KS * B_ROWB, STAGE = A_BYTES + B_BYTES;
-  constexpr int PA = A_BYTES / 1024, PT = STAGE / 1024;             // A pieces, all pieces
-  constexpr int G = (PT + 7) / 8;                                   // pieces of wave 0
-  constexpr int GLO = PT / 8;                                       // pieces of wave 7
-  static_assert(STAGE % 1024 == 0 && NS * STAGE <= 160 * 1024, "LDS");
-  static_assert((NS - 2) * G < 64, "vmcnt");
-  constexpr int KSL = KS / 16;                                      // k-slices per K-step
-  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+  constexpr int A_BYTES = 64 * A_ROWB, B_BYTES = 64 * B_ROWB, STAGE = A_BYTES + B_BYTES;
+  constexpr int GA = A_BYTES / 1024 / 8, GB = B_BYTES / 1024 / 8;   // DMA pieces per wave (4 / 6 + 3)
+  constexpr int G = GA + GB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1, hl = lane >> 5;
@@ -1603,8 +1591,7 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
   const int tm = t / tiles_n;
   const int m0 = tm * BM, n0 = (t - tm * tiles_n) * TN_BN;
   const int kbeg = z * k_chunk, kend = min(K, kbeg + k_chunk);
-  const int nk = max(0, (kend - kbeg + KS - 1) / KS);
-  const bool full = wave < PT - 8 * GLO;  // this wave issues G pieces (else GLO)
+  const int nk = max(0, (kend - kbeg + 63) / 64);
   // chunk swizzles (16-B chunks of a k-row): A rows are 512 B (every row starts on bank 0), so
   // the 4 k-rows of a transposed read take 4 disjoint 64-B slots: c ^ 4 (r & 3); B rows are
   // 384 B (odd rows start half a bank window on), c ^ 2 (r & 3) keeps them apart (simulated for
@@ -1615,44 +1602,39 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
   // per-lane source offsets (bytes from the K-step's panel base) of this wave's DMA pieces
   int voff[G];
 #pragma unroll
-  for (int i = 0; i < G; ++i) {
-    const int j = wave + 8 * i;  // stage piece (past PT for the short waves' last: unused)
-    if (j < PA) {  // A piece j: 1 KB of the [KS][BM] image (A_CH chunks per k-row; 768-B rows
-                   // also start on bank 0: the same swizzle)
-      const int e = j * 64 + lane, row = e / A_CH, c = (e % A_CH) ^ swA(row);
-      voff[i] = row * (int)(lda * 2) + c * 16;
-    } else {       // B piece j - PA: 1 KB of the [KS][192] image (24 chunks per k-row)
-      const int e = (j - PA) * 64 + lane, row = e / 24, c = (e % 24) ^ swB(row);
-      voff[i] = row * (int)(ldb * 2) + c * 16;
+  for (int p = 0; p < G; ++p) {
+    if (p < GA) {  // A piece j = wave * GA + p: 1 KB of the [64][BM] image (A_CH chunks per k-row;
+                   // 768-B rows also start on bank 0: the same swizzle)
+      const int j = wave * GA + p, e = j * 64 + lane, row = e / A_CH, c = (e % A_CH) ^ swA(row);
+      voff[p] = row * (int)(lda * 2) + c * 16;
+    } else {       // B piece j: 1 KB of the [64][192] image (24 chunks per k-row)
+      const int j = wave * GB + (p - GA), e = j * 64 + lane, row = e / 24, c = (e % 24) ^ swB(row);
+      voff[p] = row * (int)(ldb * 2) + c * 16;
     }
   }
   // buffer ranges end at row K (zeros past it); the panel base moves with the K-step
-  auto piece = [&](int kt, int st, int i) {
-    const int j = wave + 8 * i;
+  auto piece = [&](int kt, int st, int p) {
 #if MMT_TN_ABL == 1 || MMT_TN_ABL == 4  // ablation builds (tools/build_abl_tn.sh): no DMA
     if (K > 0) return;
 #endif
 #if MMT_TN_ABL == 6  // ablation: B pieces only
-    if (j < PA) return;
+    if (p < GA) return;
 #endif
 #if MMT_TN_ABL == 7  // ablation: A pieces only
-    if (j >= PA) return;
+    if (p >= GA) return;
 #endif
 #if MMT_TN_ABL == 5  // ablation: every split reads the first K chunk (L2-shared)
-    const int k0 = kt * KS;
+    const int k0 = kt * 64;
 #else
-    const int k0 = kbeg + kt * KS;
+    const int k0 = kbeg + kt * 64;
 #endif
     char* S0 = smem + st * STAGE;
-    if (j < PA)
-      dma16_asm(A + (int64_t)k0 * lda + m0, ((int64_t)(K - k0) * lda - m0) * 2, S0 + j * 1024, voff[i]);
+    if (p < GA)
+      dma16_asm(A + (int64_t)k0 * lda + m0, ((int64_t)(K - k0) * lda - m0) * 2,
+                S0 + (wave * GA + p) * 1024, voff[p]);
     else
-      dma16_asm(B + (int64_t)k0 * ldb + n0, ((int64_t)(K - k0) * ldb - n0) * 2, S0 + j * 1024, voff[i]);
-  };
-  auto issue = [&](int kt, int st) {  // G or GLO vm ops of this wave
-#pragma unroll
-    for (int i = 0; i < G; ++i)
-      if (i < GLO || full) piece(kt, st, i);
+      dma16_asm(B + (int64_t)k0 * ldb + n0, ((int64_t)(K - k0) * ldb - n0) * 2,
+                S0 + A_BYTES + (wave * GB + (p - GA)) * 1024, voff[p]);
   };
 
   floatx16 acc[MB][3];
@@ -1681,30 +1663,24 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
     return __builtin_bit_cast(bf16x8, v);
   };
 
-  // prologue: K-steps 0 .. NS - 2
+  if (nk > 0)
 #pragma unroll
-  for (int q = 0; q < NS - 1; ++q)
-    if (q < nk) issue(q, q);
+    for (int p = 0; p < G; ++p) piece(0, 0, p);
   for (int kt = 0; kt < nk; ++kt) {
-    const int st = kt % NS;
-    // K-step kt landed: younger than its DMA are the K-steps kt + 1 .. kt + NS - 2 issued (the
-    // loop issues nothing else), then publish it; every wave is past K-step kt - 1's reads, so
-    // its stage takes K-step kt + NS - 1
-    const int younger = min(NS - 2, nk - 1 - kt);
-    if (younger <= 0) tn_wait_vm<0>();
-    else if (younger == 1) { if (full) tn_wait_vm<G>(); else tn_wait_vm<GLO>(); }
-    else if constexpr (NS >= 4) {
-      if (younger == 2) { if (full) tn_wait_vm<2 * G>(); else tn_wait_vm<2 * GLO>(); }
-      else { if (full) tn_wait_vm<(NS - 2) * G>(); else tn_wait_vm<(NS - 2) * GLO>(); }
-    }
-    asm volatile("s_barrier" ::: "memory");
+    const int st = kt & 1;
+    // this K-step's DMA is the only memory operation in flight
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    const bool nxt = kt + 1 < nk;
     const char* As = smem + st * STAGE;
     const char* Bs = As + A_BYTES;
-    // the DMA of K-step kt + NS - 1 (into the stage K-step kt - 1 used), issued before any MFMA so
-    // it has NS - 1 K-steps to land (spread over the k-slices, the last pieces of a two-stage
-    // ring were issued just before the next barrier's wait: 191.7 -> 182.8 us at the MLP Dense_0
-    // dW shape)
-    if (kt + NS - 1 < nk) issue(kt + NS - 1, (kt + NS - 1) % NS);
+    // the next K-step's DMA into the other stage (free since this barrier), all of it before any
+    // MFMA so every piece has the whole K-step to land (spread over the k-slices, the last pieces
+    // were issued just before the next barrier's wait): interleaved on one box
+    // (tools/gpu_wgrad_ab2.sh) MLP Dense_0 dW 187-190 -> 181-183 us, QKV 158 -> 152-153 us,
+    // Dense_1 191-194 -> 183-184 us; step 15,924 -> 15,970 samples/s
+    if (nxt)
+#pragma unroll
+      for (int p = 0; p < G; ++p) piece(kt + 1, st ^ 1, p);
     // fragments one k-slice ahead: slice ks + 1's reads are in flight under slice ks's MFMAs (every
     // wave reaches this point together after the barrier, so the partner wave cannot cover them)
     bf16x8 af[2][MB], bfr[2][3];
@@ -1713,12 +1689,12 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
 #pragma unroll
     for (int b = 0; b < 3; ++b) bfr[0][b] = frag(Bs, B_ROWB, wn * 96 + b * 32, 0);
 #pragma unroll
-    for (int ks = 0; ks < KSL; ++ks) {
+    for (int ks = 0; ks < 4; ++ks) {
       const int cu = ks & 1;
 #if MMT_TN_ABL == 3 || MMT_TN_ABL == 4  // ablation: fragments of k-slice 0 reused (no further reads)
-      if (ks < KSL - 1 && K < 0) {
+      if (ks < 3 && K < 0) {
 #else
-      if (ks < KSL - 1) {
+      if (ks < 3) {
 #endif
 #pragma unroll
         for (int a = 0; a < MB; ++a) af[cu ^ 1][a] = frag(As, A_ROWB, wm * (32 * MB) + a * 32, ks + 1);
@@ -2927,12 +2903,7 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     static const int g_tn_bm = getenv("MMT_TN_BM") ? atoi(getenv("MMT_TN_BM")) : 384;
     const bool tall = g_tn_bm == 384 && M % 384 == 0 && g_variant != 9;
     const int work = ((M + (tall ? 383 : 255)) / (tall ? 384 : 256)) * tn * split_k;
-    // MMT_TN_DEEP=1: the 384-row tiles on 32-token K-steps through a 4-stage ring (benchmarking)
-    static const int g_tn_deep = getenv("MMT_TN_DEEP") ? atoi(getenv("MMT_TN_DEEP")) : 0;
-    if (tall && g_tn_deep)
-      hipLaunchKernelGGL((gemm_tn_dma_kernel<384, 32, 4>), dim3(work), dim3(TN_NT), 0, s, M, N, K,
-                         (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
-    else if (tall)
+    if (tall)
       hipLaunchKernelGGL(gemm_tn_dma_kernel<384>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
                          (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
     else
