@@ -170,7 +170,9 @@ def kernel_probes(model, B, reps=20):
     h = torch.empty((M, Mh), dtype=torch.bfloat16, device=dev)
     hb = (torch.empty((-(-M // 256) * 256, Mh // 32), dtype=torch.int32, device=dev)
           if K.gemm_bits_supported(M, Mh, D) and not blk.mlp.dense.fp8 else None)
-    add("mlp_up_fwd", PROBE_KERNEL if D == 384 else NT256_KERNEL,
+    up_kernel = ("gemm_xs_kernel<true" if blk.mlp.dense.fp8 else
+                 PROBE_KERNEL if D == 384 else NT256_KERNEL)  # fp8: e4m3 on the XS kernel (+ quant)
+    add("mlp_up_fwd", up_kernel,
         lambda: blk.mlp.dense.fwd(y1, out=h, act=K.ACT_RELU, rng=rng, drop_layer=0, drop_site=2,
                                   keep_prob=0.9, relu_bits=hb),
         "mfma", 2.0 * M * Mh * D, f"M={M} N={Mh} K={D}, 2MNK (+ bias, relu, dropout, relu bits)",
@@ -182,7 +184,7 @@ def kernel_probes(model, B, reps=20):
         yq, sy = K.quant_rows_fp8(y1)
         w8 = blk.mlp.dense.w
         b8 = blk.mlp.dense.b.data
-        add("mlp_up_fwd_fp8", "gemm_fp8_nt_kernel",
+        add("mlp_up_fwd_fp8", "gemm_xs_kernel<true",
             lambda: K.gemm_fp8(yq, sy, w8.q8, w8.q8_scale, out=h, bias=b8, act=K.ACT_RELU, rng=rng,
                                drop_layer=0, drop_site=2, keep_prob=0.9),
             "mfma8", 2.0 * M * Mh * D, f"M={M} N={Mh} K={D}, 2MNK in e4m3 (+ bias, relu, dropout; "
