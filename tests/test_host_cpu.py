@@ -266,3 +266,20 @@ def test_step_fixtures_randomness_and_position_kats():
     assert (rte[0] == 3 + 8 * (np.arange(256) % 16)).all() and (cte[0] == 3 + 8 * (np.arange(256) // 16)).all()
     r2, _ = R.patch_positions(0, 0, 0, 1, 1, 128, 1, 128, train=False)
     assert r2.shape == (1, 16384) and r2[0, 123] == 122
+
+
+def test_wgrad_split_sizing():
+    """layers.split_k_for: the split-K factor of a weight-gradient launch is sized for `wgs`
+    workgroups of the TN kernel's tiles (384 x 192 where n_out % 384 == 0, else 256 x 192) —
+    half the chip (128) by default for the step's side-queue launches, the whole chip (256) for a
+    standalone launch — capped at 64 and at one 256-token chunk per split."""
+    from multi_modal_transformers_tokenmerge_amd.layers import split_k_for, _TN_BM
+    if _TN_BM != 384:
+        pytest.skip("MMT_TN_BM=256 changes the tile")
+    M = 512 * 276
+    assert split_k_for(1536, 384, M) == 16           # 8 tiles: 128 // 8
+    assert split_k_for(1536, 384, M, wgs=256) == 32  # the bench's full-chip probe
+    assert split_k_for(1152, 384, M, wgs=256) == 42  # 6 tiles
+    assert split_k_for(384, 384, M, wgs=256) == 64   # 2 tiles: capped at 64
+    assert split_k_for(384, 384, 1000) == 3          # 1000 // 256 chunks
+    assert split_k_for(4096, 384, M, wgs=256) == 8   # 4096 % 384 != 0: 16 x 2 tiles of 256 x 192
