@@ -249,8 +249,10 @@ int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t lda, const 
  * OCTO-small QKV projection), X [M][ldx], W [N][ldw] bf16, C [M][ldc] bf16, N % 64 == 0, 16-B
  * aligned rows; bias fp32 [N] or NULL. The activation-stationary kernel of csrc/gemm_xs.hip (a
  * 256-row panel of X held in registers while W streams through LDS); mmt_gemm routes its
- * bias-only K = 384 products and mmt_gemm_fp8 its K = 768 bf16-output products (no gate /
- * residual) there itself (reference attention.py:20-37, 41-69 Dense layers). */
+ * K = 384 bf16 products with a bias / alpha / relu / dropout / relu_bits epilogue (M >= 32768;
+ * relu_bits needs N % 256 == 0) and mmt_gemm_fp8 its K = 768 bf16-output products (no gate /
+ * residual / relu_bits) there itself, with bit-identical outputs and bit images (reference
+ * attention.py:20-37, 41-69 Dense layers). */
 int mmt_gemm_xs(int M, int N, int K, const void* X, int64_t ldx, const void* W, int64_t ldw,
                 void* C, int64_t ldc, const float* bias, mmt_stream_t stream);
 
