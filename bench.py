@@ -65,7 +65,7 @@ def algorithmic_flops_per_sample(model) -> float:
     cfg = model.cfg
     D, M = cfg.token_embedding_dim, cfg.mlp_dim
     tr = 0.0
-    for (sets, _, ts, r, prune) in model.layer_sets:
+    for (sets, _, ts, r, prune, _plan) in model.layer_sets:
         L = sets.L
         if prune is None:   # ToMe merges after the out-projection
             Lp = L - r
@@ -134,7 +134,7 @@ def kernel_probes(model, B, reps=20):
     cfg = model.cfg
     dev = model.device
     blk = model.stack.blocks[0]
-    sets, table, ts, r, prune = model.layer_sets[0]
+    sets, table, ts, r, prune, _plan = model.layer_sets[0]
     L = sets.L
     L1 = sum(prune[1]) if prune else L - r
     D, Mh, H = cfg.token_embedding_dim, cfg.mlp_dim, cfg.num_heads
@@ -518,7 +518,7 @@ def main():
         # slabs + combine; ≈ 23 % of kernel time, profiles/r02_b512_kernel_stats_step.csv), at
         # the MLP Dense_0 dW shape; every other probe follows in `kernels`
         top = next((p for p in probes if p["name"] == "mlp_dw"), None)
-        sets0, _, _, r0, pr0 = model.layer_sets[0]
+        sets0, _, _, r0, pr0, _plan0 = model.layer_sets[0]
         M_ = B * (sum(pr0[1]) if pr0 else sets0.L - r0)
         N_, K_ = cfg.mlp_dim, cfg.token_embedding_dim
         if top is None:

@@ -62,8 +62,9 @@ class DiffusionActionHead(Bindable):
         self.attention_pooling = attention_pooling
         dm = spec(denoising_model)
         te = spec(sget(dm, "time_encoder"))
-        if int(sget(dm, "num_blocks", 1)) != 1:
-            raise NotImplementedError("OctoDenoise num_blocks != 1 (the reference configs use 1)")
+        self.num_blocks = int(sget(dm, "num_blocks", 1))
+        if self.num_blocks < 1:
+            raise ValueError("OctoDenoise num_blocks must be >= 1")
         mlp = spec(sget(dm, "mlp_block"))
         self.time_dim_cfg = sget(te, "output_dim")
         self.fourier_init = sget(te, "kernel_init")
@@ -80,7 +81,7 @@ class DiffusionActionHead(Bindable):
     @classmethod
     def create(cls, store: ParamStore, name: str, embedding_dim: int, action_dim: int = 8,
                diffusion_steps: int = 32, time_dim: int | None = None,
-               hidden: int | None = None) -> "DiffusionActionHead":
+               hidden: int | None = None, num_blocks: int = 1) -> "DiffusionActionHead":
         """The head from its dimensions, declared in ``store`` (the Octo model's path)."""
         D = embedding_dim
         T = time_dim or D
@@ -88,7 +89,7 @@ class DiffusionActionHead(Bindable):
         def mlp(h, o):
             return {"_target_": _REF_MLP, "dense": {"_target_": "flax.linen.Dense", "features": h},
                     "dense_out": {"_target_": "flax.linen.Dense", "features": o}}
-        dm = {"_target_": _REF_DENOISE, "num_blocks": 1,
+        dm = {"_target_": _REF_DENOISE, "num_blocks": num_blocks,
               "time_encoder": {"_target_": _REF_FOURIER, "output_dim": T, "mlp_block": mlp(T, T)},
               "mlp_block": mlp(hidden or D, action_dim)}
         return cls(diffusion_steps, None, dm).bind(store, name, D)
@@ -114,6 +115,13 @@ class DiffusionActionHead(Bindable):
         self.d2 = Dense(store, f"{p}/MLPBlock_0/Dense_1", self.hidden, self.A)
         if self.cat_dim % 8:
             raise ValueError("action_dim + time_dim + D must be a multiple of 8 (16-B rows)")
+        # OctoDenoise blocks 1.. (diffusion.py:62-63: a fresh MLPBlock per iteration, Flax names
+        # MLPBlock_{i}) on the previous block's (B, A) output
+        self.extra = [(Dense(store, f"{p}/MLPBlock_{i}/Dense_0", self.A, self.hidden),
+                       Dense(store, f"{p}/MLPBlock_{i}/Dense_1", self.hidden, self.A))
+                      for i in range(1, self.num_blocks)]
+        if self.extra and self.A % 8:
+            raise ValueError("OctoDenoise num_blocks > 1 needs action_dim % 8 == 0 (16-B rows)")
 
     # ------------------------------------------------------------- reference-signature methods
     def _mean_into(self, readouts: torch.Tensor, out: torch.Tensor):
@@ -189,16 +197,33 @@ class DiffusionActionHead(Bindable):
         self.t2.fwd(ht, out=cat[:, self.A:self.A + self.time_dim])
         hd = self.d1.fwd(cat, act=K.ACT_RELU)
         pred = self.d2.fwd(hd, out_mode=K.OUT_F32)
+        pred, chain = self._extra_fwd(pred)
         loss = torch.empty(1, dtype=torch.float32, device=dev)
         dpred = torch.empty((B, self.A), dtype=torch.bfloat16, device=dev)
         _C.call("mmt_diffusion_loss", _C.ptr(pred), pred.stride(0), _C.ptr(eps), B, self.A, 1.0,
                 _C.ptr(loss), _C.ptr(dpred), _C.stream_ptr())
-        return loss, dict(cat=cat, feats=feats, ht=ht, hd=hd, dpred=dpred, t=t, eps=eps, pred=pred)
+        return loss, dict(cat=cat, feats=feats, ht=ht, hd=hd, dpred=dpred, t=t, eps=eps, pred=pred,
+                          chain=chain)
+
+    def _extra_fwd(self, pred):
+        """OctoDenoise blocks 1.. on the block-0 output pred (B, A) fp32: each input cast to bf16
+        (the GEMM operand), Dense -> relu -> Dense. Returns (final pred, [(x, h) per block])."""
+        chain = []
+        for d1, d2 in self.extra:
+            x = K.cast_f32_bf16(pred, torch.empty(pred.shape, dtype=torch.bfloat16, device=pred.device))
+            h = d1.fwd(x, act=K.ACT_RELU)
+            pred = d2.fwd(h, out_mode=K.OUT_F32)
+            chain.append((x, h))
+        return pred, chain
 
     def loss_backward(self, sv: dict) -> torch.Tensor:
         """Returns d(readout mean) (B, D) bf16 view."""
         B = sv["cat"].shape[0]
-        dzd = self.d2.bwd(sv["dpred"], sv["hd"], gate=sv["hd"], gate_scale=1.0)
+        dpred = sv["dpred"]
+        for (d1, d2), (x, h) in reversed(list(zip(self.extra, sv.get("chain") or []))):
+            dz = d2.bwd(dpred, h, gate=h, gate_scale=1.0)     # relu backward in the dX epilogue
+            dpred = d1.bwd(dz, x)                              # bf16 (B, A): the previous output's
+        dzd = self.d2.bwd(dpred, sv["hd"], gate=sv["hd"], gate_scale=1.0)
         dcat = self.d1.bwd(dzd, sv["cat"])
         dtemb = dcat[:, self.A:self.A + self.time_dim]
         dzt = self.t2.bwd(dtemb, sv["ht"], gate=sv["ht"], gate_scale=1.0)
@@ -233,7 +258,7 @@ class DiffusionActionHead(Bindable):
         ht = self.t1.fwd(feats, act=K.ACT_RELU)
         self.t2.fwd(ht, out=cat[:, self.A:self.A + self.time_dim])
         hd = self.d1.fwd(cat, act=K.ACT_RELU)
-        return self.d2.fwd(hd, out_mode=K.OUT_F32)
+        return self._extra_fwd(self.d2.fwd(hd, out_mode=K.OUT_F32))[0]
 
     # ------------------------------------------------------------------------- predict_action
     def sampler_coef(self, device) -> torch.Tensor:
@@ -276,6 +301,8 @@ class DiffusionActionHead(Bindable):
             raise ValueError(f"readout_mean must be bf16 (B, {self.D}) with unit inner stride")
         if self.A != 8:
             raise ValueError("the reference sampler hard-codes an 8-dim action (diffusion.py:200)")
+        if self.extra:
+            return self._predict_action_loop(readout_mean, rng, sample_offset, z, return_noise)
         B = readout_mean.shape[0]
         dev = readout_mean.device
         if z is not None and (tuple(z.shape) != (B, self.A) or z.dtype != torch.float32
@@ -296,3 +323,31 @@ class DiffusionActionHead(Bindable):
                 _C.ptr(self.d2.w.bf16), _C.ptr(self.d2.b.data), _C.ptr(self.sampler_coef(dev)),
                 _C.ptr(z), self.hidden, _C.ptr(actions), _C.ptr(z_out), _C.stream_ptr())
         return (actions, z_out) if return_noise else actions
+
+    def _predict_action_loop(self, readout_mean, rng, sample_offset, z, return_noise):
+        """predict_action for OctoDenoise num_blocks > 1 (the fused one-launch sampler holds one
+        MLPBlock in registers): the reference's 32-step scan (:146-209) as a loop of
+        predict_denoise_term_mean launches and the clipped update on the device; the initial
+        sample z comes from the fused sampler's own counter-stream draw (a one-step launch), so
+        both paths start from the same z. The noisy sample enters the denoiser as its bf16 GEMM
+        operand (the fused kernel keeps it fp32)."""
+        B, A, dev = readout_mean.shape[0], self.A, readout_mean.device
+        if z is None:
+            z = torch.empty((B, A), dtype=torch.float32, device=dev)
+            T = self.time_dim
+            temb = self.time_embeddings(dev)
+            w1 = self.d1.w.bf16
+            Q = K.gemm(temb, w1[:, A:A + T], trans_b=True, bias=self.d1.b.data, out_mode=K.OUT_F32)
+            P = K.gemm(readout_mean, w1[:, A + T:], trans_b=True, out_mode=K.OUT_F32)
+            scratch = torch.empty((B, A), dtype=torch.float32, device=dev)
+            _C.call("mmt_diffusion_sample", _C.ptr(rng), B, A, 1, sample_offset, _C.ptr(P),
+                    P.stride(0), _C.ptr(Q), Q.stride(0), _C.ptr(w1), w1.stride(0),
+                    _C.ptr(self.d2.w.bf16), _C.ptr(self.d2.b.data), _C.ptr(self.sampler_coef(dev)),
+                    None, self.hidden, _C.ptr(scratch), _C.ptr(z), _C.stream_ptr())
+        coef = self.sampler_coef(dev)
+        x = z.clone()
+        for t in range(self.steps - 1, -1, -1):
+            tt = torch.full((B,), t, dtype=torch.int32, device=dev)
+            eps = self.predict_denoise_term_mean(readout_mean, tt, x)
+            x = torch.clamp(coef[t, 0] * (x - coef[t, 1] * eps) + coef[t, 2] * z, -5.0, 5.0)
+        return (x, z) if return_noise else x

@@ -45,14 +45,22 @@ class LayerCtx:
     layer: int
     sets: LayerSets                # token-set table entering the block
     table: K.SetTable
-    tome_set: int = -1             # index of the merged token set, -1 = no merge
-    r: int = 0
+    tome_set: int = -1             # index of the merged token set, -1 = no merge, -2 = several
+    r: int = 0                     # tokens merged away in this block (over every merged set)
     # top-k pruning: (((start, num_tokens) per set), (k per set)) or None
     prune: Optional[tuple] = None
     train: bool = True
     rng: Optional[torch.Tensor] = None
     sample_offset: int = 0         # global index of this rank's first sample (RNG counters)
-    tome_forced: Optional[tuple] = None  # injected (unm, src, dst) in place of the matching (tests)
+    tome_forced: Optional[tuple] = None  # injected (unm, src, dst) in place of the matching (tests;
+    #                                      a list of triples, one per merged set, with several)
+    tome_plan: tuple = ()          # ((set index, r), ...): one ToMe match + merge per compressed set
+
+    def tome_sets(self):
+        """The merged sets as ((set index, r), ...)."""
+        if self.tome_plan:
+            return tuple(self.tome_plan)
+        return ((self.tome_set, self.r),) if self.r > 0 else ()
 
 
 _SIDE = {}
@@ -235,7 +243,7 @@ class Encoder1DBlock(Bindable):
         self._ensure(inputs.device, int(inputs.shape[-1]))
         ctx = LayerCtx(layer=layer, sets=None, table=set_table_of(mask, inputs.shape[1]),
                        train=train, rng=rng, sample_offset=sample_offset)
-        if train and (self.rate > 0 or self.attn_rate > 0) and rng is None:
+        if train and (self.rate > 0 or self.attn_rate > 0 or self.mlp.rate > 0) and rng is None:
             raise ValueError("Encoder1DBlock(train=True) needs the dropout rng (rng=)")
         x = inputs.float().contiguous()
         return _EncoderBlockFn.apply(x, self, ctx), None
@@ -270,9 +278,13 @@ class Encoder1DBlock(Bindable):
             return (train and not self.mlp.dense.fp8 and _RELU_BITS
                     and K.gemm_bits_supported(rows, Mh, D))
         kbits = None
+        plan = ctx.tome_sets()
+        multi = len(plan) > 1
         if ctx.r > 0:  # ToMe matching needs only K: it runs beside attention + out-projection
-            s0, t = ctx.sets.starts[ctx.tome_set], ctx.sets.lens[ctx.tome_set]
-            metric = qkv.view(B, L, 3, H, Dh)[:, s0:s0 + t, 1]     # (B, t, H, Dh): sum_h K
+            metrics = []
+            for si, _ in plan:
+                s0, t = ctx.sets.starts[si], ctx.sets.lens[si]
+                metrics.append(qkv.view(B, L, 3, H, Dh)[:, s0:s0 + t, 1])  # (B, t, H, Dh): sum_h K
             L2p = L - ctx.r  # the merged length (no pruning in this block)
             if (_KEEP_BITS and train and kpm < 1.0 and ctx.prune is None and Mh % 256 == 0
                     and relu_bits_ok(B * L2p)):
@@ -280,7 +292,12 @@ class Encoder1DBlock(Bindable):
                                     device=x.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                tome_idx = ctx.tome_forced if ctx.tome_forced is not None else K.tome_match(metric, ctx.r)
+                if ctx.tome_forced is not None:
+                    tome_idx = ctx.tome_forced
+                elif multi:
+                    tome_idx = [K.tome_match(m, r) for m, (_, r) in zip(metrics, plan)]
+                else:
+                    tome_idx = K.tome_match(metrics[0], ctx.r)
                 if kbits is not None:
                     K.gemm_dropout_keep_bits(ctx.rng, ctx.layer, DROP_MLP_HIDDEN, B * L2p, Mh, kpm,
                                              ctx.sample_offset * L2p, out=kbits)
@@ -304,9 +321,22 @@ class Encoder1DBlock(Bindable):
                           out_mode=K.OUT_F32, **drop(DROP_ATTN_OUT, Lo))
         x1 = x1.view(B, Lo, D)
         tome = None
+        tome_sets = []
         new_size = size
         ln1_done = None
-        if ctx.r > 0:
+        if ctx.r > 0 and multi:
+            # several merged sets: one merge per set, the last set first so the earlier sets'
+            # starts stay valid; sizes carried per set ({set index: (B, t) sizes}); LayerNorm_1
+            # on the merged sequence after them (unfused)
+            main.wait_stream(side)
+            sizes = size if isinstance(size, dict) else {}
+            new_size = {}
+            for (si, r), (unm, src, dst) in sorted(zip(plan, tome_idx), key=lambda z: -z[0][0]):
+                s0, t = ctx.sets.starts[si], ctx.sets.lens[si]
+                x1, ns, pos = K.tome_merge_fwd(x1, s0, t, r, unm, src, dst, size_in=sizes.get(si))
+                new_size[si] = ns
+                tome_sets.append((s0, t, r, pos, sizes.get(si), ns, unm, src, dst, si))
+        elif ctx.r > 0:
             main.wait_stream(side)
             unm, src, dst = tome_idx
             if x1.dtype == torch.float32 and Lo - ctx.r <= 512:
@@ -317,7 +347,8 @@ class Encoder1DBlock(Bindable):
                 ln1_done = (y1, mu1, rs1)
             else:
                 x1, new_size, pos = K.tome_merge_fwd(x1, s0, t, ctx.r, unm, src, dst, size_in=size)
-            tome = (s0, t, ctx.r, pos, size, new_size, unm, src, dst)
+            tome = (s0, t, ctx.r, pos, size, new_size, unm, src, dst, plan[0][0])
+            tome_sets = [tome]
         L2 = x1.shape[1]
         y1, mu1, rs1 = ln1_done if ln1_done is not None else self.ln1.fwd(x1)
         # the relu gate of the backward as 1 bit per hidden unit where the launch supports it
@@ -333,7 +364,10 @@ class Encoder1DBlock(Bindable):
                                     **drop(DROP_MLP_OUT, L2, kpm))
         saved = dict(x=x, y0=y0, mu0=mu0, rs0=rs0, qkv=qkv, o=o, o_in=o_in, lse=lse, bits=bits,
                      x1=x1, y1=y1, mu1=mu1, rs1=rs1, h=h, hbits=hbits, tome=tome, prune=prune,
-                     kp=kp, kpm=kpm, kpa=kpa)
+                     kp=kp, kpm=kpm, kpa=kpa,
+                     # every merge of the block in the order applied (one set: [tome]; several:
+                     # the last set first, `tome` then None)
+                     tome_sets=tome_sets)
         return x2.view(B, L2, D), saved, new_size
 
     # ----------------------------------------------------------------------------- backward
@@ -378,8 +412,8 @@ class Encoder1DBlock(Bindable):
             dzo = dzo.view(B * Lo, D)
         else:
             dx1 = self.ln1.bwd(dy1.view(B, L2, D), sv["x1"], sv["mu1"], sv["rs1"], addend=dx2)
-            if sv["tome"] is not None:
-                s0, t, r, pos, size_in, size_out = sv["tome"][:6]
+            for tm in reversed(sv.get("tome_sets") or []):  # the merges undone in reverse order
+                s0, t, r, pos, size_in, size_out = tm[:6]
                 dx1 = K.tome_merge_bwd(dx1, s0, t, r, pos, size_in, size_out)
             dx1f = dx1.reshape(B * Lo, D)
             dzo = K.dropout_bwd(dx1f, rng, ctx.layer, DROP_ATTN_OUT, kp,

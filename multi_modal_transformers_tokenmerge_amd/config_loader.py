@@ -250,6 +250,7 @@ def octo_config_from_yaml(cfg: dict, name: str = "yaml"):
         num_observation_blocks=int(cfg.get("num_observation_blocks", 1)),
         action_space_dim=action_dim,
         diffusion_steps=int(diff.get("diffusion_steps", 32)),
+        denoise_blocks=int(den.get("num_blocks", 1)),
         action_heads=tuple(head_names),
         num_bins=int(heads_cfg.get("num_bins", 256)),
         max_action=float(heads_cfg.get("max_action", 5.0)),

@@ -932,287 +932,9 @@ static bool res_plan(const AttnMask& m, int L, ResPlan& plan) {
 }
 
 
-// ============================================ forward, persistent with double-buffered K / V
-// The resident forward above loads a (sample, head)'s K and V (75 KB at L = 292), then computes:
-// with two 4-wave workgroups per CU the DMA wait is exposed once per (sample, head) and a
-// workgroup's waves idle at its end while its longest wave finishes (profiles/r03_attn_sq.txt:
-// SQ_WAIT_ANY 36 % of wave cycles). Here one 8-wave workgroup per CU walks its (sample, head)
-// pairs p = blockIdx.x + j gridDim.x with two K/V buffers: pair j + 2's DMA runs while pair
-// j + 1 computes. Work items (pair j, query block) come from an LDS counter (each wave holds
-// the next item and prefetches its Q under the current one); a per-buffer done counter tells the
-// wave finishing pair j's last block to refill the buffer with pair j + 2 (it waits for that DMA
-// and publishes a per-buffer ready word); a wave whose item's pair is not ready yet sleeps on
-// that word. The per-block math is attn_fwd_res_kernel's (bit-identical outputs).
-// LDS: images K0 V0 K1 V1 of R = roundup(L, 8) rows (swizzled as the resident kernel), a 32-row
-// zero pad, control words at the end. Tile reads of rows R .. 32 NTILE - 1 run into the next
-// image or the pad: finite values (the whole LDS is zeroed first), masked keys / zero weights.
-constexpr int PERS_NW = 8;
-constexpr float PERS_TAU = 8.f;  // ONEPASS: lazy-rescale threshold (log2 units)
-constexpr int PERS_LDS = 163840;
-__host__ __device__ constexpr int pers_rows(int L) { return (L + 7) & ~7; }
-__host__ __device__ constexpr bool pers_fits(int L) {
-  return 4 * pers_rows(L) * 128 + 32 * 128 + 64 <= PERS_LDS;
-}
-
-template <int NTILE, bool DROP, bool WS, bool ONEPASS>
-__global__ __launch_bounds__(64 * PERS_NW, 1) void attn_fwd_pers_kernel(
-    Geo g, AttnMask mask, ResPlan plan, const uint32_t* __restrict__ drop_q, int drop_lp,
-    float drop_scale, bf16_t* __restrict__ o, int64_t o_s_b, int64_t o_s_t, float* __restrict__ lse,
-    float* __restrict__ wsum, int n_pairs) {
-  constexpr int DH = 64, NS = 4;
-  __shared__ __attribute__((aligned(16))) char smem[PERS_LDS];
-  int* const ctl = reinterpret_cast<int*>(smem + PERS_LDS - 64);  // next, done[2], ready[2]
-  const int lane = threadIdx.x & 63, hh = lane >> 5, lr = lane & 31;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int L = g.L, D = g.H * DH, R = pers_rows(L), IMG = R * 128;
-  const int np = blockIdx.x < n_pairs ? (n_pairs - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-  const int nb = plan.nblk, total = np * nb;
-  if (np == 0) return;  // workgroup-uniform
-  for (int i = threadIdx.x * 16; i < PERS_LDS - 64; i += 64 * PERS_NW * 16)
-    *reinterpret_cast<uint4*>(smem + i) = make_uint4(0u, 0u, 0u, 0u);
-  if (threadIdx.x == 0) {
-    ctl[0] = 0;
-    ctl[1] = ctl[2] = 0;
-    ctl[3] = ctl[4] = -1;
-  }
-  __syncthreads();
-  // K and V of pair j (this workgroup's j-th) into buffer j & 1, by one wave, waited for, published
-  auto load_pair = [&](int j) {
-    const int pair = (int)blockIdx.x + j * (int)gridDim.x, b = pair / g.H, h = pair - b * g.H;
-    const bf16_t* kb = g.qkv + (int64_t)b * g.s_b + D + h * DH;
-    char* dst = smem + (j & 1) * 2 * IMG;
-    const int64_t bytes = ((int64_t)(L - 1) * g.s_t + D + DH) * 2;  // K row L-1 .. V's end
-    for (int p = 0; p < 2 * (R / 8); ++p) {
-      const int t = p >= R / 8 ? 1 : 0, pr = p - t * (R / 8);
-      const int row = 8 * pr + (lane >> 3);
-      const int c = (lane & 7) ^ res_sw(row);
-      const int voff = (int)(((int64_t)min(row, L - 1) * g.s_t + t * D + 8 * c) * 2);
-      dma16_asm(kb, bytes, dst + t * IMG + pr * 1024, voff);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(&ctl[3 + (j & 1)], j, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  };
-  if (wave < 2 && wave < np) load_pair(wave);
-  auto grab = [&]() {
-    int v = 0;
-    if (lane == 0) v = __hip_atomic_fetch_add(&ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return __builtin_amdgcn_readfirstlane(v);
-  };
-
-  const float c2 = g.scale * LOG2E;
-  const int swr = res_sw(lr);
-  int koff[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) koff[s] = lr * 128 + 16 * ((2 * s + hh) ^ swr);
-  // Q fragments of item `it` (rows of its query block in its pair)
-  auto load_q = [&](int it, bf16x8 (&q)[NS]) {
-    const int j = it / nb, blk = plan.order[it - j * nb];
-    const int pair = (int)blockIdx.x + j * (int)gridDim.x, b = pair / g.H, h = pair - b * g.H;
-    const int qq = 32 * blk + lr;
-    const bool ok = qq < L;
-    const bf16_t* qp = g.qkv + (int64_t)b * g.s_b + (int64_t)(ok ? qq : L - 1) * g.s_t + h * DH;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) q[s] = row_frag_global(qp, ok, s, lane);
-  };
-  int it = grab();
-  bf16x8 qf[NS], qn[NS];
-  if (it < total) load_q(it, qf);
-  while (it < total) {  // wave-uniform
-    const int nxt = grab();
-    if (nxt < total) load_q(nxt, qn);
-    const int j = it / nb, blk = plan.order[it - j * nb];
-    const int pair = (int)blockIdx.x + j * (int)gridDim.x, b = pair / g.H, h = pair - b * g.H;
-    const char* smc = smem + (j & 1) * 2 * IMG;
-    const char* Vimg = smc + IMG;
-    // bounded: a wait that never ends (a bug) must still let the grid drain (~0.5 s, then the
-    // block computes on whatever the buffer holds)
-    for (int spin = 0; spin < (1 << 23) &&
-         __hip_atomic_load(&ctl[3 + (j & 1)], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != j;
-         ++spin)
-      __builtin_amdgcn_s_sleep(2);
-
-    const int q0 = 32 * blk, q = q0 + lr;
-    const bool qv = q < L;
-    const int qc = qv ? q : L - 1;
-    const int sq = set_of(mask, qc);
-    const int sq0 = __builtin_amdgcn_readfirstlane(sq);
-    const bool uni = mask.causal == 0u && __all(sq == sq0);
-    uint32_t vws[NTILE];
-    if (uni) {
-#pragma unroll
-      for (int t = 0; t < NTILE; ++t) vws[t] = plan.tword[sq0][t];
-    } else {
-#pragma unroll
-      for (int t = 0; t < NTILE; ++t) {
-        uint32_t vw = plan.tword[sq][t];
-        if ((mask.causal >> sq) & 1u) {
-          const int a0 = max(q + 1 - 32 * t, 0), e0 = min(mask.start[sq] + mask.len[sq] - 32 * t, 32);
-          if (a0 < e0) vw &= ~(uint32_t)(bit_range(a0, e0));
-        }
-        vws[t] = vw;
-      }
-    }
-    int nt = 0;
-#pragma unroll
-    for (int t = 0; t < NTILE; ++t)
-      if (!__all(vws[t] == 0u)) nt = t + 1;
-    bf16x8 kr[NS];
-    auto kread = [&](int t) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s) kr[s] = *reinterpret_cast<const bf16x8*>(smc + t * 4096 + koff[s]);
-    };
-    auto qk = [&]() {
-      floatx16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-      for (int s = 0; s < NS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kr[s], qf[s], acc, 0, 0, 0);
-      return acc;
-    };
-    auto maskw = [&](floatx16& acc, uint32_t vw) {
-      if (!__all(vw == 0xffffffffu)) {
-        const uint32_t w = vw >> (4 * hh);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int mk = bitmask_of(w, rbit(r));
-          acc[r] = __int_as_float((__float_as_int(acc[r]) & mk) | (~mk & (int)0xff800000u));
-        }
-      }
-    };
-    // ONEPASS: online softmax with a lazy running max (mrun, log2 units): a tile rescales the
-    // accumulators only when some row's tile max exceeds mrun by more than PERS_TAU, so the
-    // weights stay <= 2^PERS_TAU (exact in fp32, bf16-rounded like any other weight). Otherwise
-    // pass 1 computes the exact row max first (QK^T twice; the resident kernel's arithmetic).
-    float mrun = -INFINITY;
-    if constexpr (!ONEPASS) {
-      float mrow = -INFINITY;  // pass 1: the exact row max
-      if (nt > 0) kread(0);
-#pragma unroll
-      for (int t = 0; t < NTILE; ++t) {
-        if (t < nt) {
-          floatx16 S = qk();
-          if (t + 1 < NTILE && t + 1 < nt) kread(t + 1);
-          maskw(S, vws[t]);
-#pragma unroll
-          for (int r = 0; r < 16; r += 4) mrow = fmaxf(fmaxf(mrow, fmaxf(S[r], S[r + 1])), fmaxf(S[r + 2], S[r + 3]));
-        }
-      }
-      mrow = halves_max(mrow);
-      mrun = mrow == -INFINITY ? -INFINITY : mrow * c2;
-    }
-    float mc = mrun == -INFINITY ? 0.f : mrun;
-    floatx16 oacc[2];
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
-    float l4[4] = {0.f, 0.f, 0.f, 0.f}, ld4[4] = {0.f, 0.f, 0.f, 0.f};
-    floatx16 Sa;
-    TileMasks<16> dm[2];
-    if constexpr (DROP) dm[0].load(drop_q, drop_lp, blk, 0);
-    if (nt > 0) {
-      kread(0);
-      Sa = qk();
-      if (nt > 1) kread(1);
-      maskw(Sa, vws[0]);
-    }
-#pragma unroll
-    for (int t = 0; t < NTILE; ++t) {
-      if (t < nt) {
-        if constexpr (DROP)
-          if (t + 1 < NTILE) dm[(t + 1) & 1].load(drop_q, drop_lp, blk, 32 * (t + 1));
-        floatx16 Sb;
-        if (t + 1 < NTILE && t + 1 < nt) {
-          Sb = qk();
-          if (t + 2 < NTILE && t + 2 < nt) kread(t + 2);
-          maskw(Sb, vws[t + 1]);
-        }
-        bf16x8 vt[2][2];
-#pragma unroll
-        for (int d = 0; d < 2; ++d)
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) vt[d][ks] = res_trans(Vimg, 32 * t + 16 * ks, d, lane);
-        if constexpr (ONEPASS) {
-          float tm = fmaxf(fmaxf(fmaxf(Sa[0], Sa[1]), fmaxf(Sa[2], Sa[3])), fmaxf(fmaxf(Sa[4], Sa[5]), fmaxf(Sa[6], Sa[7])));
-          tm = fmaxf(tm, fmaxf(fmaxf(fmaxf(Sa[8], Sa[9]), fmaxf(Sa[10], Sa[11])), fmaxf(fmaxf(Sa[12], Sa[13]), fmaxf(Sa[14], Sa[15]))));
-          tm = halves_max(tm) * c2;
-          const bool need = tm > mrun + PERS_TAU;  // false for a row with no visible key yet
-          if (__any(need)) {  // wave-uniform: rescale only the rows that moved
-            const float mnew = need ? tm : mrun;
-            // (the accumulators are still 0 while mrun = -inf: alpha 0, never 0 x inf)
-            const float alpha = !need ? 1.f : mrun == -INFINITY ? 0.f : fast_exp2(mrun - mnew);
-#pragma unroll
-            for (int d = 0; d < 2; ++d)
-#pragma unroll
-              for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              l4[r] *= alpha;
-              if constexpr (WS) ld4[r] *= alpha;
-            }
-            mrun = mnew;
-            mc = mrun == -INFINITY ? 0.f : mrun;
-          }
-        }
-        floatx16 p;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float e = fast_exp2(fmaf(Sa[r], c2, -mc));
-          l4[r & 3] += e;
-          if constexpr (DROP) e = sel_keep(e, dm[t & 1].m[r]);
-          if constexpr (WS) ld4[r & 3] += e;
-          p[r] = e;
-        }
-        const bf16x8 p0 = pack_frag(p, 0), p1 = pack_frag(p, 1);
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vt[d][0], p0, oacc[d], 0, 0, 0);
-          oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vt[d][1], p1, oacc[d], 0, 0, 0);
-        }
-        Sa = Sb;
-      }
-    }
-    // this wave's reads of the buffer are done (the data is in registers): release the block
-    {
-      int d = 0;
-      if (lane == 0) d = __hip_atomic_fetch_add(&ctl[1 + (j & 1)], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      d = __builtin_amdgcn_readfirstlane(d);
-      if (d == nb - 1) {  // pair j's last block: refill its buffer with pair j + 2
-        if (lane == 0) ctl[1 + (j & 1)] = 0;
-        if (j + 2 < np) load_pair(j + 2);
-      }
-    }
-    {  // O = acc / l (x 1/keep_prob) as bf16 rows, lse, wsum
-      float l = (l4[0] + l4[1]) + (l4[2] + l4[3]);
-      float ld = (ld4[0] + ld4[1]) + (ld4[2] + ld4[3]);
-      l = halves_sum(l);
-      if constexpr (WS) ld = halves_sum(ld);
-      const float inv = l > 0.f ? drop_scale / l : 0.f;
-      bf16_t* orow = o + (int64_t)b * o_s_b + (int64_t)(qv ? q : L - 1) * o_s_t + h * DH;
-#pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int r4 = 0; r4 < 4; r4 += 2) {
-          const uint32_t a0 = pk2(oacc[d][4 * r4] * inv, oacc[d][4 * r4 + 1] * inv);
-          const uint32_t a1 = pk2(oacc[d][4 * r4 + 2] * inv, oacc[d][4 * r4 + 3] * inv);
-          const uint32_t b0 = pk2(oacc[d][4 * r4 + 4] * inv, oacc[d][4 * r4 + 5] * inv);
-          const uint32_t b1 = pk2(oacc[d][4 * r4 + 6] * inv, oacc[d][4 * r4 + 7] * inv);
-          const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-          const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-          if (qv)
-            *reinterpret_cast<uint4*>(orow + 32 * d + 8 * r4 + 8 * hh) = make_uint4(x0[0], x1[0], x0[1], x1[1]);
-        }
-      if (qv && lane < 32) {
-        const int64_t ri = ((int64_t)b * g.H + h) * L + q;
-        lse[ri] = l > 0.f ? mc * LN2 + logf(l) : -INFINITY;
-        if (WS) wsum[ri] = ld * inv;
-      }
-    }
-    it = nxt;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) qf[s] = qn[s];
-  }
-}
+// (A persistent 8-wave forward with double-buffered K / V, attn_fwd_pers_kernel, measured
+// slower than the resident kernel — 185.6 vs 175.3 us at L = 292, B = 512 — and was removed in
+// round 5)
 
 // ===================================================== backward, resident operands (Dh = 64)
 // One workgroup per (sample, head), two phases over LDS images of the same layout as the
@@ -2492,42 +2214,6 @@ extern "C" int mmt_attn_fwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
     ResPlan plan;
     if (res_plan(m, L, plan)) {
       const int ntile = ((L + 63) / 64) * 2;  // even tile counts are instantiated
-      if (getenv("MMT_ATTN_PERS") && atoi(getenv("MMT_ATTN_PERS")) != 0 && pers_fits(L)) {
-        const int grid = std::min(B * H, attn_cu_count());
-        const bool one = attn_res_enabled("MMT_ATTN_ONEPASS");
-#define PER1(NT_, DR_, WS_)                                                                        \
-  do {                                                                                             \
-    if (one)                                                                                       \
-      hipLaunchKernelGGL((attn_fwd_pers_kernel<NT_, DR_, WS_, true>), dim3(grid), dim3(64 * PERS_NW), \
-                         0, as_stream(stream), g, m, plan, drop_bits, lp, dscale, (bf16_t*)o, o_s_b,  \
-                         o_s_t, lse, wsum, B * H);                                                 \
-    else                                                                                           \
-      hipLaunchKernelGGL((attn_fwd_pers_kernel<NT_, DR_, WS_, false>), dim3(grid), dim3(64 * PERS_NW), \
-                         0, as_stream(stream), g, m, plan, drop_bits, lp, dscale, (bf16_t*)o, o_s_b,  \
-                         o_s_t, lse, wsum, B * H);                                                 \
-  } while (0)
-#define PER2(NT_)                                          \
-  do {                                                     \
-    if (drop_bits) {                                       \
-      if (wsum) PER1(NT_, true, true);                     \
-      else PER1(NT_, true, false);                         \
-    } else {                                               \
-      if (wsum) PER1(NT_, false, true);                    \
-      else PER1(NT_, false, false);                        \
-    }                                                      \
-  } while (0)
-        switch (ntile) {
-          case 2: PER2(2); break;
-          case 4: PER2(4); break;
-          case 6: PER2(6); break;
-          case 8: PER2(8); break;
-          default: PER2(10); break;
-        }
-#undef PER2
-#undef PER1
-        MMT_CHECK_LAUNCH("mmt_attn_fwd(pers)");
-        return MMT_OK;
-      }
       const bool one1 = attn_res_enabled("MMT_ATTN_ONEPASS");
 #define RES1(NT_, DR_, WS_)                                                                       \
   do {                                                                                            \

@@ -165,20 +165,26 @@ struct DetState {
   long long* fx;   // fixed-point shadow, same offsets as base
   int64_t n;       // elements
 };
+// Range: the shadow holds |sum| < 2^27 per element (int64 at 2^-36 resolution). A contribution
+// that is not finite or has |v| >= 2^26 never enters the shadow: it goes to the fp32 buffer as a
+// plain fp32 atomic instead (det_fits), so a NaN / Inf gradient still reaches flat_grad (and
+// survives the flush: NaN + x = NaN) — the mode trades bitwise reruns for visibility there.
 constexpr double DET_SCALE = 68719476736.0;  // 2^36
+constexpr float DET_VMAX = 67108864.f;       // 2^26
 static __constant__ DetState g_det;
 static DetState g_det_host{};  // this unit's host copy (kernel-variant choices)
 
-__device__ __forceinline__ long long det_fixed(float v) {
-  const double s = (double)v * DET_SCALE;
-  return __double2ll_rn(fmin(fmax(s, -9.0e18), 9.0e18));
+// false for NaN / Inf and for contributions too large for the shadow's range
+__device__ __forceinline__ bool det_fits(float v) { return fabsf(v) < DET_VMAX; }
+__device__ __forceinline__ long long det_fixed(float v) {  // callers check det_fits(v) first
+  return __double2ll_rn((double)v * DET_SCALE);
 }
-// dst += v: an fp32 atomic, or in deterministic mode (dst inside the registered gradient buffer)
-// a 64-bit integer atomic on the fixed-point shadow
+// dst += v: an fp32 atomic, or in deterministic mode (dst inside the registered gradient buffer,
+// v within det_fits) a 64-bit integer atomic on the fixed-point shadow
 __device__ __forceinline__ void grad_add(float* dst, float v) {
   if (g_det.fx != nullptr) {
     const int64_t i = dst - g_det.base;
-    if (i >= 0 && i < g_det.n) {
+    if (i >= 0 && i < g_det.n && det_fits(v)) {
       atomicAdd(reinterpret_cast<unsigned long long*>(g_det.fx + i), (unsigned long long)det_fixed(v));
       return;
     }

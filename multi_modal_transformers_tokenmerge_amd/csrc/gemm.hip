@@ -1732,6 +1732,336 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The two-stage TN kernel above on v_mfma_f32_16x16x32_bf16 (round 5): the same tile, K-steps,
+// DMA and wave grid, but 6 x 6 blocks of 16 x 16 per 96 x 96 wave tile and k32 MFMA steps (the
+// same LDS bytes and MFMA cycles per K-step; MI355X_MICROARCH.md "DVFS give-back" item 7: the chip
+// holds a higher clock on the 16x16 shape, 1.12-1.15x the FLOP/s of 32x32x16 with operands re-read
+// from LDS). A 16x16x32 fragment reads k-rows k1 + 8 g (g = lane >> 4 in 0..3): rows r and r + 8
+// of one read instruction, so the chunk swizzles also XOR bit 3 of the k-row (swA16 / swB16:
+// conflict-free for both fragment shapes). Per k32 step the B fragments are consumed b-outer, so
+// each B register set is refilled with the next step's fragment as soon as its 6 MFMAs issued
+// (one A set in flight ahead, B refilled in place: 216 registers). Results agree with the 32x32
+// kernels to fp32 rounding (different k grouping inside the MFMA), not bit for bit.
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+template <int BM>
+__global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma16_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
+    int64_t ldb, float* __restrict__ slab, int split_k, int k_chunk, int tiles_n) {
+  static_assert(BM == 256 || BM == 384, "tile height");
+  constexpr int MA = BM / 64;                                       // 16-row A blocks per wave
+  constexpr int A_ROWB = BM * 2, B_ROWB = TN_BN * 2;
+  constexpr int A_CH = A_ROWB / 16;
+  constexpr int A_BYTES = 64 * A_ROWB, B_BYTES = 64 * B_ROWB, STAGE = A_BYTES + B_BYTES;
+  constexpr int GA = A_BYTES / 1024 / 8, GB = B_BYTES / 1024 / 8;
+  constexpr int G = GA + GB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles = ((M + BM - 1) / BM) * tiles_n;
+  const int wi = xcd_remap(blockIdx.x, gridDim.x);
+  const int z = wi / tiles, t = wi - z * tiles;
+  const int tm = t / tiles_n;
+  const int m0 = tm * BM, n0 = (t - tm * tiles_n) * TN_BN;
+  const int kbeg = z * k_chunk, kend = min(K, kbeg + k_chunk);
+  const int nk = max(0, (kend - kbeg + 63) / 64);
+  auto swA = [](int r) { return (4 * (r & 3)) ^ (2 * ((r >> 3) & 1)); };
+  auto swB = [](int r) { return (2 * (r & 3)) ^ (2 * ((r >> 3) & 1)); };
+  int voff[G];
+#pragma unroll
+  for (int p = 0; p < G; ++p) {
+    if (p < GA) {
+      const int j = wave * GA + p, e = j * 64 + lane, row = e / A_CH, c = (e % A_CH) ^ swA(row);
+      voff[p] = row * (int)(lda * 2) + c * 16;
+    } else {
+      const int j = wave * GB + (p - GA), e = j * 64 + lane, row = e / 24, c = (e % 24) ^ swB(row);
+      voff[p] = row * (int)(ldb * 2) + c * 16;
+    }
+  }
+  auto piece = [&](int kt, int st, int p) {
+    const int k0 = kbeg + kt * 64;
+    char* S0 = smem + st * STAGE;
+    if (p < GA)
+      dma16_asm(A + (int64_t)k0 * lda + m0, ((int64_t)(K - k0) * lda - m0) * 2,
+                S0 + (wave * GA + p) * 1024, voff[p]);
+    else
+      dma16_asm(B + (int64_t)k0 * ldb + n0, ((int64_t)(K - k0) * ldb - n0) * 2,
+                S0 + A_BYTES + (wave * GB + (p - GA)) * 1024, voff[p]);
+  };
+  f32x4_t acc[MA][6];
+#pragma unroll
+  for (int a = 0; a < MA; ++a)
+#pragma unroll
+    for (int b = 0; b < 6; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[a][b][q] = 0.f;
+  // 16x16x32 fragment of rows rbase.. for k32 step ks: lane (i = lane & 15: k-row q = i >> 2,
+  // column group p4 = i & 3; g = lane >> 4) reads 4 columns of k-rows 32 ks + 8 g + q and + 4
+  const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g16 = lane >> 4;
+  auto frag = [&](const char* S, int rowb, int rbase, int ks) {
+    const int col = rbase + 4 * p4;
+    const int k1 = ks * 32 + 8 * g16 + q4;
+    const int cofs = (col & 7) * 2;
+    const int s1 = rowb == A_ROWB ? swA(k1) : swB(k1);
+    const int s2 = rowb == A_ROWB ? swA(k1 + 4) : swB(k1 + 4);
+    const short4v v1 = tr_read(reinterpret_cast<const bf16_t*>(
+        S + k1 * rowb + ((((col >> 3) ^ s1)) << 4) + cofs));
+    const short4v v2 = tr_read(reinterpret_cast<const bf16_t*>(
+        S + (k1 + 4) * rowb + ((((col >> 3) ^ s2)) << 4) + cofs));
+    short __attribute__((ext_vector_type(8))) v = {v1[0], v1[1], v1[2], v1[3],
+                                                   v2[0], v2[1], v2[2], v2[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  if (nk > 0)
+#pragma unroll
+    for (int p = 0; p < G; ++p) piece(0, 0, p);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    const char* As = smem + st * STAGE;
+    const char* Bs = As + A_BYTES;
+    if (kt + 1 < nk)
+#pragma unroll
+      for (int p = 0; p < G; ++p) piece(kt + 1, st ^ 1, p);
+    bf16x8 af[2][MA], bfr[6];
+#pragma unroll
+    for (int a = 0; a < MA; ++a) af[0][a] = frag(As, A_ROWB, wm * (16 * MA) + a * 16, 0);
+#pragma unroll
+    for (int b = 0; b < 6; ++b) bfr[b] = frag(Bs, B_ROWB, wn * 96 + b * 16, 0);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      if (ks == 0)
+#pragma unroll
+        for (int a = 0; a < MA; ++a) af[1][a] = frag(As, A_ROWB, wm * (16 * MA) + a * 16, 1);
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+#pragma unroll
+        for (int a = 0; a < MA; ++a)  // operands swapped: the accumulator holds C^T
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[ks][a], acc[a][b], 0, 0, 0);
+        if (ks == 0) bfr[b] = frag(Bs, B_ROWB, wn * 96 + b * 16, 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // fp32 slab z: lane (m = lane & 15, g) of block (a, b) holds row m, columns 4 g + {0..3}
+  float* out = slab + (int64_t)z * M * N;
+#pragma unroll
+  for (int a = 0; a < MA; ++a) {
+    const int gr = m0 + wm * (16 * MA) + a * 16 + (lane & 15);
+    if (gr >= M) continue;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const int gc = n0 + wn * 96 + b * 16 + 4 * g16;
+      if (gc >= N) continue;
+      *reinterpret_cast<float4*>(out + (int64_t)gr * N + gc) =
+          make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Weight-gradient (TN) split-K partial products on a SLICE RING (round 5). Same operands, tile
+// (BM x 192, 8 waves of (32 MB) x 96, 32x32x16 MFMAs with the accumulator holding C^T), chunk
+// swizzles, fragment reads and k order as gemm_tn_dma_kernel — the slabs are bit-identical — but
+// the LDS is a ring of NS slices of 16 k-rows (one MFMA k-step: 18 KB at BM 384) instead of two
+// 64-deep K-steps, so the DMA runs NS - 2 slices ahead of the slice whose fragments are being
+// read (BM 384, NS 8: 6 slices = 108 KB in flight per CU, 96 k-rows of lead) where the two-stage
+// kernel had one K-step (72 KB, 64 rows) and then waited on it (SQ_WAIT_ANY 52 % of wave cycles,
+// profiles/r02_b512_probe_sq.txt). Per slice j, after one s_barrier (every wave's DMA of slice
+// j + 1 landed, every wave past slice j - 1's MFMAs):
+//   * the fragments of slice j + 1 are read (ds_read_b64_tr_b16) into the other register set,
+//   * the DMA of slice j + NS - 1 goes into slice j - 1's slot,
+//   * 3 x MB MFMAs consume slice j's fragments (read one slice earlier: never exposed).
+// The 18 (14 at BM 256) 1-KB pieces of a slice are dealt wave-contiguously (waves 0-1 three,
+// 2-7 two at BM 384), so each wave waits vmcnt(y x its piece count) for the slices younger than
+// j + 1. PRIO: waves 4-7 at s_setprio 1 for the whole loop (MI355X_MICROARCH.md, two waves per
+// SIMD item 4).
+template <int V>
+__device__ __forceinline__ void vm_wait_n() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(V) : "memory");
+}
+// s_waitcnt vmcnt(y * C) for a runtime y in [0, Y] (y == Y, the steady state, tested first)
+template <int C, int Y>
+__device__ __forceinline__ void vm_wait_slices(int y) {
+  if constexpr (Y <= 0) {
+    vm_wait_n<0>();
+  } else {
+    if (y >= Y) vm_wait_n<Y * C>();
+    else vm_wait_slices<C, Y - 1>(y);
+  }
+}
+// ds_read_b64_tr_b16 as inline asm (its lgkmcnt is waited explicitly: through the builtin the
+// compiler waited for the NEXT slice's reads before the current slice's MFMAs)
+template <int OFF>
+__device__ __forceinline__ short4v tr_read_asm(uint32_t addr) {
+  short4v v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+
+template <int BM, int NS, bool PRIO>
+__global__ __launch_bounds__(TN_NT, 1) void gemm_tn_ring_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
+    int64_t ldb, float* __restrict__ slab, int split_k, int k_chunk, int tiles_n) {
+  static_assert(BM == 256 || BM == 384, "tile height");
+  constexpr int MB = BM / 128;                                      // 32-row MFMA blocks per wave
+  constexpr int SK = 16;                                            // k-rows per slice
+  constexpr int A_ROWB = BM * 2, B_ROWB = TN_BN * 2;                // bytes per k-row
+  constexpr int A_CH = A_ROWB / 16;                                 // 16-B chunks per A k-row
+  constexpr int A_BYTES = SK * A_ROWB, B_BYTES = SK * B_ROWB, SLOT = A_BYTES + B_BYTES;
+  constexpr int PA = A_BYTES / 1024, PT = SLOT / 1024;              // A pieces, all pieces
+  static_assert(A_BYTES % 1024 == 0 && B_BYTES % 1024 == 0, "1-KB pieces");
+  static_assert(NS >= 4 && NS * SLOT <= 163840, "LDS ring");
+  constexpr int GMAX = (PT + 7) / 8;                                // pieces of the fuller waves
+  constexpr int NBIG = PT - 8 * (GMAX - 1);                         // waves issuing GMAX pieces
+  static_assert(GMAX >= 2 && (NS - 2) * GMAX < 64, "vmcnt");
+  static_assert(PA % 2 == 0 && (GMAX == 2 || NBIG * GMAX % 2 == 0), "pieces of one operand per wave");
+  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1, hl = lane >> 5;
+  const int tiles = ((M + BM - 1) / BM) * tiles_n;
+  const int wi = xcd_remap(blockIdx.x, gridDim.x);
+  const int z = wi / tiles, t = wi - z * tiles;
+  const int tm = t / tiles_n;
+  const int m0 = tm * BM, n0 = (t - tm * tiles_n) * TN_BN;
+  const int kbeg = z * k_chunk, kend = min(K, kbeg + k_chunk);
+  const int nk = max(0, (kend - kbeg + SK - 1) / SK);
+  auto swA = [](int r) { return 4 * (r & 3); };
+  auto swB = [](int r) { return 2 * (r & 3); };
+  // this wave's pieces: p0 .. p0 + cnt - 1 of every slice (wave-contiguous)
+  const bool big = wave < NBIG;
+  const int p0 = (GMAX - 1) * wave + min(wave, NBIG);
+  int voff[GMAX];
+#pragma unroll
+  for (int i = 0; i < GMAX; ++i) {
+    const int j = min(p0 + i, PT - 1);
+    if (j < PA) {
+      const int e = j * 64 + lane, row = e / A_CH, c = (e % A_CH) ^ swA(row);
+      voff[i] = row * (int)(lda * 2) + c * 16;
+    } else {
+      const int e = (j - PA) * 64 + lane, row = e / 24, c = (e % 24) ^ swB(row);
+      voff[i] = row * (int)(ldb * 2) + c * 16;
+    }
+  }
+  // a wave's pieces never straddle the A / B boundary (PA even, pieces dealt in pairs from an
+  // even start): one operand, one buffer resource per slice
+  const bool isA = p0 < PA;
+  const bf16_t* const P = isA ? A + m0 : B + n0;
+  const int64_t ldp = isA ? lda : ldb, c0 = isA ? m0 : n0;
+  auto issue = [&](int s) {  // slice s (k-rows kbeg + 16 s ..) into slot s % NS
+    const int k0 = kbeg + s * SK;
+    char* S0 = smem + (s % NS) * SLOT + p0 * 1024;
+    const bf16_t* base = P + (int64_t)k0 * ldp;
+    const int64_t bytes = ((int64_t)(K - k0) * ldp - c0) * 2;
+#pragma unroll
+    for (int i = 0; i < GMAX; ++i) {
+      if (i == GMAX - 1 && !big) break;
+      dma16_asm(base, bytes, S0 + i * 1024, voff[i]);
+    }
+  };
+  // wait until this wave's pieces of every slice older than the y youngest issued have landed
+  // (y <= NS - 3 in the loop, <= NS - 2 after the prologue)
+  auto wait_slices = [&](int y) {
+    if (big) vm_wait_slices<GMAX, NS - 3>(y);
+    else vm_wait_slices<GMAX - 1, NS - 3>(y);
+  };
+
+  floatx16 acc[MB][3];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[a][b][q] = 0.f;
+
+  // fragment of rows rbase.. for the slice in LDS: lane (i = lane & 15: k-row q = i >> 2, column
+  // group p4 = i & 3; g = lane >> 4; h = lane >> 5) reads 4 columns of k-rows k1 and k1 + 4 (the
+  // chunk swizzle of k1 + 4 equals k1's); per lane one LDS byte address per fragment, the slot
+  // added per slice
+  const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g16 = lane >> 4;
+  const int k1 = 8 * hl + q4;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+  auto faddr = [&](int rowb, int sw, int rbase) {
+    const int col = rbase + 16 * (g16 & 1) + 4 * p4;
+    return (uint32_t)(k1 * rowb + (((col >> 3) ^ sw) << 4) + (col & 7) * 2);
+  };
+  uint32_t aad[MB], bad[3];
+#pragma unroll
+  for (int a = 0; a < MB; ++a) aad[a] = lds0 + faddr(A_ROWB, swA(k1), wm * (32 * MB) + a * 32);
+#pragma unroll
+  for (int b = 0; b < 3; ++b) bad[b] = lds0 + A_BYTES + faddr(B_ROWB, swB(k1), wn * 96 + b * 32);
+  auto pack = [](short4v v1, short4v v2) {
+    short __attribute__((ext_vector_type(8))) v = {v1[0], v1[1], v1[2], v1[3],
+                                                   v2[0], v2[1], v2[2], v2[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  bf16x8 fa0[MB], fb0[3], fa1[MB], fb1[3];
+  auto read_slice = [&](int s, bf16x8 (&fa)[MB], bf16x8 (&fb)[3]) {
+    const uint32_t so = (uint32_t)((s % NS) * SLOT);
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+      fa[a] = pack(tr_read_asm<0>(aad[a] + so), tr_read_asm<4 * A_ROWB>(aad[a] + so));
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+      fb[b] = pack(tr_read_asm<0>(bad[b] + so), tr_read_asm<4 * B_ROWB>(bad[b] + so));
+  };
+  // one slice: wait for slice j + 1, barrier, read j + 1, refill slot (j - 1), MFMAs on slice j
+  // (whose fragments the previous slice read and waited for)
+  auto body = [&](int j, bf16x8 (&ca)[MB], bf16x8 (&cb)[3], bf16x8 (&na)[MB], bf16x8 (&nb)[3]) {
+    if (j + 1 < nk) wait_slices(min(NS - 3, nk - 2 - j));
+    asm volatile("s_barrier" ::: "memory");
+    if (j + 1 < nk) read_slice(j + 1, na, nb);
+    if (j + NS - 1 < nk) issue(j + NS - 1);
+    __builtin_amdgcn_sched_barrier(0);  // reads and DMA issued before the MFMAs
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b)  // operands swapped: the accumulator holds C^T
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cb[b], ca[a], acc[a][b], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slice j + 1's fragments in registers
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  if (PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  // prologue: slices 0 .. NS - 2, then slice 0's fragments
+#pragma unroll
+  for (int q = 0; q < NS - 1; ++q)
+    if (q < nk) issue(q);
+  if (nk > 0) {
+    if (big) vm_wait_slices<GMAX, NS - 2>(min(NS - 2, nk - 1));
+    else vm_wait_slices<GMAX - 1, NS - 2>(min(NS - 2, nk - 1));
+    asm volatile("s_barrier" ::: "memory");
+    read_slice(0, fa0, fb0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  for (int j = 0; j < nk; j += 2) {
+    body(j, fa0, fb0, fa1, fb1);
+    if (j + 1 < nk) body(j + 1, fa1, fb1, fa0, fb0);
+  }
+  if (PRIO && wave >= 4) __builtin_amdgcn_s_setprio(0);
+  // fp32 slab z: lane (m = lane & 31, h) of block (a, b) holds row m, columns 8g + 4h + {0..3}
+  float* out = slab + (int64_t)z * M * N;
+#pragma unroll
+  for (int a = 0; a < MB; ++a) {
+    const int gr = m0 + wm * (32 * MB) + a * 32 + (lane & 31);
+    if (gr >= M) continue;
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int gc = n0 + wn * 96 + b * 32 + 8 * g + 4 * hl;
+        if (gc >= N) continue;
+        *reinterpret_cast<float4*>(out + (int64_t)gr * N + gc) =
+            make_float4(acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2],
+                        acc[a][b][4 * g + 3]);
+      }
+  }
+}
+
 // Split-K combine: v = sum_s slab[s][m][n] (fp32, slabs in order), then the GEMM epilogue, 4
 // columns per thread with up to CB slabs' loads in flight (the slabs come from the Infinity
 // Cache: the kernel is bound by loads in flight; 8 columns x 4 slabs per thread measured 37.6 us
@@ -2903,7 +3233,24 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     static const int g_tn_bm = getenv("MMT_TN_BM") ? atoi(getenv("MMT_TN_BM")) : 384;
     const bool tall = g_tn_bm == 384 && M % 384 == 0 && g_variant != 9;
     const int work = ((M + (tall ? 383 : 255)) / (tall ? 384 : 256)) * tn * split_k;
-    if (tall)
+    // the slice-ring kernel (MMT_TN_RING=1 / g_variant 11, PRIO: 12) or the two-stage one (10)
+    static const int g_tn_ring = getenv("MMT_TN_RING") ? atoi(getenv("MMT_TN_RING")) : 0;
+    const int ring = g_variant == 10 ? 0 : g_variant == 11 ? 1 : g_variant == 12 ? 2 : g_tn_ring;
+    if (g_variant == 13 && tall)
+      hipLaunchKernelGGL(gemm_tn_dma16_kernel<384>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
+                         (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
+    else if (g_variant == 13)
+      hipLaunchKernelGGL(gemm_tn_dma16_kernel<256>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
+                         (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
+    else if (ring && tall)
+      hipLaunchKernelGGL((ring == 2 ? gemm_tn_ring_kernel<384, 8, true> : gemm_tn_ring_kernel<384, 8, false>),
+                         dim3(work), dim3(TN_NT), 0, s, M, N, K, (const bf16_t*)A, lda,
+                         (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
+    else if (ring)
+      hipLaunchKernelGGL((ring == 2 ? gemm_tn_ring_kernel<256, 10, true> : gemm_tn_ring_kernel<256, 10, false>),
+                         dim3(work), dim3(TN_NT), 0, s, M, N, K, (const bf16_t*)A, lda,
+                         (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
+    else if (tall)
       hipLaunchKernelGGL(gemm_tn_dma_kernel<384>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
                          (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
     else

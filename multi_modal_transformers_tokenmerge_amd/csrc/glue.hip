@@ -138,9 +138,14 @@ __global__ __launch_bounds__(256) void embed_grad_kernel(int B, int L, int D, in
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         if constexpr (DET) {
-          const unsigned long long q = (unsigned long long)det_fixed(v[e]);
-          atomicAdd(reinterpret_cast<unsigned long long*>(&tab64[rt * EMB_COLS + cv * 8 + e]), q);
-          atomicAdd(reinterpret_cast<unsigned long long*>(&tab64[(Q + ct) * EMB_COLS + cv * 8 + e]), q);
+          if (det_fits(v[e])) {
+            const unsigned long long q = (unsigned long long)det_fixed(v[e]);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&tab64[rt * EMB_COLS + cv * 8 + e]), q);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&tab64[(Q + ct) * EMB_COLS + cv * 8 + e]), q);
+          } else {  // NaN / Inf / out of the shadow's range: straight to the fp32 gradient (visible)
+            atomicAdd(drow_emb + (int64_t)rt * D + col + e, v[e]);
+            atomicAdd(dcol_emb + (int64_t)ct * D + col + e, v[e]);
+          }
         } else {
           atomicAdd(&tab[rt * EMB_COLS + cv * 8 + e], v[e]);
           atomicAdd(&tab[(Q + ct) * EMB_COLS + cv * 8 + e], v[e]);

@@ -29,6 +29,9 @@ class OctoConfig:
     num_observation_blocks: int = 1
     action_space_dim: int = 8
     diffusion_steps: int = 32
+    # OctoDenoise num_blocks (diffusion.py:62-63): MLPBlocks applied in sequence, the first on
+    # concatenate([noisy, time_emb, readout]), the others on the previous block's output
+    denoise_blocks: int = 1
     # action heads built (octo.py:83-87 config.action_heads.heads); the bench path is diffusion only
     action_heads: tuple = ("diffusion",)
     num_bins: int = 256
@@ -47,7 +50,7 @@ class OctoConfig:
     fp8: bool = False
     fp8_residual: bool = False
     # how token_compression_sequence's per-layer counts are realised: "tome" (bipartite soft
-    # matching + merge_wavg, token_compression.py:54-129, one image set per layer) or "prune"
+    # matching + merge_wavg, token_compression.py:54-129, per compressed set) or "prune"
     # (per-set top-k on the attention importance, compressed_attention.py:302-308 +
     # token_compression.py:15-46, every set); YAML key token_compression_method
     compression: str = "tome"
@@ -75,6 +78,13 @@ PRESETS = {
     "octo-base-2cam": OctoConfig(
         name="octo-base-2cam", token_embedding_dim=768, num_heads=12, mlp_dim=3072,
         input_sequence="[TaskDescriptionPrefix{32}] [Image{256};Image{256};Readout{4}]*2",
+        num_observation_blocks=2),
+    # configs[3] with ToMe on every image set: two cameras x two steps, r = 16 per set and block
+    # (one bipartite match + merge per set, token_sequencer.py:222-238 per-set counts)
+    "octo-base-2cam-tome16": OctoConfig(
+        name="octo-base-2cam-tome16", token_embedding_dim=768, num_heads=12, mlp_dim=3072,
+        input_sequence="[TaskDescriptionPrefix{32}] [Image{256};Image{256};Readout{4}]*2",
+        token_compression_sequence="[TaskDescriptionPrefix{0}] [Image{16};Image{16};Readout{0}]*2",
         num_observation_blocks=2),
     # configs[4]: base hi-res 512^2, ToMe r=32, fp8 weight path
     "octo-base-hires-tome32": OctoConfig(

@@ -91,7 +91,8 @@ class Octo:
                                                   fp8=cfg.fp8, fp8_residual=cfg.fp8_residual)
         # ---- head
         self.head = DiffusionActionHead.create(store, "diffusion_action_head", D,
-                                               cfg.action_space_dim, cfg.diffusion_steps)
+                                               cfg.action_space_dim, cfg.diffusion_steps,
+                                               num_blocks=cfg.denoise_blocks)
         self.continuous_head = self.categorical_head = None
         if "continuous" in cfg.action_heads:
             self.continuous_head = ContinuousActionHead(store, "continuous_action_head", D,
@@ -151,19 +152,21 @@ class Octo:
                         raise ValueError(f"layer {layer}: pruning empties a token set")
                     prune = (tuple(zip(sets.starts, sets.lens)), tuple(nxt.lens))
                 self.layer_sets.append((sets, K.SetTable(sets.starts, sets.lens, sets.vis, sets.causal),
-                                        -1, 0, prune))
+                                        -1, 0, prune, ()))
                 continue
-            if len(merged) > 1:
-                raise NotImplementedError("ToMe on more than one token set per layer")
-            tome_set = merged[0] if merged else -1
-            r = 0
-            if tome_set >= 0:
-                r = self.seq._parse(layer)[tome_set].tokens_compressed_per_layer
-                t = sets.lens[tome_set]
+            # ToMe per compressed token set (token_sequencer.py:222-238 gives every set its own
+            # per-layer count): one bipartite match + merge per set, sizes carried per set
+            parsed = self.seq._parse(layer)
+            plan = []
+            for si in merged:
+                r = parsed[si].tokens_compressed_per_layer
+                t = sets.lens[si]
                 if r > t // 2:
-                    raise ValueError(f"layer {layer}: ToMe r={r} exceeds t//2={t // 2}")
+                    raise ValueError(f"layer {layer}: ToMe r={r} exceeds t//2={t // 2} in set {si}")
+                plan.append((si, r))
+            tome_set = plan[0][0] if len(plan) == 1 else (-2 if plan else -1)
             self.layer_sets.append((sets, K.SetTable(sets.starts, sets.lens, sets.vis, sets.causal),
-                                    tome_set, r, None))
+                                    tome_set, sum(r for _, r in plan), None, tuple(plan)))
         final = self.seq.set_table(cfg.num_blocks) if cfg.token_compression_sequence else self.seq.set_table(0)
         self.L_final = final.L
         rows = [s + j for s, n, m in zip(final.starts, final.lens, final.modalities) if m == "readouts"
@@ -185,8 +188,8 @@ class Octo:
 
     def layer_ctxs(self, train: bool, rng, sample_offset: int) -> List[LayerCtx]:
         return [LayerCtx(layer=i, sets=s, table=t, tome_set=ts, r=r, prune=pr, train=train, rng=rng,
-                         sample_offset=sample_offset)
-                for i, (s, t, ts, r, pr) in enumerate(self.layer_sets)]
+                         sample_offset=sample_offset, tome_plan=plan)
+                for i, (s, t, ts, r, pr, plan) in enumerate(self.layer_sets)]
 
     # ------------------------------------------------------------------ forward / backward
     def generate_readouts(self, text_tokens, images, train=True, rng=None, sample_offset=0,

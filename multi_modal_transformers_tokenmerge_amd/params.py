@@ -196,11 +196,22 @@ class ParamStore:
     def set_deterministic(self, on: bool = True):
         """Deterministic mode (include/mmt_api.h mmt_set_deterministic): the gradient sums that
         are fp32 atomics otherwise go to an int64 fixed-point shadow of flat_grad (integer adds:
-        order-independent), added into flat_grad by det_flush. One store per process holds it
-        (the library keeps one registration); synchronous, so call outside graph capture."""
+        order-independent), added into flat_grad by det_flush. Resolution 2^-36 per
+        contribution, range |sum| < 2^27 per element; a NaN / Inf or |v| >= 2^26 contribution
+        bypasses the shadow as a plain fp32 atomic, so it still shows in the gradient.
+        The library keeps ONE registration per process: a second store asking for it while
+        another holds it raises (its gradient sites would otherwise silently take the
+        registration from the first). The registration holds a reference to this store until
+        set_deterministic(False) / close() (or use ``with store.deterministic():``).
+        Synchronous, so call outside graph capture."""
         from . import _C
         if on:
-            self.det_fx = torch.zeros(self.n, dtype=torch.int64, device=self.flat_grad.device)
+            owner = ParamStore._det_owner
+            if owner is not None and owner is not self:
+                raise RuntimeError("deterministic mode is registered by another ParamStore; "
+                                   "call its set_deterministic(False) / close() first")
+            if self.det_fx is None:
+                self.det_fx = torch.zeros(self.n, dtype=torch.int64, device=self.flat_grad.device)
             _C.call("mmt_set_deterministic", _C.ptr(self.flat_grad), _C.ptr(self.det_fx), self.n)
             ParamStore._det_owner = self
         else:
@@ -211,6 +222,24 @@ class ParamStore:
 
     _det_owner = None
 
+    def close(self):
+        """Release the deterministic-mode registration if this store holds it (the explicit
+        form of leaving the mode; nothing touches the device from __del__)."""
+        self.set_deterministic(False)
+
+    def deterministic(self):
+        """``with store.deterministic(): ...`` — the mode on for the block, released on exit."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def _cm():
+            self.set_deterministic(True)
+            try:
+                yield self
+            finally:
+                self.set_deterministic(False)
+        return _cm()
+
     def det_flush(self, lo: int = 0, hi: int | None = None):
         """flat_grad[lo:hi] += shadow * 2^-36, shadow[lo:hi] = 0 (no-op outside the mode)."""
         if self.det_fx is None:
@@ -219,13 +248,6 @@ class ParamStore:
         hi = self.n if hi is None else hi
         _C.call("mmt_det_flush", _C.ptr(self.flat_grad[lo:]), _C.ptr(self.det_fx[lo:]), hi - lo,
                 _C.stream_ptr())
-
-    def __del__(self):
-        try:
-            if ParamStore._det_owner is self:
-                self.set_deterministic(False)
-        except Exception:  # interpreter shutdown: the library may be gone
-            pass
 
     def sync_shadow(self):
         """Re-derive the bf16 shadow after the master was modified outside AdamW."""

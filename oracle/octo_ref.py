@@ -424,7 +424,12 @@ class OctoRef:
         either instead of recomputing it."""
         def tr(name, v):
             if trace is not None:
-                trace[f"b{layer}/{name}"] = v.detach().clone()
+                if trace.get("_retain"):  # diagnostics (tools/golden_diag.py): keep the graph node
+                    if v.requires_grad:
+                        v.retain_grad()
+                    trace[f"b{layer}/{name}"] = v
+                else:
+                    trace[f"b{layer}/{name}"] = v.detach().clone()
             return v
         cfg, p = self.cfg, self.p
         rb, gb, rbg = self.rb, self.gb, self.rbg
@@ -497,20 +502,32 @@ class OctoRef:
             o = torch.where(keep, o / kp, torch.zeros_like(o))
         x = self._q(x + o)
         if merged and not pruning:
-            si = merged[0]
-            r = sequence[si][3]
-            s0 = sum(ln for _, ln, _ in cur[:si])
-            tcur = cur[si][1]
-            if tome_indices is not None:
-                unm, src, dst = tome_indices
-            else:  # canonical C matching on this restatement's own key metric (sum over heads)
-                from . import tome as T
-                km = k.detach().float()[:, s0:s0 + tcur].contiguous().numpy()
-                unm, src, dst, _ = T.canon_match(km, r)
-                unm, src, dst = (torch.from_numpy(a) for a in (unm, src, dst))
-            used = (unm, src, dst)
-            xs, size = tome_merge_wavg(x[:, s0:s0 + tcur], size, unm, src, dst, r)
-            x = torch.cat([x[:, :s0], xs, x[:, s0 + tcur:]], dim=1)
+            # one bipartite match + merge_wavg per compressed set (token_sequencer.py:222-238
+            # counts per set), the last set first so the earlier sets' starts stay valid; with
+            # several sets `size` / `tome_indices` / `used` are per set ({set: (B, t, 1)} /
+            # [triple per set in set order]), with one set a tensor / a triple as before
+            multi = len(merged) > 1
+            given = (list(tome_indices) if multi else [tome_indices]) if tome_indices is not None \
+                else [None] * len(merged)
+            sizes = (size or {}) if multi else {merged[0]: size}
+            new_sizes, used_l = {}, []
+            for si, tri in sorted(zip(merged, given), key=lambda z: -z[0]):
+                r = sequence[si][3]
+                s0 = sum(ln for _, ln, _ in cur[:si])
+                tcur = cur[si][1]
+                if tri is not None:
+                    unm, src, dst = tri
+                else:  # canonical C matching on this restatement's own key metric (sum over heads)
+                    from . import tome as T
+                    km = k.detach().float()[:, s0:s0 + tcur].contiguous().numpy()
+                    unm, src, dst, _ = T.canon_match(km, r)
+                    unm, src, dst = (torch.from_numpy(a) for a in (unm, src, dst))
+                xs, new_sizes[si] = tome_merge_wavg(x[:, s0:s0 + tcur], sizes.get(si), unm, src, dst, r)
+                x = torch.cat([x[:, :s0], xs, x[:, s0 + tcur:]], dim=1)
+                used_l.append((si, (unm, src, dst)))
+            used_l.sort(key=lambda z: z[0])
+            used = [u for _, u in used_l] if multi else used_l[0][1]
+            size = new_sizes if multi else new_sizes[merged[0]]
         L2 = x.shape[1]
         tr("x1", x)
         z = tr("y1", rbg(seq_layernorm(x, p[f"{blk}/LayerNorm_1/scale"], p[f"{blk}/LayerNorm_1/bias"],
@@ -562,6 +579,11 @@ class OctoRef:
         cat = rbg(torch.cat([noisy, temb, e], dim=-1))
         hd = rb(torch.relu(gb(dense(p, f"{hp}/MLPBlock_0/Dense_0", cat))))
         pred = gb(dense(p, f"{hp}/MLPBlock_0/Dense_1", hd))
+        i = 1   # OctoDenoise num_blocks > 1 (diffusion.py:62-63): the next MLPBlocks on pred
+        while f"{hp}/MLPBlock_{i}/Dense_0/kernel" in p:
+            h = rb(torch.relu(gb(dense(p, f"{hp}/MLPBlock_{i}/Dense_0", rbg(pred)))))
+            pred = gb(dense(p, f"{hp}/MLPBlock_{i}/Dense_1", h))
+            i += 1
         loss = (0.5 * (pred - eps_t) ** 2).sum(-1).mean()
         return loss, dict(pred=pred, e=e)
 

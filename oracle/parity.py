@@ -54,21 +54,37 @@ def insitu_tome_check(model, st):
     Dh = model.D // H
     checked = 0
     for layer, sv in enumerate(st["stack_sv"]):
-        if sv["tome"] is None:
-            continue
-        s0, t, r = sv["tome"][:3]
-        qkv = sv["qkv"]
-        B, L = qkv.shape[:2]
-        metric = qkv.view(B, L, 3, H, Dh)[:, s0:s0 + t, 1].float().cpu().numpy()
-        cu, cs, cd, _ = T.canon_match(metric, r)
-        for name, got, want in zip(("unm", "src", "dst"), sv["tome"][6:9], (cu, cs, cd)):
-            g = got.cpu().numpy()
-            if not np.array_equal(g, want):
-                bad = np.argwhere(g != want)[:4].tolist()
-                raise AssertionError(f"layer {layer}: in-situ ToMe {name} differs from canon_match "
-                                     f"at {bad}")
-        checked += 1
+        for tm in _tome_list(sv):   # every merged set of the block (several: one match each)
+            s0, t, r = tm[:3]
+            qkv = sv["qkv"]
+            B, L = qkv.shape[:2]
+            metric = qkv.view(B, L, 3, H, Dh)[:, s0:s0 + t, 1].float().cpu().numpy()
+            cu, cs, cd, _ = T.canon_match(metric, r)
+            for name, got, want in zip(("unm", "src", "dst"), tm[6:9], (cu, cs, cd)):
+                g = got.cpu().numpy()
+                if not np.array_equal(g, want):
+                    bad = np.argwhere(g != want)[:4].tolist()
+                    raise AssertionError(f"layer {layer} set at {s0}: in-situ ToMe {name} differs "
+                                         f"from canon_match at {bad}")
+            checked += 1
     return checked
+
+
+def _tome_list(sv):
+    """The block's merges in set order (one tuple per merged set; empty without ToMe)."""
+    tms = sv.get("tome_sets") or ([sv["tome"]] if sv.get("tome") is not None else [])
+    return sorted(tms, key=lambda tm: tm[0])
+
+
+def _size_in(sv, f):
+    """The block's incoming per-set token sizes: a tensor (one merged set), {set: tensor}
+    (several), or None."""
+    if sv.get("tome") is not None:
+        return None if sv["tome"][4] is None else f(sv["tome"][4])
+    tms = _tome_list(sv)
+    if not tms:
+        return None
+    return {tm[9]: f(tm[4]) for tm in tms if tm[4] is not None} or None
 
 
 def insitu_prune_check(model, st):
@@ -95,6 +111,8 @@ def _used(sv, f=lambda a: a.cpu()):
     None."""
     if sv["tome"] is not None:
         return tuple(f(a) for a in sv["tome"][6:9])
+    if sv.get("tome_sets"):  # several merged sets: a triple per set, in set order
+        return [tuple(f(a) for a in tm[6:9]) for tm in _tome_list(sv)]
     if sv.get("prune") is not None:
         return f(sv["prune"][0])
     return None
@@ -105,6 +123,8 @@ def _inject(x):
         return None
     if isinstance(x, tuple):
         return tuple(torch.from_numpy(np.asarray(a)) for a in x)
+    if isinstance(x, list):  # several merged sets
+        return [_inject(t) for t in x]
     return torch.from_numpy(np.asarray(x))
 
 
@@ -240,7 +260,7 @@ def hip_blockwise(cfg, B, seed=0):
     f = lambda a: None if a is None else a.detach().float().cpu()  # noqa: E731
     return dict(model=model, B=B, seed=seed, loss=float(loss.item()),
                 xs=[f(sv["x"]) for sv in svs], xL=f(st["xL"]), dxL=f(dxL), douts=douts, dins=dins,
-                size_in=[None if sv["tome"] is None else f(sv["tome"][4]) for sv in svs],
+                size_in=[_size_in(sv, f) for sv in svs],
                 tome=[_used(sv) for sv in svs],
                 prune_scores=[None if sv.get("prune") is None else f(sv["prune"][1]) for sv in svs],
                 prune_layers_checked=n_prune,
@@ -248,6 +268,16 @@ def hip_blockwise(cfg, B, seed=0):
                 t=st["head_sv"]["t"].cpu().numpy(), eps=st["head_sv"]["eps"].cpu().numpy(),
                 grads={p.name: p.grad.detach().cpu().numpy().copy() for p in model.store.params},
                 tome_layers_checked=n_tome)
+
+
+def _size_arg(size, dt=None):
+    """HIP per-set sizes (B, t) -> the oracle's (B, t, 1) (a dict per set with several)."""
+    if size is None:
+        return None
+    if isinstance(size, dict):
+        return {k: _size_arg(v, dt) for k, v in size.items()}
+    size = size.unsqueeze(-1)
+    return size if dt is None else size.to(dt)
 
 
 def oracle_blockwise(cfg, res):
@@ -265,8 +295,7 @@ def oracle_blockwise(cfg, res):
     nb = cfg.num_blocks
     for i in range(nb):
         x_in = res["xs"][i].clone().requires_grad_()
-        size = res["size_in"][i]
-        size = None if size is None else size.unsqueeze(-1)
+        size = _size_arg(res["size_in"][i])
         trace = {}
         xo, _, _ = ref.block(x_in, i, seq, size, seed=1234, step=0, tome_indices=res["tome"][i],
                              trace=trace)
@@ -314,8 +343,7 @@ def blockwise_floor(cfg, res, blocks):
             params = {k: v.detach().to(dt).requires_grad_() for k, v in params.items()}
             ref = OctoRef(cfg, params, t5p, dtype=dt, emulate_bf16=emu)
             x_in = res["xs"][i].to(dt).requires_grad_()
-            size = res["size_in"][i]
-            size = None if size is None else size.unsqueeze(-1).to(dt)
+            size = _size_arg(res["size_in"][i], dt)
             xo, _, _ = ref.block(x_in, i, seq, size, seed=1234, step=0, tome_indices=res["tome"][i])
             xo.backward(res["douts"][i].to(dt))
             pre = f"StackedEncoder1DBlock_0/Block_{i}/"

@@ -82,3 +82,42 @@ def test_shards_equal_full_batch(dev):
         if float(b.norm()) == 0:
             continue
         assert float((a - b).norm() / b.norm()) <= 1e-4, p.name
+
+
+def test_nan_and_large_contributions_stay_visible(dev):
+    """in the mode a NaN / Inf contribution or one beyond the shadow's range
+    (|v| >= 2^26) goes to the fp32 gradient as a plain atomic (csrc/common.h det_fits), so the
+    gradient shows it after the flush instead of a clamped finite value."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    from multi_modal_transformers_tokenmerge_amd.params import ParamStore, const
+    st = ParamStore()
+    p = st.add("w", (64,), const(0.0))
+    st.materialize(dev)
+    x = torch.ones((512, 64), dtype=torch.float32, device=dev)
+    x[3, 5] = float("nan")
+    x[7, 9] = float("inf")
+    x[11, 13] = 1e9
+    with st.deterministic():
+        K.colsum(x, p.grad)
+        st.det_flush()
+        torch.cuda.synchronize()
+        g = p.grad.cpu()
+    assert torch.isnan(g[5]) and g[9] == float("inf")
+    assert abs(float(g[13]) - (1e9 + 511)) <= 1e9 * 1e-6
+    rest = [i for i in range(64) if i not in (5, 9, 13)]
+    assert torch.equal(g[rest], torch.full((61,), 512.0))
+
+
+def test_second_store_cannot_take_the_registration(dev):
+    from multi_modal_transformers_tokenmerge_amd.params import ParamStore, const
+    a, b = ParamStore(), ParamStore()
+    a.add("w", (8,), const(0.0))
+    b.add("w", (8,), const(0.0))
+    a.materialize(dev)
+    b.materialize(dev)
+    with a.deterministic():
+        with pytest.raises(RuntimeError):
+            b.set_deterministic(True)
+    with b.deterministic():  # free again after a's block
+        assert ParamStore._det_owner is b
+    assert ParamStore._det_owner is None

@@ -91,3 +91,29 @@ def test_octo_head_train_steps(dev, kind):
            else model.predict_action_logits(None, images, state.rng))
     torch.cuda.synchronize()
     assert out.shape == ((B, 1, 8) if kind == "continuous" else (B, 8, 32))
+
+
+def test_octo_denoise_num_blocks_2(dev):
+    """OctoDenoise num_blocks = 2 (diffusion.py:62-63: MLPBlock_0 on concatenate([noisy, temb,
+    readout]), MLPBlock_1 on its (B, 8) output): the training step at the block-local bar
+    (the head's parameters, MLPBlock_1 included, against the emulating oracle's chain), and the
+    predict_action loop path from the fused sampler's initial draw: finite, clipped to [-5, 5],
+    and equal to the fused sampler's z."""
+    from multi_modal_transformers_tokenmerge_amd.models.octo.config import get_config
+    from oracle import parity as P
+    cfg = get_config("octo-tiny", num_blocks=2, denoise_blocks=2)
+    res = P.hip_blockwise(cfg, 3, seed=0)
+    names = [n for n in res["grads"] if "OctoDenoise_0/MLPBlock_1/" in n]
+    assert len(names) == 4 and all(np.abs(res["grads"][n]).sum() > 0 for n in names)
+    P.check_blockwise(P.oracle_blockwise(cfg, res), cfg=cfg, res=res)
+    model = res["model"]
+    rng = torch.tensor([5, 0], dtype=torch.int32, device=dev)
+    e = torch.randn((3, model.D), device=dev).bfloat16()
+    act, z = model.head.predict_action_mean(e, rng, return_noise=True)
+    torch.cuda.synchronize()
+    assert torch.isfinite(act).all() and act.abs().max() <= 5.0
+    one = get_config("octo-tiny", num_blocks=2)
+    from multi_modal_transformers_tokenmerge_amd.models.octo.octo import Octo
+    m1 = Octo(one, dev, seed=0)
+    _, z1 = m1.head.predict_action_mean(e, rng, return_noise=True)
+    assert torch.equal(z, z1)

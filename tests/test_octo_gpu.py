@@ -207,3 +207,29 @@ def test_staged_backward_matches_backward(dev):
         torch.testing.assert_close(model.store.flat_grad[lo:hi], ref[lo:hi], rtol=1e-4, atol=1e-6,
                                    msg=f"stage {k} region")
     torch.testing.assert_close(model.store.flat_grad, ref, rtol=1e-4, atol=1e-6)
+
+
+def test_blockwise_multiset_tome_base_2cam(dev):
+    """ToMe on several token sets per layer (token_sequencer.py:222-238 gives each set its own
+    per-layer count): configs[3]'s geometry with `[Image{16};Image{16};Readout{0}]*2` — two
+    cameras x two steps, four image sets each merging 16 tokens per block (L 1064 -> 1000 -> 936),
+    one bipartite match + merge_wavg per set with its own carried sizes. Every set's indices
+    checked in situ bit-exact (4 sets x 2 blocks), then the block-local bar."""
+    cfg = _cfg("octo-base-2cam-tome16", num_blocks=2, t5_layers=2)
+    res = P.hip_blockwise(cfg, 1, seed=0)
+    assert [x.shape[1] for x in res["xs"]] == [1064, 1000] and res["xL"].shape[1] == 936
+    assert res["tome_layers_checked"] == 8
+    assert all(isinstance(t, list) and len(t) == 4 for t in res["tome"])
+    P.check_blockwise(P.oracle_blockwise(cfg, res), cfg=cfg, res=res)
+
+
+def test_e2e_free_running_multiset_tome(dev):
+    """Several merged sets with different counts per set (`[Image{8};Image{4};Readout{1}]*2`:
+    4 image sets of 64 tokens, r = 8 / 4 per set, and the readouts merged too), free running at
+    2 blocks, floor-relative bar, every set's merge checked in situ."""
+    cfg = _cfg("octo-tiny", num_blocks=2, image_size=(128, 128, 3),
+               input_sequence="[Image{64};Image{64};Readout{4}]*2", num_observation_blocks=2,
+               token_compression_sequence="[Image{8};Image{4};Readout{1}]*2")
+    out = P.run_parity(cfg, 3, seed=0, floor=True)
+    assert out["tome_layers_checked"] == 2 * 6
+    P.check_against_floor(out)

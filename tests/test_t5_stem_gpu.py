@@ -69,3 +69,25 @@ def test_patch_positions_train_in_interval(dev):
     r2, c2 = K.patch_positions(B // 2, 1, H, P, Q, train=True, rng=rng, sample_offset=B // 2)
     np.testing.assert_array_equal(r2.cpu().numpy(), r[B // 2:])
     np.testing.assert_array_equal(c2.cpu().numpy(), c[B // 2:])
+
+
+def test_patch_positions_train_reference_kat(dev):
+    """The reference's stochastic KAT on the HIP kernel (test_image_tokenizer.py:56-69): a 280 x 280
+    image, patch 1, 128 tokens, train mode -> row encoding of shape (78,400,) with row[123] within
+    70 of 122. Checked over several rng keys (the reference uses one jax key; the build's counter
+    stream differs from jax.random, so the bound is what carries over) and, per draw, the interval
+    rule of image_tokenizer.py:103-108 for every patch."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    H, P, Q = 280, 1, 128
+    edges = np.floor(np.arange(0, H + P, P, dtype=np.float32) / np.float32(H) * np.float32(Q - 1)).astype(int)
+    p = np.arange(H * H)
+    lo, hi = edges[p % H], edges[p % H + 1]
+    for seed in range(4):
+        rng = torch.tensor([seed, 0], dtype=torch.int32, device=dev)
+        rt, ct = K.patch_positions(1, 1, H, P, Q, train=True, rng=rng)
+        row = rt.cpu().numpy().reshape(-1)
+        assert row.shape == ((H // P) ** 2,)                     # chex.assert_shape (78,400,)
+        assert abs(int(row[123]) - 122) <= 70                    # assert_tree_all_close atol=70
+        # an empty interval (q(start) == q(stop) at patch 1, 280 > 127 edges) draws q(start)
+        ok = np.where(hi > lo, (row >= lo) & (row < hi), row == lo)
+        assert ok.all()
