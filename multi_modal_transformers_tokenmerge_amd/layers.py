@@ -118,7 +118,7 @@ def split_k_for(n_out: int, k_out: int, m_red: int, wgs: int = 0) -> int:
     bm = _TN_BM if n_out % 384 == 0 else 256
     tiles = math.ceil(n_out / bm) * math.ceil(k_out / 192)
     want = max(1, (wgs or _WGRAD_WGS) // tiles)
-    return int(max(1, min(want, m_red // 256, 64)))
+    return int(max(1, min(want, m_red // 256, 128)))
 
 
 class Dense:

@@ -409,6 +409,13 @@ def bf16_floor(cfg, res, model):
     on the HIP run's inputs and injected randomness. How far ANY implementation that rounds at
     the build's storage points drifts from exact arithmetic at this depth — the reference point
     of the free-running end-to-end bar (the network amplifies bf16 noise with depth)."""
+    (l_emu, g_emu), (l_f64, g_f64) = oracle_pair(cfg, res, model)
+    return compare(dict(res, loss=l_emu, grads=g_emu), l_f64, g_f64)
+
+
+def oracle_pair(cfg, res, model):
+    """The bf16-emulating restatement (fp32) and the exact one (float64, no emulation) on the HIP
+    run's inputs / injected randomness: [(loss, {name: grad}) emu, (loss, grads) float64]."""
     from oracle.octo_ref import OctoRef, sequence_spec
     images, text, actions = _inputs(model, res["B"], res["seed"])
     tome = [_inject(x) for x in res["tome"]]
@@ -423,8 +430,9 @@ def bf16_floor(cfg, res, model):
                                    positions=(res["rt"], res["ct"]), t=res["t"], eps=res["eps"],
                                    tome_indices=tome, sequence=seq)
         loss.backward()
-        outs.append((float(loss.item()), {k: v.grad.double().numpy() for k, v in params.items()}))
-    return compare(dict(res, loss=outs[0][0], grads=outs[0][1]), outs[1][0], outs[1][1])
+        outs.append((float(loss.item()), {k: (v.grad.double().numpy() if v.grad is not None
+                                               else np.zeros(v.shape)) for k, v in params.items()}))
+    return outs
 
 
 def run_parity(cfg, B, seed=0, floor=False):

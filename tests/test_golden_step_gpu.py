@@ -13,19 +13,20 @@ swap two near-tied scores, so the fixture's indices are then injected into the H
 (inject["tome"]) for the end-to-end comparison; the step's own matching is checked in situ by
 the parity tests (oracle/parity.py). eps: Box-Muller in fp32, the device's logf / cosf vs
 numpy's, rtol 1e-5.
-Within bars (SURVEY §8c, bf16 path), HIP against the bf16-emulating restatement ("emu"), each
-bar widened to twice the bf16 floor where that is larger (the float64 restatement vs emu on the
-same inputs and merge indices: how far rounding at the build's bf16 storage points alone
-moves the result):
-  * block inputs, final sequence: relative L2 <= max(2e-2, 2 x floor);
-  * loss: relative <= max(2e-2, 2 x floor);
-  * every parameter gradient: relative L2 <= max(5e-2, 3 x floor) (rtol 5e-2 on
-    gradients; the reductions over many terms with heavy cancellation — GroupNorm / LayerNorm
-    scales, first biases — carry fp32 summation-order noise beyond the bf16 floor); this bounds
-    the norm ratio too (|ratio - 1| <= relative L2; sampled tensors: over the stored 1024
-    positions, the reported norm over the whole tensor); the global cosine over every stored value
-    >= 0.999, or within twice the floor's deficit (OCTO-small's floor is ~10 % per tensor on
-    block 0's MLP / LayerNorm gradients: 12 T5 layers and the stem in bf16 upstream).
+
+Within bars, HIP against the EXACT restatement (float64, no storage rounding: "f64"); the floor
+is how far the bf16-emulating restatement ("emu": rounding at every point where the build stores
+bf16) lies from that same exact result — what bf16 storage alone costs an honest implementation
+(round 5: the round-4 test measured HIP against emu, which is itself a bf16 result; on
+small_tome16_2blk HIP is the closer of the two to exact on 50 of the 51 gradient tensors, median
+error 0.70x the emulation's — profiles/r05_golden_exact.txt):
+  * block inputs, final sequence, loss: relative (L2) <= max(2e-2, 2 x floor);
+  * every parameter gradient: relative L2 <= max(5e-2, 2 x floor) (SURVEY §8c rtol 5e-2), and the
+    norm ratio |g| / |g_exact| within max(0.02, 2 |floor ratio - 1|, floor relative L2) of 1
+    — the last term because a floor error of relative size e can move the norm by up to e (the
+    floor's own ratio sits near 1 only when its error happens to be orthogonal to the gradient;
+    on the cancellation-heavy first-block bias sums the error is ~7.6 %: DESIGN §4);
+  * the global gradient cosine >= 0.999, or within twice the floor's deficit.
 """
 import ast
 from pathlib import Path
@@ -92,44 +93,44 @@ def test_step_matches_golden_fixture(dev, tag):
     np.testing.assert_allclose(st["head_sv"]["eps"].cpu().numpy().reshape(z["eps"].shape), z["eps"],
                                rtol=1e-5, atol=1e-6)
     assert sum(sv["tome"] is not None for sv in st["stack_sv"]) == int(z["n_tome"])
-    # activations
+    # activations (vs the exact restatement; floor = emu vs exact)
     acts = [(f"x{i}", sv["x"]) for i, sv in enumerate(st["stack_sv"])] + [("xL", st["xL"])]
     for key, t in acts:
         full = t.float().cpu().numpy()
-        emu, hip = _view(z, f"emu/{key}", full)
-        f64 = _view(z, f"f64/{key}", full)[0]
-        r, fl = _rel(hip, emu), _rel(f64, emu)
+        f64, hip = _view(z, f"f64/{key}", full)
+        emu = _view(z, f"emu/{key}", full)[0]
+        r, fl = _rel(hip, f64), _rel(emu, f64)
         report.append(f"{key}: rel {r:.2e} (floor {fl:.2e})")
         if r > max(2e-2, 2 * fl):
             bad.append((key, r, fl))
     # loss
     lh, le, lf = float(loss.item()), float(z["emu/loss"]), float(z["f64/loss"])
-    rl, fl = abs(lh / le - 1), abs(lf / le - 1)
+    rl, fl = abs(lh / lf - 1), abs(le / lf - 1)
     report.append(f"loss {lh:.6f} emu {le:.6f} f64 {lf:.6f}: rel {rl:.2e} (floor {fl:.2e})")
     if rl > max(2e-2, 2 * fl):
         bad.append(("loss", lh, le, lf))
     # gradients
     worst, all_h, all_e, all_f = [], [], [], []
     for p in model.store.params:
-        key = f"emu/grad/{p.name}"
+        key = f"f64/grad/{p.name}"
         full = p.grad.detach().float().cpu().numpy()
-        emu, hip = _view(z, key, full)
-        f64 = _view(z, f"f64/grad/{p.name}", full)[0]
-        ne, nf = float(z[f"{key}:norm"]), float(z[f"f64/grad/{p.name}:norm"])
+        f64, hip = _view(z, key, full)
+        emu = _view(z, f"emu/grad/{p.name}", full)[0]
+        nf, ne = float(z[f"{key}:norm"]), float(z[f"emu/grad/{p.name}:norm"])
         nh = float(np.linalg.norm(full.astype(np.float64)))
-        if ne == 0 and nh == 0:
+        if nf == 0 and nh == 0:
             continue
-        r, rfl = _rel(hip, emu), _rel(f64, emu)
-        ratio, rf = nh / ne, nf / ne
-        worst.append((r, p.name, rfl, ratio, rf, _cos(hip, emu)))
+        r, rfl = _rel(hip, f64), _rel(emu, f64)
+        ratio, rf = nh / nf, ne / nf
+        worst.append((r, p.name, rfl, ratio, rf, _cos(hip, f64)))
         all_h.append(np.asarray(hip, np.float64))
         all_e.append(np.asarray(emu, np.float64))
         all_f.append(np.asarray(f64, np.float64))
-        if r > max(5e-2, 3 * rfl):  # (bounds the norm ratio too: |ratio - 1| <= r)
+        if r > max(5e-2, 2 * rfl) or abs(ratio - 1) > max(0.02, 2 * abs(rf - 1), rfl):
             bad.append((p.name, r, rfl, ratio, rf))
     worst.sort(reverse=True)
-    cg = _cos(np.concatenate(all_h), np.concatenate(all_e))
-    cgf = _cos(np.concatenate(all_f), np.concatenate(all_e))
+    cg = _cos(np.concatenate(all_h), np.concatenate(all_f))
+    cgf = _cos(np.concatenate(all_e), np.concatenate(all_f))
     report.append(f"gradients: global cosine {cg:.6f} (floor {cgf:.6f})")
     for r, name, rfl, ratio, rf, c in worst[:6]:
         report.append(f"  grad rel {r:.3e} (floor {rfl:.3e}) cos {c:.6f} ratio {ratio:.4f} (floor {rf:.4f}) {name}")

@@ -280,7 +280,7 @@ def test_wgrad_split_sizing():
     assert split_k_for(1536, 384, M) == 16           # 8 tiles: 128 // 8
     assert split_k_for(1536, 384, M, wgs=256) == 32  # the bench's full-chip probe
     assert split_k_for(1152, 384, M, wgs=256) == 42  # 6 tiles
-    assert split_k_for(384, 384, M, wgs=256) == 64   # 2 tiles: capped at 64
+    assert split_k_for(384, 384, M, wgs=256) == 128  # 2 tiles: capped at 128
     assert split_k_for(384, 384, 1000) == 3          # 1000 // 256 chunks
     assert split_k_for(4096, 384, M, wgs=256) == 8   # 4096 % 384 != 0: 16 x 2 tiles of 256 x 192
 

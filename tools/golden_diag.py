@@ -50,9 +50,10 @@ def dump(tag):
 
     def dense_bwd(self, dy2d, x2d, *a, **kw):
         out = fb(self, dy2d, x2d, *a, **kw)
-        if out is not None:
-            keep(f"dX/{self.w.name}", out)
-        keep(f"dY/{self.w.name}", dy2d)
+        if "StackedEncoder" in self.w.name:  # the blocks only (the patch-56 stem's are 100s of MB)
+            if out is not None:
+                keep(f"dX/{self.w.name}", out)
+            keep(f"dY/{self.w.name}", dy2d)
         return out
     Ly.Dense.bwd = dense_bwd
     fa = K.attn_bwd
@@ -125,8 +126,10 @@ def _oracle(tag, emulate, dtype):
                                 record=record, tome_indices=tome,
                                 sequence=sequence_spec(cfg.input_sequence, cfg.token_compression_sequence),
                                 trace=trace)
+    xf = ex["x_final"]
+    xf.retain_grad()
     loss.backward()
-    out = {"loss": float(loss.item())}
+    out = {"loss": float(loss.item()), "dxL": xf.grad.double().numpy()}
     for li, x in enumerate(record):
         out[f"din/{li}"] = x.grad.double().numpy()
     for k, v in trace.items():

@@ -7,13 +7,16 @@ T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
 for step in "$@"; do
   case "$step" in
     golden_dump) timeout -k 10 240 python -u tools/golden_diag.py dump small_tome16_2blk && \
-                 timeout -k 10 180 python -u tools/golden_diag.py dump ref_octo_base ;;
+                 timeout -k 10 180 python -u tools/golden_diag.py dump ref_octo_base && \
+                 du -sh gpurun_out/* ;;
     tn_ring_test) timeout -k 10 240 $T tests/test_gemm_gpu.py -k "tn_" ;;
     tn_probe) timeout -k 10 300 python -u tools/tn_probe.py --variants=${TN_VARIANTS:-10,13} ;;
     tn_probe_lib) timeout -k 10 300 python -u tools/tn_probe.py ;;
     new_tests) timeout -k 10 400 $T tests/test_deterministic_gpu.py tests/test_attn_norm_gpu.py \
                  tests/test_t5_stem_gpu.py ;;
     multiset) timeout -k 10 400 $T tests/test_octo_gpu.py -k "multiset" ;;
+    attn_bias) timeout -k 10 300 python -u tools/attn_bias.py ;;
+    parity_exact) timeout -k 10 900 python -u tools/parity_exact.py --seeds=8 ;;
     heads) timeout -k 10 300 $T tests/test_heads_gpu.py ;;
     golden) timeout -k 10 240 $T -s tests/test_golden_step_gpu.py ;;
     gpu_all) timeout -k 10 900 $T -m gpu tests ;;
