@@ -215,7 +215,7 @@ def kernel_probes(model, B, reps=20):
     # it (layers.split_k_for: they share the CUs with the main queue)
     wgrad = torch.zeros((Mh, D), dtype=torch.float32, device=dev)
     sk = split_k_for(Mh, D, M, wgs=256)
-    add("mlp_dw", "gemm_tn_dma_kernel",
+    add("mlp_dw", "gemm_tn_dma16_kernel",
         lambda: K.gemm(dz1, y1, trans_a=True, out=wgrad, out_mode=K.OUT_F32_ACCUM, split_k=sk),
         "mfma", 2.0 * M * D * Mh,
         f"M={Mh} N={D} K={M}, 2MNK, split-K {sk} (the GEMM + its combine kernel together; "
@@ -522,7 +522,7 @@ def main():
         M_ = B * (sum(pr0[1]) if pr0 else sets0.L - r0)
         N_, K_ = cfg.mlp_dim, cfg.token_embedding_dim
         if top is None:
-            top = dict(achieved=None, frac=None, traffic=None, kernel="gemm_tn_dma_kernel",
+            top = dict(achieved=None, frac=None, traffic=None, kernel="gemm_tn_dma16_kernel",
                        avg_launch_us=None, flops_per_launch=None)
         roof = dict(bound="mfma", achieved=top["achieved"], peak=MFMA_BF16_PEAK_TFLOPS,
                     unit="TFLOP/s", frac=top["frac"], traffic=top["traffic"],

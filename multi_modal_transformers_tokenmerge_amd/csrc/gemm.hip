@@ -1884,6 +1884,160 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma16_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
+// TN weight gradients on a FOUR-STAGE RING of 32-row K-steps (round 5): gemm_tn_dma16_kernel's
+// tile, wave grid, swizzles, 16x16x32 MFMAs and k order (the slabs are bit-identical), but the LDS
+// holds four K-steps of 32 k-rows (36 KB each at BM 384, 144 KB) and the DMA runs three K-steps
+// ahead of the one whose MFMAs issue. The fill pattern alone (tools/dma_lab.hip, the Dense_0 dW
+// grid) takes 142 us through the two-stage kernel's wait-all + barrier per 64 rows and 117 us
+// through this ring (profiles/r05_dma_lab.txt): the two-stage structure, not the HBM, set the
+// K-step rate. Per K-step s, after one s_barrier (every wave's DMA of step s + 1 landed, every
+// wave's fragment reads of step s done):
+//   * the DMA of step s + 4 goes into step s's slot (its fragments are in registers),
+//   * 36 MFMAs consume step s's fragments while step s + 1's are read into the other A set and,
+//     B-outer, into each B register as soon as its 6 MFMAs issued (the dma16 kernel's k32 overlap
+//     carried across K-steps, so every fragment read sits under MFMAs).
+// The 36 1-KB pieces of a step are dealt 3 A + 2 B to waves 0-3 and 3 A + 1 B to waves 4-7, each
+// wave waiting vmcnt(y x its own piece count) for the younger steps.
+template <int BM, int SPREAD>
+__global__ __launch_bounds__(TN_NT, 1) void gemm_tn_r4_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
+    int64_t ldb, float* __restrict__ slab, int split_k, int k_chunk, int tiles_n) {
+  static_assert(BM == 384, "tile height");
+  constexpr int MA = BM / 64;                                       // 16-row A blocks per wave
+  constexpr int SK = 32, NS = 4;                                    // k-rows per step, slots
+  constexpr int A_ROWB = BM * 2, B_ROWB = TN_BN * 2;
+  constexpr int A_CH = A_ROWB / 16;
+  constexpr int A_BYTES = SK * A_ROWB, B_BYTES = SK * B_ROWB, STAGE = A_BYTES + B_BYTES;
+  constexpr int PA = A_BYTES / 1024, PB = B_BYTES / 1024;           // 24 + 12 pieces
+  static_assert(PA == 24 && PB == 12, "piece deal");
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles = ((M + BM - 1) / BM) * tiles_n;
+  const int wi = xcd_remap(blockIdx.x, gridDim.x);
+  const int z = wi / tiles, t = wi - z * tiles;
+  const int tm = t / tiles_n;
+  const int m0 = tm * BM, n0 = (t - tm * tiles_n) * TN_BN;
+  const int kbeg = z * k_chunk, kend = min(K, kbeg + k_chunk);
+  const int nk = max(0, (kend - kbeg + SK - 1) / SK);
+  auto swA = [](int r) { return (4 * (r & 3)) ^ (2 * ((r >> 3) & 1)); };
+  auto swB = [](int r) { return (2 * (r & 3)) ^ (2 * ((r >> 3) & 1)); };
+  const bool big = wave < 4;                                        // 5 pieces (else 4)
+  int voff[5], ldso[5];
+#pragma unroll
+  for (int p = 0; p < 5; ++p) {
+    if (p < 3) {
+      const int j = wave * 3 + p, e = j * 64 + lane, row = e / A_CH, c = (e % A_CH) ^ swA(row);
+      voff[p] = row * (int)(lda * 2) + c * 16;
+      ldso[p] = j * 1024;
+    } else {
+      const int j = min(wave + 8 * (p - 3), PB - 1);
+      const int e = j * 64 + lane, row = e / 24, c = (e % 24) ^ swB(row);
+      voff[p] = row * (int)(ldb * 2) + c * 16;
+      ldso[p] = A_BYTES + j * 1024;
+    }
+  }
+  // piece p of step s (p < 3: A, else B; p == 4 only on the big waves)
+  auto piece = [&](int s, int p) {
+    const int k0 = kbeg + s * SK;
+    char* S0 = smem + (s % NS) * STAGE;
+    if (p < 3)
+      dma16_asm(A + (int64_t)k0 * lda + m0, ((int64_t)(K - k0) * lda - m0) * 2, S0 + ldso[p], voff[p]);
+    else if (p == 3 || big)
+      dma16_asm(B + (int64_t)k0 * ldb + n0, ((int64_t)(K - k0) * ldb - n0) * 2, S0 + ldso[p], voff[p]);
+  };
+  auto issue = [&](int s) {
+#pragma unroll
+    for (int p = 0; p < 5; ++p) piece(s, p);
+  };
+  // wait until this wave's pieces of every step older than the y youngest issued have landed
+  auto wait_steps = [&](int y) {
+    if (big) vm_wait_slices<5, 3>(y);
+    else vm_wait_slices<4, 3>(y);
+  };
+  f32x4_t acc[MA][6];
+#pragma unroll
+  for (int a = 0; a < MA; ++a)
+#pragma unroll
+    for (int b = 0; b < 6; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[a][b][q] = 0.f;
+  const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g16 = lane >> 4;
+  auto frag = [&](const char* S, int rowb, int rbase) {
+    const int col = rbase + 4 * p4;
+    const int k1 = 8 * g16 + q4;
+    const int cofs = (col & 7) * 2;
+    const int s1 = rowb == A_ROWB ? swA(k1) : swB(k1);
+    const int s2 = rowb == A_ROWB ? swA(k1 + 4) : swB(k1 + 4);
+    const short4v v1 = tr_read(reinterpret_cast<const bf16_t*>(
+        S + k1 * rowb + ((((col >> 3) ^ s1)) << 4) + cofs));
+    const short4v v2 = tr_read(reinterpret_cast<const bf16_t*>(
+        S + (k1 + 4) * rowb + ((((col >> 3) ^ s2)) << 4) + cofs));
+    short __attribute__((ext_vector_type(8))) v = {v1[0], v1[1], v1[2], v1[3],
+                                                   v2[0], v2[1], v2[2], v2[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  bf16x8 af0[MA], af1[MA], bfr[6];
+  // one K-step: wait for step s + 1, barrier, refill slot s, MFMAs on s with s + 1's reads under them
+  auto body = [&](int s, bf16x8 (&ca)[MA], bf16x8 (&na)[MA]) {
+    const bool nxt = s + 1 < nk;
+    if (nxt) wait_steps(min(NS - 2, nk - 2 - s));
+    // lgkmcnt(0) through the builtin (vmcnt / expcnt fields at their maxima): the compiler's own
+    // wait insertion then knows every fragment read is retired and puts no lgkmcnt(0) in front of
+    // the first MFMA (behind the next step's reads, as it did with the wait as inline asm)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    asm volatile("s_barrier" ::: "memory");
+    const bool refill = s + NS < nk;
+    if (SPREAD == 0 && refill) issue(s + NS);
+    const char* As = smem + ((s + 1) % NS) * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+#pragma unroll
+      for (int a = 0; a < MA; ++a)  // operands swapped: the accumulator holds C^T
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], ca[a], acc[a][b], 0, 0, 0);
+      // the next step's A fragments behind the first B group's MFMAs (the last step reads a
+      // stale slot: in bounds, never consumed)
+      if (b == 0)
+#pragma unroll
+        for (int a = 0; a < MA; ++a) na[a] = frag(As, A_ROWB, wm * (16 * MA) + a * 16);
+      bfr[b] = frag(Bs, B_ROWB, wn * 96 + b * 16);
+      if (SPREAD == 1 && refill && b < 5) piece(s + NS, b);  // one piece per B group
+      __builtin_amdgcn_sched_barrier(0);  // B refilled in place: no read hoisted above its MFMAs
+    }
+  };
+#pragma unroll
+  for (int q = 0; q < NS; ++q)
+    if (q < nk) issue(q);
+  if (nk > 0) {
+    wait_steps(min(NS - 1, nk - 1));
+    asm volatile("s_barrier" ::: "memory");
+#pragma unroll
+    for (int a = 0; a < MA; ++a) af0[a] = frag(smem, A_ROWB, wm * (16 * MA) + a * 16);
+#pragma unroll
+    for (int b = 0; b < 6; ++b) bfr[b] = frag(smem + A_BYTES, B_ROWB, wn * 96 + b * 16);
+  }
+  for (int s = 0; s < nk; s += 2) {
+    body(s, af0, af1);
+    if (s + 1 < nk) body(s + 1, af1, af0);
+  }
+  float* out = slab + (int64_t)z * M * N;
+#pragma unroll
+  for (int a = 0; a < MA; ++a) {
+    const int gr = m0 + wm * (16 * MA) + a * 16 + (lane & 15);
+    if (gr >= M) continue;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const int gc = n0 + wn * 96 + b * 16 + 4 * g16;
+      if (gc >= N) continue;
+      *reinterpret_cast<float4*>(out + (int64_t)gr * N + gc) =
+          make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // TN weight gradients, STAGGERED PING-PONG (round 5): gemm_tn_dma16_kernel's tile, stages,
 // swizzles and 16x16x32 MFMAs, but each wave alternates a load segment R (the fragments of one
 // k32 step: 24 ds_read_b64_tr_b16, plus DMA pieces) and a compute segment M (that step's 36
@@ -3418,9 +3572,13 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     //      +1.6-3.4 % over 10 at the step's dW shapes (tools/tn_probe.py, interleaved rounds);
     //   10 the two-stage kernel on 32x32x16 (gemm_tn_dma_kernel);
     //   11 / 12 the slice ring (gemm_tn_ring_kernel; 12 with static priority): 12-17 % slower;
-    //   14-17 the staggered ping-pong (gemm_tn_pp_kernel): 5-12 % slower than 13
+    //   14-17 the staggered ping-pong (gemm_tn_pp_kernel): 5-12 % slower than 13;
+    //   18 / 19 the four-stage ring of 32-row K-steps (gemm_tn_r4_kernel; 384-row tiles only;
+    //      19 issues the DMA pieces between the MFMA groups): 4-6 % slower than 13 on K chunks of
+    //      4,416 rows, 4 % faster on the out-projection's 1,216-row chunks (its deeper prologue),
+    //      so the default takes it for chunks of at most 2,048 rows (bit-identical slabs)
     static const int g_tn_kernel = getenv("MMT_TN_KERNEL") ? atoi(getenv("MMT_TN_KERNEL")) : 13;
-    const int tnk = (g_variant >= 10 && g_variant <= 17) ? g_variant : g_tn_kernel;
+    const int tnk = (g_variant >= 10 && g_variant <= 19) ? g_variant : g_tn_kernel;
     const int ring = tnk == 11 ? 1 : tnk == 12 ? 2 : 0;
     if (tnk >= 14 && tnk <= 17) {  // ping-pong: 14 XD0, 15 XD1, 16 XD0+prio, 17 XD1+prio
 #define TNPP(BM_, XD_, PR_)                                                                      \
@@ -3438,10 +3596,16 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
         else TNPP(256, 1, true);
       }
 #undef TNPP
-    } else if (tnk == 13 && tall)
+    } else if (tnk == 19 && tall)
+      hipLaunchKernelGGL((gemm_tn_r4_kernel<384, 1>), dim3(work), dim3(TN_NT), 0, s, M, N, K,
+                         (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
+    else if ((tnk == 18 || (tnk == 13 && g_variant < 10 && k_chunk <= 2048)) && tall)
+      hipLaunchKernelGGL((gemm_tn_r4_kernel<384, 0>), dim3(work), dim3(TN_NT), 0, s, M, N, K,
+                         (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
+    else if (tnk == 13 && tall)
       hipLaunchKernelGGL(gemm_tn_dma16_kernel<384>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
                          (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
-    else if (tnk == 13)
+    else if (tnk == 13 || tnk == 18 || tnk == 19)
       hipLaunchKernelGGL(gemm_tn_dma16_kernel<256>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
                          (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
     else if (ring && tall)

@@ -319,7 +319,7 @@ def test_tn_slice_ring_bit_identical(dev, M, N, K, split):
     dy, x = _mk((K, M), dev, g), _mk((K, N), dev, g)
     outs = {}
     try:
-        for v in (10, 11, 12, 13, 14, 15, 16, 17):
+        for v in (10, 11, 12, 13, 14, 15, 16, 17, 18, 19):
             _C.call("mmt_gemm_set_variant", v)
             dw = torch.zeros(M, N, device=dev)
             Kn.gemm(dy, x, trans_a=True, out=dw, out_mode=Kn.OUT_F32_ACCUM, split_k=split)
@@ -331,7 +331,8 @@ def test_tn_slice_ring_bit_identical(dev, M, N, K, split):
     ref = dy.float().t() @ x.float()
     torch.testing.assert_close(outs[11], ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
     # variant 13: the two-stage kernel on 16x16x32 MFMAs (other k grouping: fp32 rounding only);
-    # 14-17: the staggered ping-pong kernel (same per-k32 MFMA order as 13: bit-identical to it)
+    # 14-17: the staggered ping-pong kernel, 18: the four-stage ring of 32-row K-steps (the same
+    # per-k32 MFMA order as 13: bit-identical to it)
     torch.testing.assert_close(outs[13], ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
-    for v in (14, 15, 16, 17):
+    for v in (14, 15, 16, 17, 18, 19):
         assert torch.equal(outs[v], outs[13]), v

@@ -17,6 +17,7 @@ for step in "$@"; do
     multiset) timeout -k 10 400 $T tests/test_octo_gpu.py -k "multiset" ;;
     attn_bias) timeout -k 10 300 python -u tools/attn_bias.py ;;
     parity_exact) timeout -k 10 900 python -u tools/parity_exact.py --seeds=8 ;;
+    dma_lab) timeout -k 10 120 tools/dma_lab ;;
     heads) timeout -k 10 300 $T tests/test_heads_gpu.py ;;
     golden) timeout -k 10 240 $T -s tests/test_golden_step_gpu.py ;;
     gpu_all) timeout -k 10 900 $T -m gpu tests ;;
