@@ -391,6 +391,176 @@ __global__ __launch_bounds__(FUSED_NT) void tome_match_fused_kernel(
   }
 }
 
+// Scores for the sets too large for the fused kernel (t > 512 at c = 64: the OCTO-base 512-px
+// image set, t = 1024 ... 672): the b half B^ of one sample resident in LDS (its [pbr][c + 1]
+// image, 133 KB at t = 1024), AG 32-row a tiles per 1024-thread workgroup. tome_score_kernel
+// re-staged the b rows 4 tiles at a time with one scalar load per element (a latency chain per
+// group, 63 us for 16 samples at t = 1024) and ran one wave per b tile; here the staging is one
+// burst of 16-B loads per thread and the 16 waves split AG x (16 / AG): wave (g, u) takes a tile g
+// against b tiles u, u + 16 / AG, ... with the k-ordered f32 MFMA chain and first-index argmax of
+// tome_score_kernel (the same per-(a row, b tile) chain and the same total-order combine, so
+// node_max / node_idx are identical). Workgroups of one sample run on one XCD (xcd_remap over
+// the flattened grid), which then reads that sample's B^ once from HBM.
+constexpr int SBIG_NT = 1024;
+constexpr int SB = 10;  // 16-B staging loads in flight per thread (the image at t = 1024: 9)
+__host__ __device__ __forceinline__ size_t score_big_lds(int t, int c, int ag) {
+  const int tb = t / 2, pbr = (tb + 31) / 32 * 32;
+  return sizeof(float) * ((size_t)(pbr + 32 * ag) * (c + 1) + 2 * 16 * 32);
+}
+template <int AG>
+__global__ __launch_bounds__(SBIG_NT) void tome_score_big_kernel(const float* __restrict__ An,
+                                                                 const float* __restrict__ Bn,
+                                                                 int t, int c, int flags, int wps,
+                                                                 float* __restrict__ nmax,
+                                                                 int32_t* __restrict__ nidx) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int WPG = 16 / AG;  // waves per a tile
+  const int ta = (t + 1) / 2, tb = t / 2, cs = c + 1;
+  const int pbr = (tb + 31) / 32 * 32, n_bt = pbr / 32;
+  const int wi = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = wi / wps, a0 = (wi - b * wps) * AG * 32;  // first a row of this workgroup
+  float* Bs = smem;                   // [pbr][cs]
+  float* As = Bs + pbr * cs;          // [32 AG][cs]
+  float* pmax = As + 32 * AG * cs;    // [16 waves][32]
+  int* pidx = reinterpret_cast<int*>(pmax + 16 * 32);
+  const float* Bb = Bn + (int64_t)b * tb * c;
+  const float* Ab = An + (int64_t)b * ta * c;
+  // stage: 16-B loads of the rows (rows past tb / ta: zeros), scalar LDS stores into the padded
+  // image (c + 1 floats per row: conflict-free column reads)
+  // (SB loads per thread issued before any store, from clamped addresses: one latency for the
+  // whole image; a load-store loop waited for each load in turn)
+  const int c4 = c / 4, tot = (pbr + 32 * AG) * c4;
+  for (int e0 = 0; e0 < tot; e0 += SB * SBIG_NT) {
+    float4 v[SB];
+#pragma unroll
+    for (int k = 0; k < SB; ++k) {
+      const int e = min(e0 + k * SBIG_NT + (int)threadIdx.x, tot - 1);
+      const int row = e / c4, q = e - row * c4;
+      const bool isb = row < pbr;
+      const int rr = isb ? min(row, tb - 1) : min(a0 + row - pbr, ta - 1);
+      v[k] = *reinterpret_cast<const float4*>((isb ? Bb : Ab) + (int64_t)rr * c + 4 * q);
+    }
+#pragma unroll
+    for (int k = 0; k < SB; ++k) {
+      const int e = e0 + k * SBIG_NT + (int)threadIdx.x;
+      if (e >= tot) break;
+      const int row = e / c4, q = e - row * c4;
+      const bool isb = row < pbr;
+      const int rr = isb ? row : row - pbr;
+      const bool live = isb ? rr < tb : a0 + rr < ta;
+      float* d = (isb ? Bs : As) + rr * cs + 4 * q;
+      d[0] = live ? v[k].x : 0.f;
+      d[1] = live ? v[k].y : 0.f;
+      d[2] = live ? v[k].z : 0.f;
+      d[3] = live ? v[k].w : 0.f;
+    }
+  }
+  __syncthreads();
+  const bool cls = flags & MMT_TOME_CLASS_TOKEN;
+  const bool dis = flags & MMT_TOME_DISTILL_TOKEN;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = wave / WPG, u = wave - g * WPG;
+  const int i = a0 + g * 32 + (lane & 31);
+  const float* bp = As + (g * 32 + (lane & 31)) * cs + (lane >> 5);
+  float best = 0.f;
+  int bidx = -1;
+  for (int jt = u; jt < n_bt; jt += WPG) {
+    const float* ap = Bs + (jt * 32 + (lane & 31)) * cs + (lane >> 5);
+    floatx16 acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+    int s2 = 0;
+    for (; s2 + 8 <= c / 2; s2 += 8) {
+      float av[8], bv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        av[k] = ap[2 * (s2 + k)];
+        bv[k] = bp[2 * (s2 + k)];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[k], bv[k], acc, 0, 0, 0);
+    }
+    for (; s2 < c / 2; ++s2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[2 * s2], bp[2 * s2], acc, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int jj = jt * 32 + (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+      if (jj >= tb) continue;
+      float v = acc[q];
+      if ((cls && i == 0) || (dis && jj == 0)) v = -INFINITY;
+      keep_best(v, jj, best, bidx);
+    }
+  }
+  const float ov = __shfl_xor(best, 32, 64);
+  const int oi = __shfl_xor(bidx, 32, 64);
+  keep_best(ov, oi, best, bidx);
+  if (lane < 32) {
+    pmax[wave * 32 + lane] = best;
+    pidx[wave * 32 + lane] = bidx;
+  }
+  __syncthreads();
+  if (threadIdx.x < 32 * AG) {
+    const int gg = threadIdx.x >> 5, l = threadIdx.x & 31;
+    float bb = 0.f;
+    int bi = -1;
+    for (int w = 0; w < WPG; ++w) keep_best(pmax[(gg * WPG + w) * 32 + l], pidx[(gg * WPG + w) * 32 + l], bb, bi);
+    const int ii = a0 + threadIdx.x;
+    if (ii < ta) {
+      nmax[(int64_t)b * ta + ii] = bb;
+      nidx[(int64_t)b * ta + ii] = bi;
+    }
+  }
+}
+
+// Rank sort of the unfused path, several workgroups per sample: workgroup (sample, y) loads
+// every key of the sample into LDS and ranks rows [128 y, 128 y + 128), 8 lanes per row (each
+// counting over an eighth of the keys, 4 keys per LDS read, summed by xor shuffles), and writes
+// each row's outputs at its rank directly (src / dst for ranks < r, unm otherwise: a rank is a
+// row's final position, so no workgroup needs another's). tome_rank_kernel (one workgroup per
+// sample, one thread per row walking all ta keys) is VALU-bound at O(ta^2) per CU: 17 us at
+// ta = 512 for any number of samples.
+constexpr int RANK8_NT = 1024, RANK8_ROWS = RANK8_NT / 8;
+__global__ __launch_bounds__(RANK8_NT) void tome_rank8_kernel(const float* __restrict__ nmax,
+                                                              const int32_t* __restrict__ nidx,
+                                                              int ta, int r,
+                                                              int32_t* __restrict__ unm_idx,
+                                                              int32_t* __restrict__ src_idx,
+                                                              int32_t* __restrict__ dst_idx,
+                                                              float* __restrict__ node_max_out) {
+  __shared__ __attribute__((aligned(16))) uint32_t keys[1024 + 32];
+  const int n = blockIdx.y;
+  const float* nm = nmax + (int64_t)n * ta;
+  const int tap = (ta + 31) & ~31;  // padding keys 0: never counted (every live key is >= 1: a
+                                    // NaN maps to 0xffffffff, a negative value's bits b to ~b,
+                                    // which is 0 only for b = 0xffffffff, a NaN, the rest to b | 2^31)
+  for (int i = threadIdx.x; i < tap; i += RANK8_NT) keys[i] = i < ta ? sort_key(nm[i]) : 0u;
+  __syncthreads();
+  const int i = blockIdx.x * RANK8_ROWS + (threadIdx.x >> 3), part = threadIdx.x & 7;
+  const uint32_t kv = i < ta ? keys[i] : 0u;
+  int rank = 0;
+  if (i < ta)
+#pragma unroll 4
+    for (int j4 = 4 * part; j4 < tap; j4 += 32) {
+      const uint4 kw = *reinterpret_cast<const uint4*>(keys + j4);
+      rank += (kw.x > kv) || (kw.x == kv && j4 > i);
+      rank += (kw.y > kv) || (kw.y == kv && j4 + 1 > i);
+      rank += (kw.z > kv) || (kw.z == kv && j4 + 2 > i);
+      rank += (kw.w > kv) || (kw.w == kv && j4 + 3 > i);
+    }
+  rank += __shfl_xor(rank, 1, 64);
+  rank += __shfl_xor(rank, 2, 64);
+  rank += __shfl_xor(rank, 4, 64);
+  if (i < ta && part == 0) {
+    if (rank < r) {
+      src_idx[(int64_t)n * r + rank] = i;
+      dst_idx[(int64_t)n * r + rank] = nidx[(int64_t)n * ta + i];
+    } else {
+      unm_idx[(int64_t)n * (ta - r) + (rank - r)] = i;
+    }
+    if (node_max_out) node_max_out[(int64_t)n * ta + i] = nm[i];
+  }
+}
+
 __global__ __launch_bounds__(RANK_NT) void tome_rank_kernel(const float* __restrict__ nmax,
                                                             const int32_t* __restrict__ nidx,
                                                             int ta, int r,
@@ -794,7 +964,28 @@ extern "C" int mmt_tome_match(const void* metric, int dtype, int n, int t, int h
                          (const bf16_t*)metric, n, t, heads, c, s_n, s_t, s_h, An, Bn);
   }
   MMT_CHECK_LAUNCH("mmt_tome_match(norm)");
-  // 2. scores + per-a-row argmax; as many 32-row b tiles per LDS group as fit (<= 4)
+  // 2. scores + per-a-row argmax: with the whole b half resident in LDS when it fits (t <= 1024
+  //    at c = 64), otherwise as many 32-row b tiles per LDS group as fit (<= 4); 3. rank
+  const int n_at = (ta + 31) / 32;
+  if (g_match_use_mfma && c % 4 == 0 && score_big_lds(t, c, 1) <= 160 * 1024) {
+    const bool two = (int64_t)n * n_at > 256 && score_big_lds(t, c, 2) <= 160 * 1024;
+    const int wps = two ? (n_at + 1) / 2 : n_at;
+#define SBIG(AG)                                                                                  \
+  do {                                                                                            \
+    static const bool attr_ = (hipFuncSetAttribute((const void*)tome_score_big_kernel<AG>,       \
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024), true);     \
+    (void)attr_;                                                                                  \
+    hipLaunchKernelGGL(tome_score_big_kernel<AG>, dim3(n * wps), dim3(SBIG_NT),                   \
+                       score_big_lds(t, c, AG), s, An, Bn, t, c, flags, wps, nmax, nidx);        \
+  } while (0)
+    if (two) SBIG(2); else SBIG(1);
+#undef SBIG
+    MMT_CHECK_LAUNCH("mmt_tome_match(score big)");
+    hipLaunchKernelGGL(tome_rank8_kernel, dim3((ta + RANK8_ROWS - 1) / RANK8_ROWS, n), dim3(RANK8_NT), 0, s,
+                       nmax, nidx, ta, r, unm_idx, src_idx, dst_idx, node_max);
+    MMT_CHECK_LAUNCH("mmt_tome_match(rank)");
+    return MMT_OK;
+  }
   const int cs = c + 1;
   const size_t tile = sizeof(float) * 32 * cs;
   const size_t fixed = tile + sizeof(float) * 8 * 32 * 2;

@@ -26,7 +26,10 @@ CASES = [(4, 256, 64, 1, 16, 0), (3, 257, 64, 1, 16, 0), (2, 64, 32, 1, 8, 1), (
          # hi-res config (configs[4]): t = 1024 image tokens, heads = 12, r = 32; the maximum t;
          # Dh = 256 (ref-octo_base); a partial last a tile (t = 1000) and a tiny odd t
          (4, 1024, 64, 12, 32, 0), (2, 2048, 64, 1, 64, 0), (2, 26, 256, 3, 5, 0),
-         (3, 1000, 64, 2, 100, 3), (2, 3, 8, 1, 1, 0)]
+         (3, 1000, 64, 2, 100, 3), (2, 3, 8, 1, 1, 0),
+         # t = 1024 / 1000 with more than 256 (sample, a tile) pairs: the b-resident score kernel
+         # takes two a tiles per workgroup (and a partial last pair at t = 1000)
+         (20, 1024, 64, 2, 32, 1), (40, 1000, 64, 1, 50, 2)]
 
 
 @pytest.mark.parametrize("n,t,c,heads,r,flags", CASES)

@@ -18,6 +18,8 @@ for step in "$@"; do
     attn_bias) timeout -k 10 300 python -u tools/attn_bias.py ;;
     parity_exact) timeout -k 10 900 python -u tools/parity_exact.py --seeds=8 ;;
     dma_lab) timeout -k 10 120 tools/dma_lab ;;
+    tome_tests) timeout -k 10 400 $T tests/test_tome_gpu.py ;;
+    tome_bench) timeout -k 10 300 python -u tools/tome_bench.py ;;
     heads) timeout -k 10 300 $T tests/test_heads_gpu.py ;;
     golden) timeout -k 10 240 $T -s tests/test_golden_step_gpu.py ;;
     gpu_all) timeout -k 10 900 $T -m gpu tests ;;
