@@ -1348,6 +1348,18 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_bwd_res_kernel(
 // partials over 3 / 5 waves instead of 4 / 4: equal to summation order).
 // Phase-A waves of the 8 (a phase-B key block costs ~1.6x a phase-A query block: 3 + 5 waves
 // balance the two phases; the bias sums then run over 3 / 5 waves)
+#if MMT_RES_ABL == 9  // diagnostic build (tools/attn_stamps.py): per-wave phase stamps
+__device__ unsigned long long g_res8_stamps[8192 * 8 * 6];
+#define RES8_STAMP(i)                                                                     \
+  do {                                                                                    \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                          \
+    if (lane == 0 && blockIdx.x < 8192) g_res8_stamps[(blockIdx.x * 8 + wave) * 6 + (i)] = t_; \
+  } while (0)
+#else
+#define RES8_STAMP(i) \
+  do {                \
+  } while (0)
+#endif
 constexpr int RES8_NA = 3;
 template <int NTILE, bool DROP>
 __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
@@ -1381,12 +1393,14 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
   float* brow = bias_grad ? bias_grad + h * DH : nullptr;
   const float sc_out = g.scale * drop_scale;
 
+  RES8_STAMP(0);
   // ---- DMA of the four images (waves 0-3: K and V, waves 4-7: Q and dO)
   if (wave < RES_NW)
     res_dma2<ROWS>(smem, base + D + h * DH, g.s_t, base + 2 * D + h * DH, g.s_t, L, wave, lane);
   else
     res_dma2<ROWS>(smem + 2 * ROWS * DH, base + h * DH, g.s_t, dbase, d_s_t, L, wave - RES_NW, lane);
   __syncthreads();  // the DMA landed (vmcnt(0) + barrier)
+  RES8_STAMP(1);
   // ---- row constants of every query row: rc0 = -lse / scale (-inf past L), rc1 = -kp delta
   //      (0 past L); delta as the two-phase kernel forms it: chunks 0, 2, 4, 6 and 1, 3, 5, 7
   //      of the row as two fmaf chains, then their sum
@@ -1412,6 +1426,7 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
   // rc is read by the other waves (L2, no stale L1 line: first touch in this workgroup)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  RES8_STAMP(2);
 
   // bias sums: each wave's folded partials through LDS once every wave is done with the images
   // (two barriers in either branch), summed over the phase's 4 waves in wave order (as
@@ -1520,6 +1535,7 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
       res_store_rows(dq, sc_out, dqkv + (int64_t)b * dq_s_b + (int64_t)qc * dq_s_t + h * DH, qv, hh);
       if (brow) res_bias_fold(dq, bq);
     }
+    RES8_STAMP(3);
     if (brow) {
       __syncthreads();
       bias_out(bq, 0, sc_out);
@@ -1631,6 +1647,7 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
         res_bias_fold(dv, bv);
       }
     }
+    RES8_STAMP(3);
     if (brow) {
       __syncthreads();
       bias_out(bk, 0, sc_out);
@@ -1640,6 +1657,7 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
       else if (wave == RES8_NA + 1) bias_sum(1, RES8_NA, 2 * RES_NW - RES8_NA, brow + 2 * D);
     }
   }
+  RES8_STAMP(4);
 }
 
 // Host plan of the resident backward: the forward's query-side words and query-block deal, and
@@ -2173,6 +2191,14 @@ inline int bwd_threads(int L) {
     if (drop_bits) ATTN_BWD_LAUNCH2(DH_, NTT_, true);  \
     else ATTN_BWD_LAUNCH2(DH_, NTT_, false);           \
   } while (0)
+
+#if MMT_RES_ABL == 9
+extern "C" int mmt_res8_stamps(void* dst, int64_t bytes) {
+  const int64_t n = (int64_t)sizeof(g_res8_stamps);
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_res8_stamps), bytes < n ? bytes : n, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" int mmt_dropout_bits(const uint32_t* rng, uint32_t layer, uint32_t site, int rows,
                                 int cols, float keep_prob, uint32_t* out, uint32_t* out_t,

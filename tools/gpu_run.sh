@@ -20,6 +20,9 @@ for step in "$@"; do
     dma_lab) timeout -k 10 120 tools/dma_lab ;;
     tome_tests) timeout -k 10 400 $T tests/test_tome_gpu.py ;;
     tome_bench) timeout -k 10 300 python -u tools/tome_bench.py ;;
+    attn_tests) timeout -k 10 400 $T tests/test_attn_norm_gpu.py -k "attention or resident" ;;
+    attn_stamps) MMT_LIB_AB=multi_modal_transformers_tokenmerge_amd/libmmt_hip_abl9.so timeout -k 10 200 python -u tools/attn_stamps.py ;;
+    attn_bench) timeout -k 10 300 python -u tools/attn_bench.py --b=512 --L=292,228 ;;
     heads) timeout -k 10 300 $T tests/test_heads_gpu.py ;;
     golden) timeout -k 10 240 $T -s tests/test_golden_step_gpu.py ;;
     gpu_all) timeout -k 10 900 $T -m gpu tests ;;
