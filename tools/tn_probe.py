@@ -53,6 +53,9 @@ def main():
     shapes = [("MLP Dense_0 dW", 1536, 384, B * L2), ("MLP Dense_1 dW", 384, 1536, B * L2),
               ("QKV dW", 1152, 384, B * L1), ("out dW", 384, 384, B * L1),
               ("square 4096", 4096, 4096, 4096)]
+    for a in sys.argv[1:]:
+        if a.startswith("--shapes="):  # e.g. --shapes=0 (the headline dW only, for counter passes)
+            shapes = [shapes[int(i)] for i in a.split("=")[1].split(",")]
     for name, M, N, Kd in shapes:
         dy = (torch.rand((Kd, M), device=dev) * 2 - 1).bfloat16()
         x = (torch.rand((Kd, N), device=dev) * 2 - 1).bfloat16()
