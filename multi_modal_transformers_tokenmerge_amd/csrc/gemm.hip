@@ -1757,15 +1757,6 @@ __device__ __forceinline__ void vm_wait_slices(int y) {
     else vm_wait_slices<C, Y - 1>(y);
   }
 }
-// ds_read_b64_tr_b16 as inline asm (its lgkmcnt is waited explicitly: through the builtin the
-// compiler waited for the NEXT slice's reads before the current slice's MFMAs)
-template <int OFF>
-__device__ __forceinline__ short4v tr_read_asm(uint32_t addr) {
-  short4v v;
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
-  return v;
-}
-
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 template <int BM>
 __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma16_kernel(
@@ -1898,7 +1889,7 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_dma16_kernel(
 //     carried across K-steps, so every fragment read sits under MFMAs).
 // The 36 1-KB pieces of a step are dealt 3 A + 2 B to waves 0-3 and 3 A + 1 B to waves 4-7, each
 // wave waiting vmcnt(y x its own piece count) for the younger steps.
-template <int BM, int SPREAD>
+template <int BM>
 __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_r4_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
     int64_t ldb, float* __restrict__ slab, int split_k, int k_chunk, int tiles_n) {
@@ -1947,7 +1938,7 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_r4_kernel(
     else if (p == 3 || big)
       dma16_asm(B + (int64_t)k0 * ldb + n0, ((int64_t)(K - k0) * ldb - n0) * 2, S0 + ldso[p], voff[p]);
   };
-  auto issue = [&](int s) {
+  auto issue = [&](int s) {  // (issued between the MFMA groups instead: 7 % slower)
 #pragma unroll
     for (int p = 0; p < 5; ++p) piece(s, p);
   };
@@ -1988,8 +1979,7 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_r4_kernel(
     // the first MFMA (behind the next step's reads, as it did with the wait as inline asm)
     __builtin_amdgcn_s_waitcnt(0xC07F);
     asm volatile("s_barrier" ::: "memory");
-    const bool refill = s + NS < nk;
-    if (SPREAD == 0 && refill) issue(s + NS);
+    if (s + NS < nk) issue(s + NS);
     const char* As = smem + ((s + 1) % NS) * STAGE;
     const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -2003,7 +1993,6 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_r4_kernel(
 #pragma unroll
         for (int a = 0; a < MA; ++a) na[a] = frag(As, A_ROWB, wm * (16 * MA) + a * 16);
       bfr[b] = frag(Bs, B_ROWB, wn * 96 + b * 16);
-      if (SPREAD == 1 && refill && b < 5) piece(s + NS, b);  // one piece per B group
       __builtin_amdgcn_sched_barrier(0);  // B refilled in place: no read hoisted above its MFMAs
     }
   };
@@ -2034,365 +2023,6 @@ __global__ __launch_bounds__(TN_NT, 1) void gemm_tn_r4_kernel(
       *reinterpret_cast<float4*>(out + (int64_t)gr * N + gc) =
           make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
     }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// TN weight gradients, STAGGERED PING-PONG (round 5): gemm_tn_dma16_kernel's tile, stages,
-// swizzles and 16x16x32 MFMAs, but each wave alternates a load segment R (the fragments of one
-// k32 step: 24 ds_read_b64_tr_b16, plus DMA pieces) and a compute segment M (that step's 36
-// MFMAs), one s_barrier after every segment, and waves 4-7 (group Y) run one segment behind
-// waves 0-3 (group X) through one extra barrier at the start: the two waves on each SIMD (w and
-// w + 4) are always in opposite segments, so one wave's MFMAs cover its partner's LDS reads and
-// DMA issue (MI355X_MICROARCH.md two waves per SIMD, items 1-3 and 9; the 8-phase template of
-// cdna_hip_programming.md §5). One fragment register set per wave (read, then consumed): 192
-// registers of fragments + accumulators.
-// Slots (barrier intervals) of K-step t (stage t & 1), X / Y:
-//   4t: R(t,0) / M(t-1,1)   4t+1: M(t,0) / R(t,0)   4t+2: R(t,1) / M(t,0)   4t+3: M(t,1) / R(t,1)
-// Stage (t+1) & 1 is free from slot 4t (every wave's reads of K-step t - 1 ended with slot 4t-1):
-// X issues its DMA pieces of K-step t + 1 in R(t,0) (XD 0) or between the MFMAs of M(t,0)
-// (XD 1), Y issues those of K-step t + 1 between the MFMAs of M(t-1,1) (slot 4t); each wave waits
-// for them before the barrier that ends slot 4t + 3 (X: end of M(t,1), Y: end of R(t,1)), the
-// first read of K-step t + 1 being X's R(t+1,0) in slot 4t + 4. Results equal gemm_tn_dma16's
-// (same per-k32 MFMA order).
-template <int BM, int XD, bool PRIO>
-__global__ __launch_bounds__(TN_NT, 1) void gemm_tn_pp_kernel(
-    int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
-    int64_t ldb, float* __restrict__ slab, int split_k, int k_chunk, int tiles_n) {
-  static_assert(BM == 256 || BM == 384, "tile height");
-  constexpr int MA = BM / 64;                                       // 16-row A blocks per wave
-  constexpr int A_ROWB = BM * 2, B_ROWB = TN_BN * 2;
-  constexpr int A_CH = A_ROWB / 16;
-  constexpr int A_BYTES = 64 * A_ROWB, B_BYTES = 64 * B_ROWB, STAGE = A_BYTES + B_BYTES;
-  constexpr int GA = A_BYTES / 1024 / 8, GB = B_BYTES / 1024 / 8;
-  constexpr int G = GA + GB;                                        // pieces per wave per K-step
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool isY = wave >= 4;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int tiles = ((M + BM - 1) / BM) * tiles_n;
-  const int wi = xcd_remap(blockIdx.x, gridDim.x);
-  const int z = wi / tiles, t0 = wi - z * tiles;
-  const int tm = t0 / tiles_n;
-  const int m0 = tm * BM, n0 = (t0 - tm * tiles_n) * TN_BN;
-  const int kbeg = z * k_chunk, kend = min(K, kbeg + k_chunk);
-  const int nk = max(0, (kend - kbeg + 63) / 64);
-  auto swA = [](int r) { return (4 * (r & 3)) ^ (2 * ((r >> 3) & 1)); };
-  auto swB = [](int r) { return (2 * (r & 3)) ^ (2 * ((r >> 3) & 1)); };
-  int voff[G];
-#pragma unroll
-  for (int p = 0; p < G; ++p) {
-    if (p < GA) {
-      const int j = wave * GA + p, e = j * 64 + lane, row = e / A_CH, c = (e % A_CH) ^ swA(row);
-      voff[p] = row * (int)(lda * 2) + c * 16;
-    } else {
-      const int j = wave * GB + (p - GA), e = j * 64 + lane, row = e / 24, c = (e % 24) ^ swB(row);
-      voff[p] = row * (int)(ldb * 2) + c * 16;
-    }
-  }
-  auto piece = [&](int kt, int p) {  // piece p of this wave for K-step kt, into stage kt & 1
-    const int k0 = kbeg + kt * 64;
-    char* S0 = smem + (kt & 1) * STAGE;
-    if (p < GA)
-      dma16_asm(A + (int64_t)k0 * lda + m0, ((int64_t)(K - k0) * lda - m0) * 2,
-                S0 + (wave * GA + p) * 1024, voff[p]);
-    else
-      dma16_asm(B + (int64_t)k0 * ldb + n0, ((int64_t)(K - k0) * ldb - n0) * 2,
-                S0 + A_BYTES + (wave * GB + (p - GA)) * 1024, voff[p]);
-  };
-  f32x4_t acc[MA][6];
-#pragma unroll
-  for (int a = 0; a < MA; ++a)
-#pragma unroll
-    for (int b = 0; b < 6; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[a][b][q] = 0.f;
-  // per-lane LDS byte address of each fragment's first k-row in stage 0, k32 step 0 (the k-row
-  // swizzle is invariant under + 4 and + 32 rows: the other read and step are offsets)
-  const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g16 = lane >> 4;
-  const int k1 = 8 * g16 + q4;
-  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
-  uint32_t aad[MA], bad[6];
-#pragma unroll
-  for (int a = 0; a < MA; ++a) {
-    const int col = wm * (16 * MA) + a * 16 + 4 * p4;
-    aad[a] = lds0 + k1 * A_ROWB + (((col >> 3) ^ swA(k1)) << 4) + (col & 7) * 2;
-  }
-#pragma unroll
-  for (int b = 0; b < 6; ++b) {
-    const int col = wn * 96 + b * 16 + 4 * p4;
-    bad[b] = lds0 + A_BYTES + k1 * B_ROWB + (((col >> 3) ^ swB(k1)) << 4) + (col & 7) * 2;
-  }
-  auto pack = [](short4v v1, short4v v2) {
-    short __attribute__((ext_vector_type(8))) v = {v1[0], v1[1], v1[2], v1[3],
-                                                   v2[0], v2[1], v2[2], v2[3]};
-    return __builtin_bit_cast(bf16x8, v);
-  };
-  bf16x8 af[MA], bfr[6];
-  auto bar = [] {
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  // R: one k32 step's fragments (24 reads), waited for within the segment
-  auto R = [&](int kt, int ks) {
-    const uint32_t so = (uint32_t)((kt & 1) * STAGE + ks * 32 * A_ROWB);
-    const uint32_t sb = (uint32_t)((kt & 1) * STAGE + ks * 32 * B_ROWB);
-#pragma unroll
-    for (int a = 0; a < MA; ++a)
-      af[a] = pack(tr_read_asm<0>(aad[a] + so), tr_read_asm<4 * A_ROWB>(aad[a] + so));
-#pragma unroll
-    for (int b = 0; b < 6; ++b)
-      bfr[b] = pack(tr_read_asm<0>(bad[b] + sb), tr_read_asm<4 * B_ROWB>(bad[b] + sb));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  };
-  // M: 6 x MA MFMAs, b-outer; with dk >= 0 this wave's DMA pieces of K-step dk between the
-  // b-groups (G pieces over 6 groups)
-  auto Mseg = [&](int dk) {
-    if (PRIO && isY) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int b = 0; b < 6; ++b) {
-#pragma unroll
-      for (int a = 0; a < MA; ++a)  // operands swapped: the accumulator holds C^T
-        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (dk >= 0) {
-#pragma unroll
-        for (int p = b * G / 6; p < (b + 1) * G / 6; ++p) piece(dk, p);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (PRIO && isY) __builtin_amdgcn_s_setprio(0);
-  };
-  auto vm0 = [] { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
-
-  // prologue: K-step 0 (every wave), and Y's pieces of K-step 1 (Y issues one K-step further
-  // ahead, in the M segment of slot 4t for K-step t + 1)
-  if (nk > 0)
-#pragma unroll
-    for (int p = 0; p < G; ++p) piece(0, p);
-  if (isY && nk > 1) {
-#pragma unroll
-    for (int p = 0; p < G; ++p) piece(1, p);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-  } else {
-    vm0();
-  }
-  bar();
-  if (isY) bar();  // the stagger: Y one barrier interval behind X
-  // one instruction stream for both groups; X and Y differ in where they issue DMA / wait:
-  //   X: DMA(t+1) in R(t,0) (XD 0) or M(t,0) (XD 1), wait at the end of M(t,1)
-  //   Y: DMA(t+2) in M(t,1), wait at the end of R(t,1)
-  for (int t = 0; t < nk; ++t) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      if (XD == 0 && !isY && ks == 0 && t + 1 < nk) {
-#pragma unroll
-        for (int p = 0; p < G; ++p) piece(t + 1, p);
-      }
-      R(t, ks);
-      if (isY && ks == 1) vm0();
-      bar();
-      const int dk = ks == 0 ? ((XD == 1 && !isY && t + 1 < nk) ? t + 1 : -1)
-                             : ((isY && t + 2 < nk) ? t + 2 : -1);
-      Mseg(dk);
-      if (!isY && ks == 1) vm0();
-      bar();
-    }
-  }
-  if (!isY) bar();  // balances Y's extra barrier
-  float* out = slab + (int64_t)z * M * N;
-#pragma unroll
-  for (int a = 0; a < MA; ++a) {
-    const int gr = m0 + wm * (16 * MA) + a * 16 + (lane & 15);
-    if (gr >= M) continue;
-#pragma unroll
-    for (int b = 0; b < 6; ++b) {
-      const int gc = n0 + wn * 96 + b * 16 + 4 * g16;
-      if (gc >= N) continue;
-      *reinterpret_cast<float4*>(out + (int64_t)gr * N + gc) =
-          make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Weight-gradient (TN) split-K partial products on a SLICE RING (round 5). Same operands, tile
-// (BM x 192, 8 waves of (32 MB) x 96, 32x32x16 MFMAs with the accumulator holding C^T), chunk
-// swizzles, fragment reads and k order as gemm_tn_dma_kernel — the slabs are bit-identical — but
-// the LDS is a ring of NS slices of 16 k-rows (one MFMA k-step: 18 KB at BM 384) instead of two
-// 64-deep K-steps, so the DMA runs NS - 2 slices ahead of the slice whose fragments are being
-// read (BM 384, NS 8: 6 slices = 108 KB in flight per CU, 96 k-rows of lead) where the two-stage
-// kernel had one K-step (72 KB, 64 rows) and then waited on it (SQ_WAIT_ANY 52 % of wave cycles,
-// profiles/r02_b512_probe_sq.txt). Per slice j, after one s_barrier (every wave's DMA of slice
-// j + 1 landed, every wave past slice j - 1's MFMAs):
-//   * the fragments of slice j + 1 are read (ds_read_b64_tr_b16) into the other register set,
-//   * the DMA of slice j + NS - 1 goes into slice j - 1's slot,
-//   * 3 x MB MFMAs consume slice j's fragments (read one slice earlier: never exposed).
-// The 18 (14 at BM 256) 1-KB pieces of a slice are dealt wave-contiguously (waves 0-1 three,
-// 2-7 two at BM 384), so each wave waits vmcnt(y x its piece count) for the slices younger than
-// j + 1. PRIO: waves 4-7 at s_setprio 1 for the whole loop (MI355X_MICROARCH.md, two waves per
-// SIMD item 4).
-template <int BM, int NS, bool PRIO>
-__global__ __launch_bounds__(TN_NT, 1) void gemm_tn_ring_kernel(
-    int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
-    int64_t ldb, float* __restrict__ slab, int split_k, int k_chunk, int tiles_n) {
-  static_assert(BM == 256 || BM == 384, "tile height");
-  constexpr int MB = BM / 128;                                      // 32-row MFMA blocks per wave
-  constexpr int SK = 16;                                            // k-rows per slice
-  constexpr int A_ROWB = BM * 2, B_ROWB = TN_BN * 2;                // bytes per k-row
-  constexpr int A_CH = A_ROWB / 16;                                 // 16-B chunks per A k-row
-  constexpr int A_BYTES = SK * A_ROWB, B_BYTES = SK * B_ROWB, SLOT = A_BYTES + B_BYTES;
-  constexpr int PA = A_BYTES / 1024, PT = SLOT / 1024;              // A pieces, all pieces
-  static_assert(A_BYTES % 1024 == 0 && B_BYTES % 1024 == 0, "1-KB pieces");
-  static_assert(NS >= 4 && NS * SLOT <= 163840, "LDS ring");
-  constexpr int GMAX = (PT + 7) / 8;                                // pieces of the fuller waves
-  constexpr int NBIG = PT - 8 * (GMAX - 1);                         // waves issuing GMAX pieces
-  static_assert(GMAX >= 2 && (NS - 2) * GMAX < 64, "vmcnt");
-  static_assert(PA % 2 == 0 && (GMAX == 2 || NBIG * GMAX % 2 == 0), "pieces of one operand per wave");
-  __shared__ __attribute__((aligned(16))) char smem[NS * SLOT];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 1, wn = wave & 1, hl = lane >> 5;
-  const int tiles = ((M + BM - 1) / BM) * tiles_n;
-  const int wi = xcd_remap(blockIdx.x, gridDim.x);
-  const int z = wi / tiles, t = wi - z * tiles;
-  const int tm = t / tiles_n;
-  const int m0 = tm * BM, n0 = (t - tm * tiles_n) * TN_BN;
-  const int kbeg = z * k_chunk, kend = min(K, kbeg + k_chunk);
-  const int nk = max(0, (kend - kbeg + SK - 1) / SK);
-  auto swA = [](int r) { return 4 * (r & 3); };
-  auto swB = [](int r) { return 2 * (r & 3); };
-  // this wave's pieces: p0 .. p0 + cnt - 1 of every slice (wave-contiguous)
-  const bool big = wave < NBIG;
-  const int p0 = (GMAX - 1) * wave + min(wave, NBIG);
-  int voff[GMAX];
-#pragma unroll
-  for (int i = 0; i < GMAX; ++i) {
-    const int j = min(p0 + i, PT - 1);
-    if (j < PA) {
-      const int e = j * 64 + lane, row = e / A_CH, c = (e % A_CH) ^ swA(row);
-      voff[i] = row * (int)(lda * 2) + c * 16;
-    } else {
-      const int e = (j - PA) * 64 + lane, row = e / 24, c = (e % 24) ^ swB(row);
-      voff[i] = row * (int)(ldb * 2) + c * 16;
-    }
-  }
-  // a wave's pieces never straddle the A / B boundary (PA even, pieces dealt in pairs from an
-  // even start): one operand, one buffer resource per slice
-  const bool isA = p0 < PA;
-  const bf16_t* const P = isA ? A + m0 : B + n0;
-  const int64_t ldp = isA ? lda : ldb, c0 = isA ? m0 : n0;
-  auto issue = [&](int s) {  // slice s (k-rows kbeg + 16 s ..) into slot s % NS
-    const int k0 = kbeg + s * SK;
-    char* S0 = smem + (s % NS) * SLOT + p0 * 1024;
-    const bf16_t* base = P + (int64_t)k0 * ldp;
-    const int64_t bytes = ((int64_t)(K - k0) * ldp - c0) * 2;
-#pragma unroll
-    for (int i = 0; i < GMAX; ++i) {
-      if (i == GMAX - 1 && !big) break;
-      dma16_asm(base, bytes, S0 + i * 1024, voff[i]);
-    }
-  };
-  // wait until this wave's pieces of every slice older than the y youngest issued have landed
-  // (y <= NS - 3 in the loop, <= NS - 2 after the prologue)
-  auto wait_slices = [&](int y) {
-    if (big) vm_wait_slices<GMAX, NS - 3>(y);
-    else vm_wait_slices<GMAX - 1, NS - 3>(y);
-  };
-
-  floatx16 acc[MB][3];
-#pragma unroll
-  for (int a = 0; a < MB; ++a)
-#pragma unroll
-    for (int b = 0; b < 3; ++b)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[a][b][q] = 0.f;
-
-  // fragment of rows rbase.. for the slice in LDS: lane (i = lane & 15: k-row q = i >> 2, column
-  // group p4 = i & 3; g = lane >> 4; h = lane >> 5) reads 4 columns of k-rows k1 and k1 + 4 (the
-  // chunk swizzle of k1 + 4 equals k1's); per lane one LDS byte address per fragment, the slot
-  // added per slice
-  const int i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3, g16 = lane >> 4;
-  const int k1 = 8 * hl + q4;
-  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
-  auto faddr = [&](int rowb, int sw, int rbase) {
-    const int col = rbase + 16 * (g16 & 1) + 4 * p4;
-    return (uint32_t)(k1 * rowb + (((col >> 3) ^ sw) << 4) + (col & 7) * 2);
-  };
-  uint32_t aad[MB], bad[3];
-#pragma unroll
-  for (int a = 0; a < MB; ++a) aad[a] = lds0 + faddr(A_ROWB, swA(k1), wm * (32 * MB) + a * 32);
-#pragma unroll
-  for (int b = 0; b < 3; ++b) bad[b] = lds0 + A_BYTES + faddr(B_ROWB, swB(k1), wn * 96 + b * 32);
-  auto pack = [](short4v v1, short4v v2) {
-    short __attribute__((ext_vector_type(8))) v = {v1[0], v1[1], v1[2], v1[3],
-                                                   v2[0], v2[1], v2[2], v2[3]};
-    return __builtin_bit_cast(bf16x8, v);
-  };
-  bf16x8 fa0[MB], fb0[3], fa1[MB], fb1[3];
-  auto read_slice = [&](int s, bf16x8 (&fa)[MB], bf16x8 (&fb)[3]) {
-    const uint32_t so = (uint32_t)((s % NS) * SLOT);
-#pragma unroll
-    for (int a = 0; a < MB; ++a)
-      fa[a] = pack(tr_read_asm<0>(aad[a] + so), tr_read_asm<4 * A_ROWB>(aad[a] + so));
-#pragma unroll
-    for (int b = 0; b < 3; ++b)
-      fb[b] = pack(tr_read_asm<0>(bad[b] + so), tr_read_asm<4 * B_ROWB>(bad[b] + so));
-  };
-  // one slice: wait for slice j + 1, barrier, read j + 1, refill slot (j - 1), MFMAs on slice j
-  // (whose fragments the previous slice read and waited for)
-  auto body = [&](int j, bf16x8 (&ca)[MB], bf16x8 (&cb)[3], bf16x8 (&na)[MB], bf16x8 (&nb)[3]) {
-    if (j + 1 < nk) wait_slices(min(NS - 3, nk - 2 - j));
-    asm volatile("s_barrier" ::: "memory");
-    if (j + 1 < nk) read_slice(j + 1, na, nb);
-    if (j + NS - 1 < nk) issue(j + NS - 1);
-    __builtin_amdgcn_sched_barrier(0);  // reads and DMA issued before the MFMAs
-#pragma unroll
-    for (int a = 0; a < MB; ++a)
-#pragma unroll
-      for (int b = 0; b < 3; ++b)  // operands swapped: the accumulator holds C^T
-        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cb[b], ca[a], acc[a][b], 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slice j + 1's fragments in registers
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  if (PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  // prologue: slices 0 .. NS - 2, then slice 0's fragments
-#pragma unroll
-  for (int q = 0; q < NS - 1; ++q)
-    if (q < nk) issue(q);
-  if (nk > 0) {
-    if (big) vm_wait_slices<GMAX, NS - 2>(min(NS - 2, nk - 1));
-    else vm_wait_slices<GMAX - 1, NS - 2>(min(NS - 2, nk - 1));
-    asm volatile("s_barrier" ::: "memory");
-    read_slice(0, fa0, fb0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  for (int j = 0; j < nk; j += 2) {
-    body(j, fa0, fb0, fa1, fb1);
-    if (j + 1 < nk) body(j + 1, fa1, fb1, fa0, fb0);
-  }
-  if (PRIO && wave >= 4) __builtin_amdgcn_s_setprio(0);
-  // fp32 slab z: lane (m = lane & 31, h) of block (a, b) holds row m, columns 8g + 4h + {0..3}
-  float* out = slab + (int64_t)z * M * N;
-#pragma unroll
-  for (int a = 0; a < MB; ++a) {
-    const int gr = m0 + wm * (32 * MB) + a * 32 + (lane & 31);
-    if (gr >= M) continue;
-#pragma unroll
-    for (int b = 0; b < 3; ++b)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int gc = n0 + wn * 96 + b * 32 + 8 * g + 4 * hl;
-        if (gc >= N) continue;
-        *reinterpret_cast<float4*>(out + (int64_t)gr * N + gc) =
-            make_float4(acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2],
-                        acc[a][b][4 * g + 3]);
-      }
   }
 }
 
@@ -3567,55 +3197,27 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     static const int g_tn_bm = getenv("MMT_TN_BM") ? atoi(getenv("MMT_TN_BM")) : 384;
     const bool tall = g_tn_bm == 384 && M % 384 == 0 && g_variant != 9;
     const int work = ((M + (tall ? 383 : 255)) / (tall ? 384 : 256)) * tn * split_k;
-    // kernel choice (A/B knobs: g_variant 10-17 via mmt_gemm_set_variant, or MMT_TN_KERNEL):
+    // kernel choice (A/B knobs: g_variant 10, 13, 18 via mmt_gemm_set_variant, or MMT_TN_KERNEL):
     //   13 (default) the two-stage kernel on 16x16x32 MFMAs (gemm_tn_dma16_kernel): round 5,
     //      +1.6-3.4 % over 10 at the step's dW shapes (tools/tn_probe.py, interleaved rounds);
     //   10 the two-stage kernel on 32x32x16 (gemm_tn_dma_kernel);
-    //   11 / 12 the slice ring (gemm_tn_ring_kernel; 12 with static priority): 12-17 % slower;
-    //   14-17 the staggered ping-pong (gemm_tn_pp_kernel): 5-12 % slower than 13;
-    //   18 / 19 the four-stage ring of 32-row K-steps (gemm_tn_r4_kernel; 384-row tiles only;
-    //      19 issues the DMA pieces between the MFMA groups): 4-6 % slower than 13 on K chunks of
-    //      4,416 rows, 4 % faster on the out-projection's 1,216-row chunks (its deeper prologue),
-    //      so the default takes it for chunks of at most 2,048 rows (bit-identical slabs)
+    //   18 the four-stage ring of 32-row K-steps (gemm_tn_r4_kernel; 384-row tiles only): 4-6 %
+    //      slower than 13 on K chunks of 4,416 rows, 4 % faster on the out-projection's 1,216-row
+    //      chunks (its deeper prologue), so the default takes it for chunks of at most 2,048 rows
+    //      (bit-identical slabs).
+    // Measured and removed in round 5: a 16-row slice ring, a staggered ping-pong,
+    // the ring with its DMA between the MFMA groups, the ring in two barrier-separated phases
     static const int g_tn_kernel = getenv("MMT_TN_KERNEL") ? atoi(getenv("MMT_TN_KERNEL")) : 13;
-    const int tnk = (g_variant >= 10 && g_variant <= 19) ? g_variant : g_tn_kernel;
-    const int ring = tnk == 11 ? 1 : tnk == 12 ? 2 : 0;
-    if (tnk >= 14 && tnk <= 17) {  // ping-pong: 14 XD0, 15 XD1, 16 XD0+prio, 17 XD1+prio
-#define TNPP(BM_, XD_, PR_)                                                                      \
-  hipLaunchKernelGGL((gemm_tn_pp_kernel<BM_, XD_, PR_>), dim3(work), dim3(TN_NT), 0, s, M, N, K, \
-                     (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn)
-      if (tall) {
-        if (tnk == 14) TNPP(384, 0, false);
-        else if (tnk == 15) TNPP(384, 1, false);
-        else if (tnk == 16) TNPP(384, 0, true);
-        else TNPP(384, 1, true);
-      } else {
-        if (tnk == 14) TNPP(256, 0, false);
-        else if (tnk == 15) TNPP(256, 1, false);
-        else if (tnk == 16) TNPP(256, 0, true);
-        else TNPP(256, 1, true);
-      }
-#undef TNPP
-    } else if (tnk == 19 && tall)
-      hipLaunchKernelGGL((gemm_tn_r4_kernel<384, 1>), dim3(work), dim3(TN_NT), 0, s, M, N, K,
-                         (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
-    else if ((tnk == 18 || (tnk == 13 && g_variant < 10 && k_chunk <= 2048)) && tall)
-      hipLaunchKernelGGL((gemm_tn_r4_kernel<384, 0>), dim3(work), dim3(TN_NT), 0, s, M, N, K,
+    const int tnk = (g_variant == 10 || g_variant == 13 || g_variant == 18) ? g_variant : g_tn_kernel;
+    if ((tnk == 18 || (tnk == 13 && g_variant < 10 && k_chunk <= 2048)) && tall)
+      hipLaunchKernelGGL(gemm_tn_r4_kernel<384>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
                          (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
     else if (tnk == 13 && tall)
       hipLaunchKernelGGL(gemm_tn_dma16_kernel<384>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
                          (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
-    else if (tnk == 13 || tnk == 18 || tnk == 19)
+    else if (tnk == 13 || tnk == 18)
       hipLaunchKernelGGL(gemm_tn_dma16_kernel<256>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
                          (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
-    else if (ring && tall)
-      hipLaunchKernelGGL((ring == 2 ? gemm_tn_ring_kernel<384, 8, true> : gemm_tn_ring_kernel<384, 8, false>),
-                         dim3(work), dim3(TN_NT), 0, s, M, N, K, (const bf16_t*)A, lda,
-                         (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
-    else if (ring)
-      hipLaunchKernelGGL((ring == 2 ? gemm_tn_ring_kernel<256, 10, true> : gemm_tn_ring_kernel<256, 10, false>),
-                         dim3(work), dim3(TN_NT), 0, s, M, N, K, (const bf16_t*)A, lda,
-                         (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
     else if (tall)
       hipLaunchKernelGGL(gemm_tn_dma_kernel<384>, dim3(work), dim3(TN_NT), 0, s, M, N, K,
                          (const bf16_t*)A, lda, (const bf16_t*)B, ldb, workspace, split_k, k_chunk, tn);
