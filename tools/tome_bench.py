@@ -49,7 +49,7 @@ def graph_time(fn, reps=20):
 def main():
     dev = torch.device("cuda")
     out = []
-    shapes = [(n, 292, 32, 256, 16, 384, 6, 64) for n in (64, 256)] + \
+    shapes = [(n, 292, 32, 256, 16, 384, 6, 64) for n in (64, 256, 512)] + \
         [(n, 1060, 32, 1024, 32, 768, 12, 64) for n in (16, 64)]      # OCTO-base hi-res block 0
     for n, L, s0, t, r, D, H, c in shapes:
         g = torch.Generator(device="cpu").manual_seed(n)
