@@ -479,8 +479,11 @@ def main():
     # N > 1: the backward runs as --overlap-stages block-range stages, each stage's gradient
     # region all-reduced asynchronously while the later stages compute (distributed.DDPStep)
     ov = args.overlap_stages
+    # the frozen T5 encoder of the next step's text runs beside this step's backward (one T5
+    # forward per step either way; the synthetic batch repeats, so the next text is txt)
+    t5_pipe = model.has_text and os.environ.get("MMT_T5_PIPELINE", "1") != "0"
     step = DDPStep(model, state, txt, img, act, reducer, stages=int(ov) if ov.isdigit() else ov,
-                   use_graph=use_graph).build()
+                   use_graph=use_graph, txt_next=txt if t5_pipe else None).build()
     loss_buf = step.loss_buf
 
     for _ in range(args.warmup):
@@ -555,6 +558,7 @@ def main():
                                    f"ToMe r={cfg.tome_r}/block, {cfg.num_blocks} blocks",
                        "global_batch": N * B, "per_gpu_batch": B, "seq_len": sets0.L,
                        "parallelism": f"dp{N}", "hip_graph": use_graph,
+                       "t5_next_step_overlap": t5_pipe,
                        "deterministic": os.environ.get("MMT_DETERMINISTIC", "0") == "1",
                        **({"overrides": over} if over else {}),
                        **({"fp8_weight_path": True} if cfg.fp8 else {})},

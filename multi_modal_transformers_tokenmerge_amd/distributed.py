@@ -86,10 +86,25 @@ class DDPStep:
     * use_graph False: the same schedules launched eagerly (the overlap still applies).
     The 1/N average is AdamW's grad_scale (reducer.grad_scale)."""
 
+    # Cross-step T5 pipeline (txt_next given): the frozen T5 encoder's output for the NEXT
+    # step's text is computed on a side stream while this step's backward runs (the encoder has
+    # no trainable parameter, so its output does not depend on this step's update), and the
+    # forward takes the output computed one step earlier. Every step still runs exactly one T5
+    # forward; it moves from the head of the forward, where nothing else can run (the sequence
+    # assembly needs the text), to beside the backward's kernels. txt_next: the device buffer
+    # holding the NEXT step's token ids when a step is called (a loader prefetching one batch
+    # ahead writes them there; bench.py's synthetic batch repeats, so it passes txt itself).
+    # build() (or the first call) runs the first step's encoder ahead, once.
+
     def __init__(self, model, state, txt, img, act, reducer: GradAllReducer | None = None,
-                 stages="auto", use_graph: bool = True):
+                 stages="auto", use_graph: bool = True, txt_next=None):
         self.model, self.state = model, state
         self.txt, self.img, self.act = txt, img, act
+        self.t5_pf = (txt_next is not None and txt is not None
+                      and getattr(model, "t5", None) is not None)
+        self.txt_next = txt_next
+        self.t5_cur = self.t5_nxt = None
+        self._t5_side = torch.cuda.Stream(device=model.device) if self.t5_pf else None
         self.reducer = reducer
         self.distributed = reducer is not None and reducer.world_size > 1
         # the backward's stage split (Octo.stage_bounds: an int, a list or "auto[:MB]")
@@ -107,23 +122,64 @@ class DDPStep:
         self._st = {}
 
     # --------------------------------------------------------------- schedule pieces
+    def _t5_prime(self):
+        """The first step's T5 output (outside the timed steps: the one encoder run the pipeline
+        moves ahead of step 1)."""
+        if self.t5_pf and self.t5_cur is None:
+            self.t5_cur = self.model.t5(self.txt).clone()
+            self.t5_nxt = torch.empty_like(self.t5_cur)
+
+    def _t5_fork(self):
+        """Next step's T5 on the side stream, forked after this step's forward."""
+        side = self._t5_side
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self.t5_nxt.copy_(self.model.t5(self.txt_next))
+
+    def _t5_join(self):
+        """After the backward (the text projection's dW read t5_cur): the next output becomes
+        the current one."""
+        torch.cuda.current_stream().wait_stream(self._t5_side)
+        self.t5_cur.copy_(self.t5_nxt)
+
+    # where the next step's encoder forks: "fwd" at the step's start (default: beside the forward
+    # and the backward), "bwd" after the forward (benchmarking knob MMT_T5_FORK; 12 584 vs
+    # 12 387 samples/s at B = 128, 16 226 vs 16 179 at B = 512, profiles/r05_t5_overlap_ab.txt)
+    t5_fork_at = os.environ.get("MMT_T5_FORK", "fwd")
+
     def _fwd_bwd(self):
         m, s = self.model, self.state
         m.store.zero_grad()
+        early = self.t5_pf and self.t5_fork_at == "fwd"
+        if early:
+            self._t5_fork()
         loss, st = m.compute_diffusion_denoise_loss(self.txt, self.img, self.act, True, s.rng,
-                                                    s.sample_offset)
+                                                    s.sample_offset, t5_out=self.t5_cur)
+        if self.t5_pf and not early:
+            self._t5_fork()
         m.backward(st)
+        if self.t5_pf:
+            self._t5_join()
         self.loss_buf.copy_(loss)
 
     def _stage(self, k):
         m, s = self.model, self.state
+        early = self.t5_pf and self.t5_fork_at == "fwd"
         if k == 0:
             m.store.zero_grad()
+            if early:
+                self._t5_fork()
             loss, st = m.compute_diffusion_denoise_loss(self.txt, self.img, self.act, True, s.rng,
-                                                        s.sample_offset)
+                                                        s.sample_offset, t5_out=self.t5_cur)
             self.loss_buf.copy_(loss)
             self._st["st"] = st
+            if self.t5_pf and not early:
+                self._t5_fork()
         m.backward_stage(self._st["st"], k, self.bounds)
+        if self.t5_pf and k == 0:  # joined inside the stage's graph (a graph is self-contained)
+            torch.cuda.current_stream().wait_stream(self._t5_side)
+        if self.t5_pf and k == self.S - 1:  # after the text projection's dW (the last stage)
+            self.t5_cur.copy_(self.t5_nxt)
 
     def _opt(self):
         self.state.apply_gradients()
@@ -168,6 +224,7 @@ class DDPStep:
         checks every buffer bitwise). The snapshot holds one extra copy of the fp32 master, the
         bf16 shadow and both AdamW moments during build(): 14 bytes per parameter (≈ 315 MB for
         OCTO-small's 22.5 M, ≈ 1.2 GB for OCTO-base), freed before capture."""
+        self._t5_prime()
         if not self.use_graph:
             return self
         if self._hp_on and self._hp is None:
@@ -185,6 +242,8 @@ class DDPStep:
         torch.cuda.synchronize()
         self._restore(snap)
         del snap
+        if self.t5_pf:  # the warm-up steps handed txt_next's encoder output over: this step's again
+            self.t5_cur.copy_(self.model.t5(self.txt))
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
 
@@ -223,6 +282,7 @@ class DDPStep:
 
     def _run(self):
         g = self.graphs
+        self._t5_prime()
         if self.S > 1:
             works = []
             for k in range(self.S):

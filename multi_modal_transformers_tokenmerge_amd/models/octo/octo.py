@@ -193,15 +193,18 @@ class Octo:
 
     # ------------------------------------------------------------------ forward / backward
     def generate_readouts(self, text_tokens, images, train=True, rng=None, sample_offset=0,
-                          positions=None, tome=None):
-        """Reference :91-126. Returns the final sequence (B, L_final, D) and the saved state."""
+                          positions=None, tome=None, t5_out=None):
+        """Reference :91-126. Returns the final sequence (B, L_final, D) and the saved state.
+        t5_out: the frozen T5 encoder's output for text_tokens, computed ahead (DDPStep's
+        cross-step T5 pipeline); None runs the encoder here."""
         B = images.shape[0]
         D = self.D
         st: Dict = dict(B=B, train=train, rng=rng, sample_offset=sample_offset)
         txt, T = None, max(self.n_text, 1)
         if self.has_text:
-            with phase("fwd/t5"):
-                t5_out = self.t5(text_tokens)                               # stop_gradient
+            if t5_out is None:
+                with phase("fwd/t5"):
+                    t5_out = self.t5(text_tokens)                           # stop_gradient
             st["t5_out"] = t5_out
             if self.text_proj is not None:
                 txt = self.text_proj.fwd(t5_out.view(B * self.n_text, -1)).view(B, self.n_text, D)
@@ -227,13 +230,14 @@ class Octo:
         return xL, st
 
     def compute_diffusion_denoise_loss(self, text_tokens, images, actions, train=True, rng=None,
-                                       sample_offset=0, inject: Optional[dict] = None):
+                                       sample_offset=0, inject: Optional[dict] = None, t5_out=None):
         """Reference :139-145. Returns (loss (1,) fp32 device tensor, saved state). inject (tests):
         positions (rt, ct), t, eps, tome (per block an (unm, src, dst) triple of int32 device
-        tensors or None) replace the step's own draws / matching."""
+        tensors or None) replace the step's own draws / matching. t5_out: the frozen encoder's
+        output for text_tokens computed ahead (generate_readouts)."""
         inject = inject or {}
         xL, st = self.generate_readouts(text_tokens, images, train, rng, sample_offset,
-                                        inject.get("positions"), inject.get("tome"))
+                                        inject.get("positions"), inject.get("tome"), t5_out)
         B = xL.shape[0]
         cat = self.head.new_cat(B, xL.device)
         _C.call("mmt_rows_mean_fwd", _C.ptr(xL), xL.stride(0), xL.stride(1), B, self.D,
