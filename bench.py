@@ -496,8 +496,11 @@ def main():
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
     evs[0].record(cur)
+    host_s = 0.0  # host time inside step() (the graph launch enqueues every node from the CPU)
     for i in range(args.steps):
+        h0 = time.perf_counter()
         step()
+        host_s += time.perf_counter() - h0
         evs[i + 1].record(cur)  # step boundaries (a step ends with AdamW on this stream)
     torch.cuda.synchronize()
     if di.enabled:
@@ -549,6 +552,7 @@ def main():
             "value": round(value, 2), "unit": "samples/s", "n_gpus": N, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3),
             "median_ms_per_step": round(float(np.median(step_ms)), 3),
+            "host_ms_per_step_call": round(host_s / args.steps * 1e3, 3),
             "p10_p90_ms_per_step": [round(float(np.percentile(step_ms, 10)), 3),
                                     round(float(np.percentile(step_ms, 90)), 3)],
             "higher_is_better": True,

@@ -87,14 +87,14 @@ class DDPStep:
     The 1/N average is AdamW's grad_scale (reducer.grad_scale)."""
 
     # Cross-step T5 pipeline (txt_next given): the frozen T5 encoder's output for the NEXT
-    # step's text is computed on a side stream while this step's backward runs (the encoder has
-    # no trainable parameter, so its output does not depend on this step's update), and the
-    # forward takes the output computed one step earlier. Every step still runs exactly one T5
-    # forward; it moves from the head of the forward, where nothing else can run (the sequence
-    # assembly needs the text), to beside the backward's kernels. txt_next: the device buffer
-    # holding the NEXT step's token ids when a step is called (a loader prefetching one batch
-    # ahead writes them there; bench.py's synthetic batch repeats, so it passes txt itself).
-    # build() (or the first call) runs the first step's encoder ahead, once.
+    # step's text is computed on a side stream beside this step (the encoder has no trainable
+    # parameter, so its output does not depend on this step's update), and the forward takes the
+    # output computed one step earlier. Every step still runs exactly one T5 forward; it moves
+    # from the head of the forward, where nothing else can run (the sequence assembly needs the
+    # text), to beside the step's kernels. txt_next: the device buffer holding the NEXT step's
+    # token ids when a step is called (a loader prefetching one batch ahead writes them there;
+    # bench.py's synthetic batch repeats, so it passes txt itself). build() (or the first call)
+    # runs the first step's encoder ahead, once.
 
     def __init__(self, model, state, txt, img, act, reducer: GradAllReducer | None = None,
                  stages="auto", use_graph: bool = True, txt_next=None):
@@ -105,6 +105,7 @@ class DDPStep:
         self.txt_next = txt_next
         self.t5_cur = self.t5_nxt = None
         self._t5_side = torch.cuda.Stream(device=model.device) if self.t5_pf else None
+        self._g_t5 = None
         self.reducer = reducer
         self.distributed = reducer is not None and reducer.world_size > 1
         # the backward's stage split (Octo.stage_bounds: an int, a list or "auto[:MB]")
@@ -130,7 +131,7 @@ class DDPStep:
             self.t5_nxt = torch.empty_like(self.t5_cur)
 
     def _t5_fork(self):
-        """Next step's T5 on the side stream, forked after this step's forward."""
+        """Next step's T5 on the side stream, all of it launched here."""
         side = self._t5_side
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -142,29 +143,51 @@ class DDPStep:
         torch.cuda.current_stream().wait_stream(self._t5_side)
         self.t5_cur.copy_(self.t5_nxt)
 
-    # where the next step's encoder forks: "fwd" at the step's start (default: beside the forward
-    # and the backward), "bwd" after the forward (benchmarking knob MMT_T5_FORK; 12 584 vs
-    # 12 387 samples/s at B = 128, 16 226 vs 16 179 at B = 512, profiles/r05_t5_overlap_ab.txt)
-    t5_fork_at = os.environ.get("MMT_T5_FORK", "fwd")
+    # where the next step's encoder runs (benchmarking knob MMT_T5_FORK): "ext" (default) its own
+    # graph replayed on the side stream right before the step's graph(s), handed over after the
+    # backward; "fwd" / "bwd" forked inside the step's graph at its start / after the forward.
+    # "ext" and "fwd" measure the same, "bwd" and forks between the forward's blocks less
+    # (profiles/r05_t5_overlap_ab.txt); "ext" leaves the step's graphs as they are without it.
+    t5_fork_at = os.environ.get("MMT_T5_FORK", "ext")
+
+    @property
+    def _t5_graphed_in(self):
+        return self.t5_pf and self.t5_fork_at in ("fwd", "bwd")
 
     def _fwd_bwd(self):
         m, s = self.model, self.state
         m.store.zero_grad()
-        early = self.t5_pf and self.t5_fork_at == "fwd"
+        early = self._t5_graphed_in and self.t5_fork_at == "fwd"
         if early:
             self._t5_fork()
         loss, st = m.compute_diffusion_denoise_loss(self.txt, self.img, self.act, True, s.rng,
                                                     s.sample_offset, t5_out=self.t5_cur)
-        if self.t5_pf and not early:
+        if self._t5_graphed_in and not early:
             self._t5_fork()
         m.backward(st)
-        if self.t5_pf:
+        if self._t5_graphed_in:
             self._t5_join()
         self.loss_buf.copy_(loss)
 
+    def _t5_ext_launch(self):
+        """"ext": the next step's encoder on the side stream, after everything before this step
+        (the previous hand-over included) and beside the step's graph."""
+        if self.t5_pf and not self._t5_graphed_in:
+            side = self._t5_side
+            side.wait_stream(torch.cuda.current_stream())
+            if self._g_t5 is not None:
+                with torch.cuda.stream(side):
+                    self._g_t5.replay()
+            else:
+                self._t5_fork()
+
+    def _t5_ext_join(self):
+        if self.t5_pf and not self._t5_graphed_in:
+            self._t5_join()
+
     def _stage(self, k):
         m, s = self.model, self.state
-        early = self.t5_pf and self.t5_fork_at == "fwd"
+        early = self._t5_graphed_in and self.t5_fork_at == "fwd"
         if k == 0:
             m.store.zero_grad()
             if early:
@@ -173,12 +196,12 @@ class DDPStep:
                                                         s.sample_offset, t5_out=self.t5_cur)
             self.loss_buf.copy_(loss)
             self._st["st"] = st
-            if self.t5_pf and not early:
+            if self._t5_graphed_in and not early:
                 self._t5_fork()
         m.backward_stage(self._st["st"], k, self.bounds)
-        if self.t5_pf and k == 0:  # joined inside the stage's graph (a graph is self-contained)
+        if self._t5_graphed_in and k == 0:  # joined inside the stage's graph (self-contained)
             torch.cuda.current_stream().wait_stream(self._t5_side)
-        if self.t5_pf and k == self.S - 1:  # after the text projection's dW (the last stage)
+        if self._t5_graphed_in and k == self.S - 1:  # after the text projection's dW
             self.t5_cur.copy_(self.t5_nxt)
 
     def _opt(self):
@@ -252,6 +275,13 @@ class DDPStep:
             with torch.cuda.graph(g, pool=pool, stream=self._hp):
                 fn()
             self.graphs.append(g)
+        if self.t5_pf and not self._t5_graphed_in:  # "ext": the encoder's own graph (own pool:
+            side = self._t5_side                       # it replays beside the step's graphs)
+            side.wait_stream(torch.cuda.current_stream())
+            self._g_t5 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._g_t5, stream=side):
+                self.t5_nxt.copy_(self.model.t5(self.txt_next))
+            torch.cuda.current_stream().wait_stream(side)
         if self.S > 1:
             for k in range(self.S):   # one graph per backward stage (the first holds the forward)
                 cap(lambda k=k: self._stage(k))
@@ -283,16 +313,19 @@ class DDPStep:
     def _run(self):
         g = self.graphs
         self._t5_prime()
+        self._t5_ext_launch()
         if self.S > 1:
             works = []
             for k in range(self.S):
                 g[k].replay() if self.use_graph else self._stage(k)
                 works.append(self._reduce_async(k))
+            self._t5_ext_join()
             for w in works:
                 w.wait()
             g[self.S].replay() if self.use_graph else self._opt()
         elif self.distributed:
             g[0].replay() if self.use_graph else self._fwd_bwd()
+            self._t5_ext_join()
             self.reducer(self.model.store.flat_grad)
             g[1].replay() if self.use_graph else self._opt()
         else:
@@ -301,3 +334,4 @@ class DDPStep:
             else:
                 self._fwd_bwd()
                 self._opt()
+            self._t5_ext_join()

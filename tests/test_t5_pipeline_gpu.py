@@ -35,9 +35,14 @@ def _batches(model, B, n, dev):
     return out
 
 
+@pytest.mark.parametrize("fork", ["ext", "fwd", "bwd"])
 @pytest.mark.parametrize("use_graph", [True, False], ids=["graph", "eager"])
-def test_pipelined_step_matches_plain(dev, use_graph):
+def test_pipelined_step_matches_plain(dev, use_graph, fork, monkeypatch):
+    """fork: where the next step's encoder runs (DDPStep.t5_fork_at): its own graph beside the
+    step's ("ext", the default) or forked inside the step's graph at its start / after the
+    forward."""
     from multi_modal_transformers_tokenmerge_amd.distributed import DDPStep
+    monkeypatch.setattr(DDPStep, "t5_fork_at", fork)
     B, n = 2, 4
     ma, sa = _setup(dev)
     mb, sb = _setup(dev)
@@ -69,11 +74,14 @@ def test_pipelined_step_matches_plain(dev, use_graph):
     assert _rel(ma.store.flat, mb.store.flat) <= 1e-5
 
 
-def test_staged_pieces_pipeline(dev):
-    """The staged schedule's pieces (_stage(k) for k < S, then _opt), eagerly over a 2-stage
-    backward split: the fork lands in stage 0 (after the forward), the hand-over in the last
-    stage (after the text projection's dW)."""
+@pytest.mark.parametrize("fork", ["ext", "fwd", "bwd"])
+def test_staged_pieces_pipeline(dev, fork, monkeypatch):
+    """The staged schedule's pieces in _run's order (the "ext" launch, _stage(k) for k < S, the
+    "ext" hand-over, _opt), eagerly over a 2-stage backward split; with an in-graph fork the
+    encoder forks in stage 0 and is handed over in the last stage (after the text projection's
+    dW)."""
     from multi_modal_transformers_tokenmerge_amd.distributed import DDPStep
+    monkeypatch.setattr(DDPStep, "t5_fork_at", fork)
     B = 2
     ma, sa = _setup(dev)
     mb, sb = _setup(dev)
@@ -87,8 +95,10 @@ def test_staged_pieces_pipeline(dev):
     for i in range(2):
         img.copy_(data[i][0]); txt.copy_(data[i][1]); act.copy_(data[i][2])
         txt_next.copy_(data[i + 1][1])
+        pa._t5_ext_launch()
         for k in range(pa.S):
             pa._stage(k)
+        pa._t5_ext_join()
         ga = ma.store.flat_grad.clone()
         pa._opt()
         mb.store.zero_grad()
