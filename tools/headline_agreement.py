@@ -42,6 +42,6 @@ print(f"    sum {tot:.1f} us")
 print(f"  the bench line's HIP-event time over the same launch (un-profiled run, {tag}_bench.json):")
 print(f"    {ev} us (the events also hold the gap between the two launches) -> frac {roof['frac']}")
 print(f"  agreement: {abs(ev - tot) / ev * 100:.1f} %")
-print(f"  traffic (PMC, {tag}_probe_pmc.json or the same digest's): {roof['traffic'] / 1e6:.1f} MB per "
+print(f"  traffic (PMC, {roof['traffic_source'].split(' (')[0]}): {roof['traffic'] / 1e6:.1f} MB per "
       f"launch against {roof['algorithmic_bytes_per_launch'] / 1e6:.1f} MB algorithmic")
 print(f"step: {line['value']} samples/s, {line['ms_per_step']} ms/step")
