@@ -98,3 +98,31 @@ def test_two_rank_staged_allreduce(dev, tmp_path, det):
         if det:
             assert rep["rerun_bitwise"] and rep["tome_equal"] and rep["tome_layers"] > 0, rep
     assert reps[0]["shards_vs_full"] <= 1e-4 and reps[0]["grad_norm"] > 0, reps[0]
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_t5_overlap_bitwise(dev, tmp_path):
+    """The N > 1 bench step with the next step's frozen T5 encoder overlapped (DDPStep txt_next)
+    and without it, two gloo ranks in deterministic mode, text changing every step: the
+    parameters after three staged steps are equal bit for bit (tests/ddp_t5_worker.py)."""
+    port = _port()
+    procs, outs = [], []
+    for r in range(2):
+        out = tmp_path / f"rank{r}.json"
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MMT_DETERMINISTIC="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "ddp_t5_worker.py"),
+                                       str(out)], env=env, cwd=ROOT))
+        outs.append(out)
+    codes = []
+    for p in procs:
+        try:
+            codes.append(p.wait(timeout=240))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            codes.append(-9)
+    assert codes == [0, 0], codes
+    for o in outs:
+        rep = json.loads(o.read_text())
+        assert rep["stages"] > 1 and rep["overlap_on"] and rep["overlap_off"], rep
+        assert rep["params_bitwise"] and rep["loss_on"] == rep["loss_off"], rep
