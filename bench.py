@@ -511,6 +511,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     loss_val = float(loss_buf.item())
+    K.device_status()  # after the timed region: no device-side index check fired in any step
 
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     if di.rank == 0:

@@ -45,6 +45,27 @@ const char* mmt_last_error(void);
 #define MMT_API_VERSION 2
 int mmt_version(void);
 
+/* Device-side index checks. The entry points that address memory through caller-supplied index
+ * arrays (mmt_tome_merge_wavg_fwd / _bwd, mmt_tome_merge_seqnorm_fwd, mmt_ln_unmerge_dropout_bwd,
+ * mmt_gather_rows, mmt_topk_scatter_bwd) cannot see those device values at launch. Their kernels
+ * range-check every index they use; an invalid one is replaced by 0 (so no access leaves its
+ * tensor and the context survives) and sets a bit of a library-wide device status word:
+ *   MMT_FAULT_TOME_INDEX     unm / src not in [0, ceil(t/2)), dst not in [0, t/2)
+ *   MMT_FAULT_TOME_PARTITION unm and src repeat an a-token (not a partition of the a half)
+ *   MMT_FAULT_POS_MAP        pos_map entry not in [0, t - r)
+ *   MMT_FAULT_ROW_INDEX      gathered / scattered row not in [0, L)
+ * mmt_device_status synchronises `stream`, returns MMT_OK if the word is clear, else clears it and
+ * returns MMT_ERR_INVALID with the decoded bits in mmt_last_error(). Not graph-capturable (it
+ * synchronises); call it after a step, a test or a bench. The reference's jnp gathers cannot fault
+ * (XLA clamps), so this adds the check the C ABI needs to keep its "never abort" convention. */
+enum {
+  MMT_FAULT_TOME_INDEX = 1,
+  MMT_FAULT_TOME_PARTITION = 2,
+  MMT_FAULT_POS_MAP = 4,
+  MMT_FAULT_ROW_INDEX = 8
+};
+int mmt_device_status(mmt_stream_t stream);
+
 /* Deterministic mode (SURVEY §5 "deterministic-mode reruns"). The gradient accumulations that are
  * otherwise fp32 atomics (bias / LayerNorm / GroupNorm / embedding / Fourier gradients, the
  * attention's QKV bias sums) go, for addresses inside the registered fp32 gradient buffer

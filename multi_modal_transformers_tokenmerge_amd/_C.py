@@ -28,6 +28,7 @@ class Epilogue(ctypes.Structure):
 # name -> argtypes (every entry point returns int status unless listed in _VOID)
 SIGNATURES: dict[str, list] = {
     "mmt_version": [],
+    "mmt_device_status": [P],
     "mmt_tome_set_match_path": [I],
     "mmt_workspace_size": [I, P, I],
     "mmt_tome_match": [P, I, I, I, I, I, L, L, L, I, I, P, P, P, P, P, L, P],

@@ -28,6 +28,14 @@ def _dev(*ts):
             raise ValueError("libmmt_hip ops take device (cuda/HIP) tensors only")
 
 
+def device_status() -> None:
+    """Synchronise the current stream and raise MMTError if a kernel's device-side index check
+    fired since the last call (mmt_device_status, include/mmt_api.h: ToMe merge maps, pos_map and
+    gathered rows are range-checked on the GPU; an invalid index is replaced by 0 and recorded
+    instead of faulting the context). Not capturable: call it after a step / graph replay."""
+    _C.call("mmt_device_status", _C.stream_ptr())
+
+
 # ------------------------------------------------------------------------------------ ToMe
 FLAG_CLASS, FLAG_DISTILL, FLAG_PLAIN_SUM, FLAG_NO_SCATTER = 1, 2, 4, 8
 

@@ -210,4 +210,21 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 inline hipStream_t as_stream(mmt_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ---------------------------------------------------------------- device-side index checks
+// Kernels that address memory through caller-supplied index arrays (the ToMe merge maps, pos_map,
+// the pruning row lists) range-check every index they use: an out-of-range value is replaced by 0
+// (a valid row, so no access leaves its tensor) and its fault bit is OR-ed into the library's
+// device status word, which mmt_device_status() reports as MMT_ERR_INVALID (include/mmt_api.h).
+// The word lives in core.hip's code object; fault_word() is its device address (NULL before HIP
+// is usable), passed to the kernels as an argument.
+unsigned int* fault_word();
+__device__ __forceinline__ int checked_index(int v, int hi, unsigned int* fault, unsigned int bit) {
+  if ((unsigned)v < (unsigned)hi) return v;
+  if (fault) atomicOr(fault, bit);
+  return 0;
+}
+__device__ __forceinline__ void record_fault(unsigned int* fault, unsigned int bit) {
+  if (fault) atomicOr(fault, bit);
+}
+
 }  // namespace mmt

@@ -333,7 +333,8 @@ __global__ __launch_bounds__(NT) void ln_unmerge_dropout_bwd_kernel(
     const float* __restrict__ size_out, const int32_t* __restrict__ pos_map,
     float* __restrict__ g_in, int64_t gs_b, int64_t gs_t, const uint32_t* __restrict__ rng,
     uint32_t layer, uint32_t site, uint32_t thresh, float scale, int64_t row_offset,
-    bf16_t* __restrict__ z, int64_t zs_b, int64_t zs_t, float* __restrict__ bias_grad) {
+    bf16_t* __restrict__ z, int64_t zs_b, int64_t zs_t, float* __restrict__ bias_grad,
+    unsigned int* fault) {
   extern __shared__ __attribute__((aligned(16))) float dyn_f[];  // [max(L2*CWT, 4*RGT*CWT)]
   constexpr int CVN = CWT / 8, RGT = NT / CVN;  // column vectors, row groups (seqnorm_bwd_kernel)
   __shared__ int32_t u_orow[kUnmergeMax];
@@ -350,7 +351,8 @@ __global__ __launch_bounds__(NT) void ln_unmerge_dropout_bwd_kernel(
       u_s[row] = -1.f;  // copy
     } else {
       const int tok = row - set_start;
-      const int q = pos_map[(int64_t)b * t + tok];
+      const int q = checked_index(pos_map[(int64_t)b * t + tok], t - r,
+                                  ln_colblk() == 0 ? fault : nullptr, MMT_FAULT_POS_MAP);
       u_orow[row] = set_start + q;
       u_s[row] = size_in ? size_in[(int64_t)b * t + tok] : 1.f;
       u_S[row] = size_out ? size_out[(int64_t)b * (t - r) + q] : 1.f;
@@ -707,7 +709,7 @@ extern "C" int mmt_ln_unmerge_dropout_bwd(
                        addend, as_b, as_t, dgamma, dbeta, L, set_start, t, r, size_in, size_out,    \
                        pos_map, g_in, gs_b, gs_t, rng, layer, site,                                  \
                        rng ? keep_threshold16(keep_prob) : 0u, rng ? 1.f / keep_prob : 1.f,          \
-                       row_offset, (bf16_t*)z, zs_b, zs_t, bias_grad);                               \
+                       row_offset, (bf16_t*)z, zs_b, zs_t, bias_grad, fault_word());                \
   } while (0)
   if (r5 == 3) LUD(3, 32);
   else if (r5 == 4) LUD(4, 32);

@@ -83,14 +83,15 @@ __global__ void topk_zero_kernel(int D, int L, T* __restrict__ dx, int64_t xs_b,
 template <typename T>
 __global__ void topk_scatter_rows_kernel(const T* __restrict__ dout, int D, int64_t ds_b,
                                          int64_t ds_t, const int32_t* __restrict__ idx, int K,
-                                         T* __restrict__ dx, int64_t xs_b, int64_t xs_t) {
+                                         T* __restrict__ dx, int64_t xs_b, int64_t xs_t, int L,
+                                         unsigned int* fault) {
   constexpr int V = 16 / sizeof(T);
   const int nch = D / V;
   const int b = blockIdx.y;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)K * nch) return;
   const int i = e / nch, ch = e - (int64_t)i * nch;
-  const int row = idx[(int64_t)b * K + i];
+  const int row = checked_index(idx[(int64_t)b * K + i], L, fault, MMT_FAULT_ROW_INDEX);
   *reinterpret_cast<uint4*>(dx + (int64_t)b * xs_b + (int64_t)row * xs_t + ch * V) =
       *reinterpret_cast<const uint4*>(dout + (int64_t)b * ds_b + (int64_t)i * ds_t + ch * V);
 }
@@ -161,12 +162,13 @@ extern "C" int mmt_topk_scatter_bwd(const void* dout, int dtype, int B, int K, i
     hipLaunchKernelGGL(topk_zero_kernel<float>, gz, dim3(256), 0, s, D, L, (float*)dx, xs_b, xs_t);
     if (K > 0)
       hipLaunchKernelGGL(topk_scatter_rows_kernel<float>, gs, dim3(256), 0, s, (const float*)dout,
-                         D, ds_b, ds_t, idx, K, (float*)dx, xs_b, xs_t);
+                         D, ds_b, ds_t, idx, K, (float*)dx, xs_b, xs_t, L, fault_word());
   } else {
     hipLaunchKernelGGL(topk_zero_kernel<bf16_t>, gz, dim3(256), 0, s, D, L, (bf16_t*)dx, xs_b, xs_t);
     if (K > 0)
       hipLaunchKernelGGL(topk_scatter_rows_kernel<bf16_t>, gs, dim3(256), 0, s,
-                         (const bf16_t*)dout, D, ds_b, ds_t, idx, K, (bf16_t*)dx, xs_b, xs_t);
+                         (const bf16_t*)dout, D, ds_b, ds_t, idx, K, (bf16_t*)dx, xs_b, xs_t, L,
+                         fault_word());
   }
   MMT_CHECK_LAUNCH("mmt_topk_scatter_bwd");
   return MMT_OK;
@@ -176,14 +178,14 @@ namespace {
 template <typename T>
 __global__ void gather_rows_kernel(const T* __restrict__ x, int D, int64_t xs_b, int64_t xs_t,
                                    const int32_t* __restrict__ idx, int K, T* __restrict__ out,
-                                   int64_t os_b, int64_t os_t) {
+                                   int64_t os_b, int64_t os_t, int L, unsigned int* fault) {
   constexpr int V = 16 / sizeof(T);
   const int nch = D / V;
   const int b = blockIdx.y;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)K * nch) return;
   const int i = e / nch, ch = e - (int64_t)i * nch;
-  const int row = idx[(int64_t)b * K + i];
+  const int row = checked_index(idx[(int64_t)b * K + i], L, fault, MMT_FAULT_ROW_INDEX);
   *reinterpret_cast<uint4*>(out + (int64_t)b * os_b + (int64_t)i * os_t + ch * V) =
       *reinterpret_cast<const uint4*>(x + (int64_t)b * xs_b + (int64_t)row * xs_t + ch * V);
 }
@@ -222,10 +224,10 @@ extern "C" int mmt_gather_rows(const void* x, int dtype, int B, int L, int D, in
   hipStream_t s = as_stream(stream);
   if (dtype == MMT_F32)
     hipLaunchKernelGGL(gather_rows_kernel<float>, grid, dim3(256), 0, s, (const float*)x, D, xs_b,
-                       xs_t, idx, K, (float*)out, os_b, os_t);
+                       xs_t, idx, K, (float*)out, os_b, os_t, L, fault_word());
   else
     hipLaunchKernelGGL(gather_rows_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, D,
-                       xs_b, xs_t, idx, K, (bf16_t*)out, os_b, os_t);
+                       xs_b, xs_t, idx, K, (bf16_t*)out, os_b, os_t, L, fault_word());
   MMT_CHECK_LAUNCH("mmt_gather_rows");
   return MMT_OK;
 }

@@ -660,6 +660,37 @@ __device__ __forceinline__ void merged_row_source(int q, int ta, int r, bool dis
   }
 }
 
+// The merge maps of sample n into LDS, range-checked (common.h "device-side index checks"): unm /
+// src in [0, ta), dst in [0, ta_b); an a token named twice by unm + src (not a partition of the a
+// half: a broken matcher, e.g. a rank with ties) is recorded too — its pos_map would keep a
+// hole that the backward would read. Ends with a barrier.
+constexpr int kSeenWords = (1024 + 512 + 31) / 32;  // ta <= nu + r <= 1024 + 512
+__device__ __forceinline__ void load_merge_maps(int n, int t, int r, const int32_t* __restrict__ unm_g,
+                                                const int32_t* __restrict__ src_g,
+                                                const int32_t* __restrict__ dst_g, int32_t* s_unm,
+                                                int32_t* s_src, int32_t* s_dst, uint32_t* s_seen,
+                                                unsigned int* fault) {
+  const int ta = (t + 1) / 2, tb = t / 2, nu = ta - r;
+  for (int k = threadIdx.x; k < kSeenWords; k += blockDim.x) s_seen[k] = 0;
+  __syncthreads();
+  auto mark = [&](int v) {
+    const uint32_t bit = 1u << (v & 31);
+    if (atomicOr(&s_seen[v >> 5], bit) & bit) record_fault(fault, MMT_FAULT_TOME_PARTITION);
+  };
+  for (int k = threadIdx.x; k < nu; k += blockDim.x) {
+    const int v = checked_index(unm_g[(int64_t)n * nu + k], ta, fault, MMT_FAULT_TOME_INDEX);
+    s_unm[k] = v;
+    mark(v);
+  }
+  for (int k = threadIdx.x; k < r; k += blockDim.x) {
+    const int v = checked_index(src_g[(int64_t)n * r + k], ta, fault, MMT_FAULT_TOME_INDEX);
+    s_src[k] = v;
+    mark(v);
+    s_dst[k] = checked_index(dst_g[(int64_t)n * r + k], tb, fault, MMT_FAULT_TOME_INDEX);
+  }
+  __syncthreads();
+}
+
 // Forward merge, one block = kMergeRows output rows of one sample. Phase 1 resolves every output
 // row (primary source row, size weight, divisor, and the list of src tokens scattered into it,
 // in increasing i = the reference's sequential scatter order) into LDS; phase 2 streams the
@@ -673,26 +704,22 @@ __global__ __launch_bounds__(256) void tome_merge_fwd_kernel(
     const T* __restrict__ x, int L, int D, int64_t xs_n, int64_t xs_t, int set_start, int t, int r,
     int flags, const float* __restrict__ size_in, const int32_t* __restrict__ unm_g,
     const int32_t* __restrict__ src_g, const int32_t* __restrict__ dst_g, T* __restrict__ out,
-    int64_t os_n, int64_t os_t, float* __restrict__ size_out, int32_t* __restrict__ pos_map) {
+    int64_t os_n, int64_t os_t, float* __restrict__ size_out, int32_t* __restrict__ pos_map,
+    unsigned int* fault) {
   __shared__ int32_t s_unm[1024];
   __shared__ int32_t s_src[512];
   __shared__ int32_t s_dst[512];
+  __shared__ uint32_t s_seen[kSeenWords];
   __shared__ int32_t m_prim[kMergeRows], m_cnt[kMergeRows], m_j[kMergeRows];
   __shared__ float m_sp[kMergeRows], m_S[kMergeRows];
   __shared__ int32_t m_list[kMergeRows][kMergeSeg];
   __shared__ float m_ss[kMergeRows][kMergeSeg];
   const int n = blockIdx.x;
   const int ta = (t + 1) / 2;
-  const int nu = ta - r;
   const bool dis = flags & MMT_TOME_DISTILL_TOKEN;
   const bool plain = flags & MMT_TOME_PLAIN_SUM;      // merge(x, "sum") without the size weights
   const bool scatter = !(flags & MMT_TOME_NO_SCATTER);  // merge(x, mode != "sum"): dst unchanged
-  for (int k = threadIdx.x; k < nu; k += blockDim.x) s_unm[k] = unm_g[(int64_t)n * nu + k];
-  for (int k = threadIdx.x; k < r; k += blockDim.x) {
-    s_src[k] = src_g[(int64_t)n * r + k];
-    s_dst[k] = dst_g[(int64_t)n * r + k];
-  }
-  __syncthreads();
+  load_merge_maps(n, t, r, unm_g, src_g, dst_g, s_unm, s_src, s_dst, s_seen, fault);
   const float* sb = size_in ? size_in + (int64_t)n * t : nullptr;
   const int Lout = L - r;
   const int row0 = blockIdx.y * kMergeRows;
@@ -805,7 +832,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void tome_merge_bwd_kernel(
     const T* __restrict__ g_out, int L, int D, int64_t go_s_n, int64_t go_s_t, int set_start,
     int t, int r, const float* __restrict__ size_in, const float* __restrict__ size_out,
-    const int32_t* __restrict__ pos_map, T* __restrict__ g_in, int64_t gi_s_n, int64_t gi_s_t) {
+    const int32_t* __restrict__ pos_map, T* __restrict__ g_in, int64_t gi_s_n, int64_t gi_s_t,
+    unsigned int* fault) {
   __shared__ int32_t m_orow[kMergeRows];
   __shared__ float m_s[kMergeRows], m_S[kMergeRows];
   __shared__ int32_t m_copy[kMergeRows];
@@ -819,7 +847,7 @@ __global__ __launch_bounds__(256) void tome_merge_bwd_kernel(
       m_copy[ri] = 1;
     } else {
       const int tok = row - set_start;
-      const int q = pos_map[(int64_t)n * t + tok];
+      const int q = checked_index(pos_map[(int64_t)n * t + tok], t - r, fault, MMT_FAULT_POS_MAP);
       m_orow[ri] = set_start + q;
       m_s[ri] = size_in ? size_in[(int64_t)n * t + tok] : 1.f;
       m_S[ri] = size_out ? size_out[(int64_t)n * (t - r) + q] : 1.f;  // NULL: plain sum
@@ -1037,10 +1065,11 @@ __global__ __launch_bounds__(256) void tome_merge_seqnorm_fwd_kernel(
     int64_t os_n, int64_t os_t, float* __restrict__ size_out, int32_t* __restrict__ pos_map,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     bf16_t* __restrict__ y, int64_t ys_n, int64_t ys_t, float* __restrict__ mean_out,
-    float* __restrict__ rstd_out) {
+    float* __restrict__ rstd_out, unsigned int* fault) {
   __shared__ int32_t s_unm[1024];
   __shared__ int32_t s_src[512];
   __shared__ int32_t s_dst[512];
+  __shared__ uint32_t s_seen[kSeenWords];
   __shared__ int32_t m_prim[kFusedRows], m_cnt[kFusedRows], m_j[kFusedRows];
   __shared__ float m_sp[kFusedRows], m_S[kFusedRows];
   __shared__ int32_t m_list[kFusedRows][kMergeSeg];
@@ -1048,17 +1077,12 @@ __global__ __launch_bounds__(256) void tome_merge_seqnorm_fwd_kernel(
   __shared__ float red[2 * kFRG * 64];
   __shared__ float s_mul[64], s_add[64];
   const int n = ln_sample(), c0 = ln_colblk() * 64;
-  const int ta = (t + 1) / 2, nu = ta - r;
+  const int ta = (t + 1) / 2;
   const bool dis = flags & MMT_TOME_DISTILL_TOKEN;
   const bool plain = flags & MMT_TOME_PLAIN_SUM;
   const bool scatter = !(flags & MMT_TOME_NO_SCATTER);
   const bool lead = ln_colblk() == 0;  // writes the sizes and the position map
-  for (int k = threadIdx.x; k < nu; k += blockDim.x) s_unm[k] = unm_g[(int64_t)n * nu + k];
-  for (int k = threadIdx.x; k < r; k += blockDim.x) {
-    s_src[k] = src_g[(int64_t)n * r + k];
-    s_dst[k] = dst_g[(int64_t)n * r + k];
-  }
-  __syncthreads();
+  load_merge_maps(n, t, r, unm_g, src_g, dst_g, s_unm, s_src, s_dst, s_seen, lead ? fault : nullptr);
   const float* sb = size_in ? size_in + (int64_t)n * t : nullptr;
   const int Lout = L - r;
   for (int o = threadIdx.x; o < Lout; o += blockDim.x) {  // phase 1 (tome_merge_fwd_kernel)
@@ -1251,7 +1275,8 @@ extern "C" int mmt_tome_merge_seqnorm_fwd(const float* x, int n, int L, int D, i
   static const bool rpt_on = !getenv("MMT_SNB_RPT") || atoi(getenv("MMT_SNB_RPT")) != 0;
   const int rpt = !rpt_on ? 0 : Lo <= 128 ? 4 : Lo <= 192 ? 6 : Lo <= 256 ? 8 : Lo <= 320 ? 10 : 0;
 #define TMS(R) hipLaunchKernelGGL((tome_merge_seqnorm_fwd_kernel<R>), grid, dim3(256), 0, as_stream(stream), ARGS_)
-#define ARGS_ x, L, D, x_s_n, x_s_t, set_start, t, r, flags, size_in, unm_idx, src_idx, dst_idx, x_out, o_s_n, o_s_t, size_out, pos_map, gamma, beta, eps, (bf16_t*)y, y_s_n, y_s_t, mean, rstd
+  unsigned int* const fault = fault_word();
+#define ARGS_ x, L, D, x_s_n, x_s_t, set_start, t, r, flags, size_in, unm_idx, src_idx, dst_idx, x_out, o_s_n, o_s_t, size_out, pos_map, gamma, beta, eps, (bf16_t*)y, y_s_n, y_s_t, mean, rstd, fault
   if (rpt == 4) TMS(4);
   else if (rpt == 6) TMS(6);
   else if (rpt == 8) TMS(8);
@@ -1280,14 +1305,15 @@ extern "C" int mmt_tome_merge_wavg_fwd(const void* x, int dtype, int n, int L, i
                 "mmt_tome_merge_wavg_fwd: D and strides must be multiples of 16 bytes");
   dim3 grid(n, (L - r + kMergeRows - 1) / kMergeRows);
   hipStream_t s = as_stream(stream);
+  unsigned int* const fault = fault_word();
   if (dtype == MMT_F32)
     hipLaunchKernelGGL(tome_merge_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)x, L, D,
                        x_s_n, x_s_t, set_start, t, r, flags, size_in, unm_idx, src_idx, dst_idx,
-                       (float*)x_out, o_s_n, o_s_t, size_out, pos_map);
+                       (float*)x_out, o_s_n, o_s_t, size_out, pos_map, fault);
   else
     hipLaunchKernelGGL(tome_merge_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, L,
                        D, x_s_n, x_s_t, set_start, t, r, flags, size_in, unm_idx, src_idx,
-                       dst_idx, (bf16_t*)x_out, o_s_n, o_s_t, size_out, pos_map);
+                       dst_idx, (bf16_t*)x_out, o_s_n, o_s_t, size_out, pos_map, fault);
   MMT_CHECK_LAUNCH("mmt_tome_merge_wavg_fwd");
   return MMT_OK;
 }
@@ -1306,14 +1332,15 @@ extern "C" int mmt_tome_merge_wavg_bwd(const void* g_out, int dtype, int n, int 
                 "mmt_tome_merge_wavg_bwd: D and strides must be multiples of 16 bytes");
   dim3 grid(n, (L + kMergeRows - 1) / kMergeRows);
   hipStream_t s = as_stream(stream);
+  unsigned int* const fault = fault_word();
   if (dtype == MMT_F32)
     hipLaunchKernelGGL(tome_merge_bwd_kernel<float>, grid, dim3(256), 0, s, (const float*)g_out, L,
                        D, go_s_n, go_s_t, set_start, t, r, size_in, size_out, pos_map,
-                       (float*)g_in, gi_s_n, gi_s_t);
+                       (float*)g_in, gi_s_n, gi_s_t, fault);
   else
     hipLaunchKernelGGL(tome_merge_bwd_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)g_out,
                        L, D, go_s_n, go_s_t, set_start, t, r, size_in, size_out, pos_map,
-                       (bf16_t*)g_in, gi_s_n, gi_s_t);
+                       (bf16_t*)g_in, gi_s_n, gi_s_t, fault);
   MMT_CHECK_LAUNCH("mmt_tome_merge_wavg_bwd");
   return MMT_OK;
 }

@@ -234,3 +234,61 @@ def test_ln_unmerge_gate_boundary(dev, L2):
         with pytest.raises(MMTError):
             K.ln_unmerge_dropout_bwd(dy, x1, mu, rs, gamma, grads[2], grads[3], None, tome, None, 3,
                                      1, 1.0, 0)
+
+
+def test_out_of_range_indices_are_reported_not_faulted(dev):
+    """A broken producer of the merge maps (the round-5 fault: an ablated matcher whose maps were
+    not a partition of the a half, so the forward left holes in pos_map and the backward read rows
+    far outside g_out) must give MMTError from mmt_device_status, never an illegal address. Every
+    index-consuming entry point is fed out-of-range and repeated indices; the context stays usable
+    (a valid merge afterwards is still bit-exact and the status is clean)."""
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    from multi_modal_transformers_tokenmerge_amd._C import MMTError
+    n, L, s0, t, D, r = 4, 292, 32, 256, 384, 16
+    ta = (t + 1) // 2
+    K.device_status()  # clean start
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn((n, L, D), generator=g).to(dev)
+    metric = torch.randn((n, t, 64), generator=g).to(dev)
+    unm, src, dst = K.tome_match(metric, r)
+    gamma, beta = torch.ones(D, device=dev), torch.zeros(D, device=dev)
+
+    def expect(bit_text, fn):
+        fn()
+        with pytest.raises(MMTError, match=bit_text):
+            K.device_status()
+        K.device_status()  # cleared by the report
+
+    huge = torch.full_like(unm, 1 << 28)
+    expect("out of range", lambda: K.tome_merge_fwd(x, s0, t, r, huge, src, dst))
+    expect("out of range", lambda: K.tome_merge_fwd(x, s0, t, r, unm, src - 4 * ta, dst))
+    expect("out of range", lambda: K.tome_merge_fwd(x, s0, t, r, unm, src, dst + t))
+    expect("out of range", lambda: K.tome_merge_seqnorm_fwd(x, s0, t, r, huge, src, dst, gamma, beta, 1e-6))
+    dup = unm.clone()
+    dup[:, 1] = dup[:, 0]  # in range, but an a token named twice: pos_map would keep a hole
+    expect("partition", lambda: K.tome_merge_fwd(x, s0, t, r, dup, src, dst))
+    expect("partition", lambda: K.tome_merge_seqnorm_fwd(x, s0, t, r, dup, src, dst, gamma, beta, 1e-6))
+    xo, so, pos = K.tome_merge_fwd(x, s0, t, r, unm, src, dst)
+    gout = torch.randn_like(xo)
+    bad_pos = pos.clone()
+    bad_pos[:, 5] = 1 << 30
+    bad_pos[:, 6] = -7
+    expect("pos_map", lambda: K.tome_merge_bwd(gout, s0, t, r, bad_pos, None, so))
+    x1, so1, pos1, _, mu, rs = K.tome_merge_seqnorm_fwd(x, s0, t, r, unm, src, dst, gamma, beta, 1e-6)
+    bad_pos1 = pos1.clone()
+    bad_pos1[:, 0] = 1 << 29
+    dy = torch.randn((n, L - r, D), generator=g).bfloat16().to(dev)
+    dgam, dbet = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+    expect("pos_map", lambda: K.ln_unmerge_dropout_bwd(dy, x1, mu, rs, gamma, dgam, dbet, None,
+                                                       (s0, t, r, bad_pos1, None, so1), None, 0, 1,
+                                                       1.0, 0))
+    rows = torch.tensor([[0, 3, L + 100], [1, -1, 2], [0, 0, 0], [5, 6, 7]], dtype=torch.int32, device=dev)
+    expect("row index", lambda: K.gather_rows(x, rows))
+    expect("row index", lambda: K.topk_scatter_bwd(torch.randn((n, 3, D), device=dev), rows, L))
+    # the context survived: a valid merge is still bit-exact against the oracle, status clean
+    cu, cs, cd = (a.cpu().numpy() for a in (unm, src, dst))
+    xc = x.cpu().numpy()
+    ref, _ = O.canon_merge_wavg(xc[:, s0:s0 + t], np.ones((n, t), np.float32), cu, cs, cd, r, 0)
+    xo2, _, _ = K.tome_merge_fwd(x, s0, t, r, unm, src, dst)
+    K.device_status()
+    np.testing.assert_array_equal(xo2[:, s0:s0 + t - r].cpu().numpy().view(np.uint32), ref.view(np.uint32))
