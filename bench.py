@@ -134,7 +134,7 @@ def kernel_probes(model, B, reps=20):
     cfg = model.cfg
     dev = model.device
     blk = model.stack.blocks[0]
-    sets, table, ts, r, prune, _plan = model.layer_sets[0]
+    sets, table, ts, r, prune, plan = model.layer_sets[0]
     L = sets.L
     L1 = sum(prune[1]) if prune else L - r
     D, Mh, H = cfg.token_embedding_dim, cfg.mlp_dim, cfg.num_heads
@@ -195,21 +195,14 @@ def kernel_probes(model, B, reps=20):
             "mfma", 2.0 * M * Mh * D, f"M={M} N={Mh} K={D}: the fp8 probe's product in bf16 (A/B)",
             _gemm_bytes(M, Mh, D, extra=4 * Mh))
     # 2. MLP input gradient dy1 = dz1 . W1 (NT on the transposed shadow): N = 384, K = 1536 — a
-    # plain narrow product: gemm_ntw_kernel (hipBLASLt with MMT_BLASLT=1, name Cijk_..., matched
-    # by that prefix in the PMC passes)
+    # plain narrow product: gemm_ntw_kernel
     dz1 = rnd(M, Mh)
     dy1 = torch.empty((M, D), dtype=torch.bfloat16, device=dev)
-    if K.library_gemm_ok(M, D, Mh):
-        add("mlp_dx", "Cijk_",
-            lambda: K.library_gemm_nt(dz1, blk.mlp.dense.w.bf16_t, out=dy1),
-            "mfma", 2.0 * M * D * Mh, f"M={M} N={D} K={Mh}, 2MNK (hipBLASLt, MMT_BLASLT=1)",
-            _gemm_bytes(M, D, Mh))
-    else:
-        add("mlp_dx", "gemm_ntw_kernel",
-            lambda: K.gemm(dz1, blk.mlp.dense.w.bf16_t, trans_b=True, out=dy1),
-            "mfma", 2.0 * M * D * Mh,
-            f"M={M} N={D} K={Mh}, 2MNK (one or two launches of the narrow-output NT kernel)",
-            _gemm_bytes(M, D, Mh))
+    add("mlp_dx", "gemm_ntw_kernel",
+        lambda: K.gemm(dz1, blk.mlp.dense.w.bf16_t, trans_b=True, out=dy1),
+        "mfma", 2.0 * M * D * Mh,
+        f"M={M} N={D} K={Mh}, 2MNK (one or two launches of the narrow-output NT kernel)",
+        _gemm_bytes(M, D, Mh))
     # 3. MLP Dense_0 weight gradient dW += dz1^T . y1 (TN, split-K fp32 slabs + combine); the
     # standalone probe splits for the whole chip (256 workgroups), the step's launches for half of
     # it (layers.split_k_for: they share the CUs with the main queue)
@@ -230,7 +223,7 @@ def kernel_probes(model, B, reps=20):
         a_in = rnd(rows, kin)
         res_in = rnd(rows, D, dt=torch.float32)
         out_f = torch.empty((rows, D), dtype=torch.float32, device=dev)
-        add(name, "gemm_nres_kernel" if K.nres_ok(rows, D, kin) else "gemm_glds_nt_kernel",
+        add(name, "gemm_glds_nt_kernel",
             lambda a_in=a_in, res_in=res_in, out_f=out_f, dn=dn: dn.fwd(
                 a_in, out=out_f, out_mode=K.OUT_F32, residual=res_in, rng=rng, drop_layer=0,
                 drop_site=3, keep_prob=0.9),
@@ -258,7 +251,10 @@ def kernel_probes(model, B, reps=20):
         B * L * (3 * D + 2 * D + 3 * D) * 2 + B * H * L * 8)
     # 6. ToMe matching and merge forward of block 0 (metric = K of the image set, fp32 residual)
     if r > 0:
-        s0, t = sets.starts[ts], sets.lens[ts]
+        # the first (set, r) of block 0's merge plan: with several merged sets (ts == -2) r is
+        # their sum, so probe one set with its own r (the step runs one match + merge per set)
+        si, r = plan[0]
+        s0, t = sets.starts[si], sets.lens[si]
         x1 = rnd(B, L, D, dt=torch.float32)
         metric = qkv.view(B, L, 3, H, Dh)[:, s0:s0 + t, 1]
         add("tome_match", "tome_match_fused_kernel",

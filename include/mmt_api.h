@@ -248,10 +248,6 @@ typedef struct {
  * waves; 4 = direct-to-LDS (global_load_lds) 128x128 kernel for NT; -1 = automatic (default).
  * Process-wide, not thread-safe. */
 void mmt_gemm_set_variant(int variant);
-/* Tuning knob: which launches take the warp-specialised residual-stream kernel (gemm_nres_kernel):
- * 0 none (default), 1 the fp32 residual-stream products, 2 also the plain bf16 narrow products;
- * -1 = the MMT_NRES environment variable. Process-wide, not thread-safe. */
-void mmt_gemm_set_nres(int mode);
 /* Rows of the epilogue's colsum slab for this launch shape (ceil(M / 256)), 0 when the kernel the
  * launch would use cannot write it (then take the column sums with mmt_colsum). */
 int mmt_gemm_colsum_rows(int M, int N, int K, int transA, int transB, int c_mode, int split_k);

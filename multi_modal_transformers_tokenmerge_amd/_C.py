@@ -43,7 +43,6 @@ SIGNATURES: dict[str, list] = {
     "mmt_topk_gather": [P, I, I, I, I, L, L, P, L, I, P, P, P, P, L, L, P, P],
     "mmt_topk_scatter_bwd": [P, I, I, I, I, L, L, P, I, P, L, L, P],
     "mmt_gemm_set_variant": [I],
-    "mmt_gemm_set_nres": [I],
     "mmt_set_deterministic": [P, P, L],
     "mmt_det_flush": [P, P, L, P],
     "mmt_gemm_colsum_rows": [I, I, I, I, I, I, I],
@@ -94,7 +93,7 @@ SIGNATURES: dict[str, list] = {
     "mmt_transpose_bf16_batched": [P, P, P, I, L, P],
     "mmt_step_advance": [P, P],
 }
-_VOID = {"mmt_tome_set_match_path", "mmt_gemm_set_variant", "mmt_gemm_set_nres"}
+_VOID = {"mmt_tome_set_match_path", "mmt_gemm_set_variant"}
 _RESTYPE = {"mmt_workspace_size": L,      # returns a byte count (negative: error)
             "mmt_gemm_colsum_rows": I,    # returns a row count
             "mmt_stem_conv_wgrad_slabs": I}

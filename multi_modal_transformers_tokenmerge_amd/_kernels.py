@@ -239,56 +239,6 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
     return out
 
 
-# MMT_BLASLT=1: the plain narrow products and the T5 relu product on hipBLASLt (a comparison knob:
-# by default every product of the step runs on libmmt_hip's kernels — gemm_ntw_kernel for these)
-_BLASLT = os.environ.get("MMT_BLASLT", "0") == "1"
-
-
-def nres_ok(M: int, N: int, K: int) -> bool:
-    """Whether an fp32 residual-stream NT product (c_mode OUT_F32, fp32 residual, no activation)
-    of this shape runs on gemm_nres_kernel (csrc/gemm.hip nres_kind; MMT_NRES=0 turns it off)."""
-    return (os.environ.get("MMT_NRES", "0") != "0" and N % 384 == 0 and K % 64 == 0
-            and M >= 4096)
-
-
-def library_gemm_ok(M: int, N: int, K: int) -> bool:
-    """With MMT_BLASLT=1 only: the plain narrow NT products (N <= 768, K >= 1152) go to hipBLASLt —
-    the MLP input gradient 141,312 x 384 x 1536, the QKV input gradient 149,504 x 384 x 1152 and
-    the frozen T5's FF output + residual 16,384 x 768 x 3072. By default libmmt_hip's
-    gemm_ntw_kernel runs them (tools/w384_probe.py: 204 / 173 / 90 us vs the library's
-    200 / 152 / 81; the whole step 36.14 vs 35.96 ms)."""
-    return _BLASLT and N <= 768 and K >= 1152 and M >= 8192
-
-
-def library_gemm_nt(a: torch.Tensor, b: torch.Tensor, residual: torch.Tensor | None = None,
-                    out: torch.Tensor | None = None) -> torch.Tensor:
-    """bf16 a (M, K) . b (N, K)^T [+ residual (M, N) bf16] on hipBLASLt (torch.mm / addmm: fp32
-    accumulation, one bf16 rounding of the result — the same contract as gemm(..., OUT_BF16))."""
-    bt = b.t()
-    if residual is not None:
-        return torch.addmm(residual, a, bt, out=out) if out is not None else torch.addmm(residual, a, bt)
-    return torch.mm(a, bt, out=out) if out is not None else torch.mm(a, bt)
-
-
-_ZERO_BIAS: dict = {}
-
-
-def library_relu_gemm_ok(M: int, N: int, K: int) -> bool:
-    """With MMT_BLASLT=1 only: the frozen T5's FF input relu(16,384 x 3072 x 768) on hipBLASLt's
-    relu epilogue (73 us vs gemm_ntw_kernel's 89)."""
-    return _BLASLT and hasattr(torch, "_addmm_activation") and N >= 2048 and K <= 1024 and M >= 8192
-
-
-def library_relu_gemm_nt(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """relu(a (M, K) . b (N, K)^T) in bf16 on hipBLASLt's relu epilogue (a zero bias: + 0.0
-    changes no value)."""
-    key = (b.shape[0], a.device)
-    z = _ZERO_BIAS.get(key)
-    if z is None:
-        z = _ZERO_BIAS[key] = torch.zeros(b.shape[0], dtype=a.dtype, device=a.device)
-    return torch._addmm_activation(z, a, b.t())
-
-
 def gemm_bits_supported(M: int, N: int, K: int, trans_a: bool = False, trans_b: bool = True,
                         out_mode: int = OUT_BF16, split_k: int | None = 1) -> bool:
     """Whether gemm(..., relu_bits= / gate_bits=) works for this launch (the 256-wide bf16 NT

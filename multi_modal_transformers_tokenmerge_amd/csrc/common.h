@@ -166,11 +166,14 @@ struct DetState {
   int64_t n;       // elements
 };
 // Range: the shadow holds |sum| < 2^27 per element (int64 at 2^-36 resolution). A contribution
-// that is not finite or has |v| >= 2^26 never enters the shadow: it goes to the fp32 buffer as a
-// plain fp32 atomic instead (det_fits), so a NaN / Inf gradient still reaches flat_grad (and
-// survives the flush: NaN + x = NaN) — the mode trades bitwise reruns for visibility there.
+// enters it only if |v| < 2^15 (det_fits), so up to 2^12 = 4096 contributions per element and
+// flush can never wrap the int64 (the step's busiest site, a column sum over B*L rows in
+// 256-row partials, gives about 550 at B = 512). A contribution that is not finite or larger
+// goes to the fp32 buffer as a plain fp32 atomic instead, so a NaN / Inf / huge gradient still
+// reaches flat_grad (and survives the flush: NaN + x = NaN): the mode trades bitwise reruns
+// for visibility there, never a silently wrapped sum.
 constexpr double DET_SCALE = 68719476736.0;  // 2^36
-constexpr float DET_VMAX = 67108864.f;       // 2^26
+constexpr float DET_VMAX = 32768.f;          // 2^15
 static __constant__ DetState g_det;
 static DetState g_det_host{};  // this unit's host copy (kernel-variant choices)
 

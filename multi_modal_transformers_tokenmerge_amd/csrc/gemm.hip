@@ -2308,290 +2308,6 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ntws_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// Residual-stream narrow NT kernel: C (fp32) = residual (fp32) + dropout(alpha A.B^T + bias) for
-// the products that feed the fp32 residual stream — the attention out-projection and MLP Dense_1
-// (reference attention.py:36-37,59-63,69: x + Dropout(Dense(.))) — and, with EP 0, the plain bf16
-// narrow product. N is a multiple of 384: a tile is 128 rows x 384 columns, so the A row panel
-// streams from HBM once per 384 columns and the weights (384 x K, 1.2 MB at K = 1536) are re-read
-// from L2 once per 128 rows.
-// Why a new kernel (round 4): the 128 x 128 direct-to-LDS kernel and the narrow kernel both moved
-// the residual-stream products at ~3.1-3.2 TB/s of algorithmic bytes: each wave both issued the
-// operand DMA and stored its epilogue, with one in-order vmcnt, and only one or two K-steps of A
-// were in flight per CU. Here the roles are split by wave (12 waves, one workgroup per CU):
-//  * wave 8 (A loader) issues every A piece (buffer_load ... lds) into a 4-stage ring, three
-//    K-steps ahead; its vmcnt counts A pieces only, so its waits never drain the deeper prefetch;
-//  * waves 9-11 (W loaders) fill a 2-stage weight ring one K-step ahead (WPATH 0: LDS-DMA,
-//    WPATH 1: global_load_dwordx4 into VGPRs + ds_write_b128 — the weight bytes then take the
-//    vector-load path, not the LDS-DMA path the A stream uses);
-//  * waves 0-7 (compute, 2 (rows) x 4 (columns) of 64 x 96, v_mfma_f32_32x32x16_bf16 with the
-//    operands swapped: lane = output row) run the MFMAs and the epilogue; their vmcnt holds only
-//    the epilogue's bias / residual loads and C stores: residual loads are issued three 8-column
-//    groups ahead of use, never behind a store they do not need.
-// One s_barrier per K-step for all 12 waves, plus one at each tile's end (the epilogue reuses the
-// weight stage of the tile's last K-step as transpose scratch). Rows: each workgroup owns a contiguous range of
-// ~M / grid rows (balanced to a row, not to a tile), walked in 128-row chunks; rows past the
-// range read zeros (buffer range) and are not stored. Outputs are bit-identical to the 128 x 128
-// kernel (same MFMA shape and k order per output, same epilogue order).
-// LDS images as the narrow kernel: [rows][64] bf16, 16-B chunk c of row r at c ^ (r & 7).
-#ifndef MMT_NRES_ABL  // ablation builds (tools/build_abl_nres.sh): 1 no W DMA, 2 no A DMA,
-#define MMT_NRES_ABL 0  // 3 no MFMA, 4 no epilogue loads / stores, 5 no DMA at all
-#endif
-constexpr int NR_NT = 768, NR_MT = 128, NR_BN = 384, NR_NSA = 4;
-constexpr int NR_A_ST = NR_MT * 128, NR_W_ST = NR_BN * 128;  // 16 KB, 48 KB per K-step
-template <int WPATH, int EP>  // EP: 0 plain bf16 out, 1 fp32 out with bias / dropout / fp32 residual
-__global__ __launch_bounds__(NR_NT, 1) void gemm_nres_kernel(
-    int M, int N, int K, const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
-    int64_t ldb, void* __restrict__ Cv, int64_t ldc, int tiles_n, Epi epi) {
-  __shared__ __attribute__((aligned(16))) char smem[NR_NSA * NR_A_ST + 2 * NR_W_ST];
-  char* const sA = smem;
-  char* const sW = smem + NR_NSA * NR_A_ST;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nk = K / 64;
-  const int64_t r0 = (int64_t)M * blockIdx.x / gridDim.x, r1 = (int64_t)M * (blockIdx.x + 1) / gridDim.x;
-  const int nch = (int)((r1 - r0 + NR_MT - 1) / NR_MT);
-  const int n_mine = nch * tiles_n;
-  const int S = n_mine * nk;
-  if (S == 0) return;  // workgroup-uniform
-
-  if (wave == 8) {
-    // ------------------------------------------------------------------ A loader
-    int voa[16];
-#pragma unroll
-    for (int p = 0; p < 16; ++p) {
-      const int row = 8 * p + (lane >> 3);
-      voa[p] = row * (int)(lda * 2) + (((lane & 7) ^ (row & 7)) << 4);
-    }
-    auto issue = [&](int s) {
-      const int i = s / nk, kt = s - i * nk;
-      const int64_t m0 = r0 + (int64_t)(i / tiles_n) * NR_MT;
-      const int rows = (int)min((int64_t)NR_MT, r1 - m0), k0 = kt * 64;
-      const bf16_t* pa = A + m0 * lda + k0;
-      const int64_t ra = ((int64_t)rows * lda - k0) * 2;  // rows past the range read zeros
-      char* dst = sA + (s % NR_NSA) * NR_A_ST;
-#pragma unroll
-      for (int p = 0; p < 16; ++p)
-        if (MMT_NRES_ABL != 2 && MMT_NRES_ABL != 5) dma16_asm(pa, ra, dst + p * 1024, voa[p]);
-    };
-#pragma unroll
-    for (int q = 0; q < NR_NSA - 1; ++q)
-      if (q < S) issue(q);
-    for (int s = 0; s < S; ++s) {
-      // K-step s landed; the (up to NSA - 2) younger K-steps stay in flight
-      const int younger = min(NR_NSA - 2, S - 1 - s);
-      if (younger >= 2) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-      else if (younger == 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_barrier" ::: "memory");
-      // into the stage K-step s - 1 used (its reads finished before this barrier)
-      if (s + NR_NSA - 1 < S) issue(s + NR_NSA - 1);
-      if (s % nk == nk - 1) asm volatile("s_barrier" ::: "memory");  // the tile's epilogue sync
-    }
-    return;
-  }
-  if (wave > 8) {
-    // ------------------------------------------------------------------ W loaders
-    const int lw = wave - 9;  // pieces 16 lw .. 16 lw + 15 (rows 8 p .. 8 p + 7)
-    int vow[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int row = 8 * (16 * lw + i) + (lane >> 3);
-      vow[i] = row * (int)(ldb * 2) + (((lane & 7) ^ (row & 7)) << 4);
-    }
-    auto wsrc = [&](int s) {
-      const int i = s / nk, kt = s - i * nk;
-      return B + (int64_t)((i % tiles_n) * NR_BN) * ldb + kt * 64;
-    };
-    if constexpr (WPATH == 0) {
-      auto issue = [&](int s) {
-        const bf16_t* pb = wsrc(s);
-        const int64_t rb = ((int64_t)NR_BN * ldb - (s % nk) * 64) * 2;
-        char* dst = sW + (s & 1) * NR_W_ST + lw * 16 * 1024;
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if (MMT_NRES_ABL != 1 && MMT_NRES_ABL != 5) dma16_asm(pb, rb, dst + i * 1024, vow[i]);
-      };
-      issue(0);
-      for (int s = 0; s < S; ++s) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // W(s) landed
-        asm volatile("s_barrier" ::: "memory");
-        if (s + 1 < S) issue(s + 1);  // into the stage K-step s - 1 used
-        if (s % nk == nk - 1) asm volatile("s_barrier" ::: "memory");  // the tile's epilogue sync
-      }
-    } else {
-      uint4 wr[16];
-      auto load = [&](int s) {
-        const char* pb = reinterpret_cast<const char*>(wsrc(s));
-#pragma unroll
-        for (int i = 0; i < 16; ++i) wr[i] = *reinterpret_cast<const uint4*>(pb + vow[i]);
-      };
-      auto put = [&](int s) {
-        char* dst = sW + (s & 1) * NR_W_ST + lw * 16 * 1024 + lane * 16;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) *reinterpret_cast<uint4*>(dst + i * 1024) = wr[i];
-      };
-      load(0);
-      put(0);
-      if (S > 1) load(1);
-      for (int s = 0; s < S; ++s) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // W(s) written
-        asm volatile("s_barrier" ::: "memory");
-        if (s + 1 < S) {
-          put(s + 1);  // into the stage K-step s - 1 used (compiler waits for the loads)
-          if (s + 2 < S) load(s + 2);
-        }
-        if (s % nk == nk - 1) asm volatile("s_barrier" ::: "memory");  // the tile's epilogue sync
-      }
-    }
-    return;
-  }
-
-  // -------------------------------------------------------------------- compute waves
-  const int wm = wave >> 2, wn = wave & 3;
-  const int l31 = lane & 31, h = lane >> 5, sw = l31 & 7;
-  int a_off[2], b_off[3];
-#pragma unroll
-  for (int mb = 0; mb < 2; ++mb) a_off[mb] = (wm * 64 + 32 * mb + l31) * 128;
-#pragma unroll
-  for (int nb = 0; nb < 3; ++nb) b_off[nb] = (wn * 96 + 32 * nb + l31) * 128;
-  floatx16 acc[2][3];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 3; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  uint32_t key = 0;
-  if (EP == 1 && epi.rng) key = stream_key(epi.rng[0], epi.rng[1], epi.drop_layer, epi.drop_site);
-  Epi rest = epi;  // dropout through epilogue_w; alpha, bias, residual inline (the 128 x 128 order)
-  rest.alpha = 1.f;
-  rest.bias = nullptr;
-  rest.act = MMT_ACT_NONE;
-  rest.gate = nullptr;
-  rest.residual = nullptr;
-
-  auto compute = [&](int s) {
-    const char* SA = sA + (s % NR_NSA) * NR_A_ST;
-    const char* SB = sW + (s & 1) * NR_W_ST;
-    bf16x8 af[2][2], bfr[2][3];
-    auto rd = [&](int ks, int cu) {
-      const int c = ((2 * ks + h) ^ sw) << 4;
-#pragma unroll
-      for (int mb = 0; mb < 2; ++mb) af[cu][mb] = *reinterpret_cast<const bf16x8*>(SA + a_off[mb] + c);
-#pragma unroll
-      for (int nb = 0; nb < 3; ++nb) bfr[cu][nb] = *reinterpret_cast<const bf16x8*>(SB + b_off[nb] + c);
-    };
-    rd(0, 0);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int cu = ks & 1;
-      if (ks + 1 < 4) rd(ks + 1, cu ^ 1);  // next k-slice's fragments under this slice's MFMAs
-#pragma unroll
-      for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-        for (int nb = 0; nb < 3; ++nb)
-          if (MMT_NRES_ABL != 3 || M < 0)
-            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[cu][nb], af[cu][mb], acc[mb][nb], 0, 0, 0);
-    }
-  };
-
-  // Epilogue through a per-wave LDS transpose: in the accumulator layout a lane holds one output
-  // row's columns 8 g + 4 h + i of each 32-column block, so direct global accesses touch 32 rows
-  // x 32 B per instruction (measured: the epilogue alone took 170 us of the Dense_1 launch). Each
-  // 32 x 32 fp32 block is written to the wave's own 32 x 36-float LDS region (conflict-free 16-B
-  // writes) and read back as 8 rows x 128 B per instruction (lane: row 8 k + lane / 8, columns
-  // 4 (lane & 7) ..): residual loads, C stores and the bias then move whole 128-B row segments.
-  // The region lies in the weight stage this tile's last K-step used: free until the next
-  // barrier, after which the W loaders refill it. The residual of the next block is loaded
-  // before the current block's stores (PF blocks ahead).
-  auto epilogue = [&](int i, int s) {
-    const int64_t m0 = r0 + (int64_t)(i / tiles_n) * NR_MT;
-    const int tn = i % tiles_n;
-    float* stg = reinterpret_cast<float*>(sW + (s & 1) * NR_W_ST + wave * (32 * 36 * 4));
-    const int er = lane >> 3, ec = 4 * (lane & 7);
-    auto row_of = [&](int q, int k) { return m0 + wm * 64 + 32 * (q / 3) + 8 * k + er; };
-    auto col_of = [&](int q) { return tn * NR_BN + wn * 96 + 32 * (q % 3) + ec; };
-    constexpr int PF = 2;
-    float resv[PF][4][4];
-    auto fetch = [&](int q) {
-      if constexpr (EP == 1 && MMT_NRES_ABL != 4) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int64_t gr = min(row_of(q, k), r1 - 1);  // clamped: unpredicated loads
-          ldw<4>(reinterpret_cast<const float*>(epi.residual) + gr * epi.ld_res + col_of(q), resv[q % PF][k]);
-        }
-      }
-    };
-    float biasv[3][4];
-    if (EP == 1 && epi.bias)
-#pragma unroll
-      for (int nb = 0; nb < 3; ++nb) ldw<4>(epi.bias + col_of(nb), biasv[nb]);
-#pragma unroll
-    for (int q = 0; q < PF; ++q) fetch(q);
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {  // blocks (mb, nb) = (q / 3, q % 3)
-      const int mb = q / 3, nb = q % 3;
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4)
-        *reinterpret_cast<float4*>(stg + l31 * 36 + 8 * g4 + 4 * h) =
-            make_float4(acc[mb][nb][4 * g4], acc[mb][nb][4 * g4 + 1], acc[mb][nb][4 * g4 + 2],
-                        acc[mb][nb][4 * g4 + 3]);
-      float v[4][4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ldw<4>(stg + (8 * k + er) * 36 + ec, v[k]);
-      const int gc = col_of(q);
-      if constexpr (EP == 1) {
-        float rr[4][4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) rr[k][e] = resv[q % PF][k][e];
-        if (q + PF < 6) fetch(q + PF);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int64_t gr = row_of(q, k);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[k][e] *= epi.alpha;
-          if (epi.bias)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[k][e] += biasv[nb][e];
-          epilogue_w<4>(rest, key, N, (int)gr, gc, v[k]);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[k][e] += rr[k][e];
-          if (gr < r1 && (MMT_NRES_ABL != 4 || v[k][0] == 123.f)) store_w<2, 4>(Cv, gr * ldc + gc, 0.f, v[k]);
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int64_t gr = row_of(q, k);
-          uint2 o;
-          o.x = (uint32_t)f2bf(v[k][0] * epi.alpha) | ((uint32_t)f2bf(v[k][1] * epi.alpha) << 16);
-          o.y = (uint32_t)f2bf(v[k][2] * epi.alpha) | ((uint32_t)f2bf(v[k][3] * epi.alpha) << 16);
-          if (gr < r1) *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(Cv) + gr * ldc + gc) = o;
-        }
-      }
-    }
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 3; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  };
-
-  for (int s = 0; s < S; ++s) {
-    // this wave's reads of K-step s - 1 completed; K-step s landed for every wave
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    compute(s);
-    if ((s % nk) == nk - 1) {
-      // every compute wave is done reading K-step s's weight stage before any overwrites it
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      epilogue(s / nk, s);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // FP8 (OCP e4m3) forward GEMM for the fp8 weight path (BASELINE configs[4]): C = epilogue(
 // (A_q . B_q^T) * sa[m] * sb[n]) with A_q [M][K] e4m3 (activation rows quantised with one scale
 // per row) and B_q [N][K] e4m3 (weight rows = output channels, one scale each). The products run
@@ -2813,25 +2529,6 @@ bool ntw_ok(int M, int N, int K, int transA, int transB, int batch, int out_kind
          (wide_plain && M >= 4096 && M <= 8192);
 }
 
-// Which epilogue of the residual-stream kernel (gemm_nres_kernel) runs this launch, -1 for none:
-// 1 = the fp32 residual-stream products (fp32 out, fp32 residual, optional bias / dropout / alpha;
-// the step's out-projection and MLP Dense_1), 0 = the plain bf16 narrow product (MMT_NRES=2 only,
-// a comparison against gemm_ntw_kernel). MMT_NRES=0 keeps the 128 x 128 kernel.
-int g_nres = -1;  // mmt_gemm_set_nres (tests / benchmarks); -1: MMT_NRES (default 0)
-int nres_kind(int M, int N, int K, int transA, int transB, int batch, int out_kind, const Epi& e) {
-  static const int env_mode = getenv("MMT_NRES") ? atoi(getenv("MMT_NRES")) : 0;
-  const int mode = g_nres >= 0 ? g_nres : env_mode;
-  if (!mode || transA || !transB || batch != 1 || K % 64 != 0 || N % NR_BN != 0 || M < 4096 ||
-      g_variant >= 0)
-    return -1;
-  if (e.gate || e.relu_bits || e.gate_bits || e.keep_bits || e.colsum || e.beta != 0.f ||
-      e.act != MMT_ACT_NONE)
-    return -1;
-  if (out_kind == 1 && e.residual && e.res_f32) return 1;
-  if (mode == 2 && out_kind == 0 && !e.residual && !e.bias && !e.rng) return 0;
-  return -1;
-}
-
 // Launch plan of gemm_ntw_kernel: tile width bn (192 / 384), `rows_big` rows in full rounds of
 // the persistent grid on 256-row tiles, the rest on tiles of mt2 rows. A tile's time is taken as
 // proportional to its operand bytes per K-step, (MT + BN) x 128, so a last round of a few big
@@ -2931,7 +2628,6 @@ extern "C" int mmt_gemm_colsum_rows(int M, int N, int K, int transA, int transB,
 }
 
 extern "C" void mmt_gemm_set_variant(int v) { g_variant = v; }
-extern "C" void mmt_gemm_set_nres(int mode) { g_nres = mode; }
 
 extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t lda,
                         const void* B, int transB, int64_t ldb, void* C, int c_mode, int64_t ldc,
@@ -3000,26 +2696,6 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
                       (uintptr_t)workspace % 16 == 0,
                   "mmt_gemm: split-K needs a 16-B aligned workspace of split_k*M*N floats");
     out_kind = 2;
-  }
-  // residual-stream narrow NT kernel (fp32 C = fp32 residual + dropout(A.B^T + bias))
-  const int nres = nres_kind(M, N, K, transA, transB, batch, out_kind, epi);
-  if (nres >= 0) {
-    const int tn = N / NR_BN;
-    const int grid = std::min(cu_count(), (M + NR_MT - 1) / NR_MT);
-    static const int wpath = getenv("MMT_NRES_W") ? atoi(getenv("MMT_NRES_W")) : 0;
-#define GNR(WP, EPV)                                                                                  \
-  hipLaunchKernelGGL((gemm_nres_kernel<WP, EPV>), dim3(grid), dim3(NR_NT), 0, s, M, N, K,             \
-                     (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, tn, epi)
-    if (nres == 1) {
-      if (wpath == 1) GNR(1, 1);
-      else GNR(0, 1);
-    } else {
-      if (wpath == 1) GNR(1, 0);
-      else GNR(0, 0);
-    }
-#undef GNR
-    MMT_CHECK_LAUNCH("mmt_gemm(nres)");
-    return MMT_OK;
   }
   // narrow-output NT kernel (products formerly on hipBLASLt)
   if (ntw_ok(M, N, K, transA, transB, batch, out_kind, epi)) {
@@ -3189,8 +2865,7 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
                      split_k, k_chunk, tiles_n, n_work, epi)
   if (pipe == 4 && !(!transA && transB && K % 8 == 0)) pipe = 1;  // glds path: NT only
   // TN split-K slabs (every weight gradient of the step): the direct-to-LDS TN kernel
-  static const int g_tn_dma = getenv("MMT_TN_DMA") ? atoi(getenv("MMT_TN_DMA")) : 1;
-  if (pipe == 3 && out_kind == 2 && transA && !transB && batch == 1 && g_tn_dma) {
+  if (pipe == 3 && out_kind == 2 && transA && !transB && batch == 1) {
     const int tn = (N + TN_BN - 1) / TN_BN;
     // 384-row tiles where M divides (every weight gradient of the step: 384 / 1152 / 1536 rows)
     // unless MMT_TN_BM=256; fewer, larger tiles: the split-K factor is the caller's

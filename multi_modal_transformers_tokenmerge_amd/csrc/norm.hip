@@ -542,17 +542,6 @@ static int snb_rpt(int L) {
   return 0;
 }
 
-// the 32-column (64 row groups) single-pass LayerNorm backward for 128 < L <= 320 (MMT_SNB512=1;
-// off by default): half the rows per thread of the 64-column form, whose 254-256 VGPRs hold two
-// waves per SIMD (this one ~156: three workgroups per CU instead of two). Measured slower at
-// B = 512, L = 276 (tools/ln_bench.py): seqnorm_bwd 168 vs 166 us, with dropout 205 vs 196, the
-// fused LN_1 + unmerge 220 vs 204 -- occupancy is not what bounds these kernels; the 128-B row
-// segments cost more than the extra workgroup gains.
-static int snb_rpt512(int L) {
-  static const bool on = getenv("MMT_SNB512") && atoi(getenv("MMT_SNB512")) != 0;
-  if (!on || snb_rpt(L) == 0 || L <= 128) return 0;
-  return (L + 63) / 64;
-}
 
 extern "C" int mmt_seqnorm_fwd(const void* x, int x_dtype, int64_t xs_b, int64_t xs_t, int B,
                                int L, int D, const float* gamma, const float* beta, float eps,
@@ -611,18 +600,7 @@ extern "C" int mmt_seqnorm_bwd(const void* dy, int dy_dtype, int64_t ds_b, int64
   hipLaunchKernelGGL((seqnorm_bwd_kernel<bf16_t, float, false, R>), grid, dim3(NT), 0, s,           \
                      (const bf16_t*)dy, ds_b, ds_t, (const float*)x, xs_b, xs_t, L, D, mean, rstd,  \
                      gamma, (const float*)addend, as_b, as_t, (float*)dx, dxs_b, dxs_t, dgamma, dbeta)
-    const int r5 = snb_rpt512(L);
-    const dim3 grid32 = ln_grid(B, (D + 31) / 32);
-    if (r5) {
-#define SNBR5(R)                                                                                    \
-  hipLaunchKernelGGL((seqnorm_bwd_kernel<bf16_t, float, false, R, NT, 32>), grid32, dim3(NT), 0, s,     \
-                     (const bf16_t*)dy, ds_b, ds_t, (const float*)x, xs_b, xs_t, L, D, mean, rstd,  \
-                     gamma, (const float*)addend, as_b, as_t, (float*)dx, dxs_b, dxs_t, dgamma, dbeta)
-      if (r5 == 3) SNBR5(3);
-      else if (r5 == 4) SNBR5(4);
-      else SNBR5(5);
-#undef SNBR5
-    } else if (rpt == 4) SNBR(4);
+    if (rpt == 4) SNBR(4);
     else if (rpt == 6) SNBR(6);
     else if (rpt == 8) SNBR(8);
     else SNBR(10);
@@ -693,8 +671,7 @@ extern "C" int mmt_ln_unmerge_dropout_bwd(
                     (!addend || as_t % 8 == 0),
                 "mmt_ln_unmerge_dropout_bwd: strides must be multiples of 8");
   MMT_CHECK_ARG(!rng || (keep_prob > 0.f && keep_prob <= 1.f), "mmt_ln_unmerge_dropout_bwd: keep_prob");
-  const int r5 = snb_rpt512(L2);  // the 32-column form where seqnorm_bwd takes it (same sums)
-  const int cwt = r5 ? 32 : CW;
+  const int cwt = CW;
   const size_t dyn = sizeof(float) * (size_t)std::max(L2 * cwt, 4 * (NT / (cwt / 8)) * cwt);
   const dim3 grid = ln_grid(B, (D + cwt - 1) / cwt);
   const int rpt = snb_rpt(L2);
@@ -711,10 +688,7 @@ extern "C" int mmt_ln_unmerge_dropout_bwd(
                        rng ? keep_threshold16(keep_prob) : 0u, rng ? 1.f / keep_prob : 1.f,          \
                        row_offset, (bf16_t*)z, zs_b, zs_t, bias_grad, fault_word());                \
   } while (0)
-  if (r5 == 3) LUD(3, 32);
-  else if (r5 == 4) LUD(4, 32);
-  else if (r5 == 5) LUD(5, 32);
-  else if (rpt == 4) LUD(4, CW);
+  if (rpt == 4) LUD(4, CW);
   else if (rpt == 6) LUD(6, CW);
   else if (rpt == 8) LUD(8, CW);
   else if (rpt == 10) LUD(10, CW);
@@ -746,16 +720,7 @@ extern "C" int mmt_seqnorm_dropout_bwd(const void* dy, int64_t ds_b, int64_t ds_
   hipLaunchKernelGGL((seqnorm_bwd_kernel<bf16_t, float, true, R>), grid, dim3(NT), 0,               \
                      as_stream(stream), (const bf16_t*)dy, ds_b, ds_t, x, xs_b, xs_t, L, D, mean,   \
                      rstd, gamma, addend, as_b, as_t, dx, dxs_b, dxs_t, dgamma, dbeta, dz)
-#define SDZ5(R)                                                                                     \
-  hipLaunchKernelGGL((seqnorm_bwd_kernel<bf16_t, float, true, R, NT, 32>), grid32, dim3(NT), 0,         \
-                     as_stream(stream), (const bf16_t*)dy, ds_b, ds_t, x, xs_b, xs_t, L, D, mean,   \
-                     rstd, gamma, addend, as_b, as_t, dx, dxs_b, dxs_t, dgamma, dbeta, dz)
-  const int r5 = snb_rpt512(L);
-  const dim3 grid32 = ln_grid(B, (D + 31) / 32);
-  if (r5 == 3) SDZ5(3);
-  else if (r5 == 4) SDZ5(4);
-  else if (r5 == 5) SDZ5(5);
-  else if (rpt == 4) SDZ(4);
+  if (rpt == 4) SDZ(4);
   else if (rpt == 6) SDZ(6);
   else if (rpt == 8) SDZ(8);
   else if (rpt == 10) SDZ(10);

@@ -93,8 +93,10 @@ class DDPStep:
     # from the head of the forward, where nothing else can run (the sequence assembly needs the
     # text), to beside the step's kernels. txt_next: the device buffer holding the NEXT step's
     # token ids when a step is called (a loader prefetching one batch ahead writes them there;
-    # bench.py's synthetic batch repeats, so it passes txt itself). build() (or the first call)
-    # runs the first step's encoder ahead, once.
+    # bench.py's synthetic batch repeats, so it passes txt itself). The first call after build()
+    # (or after reset_text()) encodes the step's own `txt` before it starts, so a loader may
+    # write the first batch after build(); from then on `txt` is not read for the encoder — each
+    # step's text arrives through txt_next one call earlier (write both buffers, one batch apart).
 
     def __init__(self, model, state, txt, img, act, reducer: GradAllReducer | None = None,
                  stages="auto", use_graph: bool = True, txt_next=None):
@@ -104,6 +106,7 @@ class DDPStep:
                       and getattr(model, "t5", None) is not None)
         self.txt_next = txt_next
         self.t5_cur = self.t5_nxt = None
+        self._t5_primed = False  # t5_cur holds T5(txt) of the coming step
         self._t5_side = torch.cuda.Stream(device=model.device) if self.t5_pf else None
         self._g_t5 = None
         self.reducer = reducer
@@ -129,6 +132,16 @@ class DDPStep:
         if self.t5_pf and self.t5_cur is None:
             self.t5_cur = self.model.t5(self.txt).clone()
             self.t5_nxt = torch.empty_like(self.t5_cur)
+
+    def reset_text(self):
+        """The next call encodes its own `txt` again instead of the encoder output handed over by
+        the previous call (e.g. after the loader restarted, or `txt` was rewritten alone)."""
+        self._t5_primed = False
+
+    def _t5_first_call(self):
+        if self.t5_pf and not self._t5_primed:
+            self.t5_cur.copy_(self.model.t5(self.txt))
+            self._t5_primed = True
 
     def _t5_fork(self):
         """Next step's T5 on the side stream, all of it launched here."""
@@ -250,8 +263,6 @@ class DDPStep:
         self._t5_prime()
         if not self.use_graph:
             return self
-        if self._hp_on and self._hp is None:
-            self._hp = torch.cuda.Stream(priority=-1)
         snap = self._snapshot()
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
@@ -265,14 +276,13 @@ class DDPStep:
         torch.cuda.synchronize()
         self._restore(snap)
         del snap
-        if self.t5_pf:  # the warm-up steps handed txt_next's encoder output over: this step's again
-            self.t5_cur.copy_(self.model.t5(self.txt))
+        self._t5_primed = False  # the first call encodes the txt it finds then
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
 
         def cap(fn):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool, stream=self._hp):
+            with torch.cuda.graph(g, pool=pool):
                 fn()
             self.graphs.append(g)
         if self.t5_pf and not self._t5_graphed_in:  # "ext": the encoder's own graph (own pool:
@@ -296,23 +306,10 @@ class DDPStep:
             cap(whole)
         return self
 
-    # MMT_MAIN_PRIO=1 (benchmarking): capture and replay the step on a high-priority stream, so
-    # the critical path's kernels dispatch ahead of the dW side queue's
-    _hp_on = os.environ.get("MMT_MAIN_PRIO", "0") == "1"
-    _hp = None
-
     def __call__(self):
-        if self._hp is None:
-            return self._run()
-        cur = torch.cuda.current_stream()
-        self._hp.wait_stream(cur)
-        with torch.cuda.stream(self._hp):
-            self._run()
-        cur.wait_stream(self._hp)
-
-    def _run(self):
         g = self.graphs
         self._t5_prime()
+        self._t5_first_call()
         self._t5_ext_launch()
         if self.S > 1:
             works = []

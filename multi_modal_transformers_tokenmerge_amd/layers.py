@@ -33,9 +33,7 @@ class wgrad_overlap:
     def __init__(self, device):
         key = torch.device(device).index
         if key not in wgrad_overlap._streams:
-            # MMT_WGRAD_PRIO (benchmarking): stream priority of the dW queue (-1 high, 0 default)
-            wgrad_overlap._streams[key] = torch.cuda.Stream(
-                device=device, priority=int(os.environ.get("MMT_WGRAD_PRIO", "0")))
+            wgrad_overlap._streams[key] = torch.cuda.Stream(device=device)
         self.stream = wgrad_overlap._streams[key]
 
     enabled = os.environ.get("MMT_WGRAD_OVERLAP", "1") != "0"  # benchmarking knob
@@ -51,28 +49,6 @@ class wgrad_overlap:
     # kernels the side queue keeps up without the join
     lag = int(os.environ.get("MMT_WGRAD_LAG", "0"))
     _marks: list = []
-    # MMT_WGRAD_BATCH=1: one fork per block instead of one per Dense — the block's dW products are
-    # queued and issued on the side stream together at block_done() (each fork is a dependency
-    # edge in the graph, ≈ 6 us of idle main queue at replay). Measured 3.7 % slower (14.33k vs
-    # 14.89k samples/s, B = 512, 3 interleaved rounds): starting each dW as soon as its dY exists
-    # is worth more than the fork gaps; off by default
-    batch = os.environ.get("MMT_WGRAD_BATCH", "0") == "1"
-    _pending: list = []
-
-    @staticmethod
-    def flush():
-        """Issue the queued dW products (MMT_WGRAD_BATCH) on the side stream behind one fork."""
-        a = wgrad_overlap.active
-        if a is None or not wgrad_overlap._pending:
-            return
-        fork = torch.cuda.Event()
-        fork.record(torch.cuda.current_stream())
-        a[0].wait_event(fork)
-        with torch.cuda.stream(a[0]):
-            for fn in wgrad_overlap._pending:
-                fn()
-        wgrad_overlap._pending.clear()
-
     @staticmethod
     def block_done():
         """End of one block's backward: with lag > 0 the main stream waits for the dW work of the
@@ -80,7 +56,6 @@ class wgrad_overlap:
         path first and the side stream's dW products late — the side queue idle for the first
         6 ms, then 2.5 ms of dW alone; round 3's faster kernels reversed the balance: lag 0, the
         default, is 1.4 % faster)."""
-        wgrad_overlap.flush()
         a = wgrad_overlap.active
         if a is None or wgrad_overlap.lag <= 0:
             return
@@ -91,7 +66,6 @@ class wgrad_overlap:
             torch.cuda.current_stream().wait_event(wgrad_overlap._marks.pop(0))
 
     def __exit__(self, *exc):
-        wgrad_overlap.flush()
         wgrad_overlap._marks.clear()
         if wgrad_overlap.active is not None:
             torch.cuda.current_stream().wait_stream(self.stream)
@@ -156,22 +130,15 @@ class Dense:
             if self.b is not None and not bias_grad_done:
                 K.colsum(dy_colsum if dy_colsum is not None else dy2d, self.b.grad)
         def dgrad():
-            # dX = dY . W as an NT product on the transposed shadow W^T (in, out); plain narrow
-            # long-K products on hipBLASLt (K.library_gemm_ok)
+            # dX = dY . W as an NT product on the transposed shadow W^T (in, out)
             if not need_dx:
                 return None
-            if not dx_epi and K.library_gemm_ok(M, self.in_f, self.out_f):
-                return K.library_gemm_nt(dy2d, self.w.bf16_t, out=dx_out)
             return K.gemm(dy2d, self.w.bf16_t, trans_b=True, out=dx_out, **dx_epi)
         if wgrad_overlap.active is None:
             wgrad()
             return dgrad()
         side, keep = wgrad_overlap.active
         keep.extend((dy2d, x2d, dy_colsum))
-        if wgrad_overlap.batch:  # issued at the block's end (wgrad_overlap.flush)
-            dx = dgrad()
-            wgrad_overlap._pending.append(wgrad)
-            return dx
         # fork point before dX, dX issued first: the graph's first child of the fork is the
         # critical-path product, which keeps it on the main stream's hardware queue (issued after
         # the fork, it was queued behind the dW GEMM and its split-K combine on one queue)

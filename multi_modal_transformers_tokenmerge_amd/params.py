@@ -18,6 +18,7 @@ fan_in, truncated_normal), normal(0.01) biases, LayerNorm ones/zeros, ...).
 from __future__ import annotations
 
 import math
+import weakref
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Tuple
 
@@ -197,30 +198,40 @@ class ParamStore:
         """Deterministic mode (include/mmt_api.h mmt_set_deterministic): the gradient sums that
         are fp32 atomics otherwise go to an int64 fixed-point shadow of flat_grad (integer adds:
         order-independent), added into flat_grad by det_flush. Resolution 2^-36 per
-        contribution, range |sum| < 2^27 per element; a NaN / Inf or |v| >= 2^26 contribution
-        bypasses the shadow as a plain fp32 atomic, so it still shows in the gradient.
+        contribution, range |sum| < 2^27 per element; a NaN / Inf or |v| >= 2^15 contribution
+        bypasses the shadow as a plain fp32 atomic, so it still shows in the gradient (and at
+        most 4096 shadow contributions per element per flush cannot wrap the int64).
         The library keeps ONE registration per process: a second store asking for it while
-        another holds it raises (its gradient sites would otherwise silently take the
-        registration from the first). The registration holds a reference to this store until
-        set_deterministic(False) / close() (or use ``with store.deterministic():``).
-        Synchronous, so call outside graph capture."""
+        another LIVE store holds it raises (its gradient sites would otherwise silently take the
+        registration from the first). The registration refers to its store weakly: a store
+        dropped without close() counts as released, and the next store to ask takes the
+        registration over. Until then the class keeps the two device buffers the library points
+        at (flat_grad and the shadow) alive, so no kernel can write into freed memory; the
+        takeover (or set_deterministic(False) / close() / ``with store.deterministic():``) lets
+        them go. Synchronous, so call outside graph capture."""
         from . import _C
         if on:
-            owner = ParamStore._det_owner
+            owner = ParamStore._det_owner() if ParamStore._det_owner is not None else None
             if owner is not None and owner is not self:
                 raise RuntimeError("deterministic mode is registered by another ParamStore; "
                                    "call its set_deterministic(False) / close() first")
             if self.det_fx is None:
                 self.det_fx = torch.zeros(self.n, dtype=torch.int64, device=self.flat_grad.device)
             _C.call("mmt_set_deterministic", _C.ptr(self.flat_grad), _C.ptr(self.det_fx), self.n)
-            ParamStore._det_owner = self
+            ParamStore._det_owner = weakref.ref(self)
+            ParamStore._det_buffers = (self.flat_grad, self.det_fx)
         else:
-            if ParamStore._det_owner is self:
+            if self._holds_det():
                 _C.call("mmt_set_deterministic", None, None, 0)
                 ParamStore._det_owner = None
+                ParamStore._det_buffers = None
             self.det_fx = None
 
-    _det_owner = None
+    _det_owner = None    # weakref.ref to the registered store
+    _det_buffers = None  # (flat_grad, shadow) the library points at while registered
+
+    def _holds_det(self) -> bool:
+        return ParamStore._det_owner is not None and ParamStore._det_owner() is self
 
     def close(self):
         """Release the deterministic-mode registration if this store holds it (the explicit

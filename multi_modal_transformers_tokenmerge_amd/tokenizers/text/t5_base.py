@@ -117,14 +117,8 @@ class T5Tokenizer:
             a, _ = K.attn_fwd(q, c.num_heads, 1.0, None, None, 1.0, bias=bias)
             x = K.gemm(a.view(B * T, -1), o.bf16, trans_b=True, residual=x)
             n = K.rmsnorm(x, ln1.bf16, c.layer_norm_epsilon)
-            if K.library_relu_gemm_ok(B * T, wi.bf16.shape[0], c.d_model):
-                h = K.library_relu_gemm_nt(n, wi.bf16)
-            else:
-                h = K.gemm(n, wi.bf16, trans_b=True, act=K.ACT_RELU)
-            if K.library_gemm_ok(B * T, c.d_model, h.shape[1]):  # plain product + residual
-                x = K.library_gemm_nt(h, wo.bf16, residual=x)
-            else:
-                x = K.gemm(h, wo.bf16, trans_b=True, residual=x)
+            h = K.gemm(n, wi.bf16, trans_b=True, act=K.ACT_RELU)
+            x = K.gemm(h, wo.bf16, trans_b=True, residual=x)
             if layer_outputs is not None:
                 layer_outputs.append(x.view(B, T, c.d_model))
         x = K.rmsnorm(x, self.final_ln.bf16, c.layer_norm_epsilon)

@@ -50,9 +50,13 @@ def time_embedding(steps: int, fourier_w, w_t1, b_t1, w_t2, b_t2) -> np.ndarray:
     return bf16(ht @ bf16(w_t2).T + np.asarray(b_t2, np.float64))
 
 
-def predict_action(readout_mean, z, temb, w1, b1, w2, b2, coef, clip: float = 5.0) -> np.ndarray:
+def predict_action(readout_mean, z, temb, w1, b1, w2, b2, coef, clip: float = 5.0,
+                   stored_bf16: bool = False) -> np.ndarray:
     """readout_mean (B, D); z (B, A) initial sample; temb (steps, T); w1 (H, A+T+D) [out][in];
-    b1 (H,); w2 (A, H); b2 (A,); coef (steps, 3). Returns the (B, A) actions (float64)."""
+    b1 (H,); w2 (A, H); b2 (A,); coef (steps, 3). Returns the (B, A) actions (float64).
+    stored_bf16: the noisy sample and the hidden layer rounded to bf16 where the per-step launch
+    form (DiffusionActionHead._predict_action_loop: predict_denoise_term_mean per step) stores
+    them; the fused one-launch sampler keeps both fp32 (False)."""
     z = np.asarray(z, dtype=np.float64)
     A = z.shape[1]
     temb = np.asarray(temb, dtype=np.float64)
@@ -64,7 +68,10 @@ def predict_action(readout_mean, z, temb, w1, b1, w2, b2, coef, clip: float = 5.
     Q = temb @ w1[:, A:A + T].T + np.asarray(b1, np.float64)          # (steps, H)
     x = z.copy()
     for t in range(coef.shape[0] - 1, -1, -1):
-        h = np.maximum(x @ w1[:, :A].T + Q[t][None, :] + P, 0.0)
+        xin = bf16(x) if stored_bf16 else x
+        h = np.maximum(xin @ w1[:, :A].T + Q[t][None, :] + P, 0.0)
+        if stored_bf16:
+            h = bf16(h)
         eps = h @ w2.T + np.asarray(b2, np.float64)
         c1, c2, c3 = (float(v) for v in coef[t])
         x = np.clip(c1 * (x - c2 * eps) + c3 * z, -clip, clip)

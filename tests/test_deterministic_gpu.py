@@ -85,9 +85,12 @@ def test_shards_equal_full_batch(dev):
 
 
 def test_nan_and_large_contributions_stay_visible(dev):
-    """in the mode a NaN / Inf contribution or one beyond the shadow's range
-    (|v| >= 2^26) goes to the fp32 gradient as a plain atomic (csrc/common.h det_fits), so the
-    gradient shows it after the flush instead of a clamped finite value."""
+    """in the mode a NaN / Inf contribution or one beyond the shadow's
+    per-contribution bound (|v| >= 2^15) goes to the fp32 gradient as a plain atomic
+    (csrc/common.h det_fits), so the gradient shows it after the flush instead of a clamped
+    finite value — and many large contributions whose sum exceeds the int64 shadow's 2^27 range
+    (4096 rows of 2^17: 2^29, which wrapped under the round-5 per-contribution bound of 2^26)
+    come out exact instead of wrapped."""
     from multi_modal_transformers_tokenmerge_amd import _kernels as K
     from multi_modal_transformers_tokenmerge_amd.params import ParamStore, const
     st = ParamStore()
@@ -106,6 +109,12 @@ def test_nan_and_large_contributions_stay_visible(dev):
     assert abs(float(g[13]) - (1e9 + 511)) <= 1e9 * 1e-6
     rest = [i for i in range(64) if i not in (5, 9, 13)]
     assert torch.equal(g[rest], torch.full((61,), 512.0))
+    p.grad.zero_()
+    with st.deterministic():
+        K.colsum(torch.full((4096, 64), 2.0 ** 17, device=dev), p.grad)
+        st.det_flush()
+        torch.cuda.synchronize()
+        assert torch.equal(p.grad.cpu(), torch.full((64,), 2.0 ** 29))
 
 
 def test_second_store_cannot_take_the_registration(dev):
@@ -119,5 +128,35 @@ def test_second_store_cannot_take_the_registration(dev):
         with pytest.raises(RuntimeError):
             b.set_deterministic(True)
     with b.deterministic():  # free again after a's block
-        assert ParamStore._det_owner is b
+        assert ParamStore._det_owner() is b
     assert ParamStore._det_owner is None
+
+
+def test_dropped_store_releases_the_registration(dev):
+    """A store dropped without close() (e.g. a model built under MMT_DETERMINISTIC=1 and thrown
+    away) must not lock the mode for the rest of the process: the registration refers to it
+    weakly, the library's buffers stay alive until the next store takes over, and that store's
+    sums are exact again."""
+    import gc
+    from multi_modal_transformers_tokenmerge_amd import _kernels as K
+    from multi_modal_transformers_tokenmerge_amd.params import ParamStore, const
+    a = ParamStore()
+    a.add("w", (64,), const(0.0))
+    a.materialize(dev)
+    a.set_deterministic(True)
+    del a
+    gc.collect()
+    assert ParamStore._det_buffers is not None  # the device buffers outlive the store
+    b = ParamStore()
+    p = b.add("w", (64,), const(0.0))
+    b.materialize(dev)
+    b.set_deterministic(True)  # takes the registration over
+    try:
+        assert ParamStore._det_owner() is b and ParamStore._det_buffers[1] is b.det_fx
+        K.colsum(torch.ones((300, 64), device=dev), p.grad)
+        b.det_flush()
+        torch.cuda.synchronize()
+        assert torch.equal(p.grad.cpu(), torch.full((64,), 300.0))
+    finally:
+        b.close()
+    assert ParamStore._det_owner is None and ParamStore._det_buffers is None

@@ -148,35 +148,14 @@ def test_auto_split_small_m(dev):
     _close_bf16(o_one, ref)
 
 
-@pytest.mark.parametrize("N,K,res", [(384, 1536, False), (768, 3072, True)])
-def test_library_gemm_plain_products(dev, N, K, res):
-    """The plain narrow long-K products routed to hipBLASLt (Dense input gradients, the frozen T5's
-    FF output + residual) agree with libmmt_hip's kernel on the same bf16 operands (fp32
-    accumulation either way: one bf16 rounding apart)."""
-    from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
-    M = 8192
-    assert Kn.library_gemm_ok(M, N, K) == Kn._BLASLT
-    g = torch.Generator().manual_seed(N + K)
-    a, b = _mk((M, K), dev, g), _mk((N, K), dev, g)
-    r = _mk((M, N), dev, g) if res else None
-    lib = Kn.library_gemm_nt(a, b, residual=r)
-    ours = Kn.gemm(a, b, False, True, residual=r)
-    ref = a.float() @ b.float().t() + (r.float() if res else 0.0)
-    _close_bf16(lib, ref)
-    _close_bf16(ours, ref)
-
-
-def test_library_relu_product(dev):
-    """The frozen T5's FF input on hipBLASLt's relu epilogue equals libmmt_hip's relu product."""
+def test_t5_relu_product(dev):
+    """The frozen T5's FF input relu(x W_i^T) (t5_base.py) on libmmt_hip against fp32 torch."""
     from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
     M, N, K = 8192, 3072, 768
     g = torch.Generator().manual_seed(5)
     a, b = _mk((M, K), dev, g), _mk((N, K), dev, g)
     ref = torch.relu(a.float() @ b.float().t())
-    ours = Kn.gemm(a, b, False, True, act=Kn.ACT_RELU)
-    _close_bf16(ours, ref)
-    if Kn.library_relu_gemm_ok(M, N, K):
-        _close_bf16(Kn.library_relu_gemm_nt(a, b), ref)
+    _close_bf16(Kn.gemm(a, b, False, True, act=Kn.ACT_RELU), ref)
 
 
 @pytest.mark.parametrize("M,N,K,ep,variant", [
@@ -210,12 +189,12 @@ def test_narrow_nt_kernel(dev, M, N, K, ep, variant):
                                          (8200, 384, 384, 0.5), (4100, 768, 128, 1.0),
                                          (5000, 384, 64, 1.0)])
 def test_residual_stream_kernel(dev, M, N, K, alpha):
-    """gemm_nres_kernel (fp32 C = fp32 residual + dropout(alpha A.W^T + bias): the step's
-    out-projection and MLP Dense_1, reference attention.py:36-37,59-63): bit-identical to the
-    128 x 128 direct-to-LDS kernel (variant 4) on the same launch — same MFMA shape and k order per
-    output, same epilogue order — at the B = 512 block-0 shapes, ragged row ranges, two 384-column
-    tiles and one-K-step reductions; and within fp32 accumulation order of a torch reference."""
-    from multi_modal_transformers_tokenmerge_amd import _C
+    """The residual-stream products as the step runs them (fp32 C = fp32 residual + dropout(alpha
+    A.W^T + bias): the out-projection and MLP Dense_1, reference attention.py:36-37,59-63, on the
+    128 x 128 direct-to-LDS kernel) at the B = 512 block-0 shapes, ragged rows and one-K-step
+    reductions: the dropout keeps are the shared counter stream's (oracle/rng.py), the sum within
+    fp32 accumulation order of a torch reference. (Round 4's warp-specialised kernel for these
+    products measured slower and was deleted in round 6.)"""
     from multi_modal_transformers_tokenmerge_amd import _kernels as Kn
     g = torch.Generator().manual_seed(M + N + K)
     a, w = _mk((M, K), dev, g), _mk((N, K), dev, g)
@@ -224,16 +203,8 @@ def test_residual_stream_kernel(dev, M, N, K, alpha):
     rng = torch.tensor([31, 4], dtype=torch.int32, device=dev)
     kw = dict(bias=bias, rng=rng, drop_layer=2, drop_site=3, keep_prob=0.9, drop_row_offset=3 * M,
               residual=res, alpha=alpha, out_mode=Kn.OUT_F32)
-    _C.call("mmt_gemm_set_nres", 1)
-    try:
-        out = Kn.gemm(a, w, False, True, **kw)
-        _C.call("mmt_gemm_set_variant", 4)
-        old = Kn.gemm(a, w, False, True, **kw)
-        torch.cuda.synchronize()
-    finally:
-        _C.call("mmt_gemm_set_variant", -1)
-        _C.call("mmt_gemm_set_nres", -1)
-    assert torch.equal(out.view(torch.int32), old.view(torch.int32))
+    out = Kn.gemm(a, w, False, True, **kw)
+    torch.cuda.synchronize()
     keep = torch.from_numpy(R.dropout_mask_2d(31, 4, 2, 3, M, N, 3 * M, 0.9)).to(dev)
     ref = alpha * (a.float() @ w.float().t()) + bias
     ref = torch.where(keep, ref / 0.9, torch.zeros_like(ref)) + res

@@ -107,3 +107,30 @@ def test_predict_denoise_term_matches_oracle(dev):
     h = ref.bf16(np.maximum(x @ w1.T + b1, 0.0))
     want = h @ _np(head.d2.w.bf16).T + _np(head.d2.b.data)
     np.testing.assert_allclose(_np(eps), want, atol=2e-3, rtol=2e-3)
+
+
+def test_sampler_loop_form_matches_oracle(dev):
+    """The per-step launch form of predict_action (OctoDenoise num_blocks > 1 takes it:
+    DiffusionActionHead._predict_action_loop) forced at num_blocks = 1, where the fused sampler
+    exists: from the same initial sample z, (1) against the oracle's 32-step loop with the noisy
+    sample and the hidden layer rounded to bf16 where this form stores them (pins its update
+    order, coefficients and operand handling), (2) against the fused sampler (fp32 noisy sample
+    and hidden) within the bf16 storage difference over 32 steps."""
+    head = _head(dev, 384, seed=13)
+    B = 9
+    g = torch.Generator().manual_seed(5)
+    readout = (torch.randn((B, 384), generator=g) * 0.5).to(torch.bfloat16).to(dev)
+    rng = torch.tensor([77, 2], dtype=torch.int32, device=dev)
+    fused, z = head.predict_action_mean(readout, rng, sample_offset=3, return_noise=True)
+    loop = head._predict_action_loop(readout, None, 0, z.clone(), False)
+    temb = head.time_embeddings(dev)
+    torch.cuda.synchronize()
+    coef = ref.sampler_coefficients(head.betas_np, head.alpha_hats_np)
+    want = ref.predict_action(_np(readout), _np(z), _np(temb), _np(head.d1.w.bf16), _np(head.d1.b.data),
+                              _np(head.d2.w.bf16), _np(head.d2.b.data), coef, stored_bf16=True)
+    got = _np(loop)
+    assert np.all(np.abs(got) <= 5.0)
+    np.testing.assert_allclose(got, want, atol=5e-3, rtol=5e-3)
+    f = _np(fused)
+    rel = np.linalg.norm(got - f) / np.linalg.norm(f)
+    assert rel <= 2e-2, rel

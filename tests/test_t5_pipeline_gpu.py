@@ -49,8 +49,8 @@ def test_pipelined_step_matches_plain(dev, use_graph, fork, monkeypatch):
     assert torch.equal(ma.store.flat, mb.store.flat)
     data = _batches(ma, B, n + 1, dev)
     bufs = []
-    for m in (ma, mb):
-        img, txt, act = (x.clone() for x in data[0])
+    for m in (ma, mb):  # built on a batch no step trains on: the loader writes batch 0 after build()
+        img, txt, act = (x.clone() for x in data[n])
         bufs.append((img, txt, act))
     txt_next = data[1][1].clone()
     pa = DDPStep(ma, sa, bufs[0][1], bufs[0][0], bufs[0][2], None, use_graph=use_graph,
@@ -72,6 +72,14 @@ def test_pipelined_step_matches_plain(dev, use_graph, fork, monkeypatch):
         # the output held for step i + 1 is the encoder of step i + 1's text, bit for bit
         assert torch.equal(pa.t5_cur, ma.t5(data[i + 1][1]))
     assert _rel(ma.store.flat, mb.store.flat) <= 1e-5
+    # reset_text(): the next call encodes its own txt again (here: a batch txt_next never held)
+    for (img, txt, act) in bufs:
+        img.copy_(data[1][0]); txt.copy_(data[1][1]); act.copy_(data[1][2])
+    pa.reset_text()
+    pa()
+    pb()
+    torch.cuda.synchronize()
+    assert abs(float(pa.loss_buf) - float(pb.loss_buf)) <= 1e-4 * abs(float(pb.loss_buf)) + 1e-6
 
 
 @pytest.mark.parametrize("fork", ["ext", "fwd", "bwd"])

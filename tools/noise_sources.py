@@ -49,6 +49,7 @@ def main():
         for tag, h in (("hip", h1), ("det", hd)):
             ref_loss, ref_grads = P.oracle_step(cfg, h, model=h["model"])
             r[tag] = (abs(h["loss"] / ref_loss - 1), 1 - gcos(h["grads"], ref_grads))
+        hd["model"].store.close()  # release the deterministic registration for the next seed
         f = P.bf16_floor(cfg, h1, h1["model"])
         r["floor"] = (abs(f["loss"] / f["ref_loss"] - 1), 1 - f["cos_all"])
         rows.append(r)
