@@ -21,12 +21,14 @@ bf16) lies from that same exact result — what bf16 storage alone costs an hone
 small_tome16_2blk HIP is the closer of the two to exact on 50 of the 51 gradient tensors, median
 error 0.70x the emulation's — profiles/r05_golden_exact.txt):
   * block inputs, final sequence, loss: relative (L2) <= max(2e-2, 2 x floor);
-  * every parameter gradient: relative L2 <= max(5e-2, 2 x floor) (SURVEY §8c rtol 5e-2), and the
-    norm ratio |g| / |g_exact| within max(0.02, 2 |floor ratio - 1|, floor relative L2) of 1
-    — the last term because a floor error of relative size e can move the norm by up to e (the
-    floor's own ratio sits near 1 only when its error happens to be orthogonal to the gradient;
-    on the cancellation-heavy first-block bias sums the error is ~7.6 %: DESIGN §4);
+  * every parameter gradient: relative L2 <= max(5e-2, 2 x floor) (SURVEY §8c rtol 5e-2);
   * the global gradient cosine >= 0.999, or within twice the floor's deficit.
+The norm ratio |g| / |g_exact| of one fixture is one draw of bf16 noise (on the cancellation-
+heavy first-block bias sums both bf16 implementations err by ~7 %, and the projection of that
+error on the gradient moves the norm by a few per cent either way), so it is not barred per
+fixture: test_gradients_against_exact_over_seeds bars it over 8 seeds, per tensor, without a
+floor term: the median ratio within 0.02 of 1, and HIP's median error at
+most 1.3x the emulation's.
 """
 import ast
 from pathlib import Path
@@ -126,7 +128,7 @@ def test_step_matches_golden_fixture(dev, tag):
         all_h.append(np.asarray(hip, np.float64))
         all_e.append(np.asarray(emu, np.float64))
         all_f.append(np.asarray(f64, np.float64))
-        if r > max(5e-2, 2 * rfl) or abs(ratio - 1) > max(0.02, 2 * abs(rf - 1), rfl):
+        if r > max(5e-2, 2 * rfl):
             bad.append((p.name, r, rfl, ratio, rf))
     worst.sort(reverse=True)
     cg = _cos(np.concatenate(all_h), np.concatenate(all_f))
@@ -136,4 +138,57 @@ def test_step_matches_golden_fixture(dev, tag):
         report.append(f"  grad rel {r:.3e} (floor {rfl:.3e}) cos {c:.6f} ratio {ratio:.4f} (floor {rf:.4f}) {name}")
     print(f"\n[{tag}] " + "\n".join(report))
     assert cg >= 0.999 or 1 - cg <= 2 * (1 - cgf) + 1e-4, (cg, cgf)
+    assert not bad, bad
+
+
+def test_gradients_against_exact_over_seeds(dev):
+    """Per parameter tensor over 8 seeds of the OCTO-small ToMe r = 16 step (2 blocks, B = 2,
+    2-layer T5; each seed its own parameters, inputs and randomness; the oracle on the HIP run's
+    injected randomness and ToMe indices), HIP and the bf16-emulating restatement both against the
+    EXACT float64 restatement (oracle.parity.oracle_pair), as tools/parity_exact.py measures it:
+      * the median over seeds of |g_hip| / |g_exact| within 0.02 of 1 — no systematic shrink or
+        growth of any tensor, the block-0 bias sums included, with no floor term;
+      * the median over seeds of err_hip / err_emu (relative L2 to exact) at most 1.3 — HIP's
+        fp32 summation order and v_exp_f32 may add to the bf16 storage error, not multiply it;
+      * the global gradient: median norm ratio within 0.01 of 1, median cosine >= 0.99.
+    The table it prints is profiles/r06_golden_multiseed.txt."""
+    import statistics as stt
+
+    from multi_modal_transformers_tokenmerge_amd.models.octo.config import get_config
+    from multi_modal_transformers_tokenmerge_amd.tokenizers.text.t5_base import T5Config
+    from oracle import parity as P
+    cfg = get_config("octo-small-tome16", num_blocks=2, t5=T5Config(num_layers=2))
+    per, glob = {}, []
+    for seed in range(8):
+        h = P.hip_step(cfg, 2, seed)
+        (_, ge), (_, gf) = P.oracle_pair(cfg, h, h["model"])
+        H, F = [], []
+        for k in sorted(gf):
+            f = np.asarray(gf[k], np.float64).ravel()
+            n = np.linalg.norm(f)
+            if n == 0:
+                continue
+            hh = np.asarray(h["grads"][k], np.float64).ravel()
+            ee = np.asarray(ge[k], np.float64).ravel()
+            eh, em = np.linalg.norm(hh - f) / n, np.linalg.norm(ee - f) / n
+            per.setdefault(k, []).append((np.linalg.norm(hh) / n, eh, em, eh / max(em, 1e-30)))
+            H.append(hh)
+            F.append(f)
+        H, F = np.concatenate(H), np.concatenate(F)
+        glob.append((np.linalg.norm(H) / np.linalg.norm(F), _cos(H, F)))
+        del h
+    lines, bad = [], []
+    for k, v in sorted(per.items()):
+        ratio = stt.median(x[0] for x in v)
+        err_ratio = stt.median(x[3] for x in v)
+        lines.append(f"  ratio {ratio:.4f} [{min(x[0] for x in v):.4f}, {max(x[0] for x in v):.4f}]"
+                     f"  err hip {stt.median(x[1] for x in v):.2e} emu {stt.median(x[2] for x in v):.2e}"
+                     f"  hip/emu {err_ratio:.3f}  {k}")
+        if abs(ratio - 1) > 0.02 or err_ratio > 1.3:
+            bad.append((k, ratio, err_ratio))
+    gr, gc = stt.median(x[0] for x in glob), stt.median(x[1] for x in glob)
+    print(f"\n8 seeds, octo-small-tome16 2 blocks B = 2 vs float64: global norm ratio median {gr:.4f}, "
+          f"cosine median {gc:.5f}; err_hip/err_emu median over tensors "
+          f"{stt.median(stt.median(x[3] for x in v) for v in per.values()):.3f}\n" + "\n".join(lines))
+    assert abs(gr - 1) <= 0.01 and gc >= 0.99, (gr, gc)
     assert not bad, bad
