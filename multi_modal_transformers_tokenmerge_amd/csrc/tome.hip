@@ -1066,15 +1066,21 @@ __global__ __launch_bounds__(256) void tome_merge_seqnorm_fwd_kernel(
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     bf16_t* __restrict__ y, int64_t ys_n, int64_t ys_t, float* __restrict__ mean_out,
     float* __restrict__ rstd_out, unsigned int* fault) {
-  __shared__ int32_t s_unm[1024];
-  __shared__ int32_t s_src[512];
-  __shared__ int32_t s_dst[512];
+  // LDS sized for the rows this instantiation handles (RPT > 0: Lout <= 32 RPT; nu, r <= Lout),
+  // and the pass-1 reduction scratch aliases the source lists (dead by then, behind a barrier):
+  // 35-52 KB per workgroup instead of 68 KB, three or four workgroups per CU instead of two
+  constexpr int MR = RPT > 0 ? 32 * RPT : kFusedRows;
+  __shared__ int32_t s_unm[RPT > 0 ? MR : 1024];
+  __shared__ int32_t s_src[RPT > 0 ? MR : 512];
+  __shared__ int32_t s_dst[RPT > 0 ? MR : 512];
   __shared__ uint32_t s_seen[kSeenWords];
-  __shared__ int32_t m_prim[kFusedRows], m_cnt[kFusedRows], m_j[kFusedRows];
-  __shared__ float m_sp[kFusedRows], m_S[kFusedRows];
-  __shared__ int32_t m_list[kFusedRows][kMergeSeg];
-  __shared__ float m_ss[kFusedRows][kMergeSeg];
-  __shared__ float red[2 * kFRG * 64];
+  __shared__ int32_t m_prim[MR], m_cnt[MR], m_j[MR];
+  __shared__ float m_sp[MR], m_S[MR];
+  constexpr int LIST_B = MR * kMergeSeg * 8, RED_B = 2 * kFRG * 64 * 4;
+  __shared__ __attribute__((aligned(16))) char m_lists[LIST_B > RED_B ? LIST_B : RED_B];
+  int32_t (*m_list)[kMergeSeg] = reinterpret_cast<int32_t (*)[kMergeSeg]>(m_lists);
+  float (*m_ss)[kMergeSeg] = reinterpret_cast<float (*)[kMergeSeg]>(m_lists + MR * kMergeSeg * 4);
+  float* red = reinterpret_cast<float*>(m_lists);
   __shared__ float s_mul[64], s_add[64];
   const int n = ln_sample(), c0 = ln_colblk() * 64;
   const int ta = (t + 1) / 2;
@@ -1197,6 +1203,7 @@ __global__ __launch_bounds__(256) void tome_merge_seqnorm_fwd_kernel(
       merge_row(o, v);
     }
   }
+  __syncthreads();  // every merge_row has read the source lists that red overwrites
 #pragma unroll
   for (int vv = 0; vv < 2; ++vv)
 #pragma unroll
