@@ -1339,9 +1339,10 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_bwd_res_kernel(
 // one after the other, each behind its own DMA; ablations at L = 292, B = 512: 513 us of which
 // 110 us are phase-A tiles, 174 us phase-B tiles and ~230 us memory not overlapped with them.
 // Here one 8-wave workgroup per (sample, head) holds K, V, Q and dO (4 x 40 KB at L <= 320:
-// the CU's 160 KB) loaded once; after a prologue that writes the row constants rc of every
-// query row (delta = rowsum(dO O) from the dO image and O rows, the same summation order as
-// the two-phase kernel), waves 0 .. RES8_NA - 1 run phase A (dQ, queries on the lanes) and the
+// the CU's 160 KB) loaded once; after a prologue that writes the row constants of every query
+// row into LDS (delta = rowsum(dO O) from the dO image and O rows loaded under the DMA, the same
+// summation order as the two-phase kernel; round 6: they were a global workspace that phase B
+// waited on per key tile, and the images were 32 NTILE rows instead of L rounded to 8), waves 0 .. RES8_NA - 1 run phase A (dQ, queries on the lanes) and the
 // rest phase B (dK / dV, keys on the lanes) at the same time, blocks dealt longest-first by
 // visible tiles, every row fragment read from the images. Same arithmetic and order per output
 // as attn_bwd_res_kernel: bit-identical dQ / dK / dV (the bias column sums add the per-wave
@@ -1361,6 +1362,34 @@ __device__ unsigned long long g_res8_stamps[8192 * 8 * 6];
   } while (0)
 #endif
 constexpr int RES8_NA = 3;
+// Rows per LDS image: L rounded up to 8 (one DMA piece = 8 rows), at most the tile rows. The
+// tiles' reads past IR land in the next image (finite rows: masked keys / P = 0 queries there)
+// or, after the dO image, in a zeroed slack; the row constants follow.
+__host__ __device__ constexpr int res8_rows(int L, int ntile) {
+  return ((L + 7) & ~7) < 32 * ntile ? ((L + 7) & ~7) : 32 * ntile;
+}
+__host__ __device__ constexpr int res8_need(int L, int ntile) {
+  return 3 * res8_rows(L, ntile) * 128 + 32 * ntile * 128 + 2 * 32 * ntile * 4;
+}
+// static LDS of an instantiation: the largest layout that fits the CU's 160 KB (NTILE 10: L <= 312;
+// the host falls back to the two-phase kernel past it), at least the bias partials' 64 KB
+__host__ __device__ constexpr int res8_lds(int ntile) {
+  return res8_need(32 * ntile, ntile) <= 163840 ? (res8_need(32 * ntile, ntile) > 65536 ? res8_need(32 * ntile, ntile) : 65536)
+                                                 : 163840;
+}
+// DMA of rows [0, 8 np) (clamped to L - 1) of two (row stride s) bf16 tensors into two swizzled
+// images at da / db: one wave-instruction = 8 rows x 128 B
+__device__ __forceinline__ void res_dma2r(char* da, const bf16_t* a, int64_t sa, char* db, const bf16_t* b,
+                                          int64_t sb, int L, int np, int wave, int lane) {
+  for (int p = wave; p < 2 * np; p += RES_NW) {
+    const int t = p >= np, pr = p - t * np;
+    const int row = 8 * pr + (lane >> 3);
+    const int c = (lane & 7) ^ res_sw(row);
+    const bf16_t* src = (t ? b : a) + (int64_t)min(row, L - 1) * (t ? sb : sa) + 8 * c;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)((t ? db : da) + pr * 1024), 16, 0, 0);
+  }
+}
 template <int NTILE, bool DROP>
 __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
     Geo g, AttnMask mask, ResPlanB plan, const uint32_t* __restrict__ drop_q,
@@ -1368,25 +1397,25 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
     const bf16_t* __restrict__ dout, int64_t d_s_b, int64_t d_s_t, const float* __restrict__ lse,
     const bf16_t* __restrict__ o, int64_t o_s_b, int64_t o_s_t, float* __restrict__ rc,
     bf16_t* __restrict__ dqkv, int64_t dq_s_b, int64_t dq_s_t, float* __restrict__ bias_grad) {
-  constexpr int DH = 64, NS = 4, ROWS = 32 * NTILE, LP = ROWS, IMG = ROWS * DH * 2;
-  constexpr int RED_BYTES = 2 * 2 * RES_NW * 64 * 16 * 4;  // the bias partials, after the phases
-  // K | V | Q | dO images (the bias partials reuse them: 64 KB, more than the images at NTILE 2)
-  __shared__ __attribute__((aligned(16))) char smem_raw[4 * IMG > RED_BYTES ? 4 * IMG : RED_BYTES];
-  bf16_t* smem = reinterpret_cast<bf16_t*>(smem_raw);
+  constexpr int DH = 64, NS = 4, ROWS = 32 * NTILE, LP = ROWS;
+  // K | V | Q | dO images of IR rows each, the zeroed slack, the row constants (res8_lds); the
+  // bias partials reuse the space after the phases
+  __shared__ __attribute__((aligned(16))) char smem_raw[res8_lds(NTILE)];
   const int bh = blockIdx.x, b = bh / g.H, h = bh - b * g.H;
   const int lane = threadIdx.x & 63, hh = lane >> 5, lr = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int L = g.L, D = g.H * DH;
   const bf16_t* base = g.qkv + (int64_t)b * g.s_b;
   const bf16_t* dbase = dout + (int64_t)b * d_s_b + h * DH;
-  float* rc0 = rc + (int64_t)bh * 2 * LP;
-  float* rc1 = rc0 + LP;
   const float c2 = g.scale * LOG2E;
   const float kp = 1.f / drop_scale;
+  const int IR = res8_rows(L, NTILE), IS = IR * 128;
   const char* imgK = smem_raw;
-  const char* imgV = imgK + IMG;
-  const char* imgQ = imgV + IMG;
-  const char* imgD = imgQ + IMG;
+  const char* imgV = imgK + IS;
+  const char* imgQ = imgV + IS;
+  const char* imgD = imgQ + IS;
+  float* rl0 = reinterpret_cast<float*>(smem_raw + 3 * IS + ROWS * 128);  // rc0 / rc1 (below)
+  float* rl1 = rl0 + LP;
   int koff[NS];  // row-fragment offsets (row lr of a 32-row tile, chunk 2 s + hh)
 #pragma unroll
   for (int s = 0; s < NS; ++s) koff[s] = lr * 128 + 16 * ((2 * s + hh) ^ res_sw(lr));
@@ -1394,37 +1423,50 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
   const float sc_out = g.scale * drop_scale;
 
   RES8_STAMP(0);
-  // ---- DMA of the four images (waves 0-3: K and V, waves 4-7: Q and dO)
+  // ---- DMA of the four images (waves 0-3: K and V, waves 4-7: Q and dO), IR rows each; the
+  //      O rows and lse of the row constants are loaded under it
   if (wave < RES_NW)
-    res_dma2<ROWS>(smem, base + D + h * DH, g.s_t, base + 2 * D + h * DH, g.s_t, L, wave, lane);
+    res_dma2r(smem_raw, base + D + h * DH, g.s_t, smem_raw + IS, base + 2 * D + h * DH, g.s_t, L,
+              IR / 8, wave, lane);
   else
-    res_dma2<ROWS>(smem + 2 * ROWS * DH, base + h * DH, g.s_t, dbase, d_s_t, L, wave - RES_NW, lane);
+    res_dma2r(smem_raw + 2 * IS, base + h * DH, g.s_t, smem_raw + 3 * IS, dbase, d_s_t, L, IR / 8,
+              wave - RES_NW, lane);
+  {  // the slack after the dO image (read as its rows >= IR): zeros
+    const int nsl = (ROWS * 128 - IS) / 16;
+    for (int i = threadIdx.x; i < nsl; i += 128 * RES_NW)
+      reinterpret_cast<uint4*>(smem_raw + 4 * IS)[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  const int pq = threadIdx.x;
+  const bool pv = pq < ROWS && pq < L;
+  bf16x8 orow[8];
+  float lq = 0.f;
+  if (pv) {
+    const bf16_t* op = o + (int64_t)b * o_s_b + (int64_t)pq * o_s_t + h * DH;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) orow[c] = *reinterpret_cast<const bf16x8*>(op + 8 * c);
+    lq = lse[(int64_t)bh * L + pq];
+  }
   __syncthreads();  // the DMA landed (vmcnt(0) + barrier)
   RES8_STAMP(1);
   // ---- row constants of every query row: rc0 = -lse / scale (-inf past L), rc1 = -kp delta
   //      (0 past L); delta as the two-phase kernel forms it: chunks 0, 2, 4, 6 and 1, 3, 5, 7
   //      of the row as two fmaf chains, then their sum
-  if (threadIdx.x < ROWS) {
-    const int q = threadIdx.x;
+  if (pq < ROWS) {
     float v0 = -INFINITY, v1 = 0.f;
-    if (q < L) {
-      const bf16_t* orow = o + (int64_t)b * o_s_b + (int64_t)q * o_s_t + h * DH;
+    if (pv) {
       float part[2] = {0.f, 0.f};
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        const bf16x8 of = *reinterpret_cast<const bf16x8*>(orow + 8 * c);
-        const bf16x8 df = *reinterpret_cast<const bf16x8*>(imgD + q * 128 + 16 * (c ^ res_sw(q)));
+        const bf16x8 df = *reinterpret_cast<const bf16x8*>(imgD + pq * 128 + 16 * (c ^ res_sw(pq)));
 #pragma unroll
-        for (int j = 0; j < 8; ++j) part[c & 1] = fmaf((float)of[j], (float)df[j], part[c & 1]);
+        for (int j = 0; j < 8; ++j) part[c & 1] = fmaf((float)orow[c][j], (float)df[j], part[c & 1]);
       }
-      v0 = -lse[(int64_t)bh * L + q] / g.scale;
+      v0 = -lq / g.scale;
       v1 = -((part[0] + part[1]) * kp);
     }
-    rc0[q] = v0;
-    rc1[q] = v1;
+    rl0[pq] = v0;
+    rl1[pq] = v1;
   }
-  // rc is read by the other waves (L2, no stale L1 line: first touch in this workgroup)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   RES8_STAMP(2);
 
@@ -1465,7 +1507,7 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
         qf[s] = *reinterpret_cast<const bf16x8*>(imgQ + blk * 4096 + koff[s]);
         df[s] = *reinterpret_cast<const bf16x8*>(imgD + blk * 4096 + koff[s]);
       }
-      const float dkp = -rc1[q];  // kp delta (0 past L)
+      const float dkp = -rl1[q];  // kp delta (0 past L)
       const float lse2 = qv ? lse[(int64_t)bh * L + q] * LOG2E : INFINITY;
       const int sq = set_of(mask, qc);
       const int sq0 = __builtin_amdgcn_readfirstlane(sq);
@@ -1594,8 +1636,8 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
           floatx16 sacc, ca;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float4 x = *reinterpret_cast<const float4*>(rc0 + 32 * t + 8 * j + 4 * hh);
-            const float4 y = *reinterpret_cast<const float4*>(rc1 + 32 * t + 8 * j + 4 * hh);
+            const float4 x = *reinterpret_cast<const float4*>(rl0 + 32 * t + 8 * j + 4 * hh);
+            const float4 y = *reinterpret_cast<const float4*>(rl1 + 32 * t + 8 * j + 4 * hh);
             sacc[4 * j] = x.x; sacc[4 * j + 1] = x.y; sacc[4 * j + 2] = x.z; sacc[4 * j + 3] = x.w;
             ca[4 * j] = y.x; ca[4 * j + 1] = y.y; ca[4 * j + 2] = y.z; ca[4 * j + 3] = y.w;
           }
@@ -2346,7 +2388,8 @@ extern "C" int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
     // for bit). Alone (tools/attn_bench.py, B = 512) it wins at L = 292 (464 vs 516 us) and
     // L <= 164 (1.06-1.13x) and loses 0-6 % at L = 196 .. 276 (one workgroup per CU there);
     // in the step it is faster at every L (all: 14.75k, per-L choice: 14.73k, two-phase: 14.66k)
-    const bool bwd8 = attn_res_enabled("MMT_ATTN_BWD8");
+    const bool bwd8 = attn_res_enabled("MMT_ATTN_BWD8") &&
+                      res8_need(L, ((L + 63) / 64) * 2) <= res8_lds(((L + 63) / 64) * 2);
     ResPlanB plan;
     if (bwd8 ? res_plan_bwd(m, L, plan, RES8_NA, 2 * RES_NW - RES8_NA) : res_plan_bwd(m, L, plan)) {
       const int ntile = ((L + 63) / 64) * 2;

@@ -349,7 +349,7 @@ def test_resident_attention_vs_tiled_and_torch(dev, B, L, H, mode, drop, monkeyp
 @pytest.mark.parametrize("B,L,H,mode,drop", [
     (2, 33, 3, "none", True), (3, 65, 2, "octo", True), (2, 101, 3, "causal", True),
     (2, 212, 6, "octo", True), (2, 292, 6, "octo", False), (1, 301, 2, "causal", False),
-    (2, 320, 2, "octo", True)])
+    (2, 312, 2, "octo", True), (2, 320, 2, "octo", True)])
 def test_resident_backward_concurrent_phases_bit_identical(dev, B, L, H, mode, drop, monkeypatch):
     """The 8-wave resident backward (K, V, Q, dO all in LDS, phase A on waves 0-3 and phase B on
     waves 4-7 at the same time; the default) against the two-phase 4-wave kernel
