@@ -1290,7 +1290,10 @@ __global__ __launch_bounds__(NT3, 1) void gemm_nt256_kernel(
 //    swapped so the accumulator is C^T (lane = output row, 16 columns in runs of 4);
 //  * operands DMA'd global->LDS (buffer_load ... lds, 1 KB per wave-instruction, buffer
 //    resources rebuilt per tile) into unpadded [rows][64] bf16 images, 16-B chunk c of row r at
-//    c ^ (r & 7) (source-address swizzle; conflict-free fragment ds_read_b128);
+//    c ^ ((r >> 1) & 7) (source-address swizzle; conflict-free fragment ds_read_b128: each of the
+//    instruction's 16-lane groups takes 16 distinct (row parity, chunk) bank sets. Through round 6
+//    it was c ^ (r & 7), which pairs rows r and r + 8 of a group on one bank set: 2-way conflicts
+//    on every fragment read, half the kernel's LDS cycles; MLP dX 218 -> 211 us);
 //  * the host plans the launch so no round of the persistent grid is mostly idle (mmt_gemm);
 //  * epilogue from registers: v_permlane32_swap pairs the two half-waves' column runs into 8
 //    contiguous columns per lane (16-B residual loads and C stores).
@@ -1336,12 +1339,12 @@ __global__ __launch_bounds__(NTW_NT, 2) void gemm_ntw_kernel(
 #pragma unroll
   for (int p = 0; p < PA; ++p) {
     const int row = 8 * (wave * PA + p) + (lane >> 3);
-    voa[p] = row * (int)(lda * 2) + (((lane & 7) ^ (row & 7)) << 4);
+    voa[p] = row * (int)(lda * 2) + (((lane & 7) ^ ((row >> 1) & 7)) << 4);
   }
 #pragma unroll
   for (int p = 0; p < PB; ++p) {
     const int row = 8 * (wave * PB + p) + (lane >> 3);
-    vob[p] = row * (int)(ldb * 2) + (((lane & 7) ^ (row & 7)) << 4);
+    vob[p] = row * (int)(ldb * 2) + (((lane & 7) ^ ((row >> 1) & 7)) << 4);
   }
 #if defined(__HIP_DEVICE_COMPILE__)
   // A and B DMA positions advance separately (A runs NSA - 2 K-steps further ahead)
@@ -1403,12 +1406,12 @@ __global__ __launch_bounds__(NTW_NT, 2) void gemm_ntw_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
   const int l31 = lane & 31, h = lane >> 5;
-  int a_off[MB], b_off[NB];  // fragment row byte offsets; the rows' swizzle is l31 & 7
+  int a_off[MB], b_off[NB];  // fragment row byte offsets; the rows' swizzle is (l31 >> 1) & 7
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) a_off[mb] = (wm * WM + 32 * mb + l31) * 128;
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) b_off[nb] = (wn * 96 + 32 * nb + l31) * 128;
-  const int sw = l31 & 7;
+  const int sw = (l31 >> 1) & 7;
 
   // the K-step in A stage sta / B stage stb; the DMA of the next B K-step and of the A K-step
   // NSA - 1 ahead (in that order) goes between the MFMA groups, so the SIMD partner wave keeps
