@@ -624,6 +624,26 @@ __device__ __forceinline__ bf16x8 res_trans(const char* img, int rbase, int dsub
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// res_trans split into a per-lane byte offset (o[dsub][read], rows of rbase 0) and the tile base:
+// valid for any rbase that is a multiple of 16 (res_sw reads row bits 1-3 only), so a kernel
+// keeps four offset registers instead of one address per (tile, half, dsub)
+__device__ __forceinline__ void res_trans_offs(int lane, int (&o)[2][2]) {
+  const int ti = lane & 15, tq = ti >> 2, tp = ti & 3, tg = lane >> 4, hh = lane >> 5;
+#pragma unroll
+  for (int dsub = 0; dsub < 2; ++dsub) {
+    const int col = 32 * dsub + 16 * (tg & 1) + 4 * tp;
+    const int r1 = 4 * hh + tq, r2 = r1 + 8;
+    o[dsub][0] = r1 * 128 + 16 * ((col >> 3) ^ res_sw(r1)) + 2 * (col & 7);
+    o[dsub][1] = r2 * 128 + 16 * ((col >> 3) ^ res_sw(r2)) + 2 * (col & 7);
+  }
+}
+__device__ __forceinline__ bf16x8 res_trans_at(const char* img_rows, const int (&o)[2]) {
+  const short4v a = tr_read(reinterpret_cast<const bf16_t*>(img_rows + o[0]));
+  const short4v b = tr_read(reinterpret_cast<const bf16_t*>(img_rows + o[1]));
+  const short8v v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 template <int NTILE, bool DROP, bool WS, bool ONEPASS>
 __global__ __launch_bounds__(64 * RES_NW, 2) void attn_fwd_res_kernel(
     Geo g, AttnMask mask, ResPlan plan, const uint32_t* __restrict__ drop_q, int drop_lp,
@@ -959,6 +979,10 @@ struct ResPlanB {
   uint32_t kword[MAX_SETS][RES_TILES];  // phase B: queries of tile t that see key set s
   uint8_t qblk[2 * RES_NW][RES_SLOTS];  // query blocks of each phase-A wave (0xff-terminated)
   uint8_t kblk[2 * RES_NW][RES_SLOTS];  // key blocks of each phase-B wave
+  // attn_bwd_res8_kernel's work list (0 items: the static deal above): query blocks (b) and key
+  // blocks (0x80 | b) of both phases, longest first
+  uint8_t items[2 * RES_TILES];
+  int n_items;
 };
 
 // DMA of rows [0, 32 NTILE) (clamped to L - 1) of two (row stride s) bf16 tensors into the two
@@ -1368,13 +1392,13 @@ constexpr int RES8_NA = 3;
 __host__ __device__ constexpr int res8_rows(int L, int ntile) {
   return ((L + 7) & ~7) < 32 * ntile ? ((L + 7) & ~7) : 32 * ntile;
 }
-__host__ __device__ constexpr int res8_need(int L, int ntile) {
-  return 3 * res8_rows(L, ntile) * 128 + 32 * ntile * 128 + 2 * 32 * ntile * 4;
+__host__ __device__ constexpr int res8_need(int L, int ntile) {  // + the work-list counter
+  return 3 * res8_rows(L, ntile) * 128 + 32 * ntile * 128 + 2 * 32 * ntile * 4 + 16;
 }
 // static LDS of an instantiation: the largest layout that fits the CU's 160 KB (NTILE 10: L <= 312;
-// the host falls back to the two-phase kernel past it), at least the bias partials' 64 KB
+// the host falls back to the two-phase kernel past it), at least the bias partials' 96 KB
 __host__ __device__ constexpr int res8_lds(int ntile) {
-  return res8_need(32 * ntile, ntile) <= 163840 ? (res8_need(32 * ntile, ntile) > 65536 ? res8_need(32 * ntile, ntile) : 65536)
+  return res8_need(32 * ntile, ntile) <= 163840 ? (res8_need(32 * ntile, ntile) > 98304 ? res8_need(32 * ntile, ntile) : 98304)
                                                  : 163840;
 }
 // DMA of rows [0, 8 np) (clamped to L - 1) of two (row stride s) bf16 tensors into two swizzled
@@ -1416,9 +1440,12 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
   const char* imgD = imgQ + IS;
   float* rl0 = reinterpret_cast<float*>(smem_raw + 3 * IS + ROWS * 128);  // rc0 / rc1 (below)
   float* rl1 = rl0 + LP;
+  int* wq = reinterpret_cast<int*>(rl1 + LP);  // the work-list counter
   int koff[NS];  // row-fragment offsets (row lr of a 32-row tile, chunk 2 s + hh)
 #pragma unroll
   for (int s = 0; s < NS; ++s) koff[s] = lr * 128 + 16 * ((2 * s + hh) ^ res_sw(lr));
+  int tro[2][2];  // transposed-read offsets
+  res_trans_offs(lane, tro);
   float* brow = bias_grad ? bias_grad + h * DH : nullptr;
   const float sc_out = g.scale * drop_scale;
 
@@ -1436,6 +1463,7 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
     for (int i = threadIdx.x; i < nsl; i += 128 * RES_NW)
       reinterpret_cast<uint4*>(smem_raw + 4 * IS)[i] = make_uint4(0u, 0u, 0u, 0u);
   }
+  if (threadIdx.x == 0) *wq = 0;
   const int pq = threadIdx.x;
   const bool pv = pq < ROWS && pq < L;
   bf16x8 orow[8];
@@ -1470,10 +1498,10 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
   __syncthreads();
   RES8_STAMP(2);
 
-  // bias sums: each wave's folded partials through LDS once every wave is done with the images
-  // (two barriers in either branch), summed over the phase's 4 waves in wave order (as
-  // res_bias_reduce), one atomic per d: dq by wave 0, dk by wave 4, dv by wave 5
-  float* red = reinterpret_cast<float*>(smem_raw);  // [2][8 waves][64 lanes][16]
+  // bias sums: each wave's folded partials through LDS once every wave is done with the images,
+  // summed over the 8 waves in wave order (as res_bias_reduce), one atomic per d: dq by wave 0,
+  // dk by wave 1, dv by wave 2
+  float* red = reinterpret_cast<float*>(smem_raw);  // [3][8 waves][64 lanes][16]
   auto bias_out = [&](const float (&bs)[16], int i, float sc) {
     float4* my = reinterpret_cast<float4*>(red + ((i * 8 + wave) * 64 + lane) * 16);
 #pragma unroll
@@ -1490,214 +1518,219 @@ __global__ __launch_bounds__(64 * 2 * RES_NW, 1) void attn_bwd_res8_kernel(
     grad_add(dst + d, sum);
   };
 
-  if (wave < RES8_NA) {
-    float bq[16];
+  float bq[16], bk[16], bv[16];  // bias-gradient partials (dq, dk, dv column sums)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) bq[r] = 0.f;
-    // ================= phase A: dQ (queries on the lanes)
-    for (int slot = 0; slot < RES_SLOTS; ++slot) {
-      const int blk = plan.qblk[wave][slot];
-      if (blk == 0xff) break;  // wave-uniform
-      const int q = 32 * blk + lr;
-      const bool qv = q < L;
-      const int qc = qv ? q : L - 1;
-      bf16x8 qf[NS], df[NS];
+  for (int r = 0; r < 16; ++r) {
+    bq[r] = 0.f;
+    bk[r] = 0.f;
+    bv[r] = 0.f;
+  }
+  // ================= phase A: dQ of query block blk (queries on the lanes)
+  auto do_a = [&](int blk) {
+    const int q = 32 * blk + lr;
+    const bool qv = q < L;
+    const int qc = qv ? q : L - 1;
+    bf16x8 qf[NS], df[NS];
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        qf[s] = *reinterpret_cast<const bf16x8*>(imgQ + blk * 4096 + koff[s]);
-        df[s] = *reinterpret_cast<const bf16x8*>(imgD + blk * 4096 + koff[s]);
-      }
-      const float dkp = -rl1[q];  // kp delta (0 past L)
-      const float lse2 = qv ? lse[(int64_t)bh * L + q] * LOG2E : INFINITY;
-      const int sq = set_of(mask, qc);
-      const int sq0 = __builtin_amdgcn_readfirstlane(sq);
-      const bool uni = mask.causal == 0u && __all(sq == sq0);
-      uint32_t vws[NTILE];
-#pragma unroll
-      for (int t = 0; t < NTILE; ++t) {
-        uint32_t vw = uni ? plan.qword[sq0][t] : plan.qword[sq][t];
-        if (!uni && ((mask.causal >> sq) & 1u)) {
-          const int a0 = max(q + 1 - 32 * t, 0), e0 = min(mask.start[sq] + mask.len[sq] - 32 * t, 32);
-          if (a0 < e0) vw &= ~(uint32_t)(bit_range(a0, e0));
-        }
-        vws[t] = vw;
-      }
-      floatx16 dq[2];
-#pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
-      // the dropout lane masks (scalar loads) one tile ahead: waited for at first use otherwise
-      TileMasks<16> dmq[2];
-      if constexpr (DROP) dmq[0].load(drop_q, drop_lp, blk, 0);
-#pragma unroll
-      for (int t = 0; t < NTILE; ++t) {
-        const uint32_t vw = vws[t];
-        if constexpr (DROP)
-          if (t + 1 < NTILE) dmq[(t + 1) & 1].load(drop_q, drop_lp, blk, 32 * (t + 1));
-        if (!__all(vw == 0u)) {  // wave-uniform
-          const TileMasks<16>& dm = dmq[t & 1];
-          floatx16 sacc, pacc;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            sacc[r] = 0.f;
-            pacc[r] = 0.f;
-          }
-#pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(imgK + t * 4096 + koff[s]);
-            const bf16x8 vf = *reinterpret_cast<const bf16x8*>(imgV + t * 4096 + koff[s]);
-            sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc, 0, 0, 0);
-            pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, df[s], pacc, 0, 0, 0);
-          }
-          if (!__all(vw == 0xffffffffu)) {
-            const uint32_t w = vw >> (4 * hh);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int mk = bitmask_of(w, rbit(r));
-              sacc[r] = __int_as_float((__float_as_int(sacc[r]) & mk) | (~mk & (int)0xff800000u));
-            }
-          }
-          floatx16 ds;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float p = fast_exp2(fmaf(sacc[r], c2, -lse2));
-            float tt = pacc[r];
-            if constexpr (DROP) tt = sel_keep(tt, dm.m[r]);
-            ds[r] = p * (tt - dkp);
-          }
-          const bf16x8 d0 = pack_frag(ds, 0), d1 = pack_frag(ds, 1);
-#pragma unroll
-          for (int d = 0; d < 2; ++d) {
-            dq[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(imgK, 32 * t, d, lane), d0, dq[d], 0, 0, 0);
-            dq[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(imgK, 32 * t + 16, d, lane), d1, dq[d], 0, 0, 0);
-          }
-        }
-      }
-      res_store_rows(dq, sc_out, dqkv + (int64_t)b * dq_s_b + (int64_t)qc * dq_s_t + h * DH, qv, hh);
-      if (brow) res_bias_fold(dq, bq);
+    for (int s = 0; s < NS; ++s) {
+      qf[s] = *reinterpret_cast<const bf16x8*>(imgQ + blk * 4096 + koff[s]);
+      df[s] = *reinterpret_cast<const bf16x8*>(imgD + blk * 4096 + koff[s]);
     }
-    RES8_STAMP(3);
-    if (brow) {
-      __syncthreads();
-      bias_out(bq, 0, sc_out);
-      __syncthreads();
-      if (wave == 0) bias_sum(0, 0, RES8_NA, brow);
-    }
-  } else {
-    // ================= phase B: dK / dV (keys on the lanes)
-    const int wb = wave - RES8_NA;
-    float bk[16], bv[16];
+    const float dkp = -rl1[q];  // kp delta (0 past L)
+    const float lse2 = qv ? lse[(int64_t)bh * L + q] * LOG2E : INFINITY;
+    const int sq = set_of(mask, qc);
+    const int sq0 = __builtin_amdgcn_readfirstlane(sq);
+    const bool uni = mask.causal == 0u && __all(sq == sq0);
+    uint32_t vws[NTILE];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      bk[r] = 0.f;
-      bv[r] = 0.f;
-    }
-    for (int slot = 0; slot < RES_SLOTS; ++slot) {
-      const int blk = plan.kblk[wb][slot];
-      if (blk == 0xff) break;  // wave-uniform
-      const int key = 32 * blk + lr;
-      const bool kv = key < L;
-      const int kc = kv ? key : L - 1;
-      bf16x8 kf[NS], vf[NS];
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        kf[s] = *reinterpret_cast<const bf16x8*>(imgK + blk * 4096 + koff[s]);
-        vf[s] = *reinterpret_cast<const bf16x8*>(imgV + blk * 4096 + koff[s]);
+    for (int t = 0; t < NTILE; ++t) {
+      uint32_t vw = uni ? plan.qword[sq0][t] : plan.qword[sq][t];
+      if (!uni && ((mask.causal >> sq) & 1u)) {
+        const int a0 = max(q + 1 - 32 * t, 0), e0 = min(mask.start[sq] + mask.len[sq] - 32 * t, 32);
+        if (a0 < e0) vw &= ~(uint32_t)(bit_range(a0, e0));
       }
-      const int sk = set_of(mask, kc);
-      const int sk0 = __builtin_amdgcn_readfirstlane(sk);
-      const bool uni = mask.causal == 0u && __all(sk == sk0);
-      uint32_t qws[NTILE];
+      vws[t] = vw;
+    }
+    floatx16 dq[2];
 #pragma unroll
-      for (int t = 0; t < NTILE; ++t) {
-        uint32_t qw = uni ? plan.kword[sk0][t] : plan.kword[sk][t];
-        if (!uni && ((mask.causal >> sk) & 1u)) {
-          const int a0 = max(mask.start[sk] - 32 * t, 0), e0 = min(key - 32 * t, 32);
-          if (a0 < e0) qw &= ~(uint32_t)(bit_range(a0, e0));
-        }
-        if (!kv) qw = 0u;
-        qws[t] = qw;
-      }
-      floatx16 dk[2], dv[2];
+    for (int d = 0; d < 2; ++d)
 #pragma unroll
-      for (int d = 0; d < 2; ++d)
+      for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
+    // the dropout lane masks (scalar loads) one tile ahead: waited for at first use otherwise
+    TileMasks<16> dmq[2];
+    if constexpr (DROP) dmq[0].load(drop_q, drop_lp, blk, 0);
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t) {
+      const uint32_t vw = vws[t];
+      if constexpr (DROP)
+        if (t + 1 < NTILE) dmq[(t + 1) & 1].load(drop_q, drop_lp, blk, 32 * (t + 1));
+      if (!__all(vw == 0u)) {  // wave-uniform
+        const TileMasks<16>& dm = dmq[t & 1];
+        floatx16 sacc, pacc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          dk[d][r] = 0.f;
-          dv[d][r] = 0.f;
+          sacc[r] = 0.f;
+          pacc[r] = 0.f;
         }
 #pragma unroll
-      for (int t = 0; t < NTILE; ++t) {
-        const uint32_t qw = qws[t];
-        if (!__all(qw == 0u)) {  // wave-uniform
-          TileMasks<16> dm;
-          if constexpr (DROP) dm.load(drop_k, drop_lp, blk, 32 * t);
-          floatx16 sacc, ca;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float4 x = *reinterpret_cast<const float4*>(rl0 + 32 * t + 8 * j + 4 * hh);
-            const float4 y = *reinterpret_cast<const float4*>(rl1 + 32 * t + 8 * j + 4 * hh);
-            sacc[4 * j] = x.x; sacc[4 * j + 1] = x.y; sacc[4 * j + 2] = x.z; sacc[4 * j + 3] = x.w;
-            ca[4 * j] = y.x; ca[4 * j + 1] = y.y; ca[4 * j + 2] = y.z; ca[4 * j + 3] = y.w;
-          }
-          floatx16 pacc = ca;
-#pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            const bf16x8 qr = *reinterpret_cast<const bf16x8*>(imgQ + t * 4096 + koff[s]);
-            const bf16x8 dr_ = *reinterpret_cast<const bf16x8*>(imgD + t * 4096 + koff[s]);
-            sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qr, kf[s], sacc, 0, 0, 0);
-            pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dr_, vf[s], pacc, 0, 0, 0);
-          }
-          if (!__all(qw == 0xffffffffu)) {
-            const uint32_t w = qw >> (4 * hh);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int mk = bitmask_of(w, rbit(r));
-              sacc[r] = __int_as_float((__float_as_int(sacc[r]) & mk) | (~mk & (int)0xff800000u));
-            }
-          }
-          floatx16 pk, ds;
+        for (int s = 0; s < NS; ++s) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(imgK + t * 4096 + koff[s]);
+          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(imgV + t * 4096 + koff[s]);
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc, 0, 0, 0);
+          pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, df[s], pacc, 0, 0, 0);
+        }
+        if (!__all(vw == 0xffffffffu)) {
+          const uint32_t w = vw >> (4 * hh);
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const float p = fast_exp2(sacc[r] * c2);
-            if constexpr (DROP) {
-              const bool keep = __builtin_amdgcn_inverse_ballot_w64(dm.m[r]);
-              pk[r] = keep ? p : 0.f;
-              ds[r] = p * (keep ? pacc[r] : ca[r]);
-            } else {
-              pk[r] = p;
-              ds[r] = p * pacc[r];
-            }
-          }
-          const bf16x8 p0 = pack_frag(pk, 0), p1 = pack_frag(pk, 1);
-          const bf16x8 s0 = pack_frag(ds, 0), s1 = pack_frag(ds, 1);
-#pragma unroll
-          for (int d = 0; d < 2; ++d) {
-            dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(imgD, 32 * t, d, lane), p0, dv[d], 0, 0, 0);
-            dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(imgD, 32 * t + 16, d, lane), p1, dv[d], 0, 0, 0);
-            dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(imgQ, 32 * t, d, lane), s0, dk[d], 0, 0, 0);
-            dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans(imgQ, 32 * t + 16, d, lane), s1, dk[d], 0, 0, 0);
+            const int mk = bitmask_of(w, rbit(r));
+            sacc[r] = __int_as_float((__float_as_int(sacc[r]) & mk) | (~mk & (int)0xff800000u));
           }
         }
-      }
-      bf16_t* kro = dqkv + (int64_t)b * dq_s_b + (int64_t)kc * dq_s_t + D + h * DH;
-      res_store_rows(dk, sc_out, kro, kv, hh);
-      res_store_rows(dv, drop_scale, kro + D, kv, hh);
-      if (brow) {
-        res_bias_fold(dk, bk);
-        res_bias_fold(dv, bv);
+        floatx16 ds;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fast_exp2(fmaf(sacc[r], c2, -lse2));
+          float tt = pacc[r];
+          if constexpr (DROP) tt = sel_keep(tt, dm.m[r]);
+          ds[r] = p * (tt - dkp);
+        }
+        const bf16x8 d0 = pack_frag(ds, 0), d1 = pack_frag(ds, 1);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          dq[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans_at(imgK + 32 * t * 128, tro[d]), d0, dq[d], 0, 0, 0);
+          dq[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans_at(imgK + (32 * t + 16) * 128, tro[d]), d1, dq[d], 0, 0, 0);
+        }
       }
     }
-    RES8_STAMP(3);
+    res_store_rows(dq, sc_out, dqkv + (int64_t)b * dq_s_b + (int64_t)qc * dq_s_t + h * DH, qv, hh);
+    if (brow) res_bias_fold(dq, bq);
+  };
+  // ================= phase B: dK / dV of key block blk (keys on the lanes)
+  auto do_b = [&](int blk) {
+    const int key = 32 * blk + lr;
+    const bool kv = key < L;
+    const int kc = kv ? key : L - 1;
+    bf16x8 kf[NS], vf[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      kf[s] = *reinterpret_cast<const bf16x8*>(imgK + blk * 4096 + koff[s]);
+      vf[s] = *reinterpret_cast<const bf16x8*>(imgV + blk * 4096 + koff[s]);
+    }
+    const int sk = set_of(mask, kc);
+    const int sk0 = __builtin_amdgcn_readfirstlane(sk);
+    const bool uni = mask.causal == 0u && __all(sk == sk0);
+    uint32_t qws[NTILE];
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t) {
+      uint32_t qw = uni ? plan.kword[sk0][t] : plan.kword[sk][t];
+      if (!uni && ((mask.causal >> sk) & 1u)) {
+        const int a0 = max(mask.start[sk] - 32 * t, 0), e0 = min(key - 32 * t, 32);
+        if (a0 < e0) qw &= ~(uint32_t)(bit_range(a0, e0));
+      }
+      if (!kv) qw = 0u;
+      qws[t] = qw;
+    }
+    floatx16 dk[2], dv[2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        dk[d][r] = 0.f;
+        dv[d][r] = 0.f;
+      }
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t) {
+      const uint32_t qw = qws[t];
+      if (!__all(qw == 0u)) {  // wave-uniform
+        TileMasks<16> dm;
+        if constexpr (DROP) dm.load(drop_k, drop_lp, blk, 32 * t);
+        floatx16 sacc, ca;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 x = *reinterpret_cast<const float4*>(rl0 + 32 * t + 8 * j + 4 * hh);
+          const float4 y = *reinterpret_cast<const float4*>(rl1 + 32 * t + 8 * j + 4 * hh);
+          sacc[4 * j] = x.x; sacc[4 * j + 1] = x.y; sacc[4 * j + 2] = x.z; sacc[4 * j + 3] = x.w;
+          ca[4 * j] = y.x; ca[4 * j + 1] = y.y; ca[4 * j + 2] = y.z; ca[4 * j + 3] = y.w;
+        }
+        floatx16 pacc = ca;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const bf16x8 qr = *reinterpret_cast<const bf16x8*>(imgQ + t * 4096 + koff[s]);
+          const bf16x8 dr_ = *reinterpret_cast<const bf16x8*>(imgD + t * 4096 + koff[s]);
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qr, kf[s], sacc, 0, 0, 0);
+          pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dr_, vf[s], pacc, 0, 0, 0);
+        }
+        if (!__all(qw == 0xffffffffu)) {
+          const uint32_t w = qw >> (4 * hh);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int mk = bitmask_of(w, rbit(r));
+            sacc[r] = __int_as_float((__float_as_int(sacc[r]) & mk) | (~mk & (int)0xff800000u));
+          }
+        }
+        floatx16 pk, ds;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fast_exp2(sacc[r] * c2);
+          if constexpr (DROP) {
+            const bool keep = __builtin_amdgcn_inverse_ballot_w64(dm.m[r]);
+            pk[r] = keep ? p : 0.f;
+            ds[r] = p * (keep ? pacc[r] : ca[r]);
+          } else {
+            pk[r] = p;
+            ds[r] = p * pacc[r];
+          }
+        }
+        const bf16x8 p0 = pack_frag(pk, 0), p1 = pack_frag(pk, 1);
+        const bf16x8 s0 = pack_frag(ds, 0), s1 = pack_frag(ds, 1);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans_at(imgD + 32 * t * 128, tro[d]), p0, dv[d], 0, 0, 0);
+          dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans_at(imgD + (32 * t + 16) * 128, tro[d]), p1, dv[d], 0, 0, 0);
+          dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans_at(imgQ + 32 * t * 128, tro[d]), s0, dk[d], 0, 0, 0);
+          dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(res_trans_at(imgQ + (32 * t + 16) * 128, tro[d]), s1, dk[d], 0, 0, 0);
+        }
+      }
+    }
+    bf16_t* kro = dqkv + (int64_t)b * dq_s_b + (int64_t)kc * dq_s_t + D + h * DH;
+    res_store_rows(dk, sc_out, kro, kv, hh);
+    res_store_rows(dv, drop_scale, kro + D, kv, hh);
     if (brow) {
-      __syncthreads();
-      bias_out(bk, 0, sc_out);
-      bias_out(bv, 1, drop_scale);
-      __syncthreads();
-      if (wave == RES8_NA) bias_sum(0, RES8_NA, 2 * RES_NW - RES8_NA, brow + D);
-      else if (wave == RES8_NA + 1) bias_sum(1, RES8_NA, 2 * RES_NW - RES8_NA, brow + 2 * D);
+      res_bias_fold(dk, bk);
+      res_bias_fold(dv, bv);
     }
+  };
+  // the work list (plan.n_items > 0): every block of both phases, longest first (host plan); each
+  // wave takes the next item from an LDS counter, so a wave whose SIMD partner runs long takes
+  // fewer. Otherwise (deterministic mode: the bias partials per wave must be the same every run)
+  // the static deal: query blocks on waves 0 .. RES8_NA - 1, key blocks on the rest.
+  const bool dyn = plan.n_items > 0;
+  for (int slot = 0;; ++slot) {
+    int item;
+    if (dyn) {
+      int it = 0;
+      if (lane == 0) it = atomicAdd(wq, 1);
+      it = __builtin_amdgcn_readfirstlane(it);
+      if (it >= plan.n_items) break;  // wave-uniform
+      item = plan.items[it];
+    } else {
+      if (slot >= RES_SLOTS) break;
+      const int blk = wave < RES8_NA ? plan.qblk[wave][slot] : plan.kblk[wave - RES8_NA][slot];
+      if (blk == 0xff) break;  // wave-uniform
+      item = wave < RES8_NA ? blk : 0x80 | blk;
+    }
+    if (item & 0x80) do_b(item & 0x7f);
+    else do_a(item);
+  }
+  RES8_STAMP(3);
+  if (brow) {  // over all 8 waves (a wave that took no block of a kind adds exact zeros)
+    __syncthreads();
+    bias_out(bq, 0, sc_out);
+    bias_out(bk, 1, sc_out);
+    bias_out(bv, 2, drop_scale);
+    __syncthreads();
+    if (wave < 3) bias_sum(wave, 0, 2 * RES_NW, brow + wave * D);
   }
   RES8_STAMP(4);
 }
@@ -1765,6 +1798,27 @@ static bool res_plan_bwd(const AttnMask& m, int L, ResPlanB& pb, int na = RES_NW
   int kc[RES_TILES];
   res_costs(m, L, pb.kword, kc);
   return res_deal(kc, nt, nb, pb.kblk);
+}
+
+// attn_bwd_res8_kernel's work list: every query block (phase A) and key block (phase B) by
+// estimated cost, longest first; a key block costs ~1.6x a query block of the same visible tiles
+// (16 MFMAs and two more selects per tile against 12)
+static void res8_items(const AttnMask& m, int L, ResPlanB& pb) {
+  const int nt = (L + 31) / 32;
+  int qc[RES_TILES], kc[RES_TILES], cost[2 * RES_TILES];
+  res_costs(m, L, pb.qword, qc);
+  res_costs(m, L, pb.kword, kc);
+  for (int i = 0; i < nt; ++i) {
+    pb.items[i] = (uint8_t)i;
+    cost[i] = 5 * qc[i];
+    pb.items[nt + i] = (uint8_t)(0x80 | i);
+    cost[nt + i] = 8 * kc[i];
+  }
+  std::stable_sort(pb.items, pb.items + 2 * nt, [&](uint8_t a, uint8_t b) {
+    const int ca = cost[(a & 0x80) ? nt + (a & 0x7f) : a], cb = cost[(b & 0x80) ? nt + (b & 0x7f) : b];
+    return ca > cb;
+  });
+  pb.n_items = 2 * nt;
 }
 
 // =============================================================================== bwd: dQ
@@ -2392,6 +2446,12 @@ extern "C" int mmt_attn_bwd(const void* qkv, int64_t s_b, int64_t s_t, int B, in
                       res8_need(L, ((L + 63) / 64) * 2) <= res8_lds(((L + 63) / 64) * 2);
     ResPlanB plan;
     if (bwd8 ? res_plan_bwd(m, L, plan, RES8_NA, 2 * RES_NW - RES8_NA) : res_plan_bwd(m, L, plan)) {
+      // the work list at 192 < L <= 256 (tools/attn_bench.py B = 512, backward: L = 228 291 vs
+      // 311 us with the static deal; L = 292 458 vs 452, L = 164 200 vs 194, so not there), not
+      // in deterministic mode (its bias partials must not depend on which wave took a block);
+      // MMT_ATTN_BWD8_DEAL=1: the static deal everywhere (A/B)
+      static const bool deal = getenv("MMT_ATTN_BWD8_DEAL") && atoi(getenv("MMT_ATTN_BWD8_DEAL")) == 1;
+      if (bwd8 && !deal && g_det_host.fx == nullptr && ((L + 63) / 64) * 2 == 8) res8_items(m, L, plan);
       const int ntile = ((L + 63) / 64) * 2;
 #define RESB1(NT_, DR_)                                                                             \
   do {                                                                                              \
