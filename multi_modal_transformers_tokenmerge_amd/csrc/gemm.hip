@@ -2512,6 +2512,12 @@ int ntws_mode() {
   return m;
 }
 
+// The frozen T5's 768-wide bf16-residual products (o-projection, FF output) at 8192 < M <= 16384:
+// nt256 with 192-wide tiles (measured, see ntw_ok)
+bool t5_res768(int M, int N, const Epi& e) {
+  return N == 768 && e.residual && !e.res_f32 && M > 8192 && M <= 16384 && g_variant < 0;
+}
+
 bool ntw_ok(int M, int N, int K, int transA, int transB, int batch, int out_kind, const Epi& e) {
   if (transA || !transB || batch != 1 || out_kind != 0 || N % 192 != 0 || K % 64 != 0) return false;
   if (e.bias || e.rng || e.gate || e.relu_bits || e.gate_bits || e.keep_bits || e.colsum || e.alpha != 1.f ||
@@ -2524,12 +2530,16 @@ bool ntw_ok(int M, int N, int K, int transA, int transB, int batch, int out_kind
   const bool relu = e.act == MMT_ACT_RELU && !e.residual && N >= 2048 && K <= 1024 && ntws_mode() != 2;
   // the frozen T5's other products at small batch (M = 32 B; tools/t5_small_probe.py, us per
   // launch, automatic choice vs this kernel): the plain QKV product 2304 x 768 at M 4096 / 8192
-  // (30.1 / 46.9 vs 23.8 / 36.5; equal at 16384), the o-projection + residual 768 x 768 at
-  // M 8192 / 16384 (21.9 / 34.1 vs 20.4 / 29.0), the relu product from M 4096 (28.9 vs 25.6)
+  // (30.1 / 46.9 vs 23.8 / 36.5), the o-projection + residual 768 x 768 at M 8192 (21.9 vs 20.4),
+  // the relu product from M 4096 (28.9 vs 25.6). Round 6, at the bench batch (M = 16384,
+  // tools/gpu_t5_variants.sh + tools/t5_products.py, this kernel with its conflict-free swizzle):
+  // the QKV product 69.7 here vs 76.1 on nt256 (192-wide tiles); the two 768-wide residual
+  // products faster on nt256's 192-wide tiles (t5_res768 below): o-projection 33.7 vs 36.0, FF
+  // output 91.3 vs 97.8
   const bool wide_plain = e.act == MMT_ACT_NONE && !e.residual && N >= 2048 && K <= 1024;
   const bool square_res = e.residual && N == 768 && K <= 1024;
-  return ((narrow || square_res) && M >= 8192) || (relu && M >= 4096) ||
-         (wide_plain && M >= 4096 && M <= 8192);
+  if (t5_res768(M, N, e)) return false;
+  return ((narrow || square_res) && M >= 8192) || (relu && M >= 4096) || (wide_plain && M >= 4096);
 }
 
 // Launch plan of gemm_ntw_kernel: tile width bn (192 / 384), `rows_big` rows in full rounds of
@@ -2788,7 +2798,11 @@ extern "C" int mmt_gemm(int M, int N, int K, const void* A, int transA, int64_t 
     return MMT_OK;
   }
   // Persistent 256 x BN NT kernel (variant -1 auto, 5/6/7 force BN 256/192/128)
-  const int bn =(epi.bias && N > NT_BIAS_LDS) ? 0 : nt_bn(M, N, K, transA, transB, batch, out_kind, final_kind);
+  const int bn = (epi.bias && N > NT_BIAS_LDS) ? 0
+                 : (t5_res768(M, N, epi) && !transA && transB && batch == 1 && out_kind == 0 &&
+                    final_kind == 0 && K % 64 == 0 && !epi.bias && epi.act == MMT_ACT_NONE)
+                     ? 192
+                     : nt_bn(M, N, K, transA, transB, batch, out_kind, final_kind);
   MMT_CHECK_ARG(!(epi.relu_bits || epi.gate_bits) || (bn == 256 && final_kind == 0),
                 "mmt_gemm: relu_bits / gate_bits need the 256-wide bf16 nt path (mmt_gemm_colsum_rows)");
   if (bn) {
