@@ -938,7 +938,9 @@ extern "C" int mmt_stem_conv_pool(const void* img, int B, int I, int Himg, const
 extern "C" int mmt_stem_conv_wgrad_slabs(int B, int I, int Himg) {
   if (B <= 0 || I <= 0 || Himg < 16 || Himg % 16) return 0;
   const int PPD = Himg / 16;
-  return (int)std::min<int64_t>((int64_t)B * I * PPD * ((PPD + 15) / 16), 256);
+  // two workgroups per CU (the kernel's launch bound): one per CU left the tile loop's
+  // fetch / LDS staging / MFMA phases unoverlapped (one wave per SIMD)
+  return (int)std::min<int64_t>((int64_t)B * I * PPD * ((PPD + 15) / 16), 2 * 256);
 }
 
 extern "C" int mmt_stem_conv_wgrad(const void* img, int B, int I, int Himg, const float* dpooled,
