@@ -17,6 +17,7 @@ def main():
     Ls = (292, 212, 132)
     t5 = True
     H = 6
+    drop = "--nodrop" not in sys.argv  # the OCTO cases without attention dropout
     for a in sys.argv[1:]:
         if a.startswith("--h="):
             H = int(a.split("=")[1])
@@ -30,7 +31,7 @@ def main():
     for L in Ls:  # default: layers 0, 5, 10 of the ToMe r=16 schedule
         n_img = L - 36
         cases.append((f"octo L={L}", L, H, 64,
-                      K.SetTable([0, 32, 32 + n_img], [32, n_img, 4], [0b001, 0b011, 0b111]), True, False))
+                      K.SetTable([0, 32, 32 + n_img], [32, n_img, 4], [0b001, 0b011, 0b111]), drop, False))
     if t5:
         cases.append(("t5 L=32 (bias)", 32, 12, 64, None, False, True))
     for name, L, H, Dh, table, drop, bias in cases:
