@@ -859,7 +859,14 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_fwd_res_kernel(
         for (int d = 0; d < 2; ++d)
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) vt[d][ks] = res_trans(Vimg, 32 * t + 16 * ks, d, lane);
+        floatx16 p;
         if constexpr (ONEPASS) {
+          // the weights with the running max as it stands, issued before the tile max is known:
+          // the exponentials do not wait on its cross-lane reduction and vote; the rare tile that
+          // moves a row's max by more than RES_TAU recomputes them (same values as computing them
+          // after the test: bit-identical)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) p[r] = fast_exp2(fmaf(Sa[r], c2, -mc));
           float tm = fmaxf(fmaxf(fmaxf(Sa[0], Sa[1]), fmaxf(Sa[2], Sa[3])), fmaxf(fmaxf(Sa[4], Sa[5]), fmaxf(Sa[6], Sa[7])));
           tm = fmaxf(tm, fmaxf(fmaxf(fmaxf(Sa[8], Sa[9]), fmaxf(Sa[10], Sa[11])), fmaxf(fmaxf(Sa[12], Sa[13]), fmaxf(Sa[14], Sa[15]))));
           tm = halves_max(tm) * c2;
@@ -879,12 +886,16 @@ __global__ __launch_bounds__(64 * RES_NW, 2) void attn_fwd_res_kernel(
             }
             mrun = mnew;
             mc = mrun == -INFINITY ? 0.f : mrun;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) p[r] = fast_exp2(fmaf(Sa[r], c2, -mc));
           }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) p[r] = fast_exp2(fmaf(Sa[r], c2, -mc));
         }
-        floatx16 p;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float e = fast_exp2(fmaf(Sa[r], c2, -mc));
+          float e = p[r];
           l4[r & 3] += e;
           if constexpr (DROP) e = sel_keep(e, dm[t & 1].m[r]);
           if constexpr (WS) ld4[r & 3] += e;
