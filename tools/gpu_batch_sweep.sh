@@ -1,10 +1,9 @@
 #!/bin/bash
-# per-GPU batch sweep of the bench step (throughput vs B)
+# step throughput at several per-GPU batches, interleaved with the metric batch (one box)
 set -o pipefail
-export TMPDIR=/tmp
+TAG=${1:-bsweep}
 mkdir -p gpurun_out
-rm -f gpurun_out/bsweep.log
-for b in ${BATCHES:-256 384 512 192 320 256}; do
-  timeout -k 10 250 python bench.py --batch $b --steps 40 --warmup 10 --no-cpu-baseline --no-probes > gpurun_out/bs_$b.log 2>&1 || exit 1
-  echo "B=$b $(grep -o '"value": [0-9.]*' gpurun_out/bs_$b.log)" >> gpurun_out/bsweep.log
+for b in 512 64 128 256 512; do
+  timeout -k 10 300 python -u bench.py --batch $b --steps 40 --warmup 10 --no-cpu-baseline --no-probes > gpurun_out/${TAG}_b$b.log 2>&1 || exit 1
+  grep '^{' gpurun_out/${TAG}_b$b.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print($b, d['value'], d['ms_per_step'])" >> gpurun_out/${TAG}.txt || exit 1
 done
